@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): queries/s (whole node) + ms/build, 900K points, k=16.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 900000] [--k 16]
+  torchrun --nproc-per-node N bench.py --gpus N ...          (driver launch for N > 1)
+
+One *step* = the reference's kn_prepare + kn_solve on device-resident points (knearests.cu
+:235-392): bounding box, binning (count/scan/scatter), LDS-tiled kNN of EVERY point,
+exact-path fallback, results in original order with squared distances. On 1 GPU the step
+is replayed from a HIP graph. On N GPUs (weak scaling: N x 900K points, uniform in the
+shared [0,1000]^3 cube, generated independently per rank, i.e. NOT pre-partitioned) a
+step additionally redistributes the points to their spatial owner and exchanges halos with
+RCCL all-to-alls (see cuda_knearests_amd/parallel/distributed.py).
+
+Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize + barrier; the
+per-rank time is MAX-reduced; rank 0 prints one JSON line. Correctness is spot-checked
+outside the timed region against a GPU brute force on a random subset of queries.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "queries/sec (whole node) + ms/build for 900K pts, k=16, at 1/2/4/8 MI355X"
+CPU_ORACLE_QPS = 1.35e6  # reference kd_tree.cpp, 900K uniform, K=16, 8-vCPU host
+
+
+def brute_check(points: torch.Tensor, idx: torch.Tensor, d2: torch.Tensor, k: int, nsample: int = 2048,
+                ids: torch.Tensor | None = None, queries: torch.Tensor | None = None) -> dict:
+    """Compare a random subset of rows with an exact brute force (fp32, same fma order)."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(1234)
+    nq = idx.size(0)
+    sel = torch.randperm(nq, generator=g)[: min(nsample, nq)].to(points.device)
+    q = (queries if queries is not None else points)[sel]
+    bad = 0
+    for c0 in range(0, sel.numel(), 256):
+        qs = q[c0:c0 + 256]
+        dx = points[None, :, 0] - qs[:, None, 0]
+        dy = points[None, :, 1] - qs[:, None, 1]
+        dz = points[None, :, 2] - qs[:, None, 2]
+        dd = torch.addcmul(torch.addcmul(dx * dx, dy, dy), dz, dz)
+        self_idx = sel[c0:c0 + 256] if queries is None else None
+        if self_idx is not None:
+            dd[torch.arange(qs.size(0), device=dd.device), self_idx] = float("inf")
+        else:
+            dd[dd == 0] = float("inf")  # distributed: exclude self by zero distance (ids differ)
+        ref = torch.topk(dd, k, dim=1, largest=False).values
+        got = d2[sel[c0:c0 + 256]]
+        # brute force rounds without fma: allow 1e-5 relative
+        bad += int(((got - ref).abs() > 1e-5 * ref.abs().clamp(min=1e-6)).any(1).sum())
+    return {"checked": int(sel.numel()), "bad_rows": bad}
+
+
+def run_single(args) -> dict:
+    from cuda_knearests_amd import KNearests
+    from cuda_knearests_amd.utils import uniform_cloud
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    pts = uniform_cloud(args.n, seed=args.seed, device=dev)
+    kn = KNearests(k=args.k, device=dev, deterministic=not args.nondet)
+    kn.prepare(pts)
+    kn.solve()  # eager pass: plan + per-phase device timings + counters
+    ms_build, ms_solve = kn.timings["ms_build"], kn.timings["ms_solve"]
+    info = dict(kn.info)
+    for _ in range(args.warmup):
+        kn.step(pts, capture=not args.no_graph)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        kn.step(pts, capture=not args.no_graph)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    chk = brute_check(pts, kn.neighbors, kn.distances, args.k) if not args.no_check else {}
+    # per-phase device times, median of a few eager runs
+    bts, sts = [], []
+    for _ in range(5):
+        kn.prepare(pts)
+        kn.solve()
+        bts.append(kn.timings["ms_build"])
+        sts.append(kn.timings["ms_solve"])
+    bts.sort(), sts.sort()
+    return {"t": dt, "ms_build": bts[2], "ms_solve": sts[2], "ms_build_first": ms_build,
+            "ms_solve_first": ms_solve, "info": info, "check": chk, "n_total": args.n}
+
+
+def run_dist(args) -> dict:
+    import torch.distributed as dist
+
+    from cuda_knearests_amd.parallel import DistributedKNearests
+    from cuda_knearests_amd.utils import uniform_cloud
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    pts = uniform_cloud(args.n, seed=args.seed + 7919 * rank, device=dev)
+    dk = DistributedKNearests(k=args.k)
+    res = None
+    for _ in range(args.warmup):
+        res = dk.solve(pts, partitioned=args.layout == "partitioned")
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = dk.solve(pts, partitioned=args.layout == "partitioned")
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    chk = {}
+    if not args.no_check and res is not None:
+        # gather the global cloud ordered by id for a brute-force spot check on rank 0's queries
+        n_all = [torch.zeros(1, dtype=torch.long, device=dev) for _ in range(world)]
+        dist.all_gather(n_all, torch.tensor([pts.size(0)], device=dev))
+        allp = [torch.empty(int(c.item()), 3, device=dev) for c in n_all]
+        dist.all_gather(allp, pts)
+        cloud = torch.cat(allp)
+        qpts = cloud[res.ids.long()]
+        chk = brute_check(cloud, res.neighbors, res.d2, args.k, nsample=1024, queries=qpts)
+        c = torch.tensor([chk["bad_rows"]], device=dev)
+        dist.all_reduce(c)
+        chk["bad_rows_all_ranks"] = int(c.item())
+    out = {"t": float(t.item()), "stats": res.stats if res else {}, "check": chk, "n_total": args.n * world,
+           "rank": rank, "world": world}
+    dist.barrier()
+    dist.destroy_process_group()
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=900_000, help="points per GPU")
+    ap.add_argument("--k", type=int, default=16)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--layout", choices=["scattered", "partitioned"], default="scattered")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--nondet", action="store_true")
+    args = ap.parse_args()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env == 1:
+        # convenience: relaunch under torch.distributed.run (before any GPU init)
+        import subprocess
+
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29517")] + sys.argv
+        return subprocess.call(cmd)
+    if world_env > 1:
+        r = run_dist(args)
+        if r["rank"] != 0:
+            return 0
+        n_gpus = r["world"]
+        extra = {"halo_width": r["stats"].get("halo_width"), "n_halo_rank0": r["stats"].get("n_halo"),
+                 "rounds": r["stats"].get("rounds"), "rank_grid": r["stats"].get("grid"), "layout": args.layout}
+    else:
+        r = run_single(args)
+        n_gpus = 1
+        extra = {"ms_build": round(r["ms_build"], 4), "ms_solve": round(r["ms_solve"], 4),
+                 "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph}
+    ms = r["t"] / args.steps * 1e3
+    qps = r["n_total"] * args.steps / r["t"]
+    line = {
+        "metric": METRIC, "value": qps, "unit": "queries/s", "n_gpus": n_gpus, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic uniform random [0,1000]^3 (seeded per rank)",
+        "config": {"model": f"uniform-grid kNN, {args.n} pts/GPU, k={args.k}", "global_batch": r["n_total"],
+                   "seq_len": args.k, "parallelism": f"spatial{n_gpus}" if n_gpus > 1 else "single"},
+        "vs_cpu_oracle": qps / CPU_ORACLE_QPS, "check": r.get("check", {}), **extra,
+    }
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

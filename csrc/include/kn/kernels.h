@@ -1,0 +1,111 @@
+// kn/kernels.h -- host-side launchers for the gfx950 HIP kernels.
+//
+// Every launcher is stream-ordered, allocation-free and synchronisation-free, so the
+// whole build+solve pipeline can be captured into a hipGraph (engine.cpp) or run on the
+// current PyTorch stream (torch/bindings.cpp). Buffers are owned by the caller.
+//
+// Pipeline (replaces reference knearests.cu:152-201 kn_firstbuild and :348-392 kn_solve):
+//   bbox -> geom -> count(+rank) -> scan(blocks, top) -> scatter(+cell_start) [-> cell sort]
+//   -> knn_tile (LDS-staged, certified) -> knn_fallback (exact ring walk for the rest)
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace kn {
+
+// Device-resident grid geometry. Written by geom_kernel (or geom_from_box) so the host
+// never has to read the data-dependent bounding box back (graph-capturable pipeline).
+struct GridGeom {
+    float origin[3];    // world position of cell (0,0,0)'s lower corner
+    float cell[3];      // cell edge per axis
+    float inv_cell[3];  // 1 / cell
+    float eps;          // conservative slack for box-distance bounds (world units)
+    int dims[3];
+    int pad;
+};
+
+// Box inside which the local point set is complete (all points of the global cloud that lie
+// in it are present). Single GPU: infinite. Multi-GPU: the rank's owned box grown by its halo.
+struct CompleteBox {
+    float lo[3];
+    float hi[3];
+};
+
+constexpr int kScanItems = 4096;  // elements per scan block (256 threads x 16)
+
+struct BuildBuffers {
+    // inputs
+    const float* points;      // N x 3 floats (AoS, 12-byte stride)
+    int n;
+    int dims[3];
+    // scratch / outputs (caller-allocated)
+    unsigned* bbox_words;     // 8 words, zeroed by the launcher (memset node)
+    GridGeom* geom;           // 1
+    int* cell_count;          // C      (zeroed by the launcher)
+    int* cell_scan;           // C      block-local exclusive scan
+    int* block_sums;          // ceil(C / kScanItems) + 1
+    int* cell_start;          // C + 1  final exclusive scan, cell_start[C] = N
+    int2* cell_rank;          // N      (cell, rank inside cell)
+    float4* sorted;           // N      {x, y, z, bits(original index)}
+    unsigned* perm;           // N      perm[stored] = original index
+    int deterministic;        // 1: sort each cell by original index
+    // optional fixed domain (multi-GPU ranks): if use_box, bbox is not computed
+    int use_box;
+    float box_lo[3], box_hi[3];
+};
+
+size_t scan_block_count(int num_cells);
+hipError_t launch_build(const BuildBuffers& b, hipStream_t stream);
+
+struct QueryBuffers {
+    const float4* sorted;
+    const int* cell_start;
+    const unsigned* perm;
+    const GridGeom* geom;
+    int n;                    // number of stored points
+    int dims[3];
+    int k;
+    int n_queries;            // points with original index < n_queries are queries
+    const unsigned* id_map;   // optional: output id = id_map[original index]
+    CompleteBox complete;
+    unsigned* out_idx;        // n_queries x k   (row = original index), UINT_MAX = empty
+    float* out_dist;          // optional n_queries x k squared distances
+    unsigned* fallback_list;  // n   (stored indices of queries needing the exact path)
+    unsigned* counters;       // 4 words: [0] fallback count, [1] uncertified, [2] tile overflow, [3] spare
+    unsigned* uncert_list;    // optional n_queries: original indices of uncertified queries
+    int tile[3];
+    int halo;
+    int lds_capacity;         // points staged per workgroup (power of two)
+    int use_tiles;            // 0: exact ring walk for every query (debug / reference path)
+};
+
+hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);
+
+// out_sorted[i*k + j] = inv(out_orig[perm[i]*k + j]) : reference (stored-space) view.
+hipError_t launch_to_stored_space(const unsigned* out_orig, const unsigned* perm,
+                                  const unsigned* inv_perm, int n, int k,
+                                  unsigned* out_sorted, const float* dist_orig,
+                                  float* dist_sorted, hipStream_t stream);
+hipError_t launch_invert_perm(const unsigned* perm, int n, unsigned* inv, hipStream_t stream);
+
+// Grid-occupancy statistics (reference kn_print_stats, knearests.cu:440-466):
+// out[0]=min, out[1]=max, out[2]=empty cells, out[3..3+hist_len) = histogram of counts.
+hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int hist_len,
+                             hipStream_t stream);
+
+// Heuristics shared by the engine, the torch binding and the CLI.
+struct AutoParams {
+    int dims[3];
+    int tile[3];
+    int halo;
+    int lds_capacity;
+    size_t lds_bytes;
+};
+AutoParams auto_params(int n, int k, float points_per_cell, const int* tile_hint, int halo_hint,
+                       const float* extent /* nullable: cubic grid */);
+size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity);
+int lds_capacity_for(double staged_points);
+
+}  // namespace kn

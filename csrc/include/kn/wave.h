@@ -1,0 +1,84 @@
+// kn/wave.h -- wave64 device helpers for gfx950 (DPP reductions, med3, cell mapping).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "kn/kernels.h"
+
+namespace kn {
+
+// DPP controls (gfx9 encoding)
+#define KN_DPP_QUAD_1032 0xB1
+#define KN_DPP_QUAD_2301 0x4E
+#define KN_DPP_ROW_MIRROR 0x140
+#define KN_DPP_ROW_HALF_MIRROR 0x141
+
+// Row (16-lane) reduction with DPP, then combine the 4 rows through readlane (SGPR result,
+// wave-uniform). ~12 instructions, no LDS traffic.
+#define KN_WAVE_REDUCE(NAME, T, OP)                                                            \
+    __device__ __forceinline__ T NAME(T x) {                                                   \
+        x = OP(x, (T)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false)); \
+        x = OP(x, (T)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false)); \
+        x = OP(x, (T)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false)); \
+        x = OP(x, (T)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_MIRROR, 0xF, 0xF, false)); \
+        const T a = (T)__builtin_amdgcn_readlane((int)x, 0);                                   \
+        const T b = (T)__builtin_amdgcn_readlane((int)x, 16);                                  \
+        const T c = (T)__builtin_amdgcn_readlane((int)x, 32);                                  \
+        const T d = (T)__builtin_amdgcn_readlane((int)x, 48);                                  \
+        return OP(OP(a, b), OP(c, d));                                                         \
+    }
+
+__device__ __forceinline__ unsigned kn_umin(unsigned a, unsigned b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned kn_umax(unsigned a, unsigned b) { return a > b ? a : b; }
+__device__ __forceinline__ int kn_imin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int kn_imax(int a, int b) { return a > b ? a : b; }
+
+KN_WAVE_REDUCE(wave_min_u32, unsigned, kn_umin)
+KN_WAVE_REDUCE(wave_max_u32, unsigned, kn_umax)
+KN_WAVE_REDUCE(wave_min_i32, int, kn_imin)
+KN_WAVE_REDUCE(wave_max_i32, int, kn_imax)
+
+// Inclusive prefix sum over the 64 lanes.
+__device__ __forceinline__ int wave_inclusive_scan_add(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+// v_med3_u32: the median of three. With lo <= hi this is clamp(x, lo, hi), the single-op
+// step of a sorted-array insertion (new[j] = med3(old[j-1], x, old[j])).
+__device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c) {
+    unsigned r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Point -> cell coordinate along one axis. Identical arithmetic everywhere (binning, queries,
+// fallback) so a point's cell is reproducible bit-for-bit.
+__device__ __forceinline__ int cell_coord(const GridGeom& g, int a, float p) {
+    const float f = (p - g.origin[a]) * g.inv_cell[a];
+    const int i = (int)floorf(fminf(fmaxf(f, -1.f), (float)g.dims[a]));
+    return clampi(i, 0, g.dims[a] - 1);
+}
+__device__ __forceinline__ int cell_of(const GridGeom& g, const float p[3]) {
+    const int i = cell_coord(g, 0, p[0]);
+    const int j = cell_coord(g, 1, p[1]);
+    const int k = cell_coord(g, 2, p[2]);
+    return i + g.dims[0] * (j + g.dims[1] * k);
+}
+
+// Lower bound of the distance from coordinate q to the slab of cells [c0, c1] on axis a
+// (conservative by g.eps so rounding in binning can never make it exceed a true distance).
+__device__ __forceinline__ float slab_dist(const GridGeom& g, int a, float q, int c0, int c1) {
+    const float lo = g.origin[a] + (float)c0 * g.cell[a] - g.eps;
+    const float hi = g.origin[a] + (float)(c1 + 1) * g.cell[a] + g.eps;
+    return fmaxf(0.f, fmaxf(lo - q, q - hi));
+}
+
+}  // namespace kn

@@ -1,0 +1,125 @@
+/*
+ * knearests.h -- public C API of the MI355X-native k-nearest-neighbour engine.
+ *
+ * Source-compatible with the reference API (reference knearests.h:3-29):
+ *   kn_problem, kn_prepare, kn_solve, kn_free, kn_get_points, kn_get_knearests,
+ *   kn_get_permutation, kn_print_stats
+ * with the same index-space semantics (reference knearests.cu:129,145 / test_knearests.cu:158):
+ *   - kn_get_points()      : points in *stored* (cell-bucketed) order,
+ *   - kn_get_permutation() : perm[stored] = original index,
+ *   - kn_get_knearests()   : N x K uint32, row i = neighbours of stored point i, values are
+ *                            stored indices, ascending by distance, self excluded,
+ *                            UINT_MAX marks slots that could not be filled (N <= K).
+ * Getters return malloc()'d host buffers that the caller releases with free().
+ *
+ * Extensions (not in the reference): runtime K and tuning (kn_config / kn_prepare_ex),
+ * squared distances (kn_get_distances), original-order results (kn_get_neighbors),
+ * per-phase timings and counters (kn_get_stats), error codes instead of exit()
+ * (kn_last_error), re-solve without rebuild (kn_set_k), binary save/load of the binned
+ * structure (kn_save / kn_load).
+ */
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Host-side 3-float point. Layout-identical to HIP's float3 (12 bytes, 4-byte aligned),
+ * so `(float3*)vec.data()` callers of the reference keep working. */
+#ifndef KN_HAVE_FLOAT3
+#if defined(__HIP__) || defined(__HIPCC__) || defined(HIP_INCLUDE_HIP_HIP_RUNTIME_H) || \
+    defined(HIP_INCLUDE_HIP_AMD_DETAIL_HIP_VECTOR_TYPES_H)
+#define KN_HAVE_FLOAT3 1
+typedef float3 kn_float3;
+#else
+typedef struct { float x, y, z; } kn_float3;
+#endif
+#endif
+
+#define KN_DEFAULT_K 50 /* reference params.h:4 (DEFAULT_NB_PLANES) */
+#define KN_MAX_K 128
+
+typedef enum {
+    KN_OK = 0,
+    KN_ERR_INVALID_ARGUMENT = 1,
+    KN_ERR_OUT_OF_MEMORY = 2,
+    KN_ERR_DEVICE = 3,
+    KN_ERR_IO = 4,
+    KN_ERR_STATE = 5
+} kn_status;
+
+/* Runtime configuration (replaces the reference's compile-time params.h). */
+typedef struct {
+    int k;                   /* neighbours per point (1..KN_MAX_K), default 50            */
+    float points_per_cell;   /* grid density target; <=0 -> automatic (>= 3.1, ref :249)  */
+    int tile[3];             /* query tile in cells (x,y,z); 0 -> automatic                */
+    int halo;                /* halo rings staged around a tile; 0 -> automatic            */
+    int deterministic;       /* 1 -> stable in-cell order (sorted by original id)          */
+    int device;              /* HIP device ordinal                                        */
+    int verbose;             /* 0 silent, 1 timings (reference IF_VERBOSE), 2 debug        */
+    int exact_only;          /* 1 -> skip the LDS tile kernel (exact ring walk for all)      */
+} kn_config;
+
+/* Per-solve statistics (reference kn_print_stats + cell_max, knearests.cu:378-466). */
+typedef struct {
+    int num_points;
+    int k;
+    int dims[3];
+    int num_cells;
+    int min_cell, max_cell;   /* occupancy */
+    float avg_cell;
+    int empty_cells;
+    int fallback_queries;     /* queries not certified by the tiled kernel          */
+    int uncertified_queries;  /* queries with fewer than K neighbours in the cloud  */
+    float ms_build;           /* bbox + count + scan + scatter (device time)        */
+    float ms_solve;           /* tiled query + fallback (device time)               */
+} kn_stats;
+
+typedef struct {
+    int allocated_points;        /* number of input points (reference field)               */
+    int dimx, dimy, dimz;        /* grid resolution (reference field)                      */
+    int num_cell_offsets;        /* kept for source compatibility; ring walk is analytic   */
+    int k;                       /* neighbours per point                                   */
+    unsigned int *d_permutation; /* device: perm[stored] = original index                  */
+    int *d_cell_start;           /* device: first stored index of each cell, C+1 entries   */
+    float *d_stored_points;      /* device: float4 {x,y,z,bits(original index)} per point  */
+    unsigned int *d_knearests;   /* device: N x K neighbours in stored space               */
+    void *impl;                  /* engine state (opaque)                                  */
+} kn_problem;
+
+/* ---- reference-compatible API ---------------------------------------------------- */
+kn_problem *kn_prepare(const kn_float3 *points, int numpoints);
+void kn_solve(kn_problem *kn);
+void kn_free(kn_problem **kn);
+
+kn_float3 *kn_get_points(kn_problem *kn);
+unsigned int *kn_get_knearests(kn_problem *kn);
+unsigned int *kn_get_permutation(kn_problem *kn);
+
+void kn_print_stats(kn_problem *kn);
+
+/* ---- extensions ------------------------------------------------------------------- */
+kn_config kn_default_config(void);
+kn_problem *kn_prepare_ex(const kn_float3 *points, int numpoints, const kn_config *cfg);
+kn_status kn_solve_ex(kn_problem *kn);
+kn_status kn_set_k(kn_problem *kn, int k);                 /* re-solve with another K, no rebuild */
+float *kn_get_distances(kn_problem *kn);                   /* N x K squared distances, stored space */
+unsigned int *kn_get_neighbors(kn_problem *kn);            /* N x K, original space (row = original id) */
+kn_status kn_get_stats(kn_problem *kn, kn_stats *out);
+const char *kn_last_error(void);
+kn_status kn_save(kn_problem *kn, const char *path);
+kn_problem *kn_load(const char *path, const kn_config *cfg);
+
+/* ---- point-file helpers (reference test_knearests.cu:15-80) --------------------- */
+/* Reads a .xyz file (first line = count, then "x y z" per line). If normalize != 0 the
+ * cloud is mapped into [0,1000]^3 with a 0.1%-inflated bbox and uniform scale. Returns
+ * a malloc()'d array of *n points, or NULL (see kn_last_error()). */
+kn_float3 *kn_read_xyz(const char *path, int *n, int normalize);
+kn_status kn_write_xyz(const char *path, const kn_float3 *pts, int n);
+
+#ifdef __cplusplus
+}
+#endif

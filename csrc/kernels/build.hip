@@ -1,0 +1,278 @@
+// build.hip -- grid construction on gfx950 (wave64).
+//
+// Replaces the reference's count / reserve / store kernels (knearests.cu:32-60,152-201):
+//  * bbox_kernel     : data-driven domain (reference hard-codes [0,1000]^3, knearests.cu:21)
+//  * count_kernel    : per-point cell id + atomic *rank* capture, so the scatter needs no
+//                      second atomic pass (reference re-zeroes and re-counts, :183-187)
+//  * scan_*          : deterministic exclusive scan (reference uses an unordered atomic bump
+//                      allocator, `reserve` :40-48, which scatters cells randomly in memory)
+//  * scatter_kernel  : counting-sort scatter into float4 {x,y,z,bits(orig)} + permutation,
+//                      and finalises cell_start in the same launch
+//  * cell_sort_kernel: optional stable in-cell order (by original index) for bitwise
+//                      reproducible output (reference order is nondeterministic, :56)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "kn/kernels.h"
+#include "kn/wave.h"
+
+namespace kn {
+
+namespace {
+
+__device__ __forceinline__ unsigned ord_float(float f) {
+    unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_float(unsigned u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// 6 reductions: words[0..2] = max(~ord(min)), words[3..5] = max(ord(max)); all start at 0.
+__global__ __launch_bounds__(256) void bbox_kernel(const float* __restrict__ pts, int n,
+                                                   unsigned* __restrict__ words) {
+    float mn[3] = {INFINITY, INFINITY, INFINITY};
+    float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float x = pts[3 * i + 0], y = pts[3 * i + 1], z = pts[3 * i + 2];
+        mn[0] = fminf(mn[0], x); mx[0] = fmaxf(mx[0], x);
+        mn[1] = fminf(mn[1], y); mx[1] = fmaxf(mx[1], y);
+        mn[2] = fminf(mn[2], z); mx[2] = fmaxf(mx[2], z);
+    }
+    __shared__ unsigned red[6][4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        unsigned lo = wave_max_u32(~ord_float(mn[a]));
+        unsigned hi = wave_max_u32(ord_float(mx[a]));
+        if (lane == 0) { red[a][wid] = lo; red[3 + a][wid] = hi; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        unsigned v = red[threadIdx.x][0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) v = max(v, red[threadIdx.x][w]);
+        atomicMax(words + threadIdx.x, v);
+    }
+}
+
+__device__ void write_geom(GridGeom* g, const float lo[3], const float hi[3], const int dims[3]) {
+    float maxext = 0.f;
+    for (int a = 0; a < 3; ++a) maxext = fmaxf(maxext, hi[a] - lo[a]);
+    if (!(maxext > 0.f)) maxext = 1.f;
+    for (int a = 0; a < 3; ++a) {
+        float ext = hi[a] - lo[a];
+        // pad so that the max point falls strictly inside the last cell; keep degenerate
+        // (flat) axes at a sane size relative to the cloud.
+        ext = fmaxf(ext, maxext * 1e-3f);
+        const float pad = ext * 1e-5f + fabsf(lo[a]) * 1e-6f + 1e-30f;
+        const float o = lo[a] - pad;
+        const float e = ext + 2.f * pad + fabsf(hi[a]) * 1e-6f;
+        g->origin[a] = o;
+        g->cell[a] = e / (float)dims[a];
+        g->inv_cell[a] = (float)dims[a] / e;
+        g->dims[a] = dims[a];
+    }
+    g->eps = maxext * 2e-6f + 1e-30f;
+    g->pad = 0;
+}
+
+__global__ void geom_kernel(const unsigned* __restrict__ words, int d0, int d1, int d2,
+                            GridGeom* g) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = unord_float(~words[a]);
+        hi[a] = unord_float(words[3 + a]);
+        if (!(hi[a] >= lo[a])) { lo[a] = 0.f; hi[a] = 1.f; }  // empty input
+    }
+    const int dims[3] = {d0, d1, d2};
+    write_geom(g, lo, hi, dims);
+}
+
+__global__ void geom_box_kernel(float l0, float l1, float l2, float h0, float h1, float h2, int d0,
+                                int d1, int d2, GridGeom* g) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const float lo[3] = {l0, l1, l2}, hi[3] = {h0, h1, h2};
+    const int dims[3] = {d0, d1, d2};
+    write_geom(g, lo, hi, dims);
+}
+
+__global__ __launch_bounds__(256) void count_kernel(const float* __restrict__ pts, int n,
+                                                    const GridGeom* __restrict__ g,
+                                                    int* __restrict__ cell_count,
+                                                    int2* __restrict__ cell_rank) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float p[3] = {pts[3 * i + 0], pts[3 * i + 1], pts[3 * i + 2]};
+    const int c = cell_of(*g, p);
+    const int r = atomicAdd(cell_count + c, 1);
+    cell_rank[i] = make_int2(c, r);
+}
+
+// Block-local exclusive scan of kScanItems ints (256 threads x 16 items), block total out.
+__global__ __launch_bounds__(256) void scan_blocks_kernel(const int* __restrict__ in, int n,
+                                                          int* __restrict__ out,
+                                                          int* __restrict__ block_sums) {
+    constexpr int T = 256, I = kScanItems / T;
+    const int base = blockIdx.x * kScanItems + threadIdx.x * I;
+    int v[I];
+    if (base + I <= n) {
+        const int4* p = reinterpret_cast<const int4*>(in + base);
+#pragma unroll
+        for (int j = 0; j < I / 4; ++j) {
+            int4 q = p[j];
+            v[4 * j] = q.x; v[4 * j + 1] = q.y; v[4 * j + 2] = q.z; v[4 * j + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < I; ++j) v[j] = (base + j < n) ? in[base + j] : 0;
+    }
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < I; ++j) { const int t = v[j]; v[j] = s; s += t; }
+    // wave inclusive scan of the per-thread totals
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int incl = wave_inclusive_scan_add(s);
+    __shared__ int wsum[4];
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int woff = 0;
+    for (int w = 0; w < wid; ++w) woff += wsum[w];
+    const int off = woff + incl - s;
+    if (base + I <= n) {
+        int4* p = reinterpret_cast<int4*>(out + base);
+#pragma unroll
+        for (int j = 0; j < I / 4; ++j)
+            p[j] = make_int4(v[4 * j] + off, v[4 * j + 1] + off, v[4 * j + 2] + off, v[4 * j + 3] + off);
+    } else {
+#pragma unroll
+        for (int j = 0; j < I; ++j)
+            if (base + j < n) out[base + j] = v[j] + off;
+    }
+    if (threadIdx.x == T - 1) block_sums[blockIdx.x] = off + s;
+}
+
+// Single workgroup: exclusive scan of the block totals (any count, chunks of 1024).
+__global__ __launch_bounds__(1024) void scan_top_kernel(int* __restrict__ sums, int nb) {
+    __shared__ int wsum[16];
+    __shared__ int carry_s;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int base = 0; base < nb; base += 1024) {
+        const int i = base + threadIdx.x;
+        const int v = (i < nb) ? sums[i] : 0;
+        const int incl = wave_inclusive_scan_add(v);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        int woff = 0;
+        for (int w = 0; w < wid; ++w) woff += wsum[w];
+        const int carry = carry_s;
+        if (i < nb) sums[i] = carry + woff + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry_s = carry + woff + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sums[nb] = carry_s;
+}
+
+__global__ __launch_bounds__(256) void scatter_kernel(
+    const float* __restrict__ pts, int n, const int2* __restrict__ cell_rank,
+    const int* __restrict__ cell_scan, const int* __restrict__ block_sums, int num_cells,
+    int* __restrict__ cell_start, float4* __restrict__ sorted, unsigned* __restrict__ perm) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const int2 cr = cell_rank[i];
+        const int pos = cell_scan[cr.x] + block_sums[cr.x / kScanItems] + cr.y;
+        sorted[pos] = make_float4(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], __uint_as_float((unsigned)i));
+        perm[pos] = (unsigned)i;
+    }
+    // finalise cell_start (grid-stride; the scatter grid has >= num_cells+1 threads only if
+    // N >= C, so loop)
+    for (int c = i; c <= num_cells; c += gridDim.x * blockDim.x) {
+        cell_start[c] = (c < num_cells) ? cell_scan[c] + block_sums[c / kScanItems] : n;
+    }
+}
+
+// One thread per cell: insertion sort of the cell's entries by original index.
+__global__ __launch_bounds__(256) void cell_sort_kernel(const int* __restrict__ cell_start,
+                                                        int num_cells, float4* __restrict__ sorted,
+                                                        unsigned* __restrict__ perm) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= num_cells) return;
+    const int a = cell_start[c], b = cell_start[c + 1];
+    for (int i = a + 1; i < b; ++i) {
+        const float4 v = sorted[i];
+        const unsigned key = __float_as_uint(v.w);
+        int j = i - 1;
+        while (j >= a && __float_as_uint(sorted[j].w) > key) {
+            sorted[j + 1] = sorted[j];
+            perm[j + 1] = perm[j];
+            --j;
+        }
+        sorted[j + 1] = v;
+        perm[j + 1] = key;
+    }
+}
+
+__global__ __launch_bounds__(256) void cell_stats_kernel(const int* __restrict__ cell_start,
+                                                         int num_cells, int* __restrict__ out,
+                                                         int hist_len) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= num_cells) return;
+    const int cnt = cell_start[c + 1] - cell_start[c];
+    atomicMin(out + 0, cnt);
+    atomicMax(out + 1, cnt);
+    if (cnt == 0) atomicAdd(out + 2, 1);
+    atomicAdd(out + 3 + min(cnt, hist_len - 1), 1);
+}
+
+inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace
+
+size_t scan_block_count(int num_cells) { return cdiv((size_t)num_cells, kScanItems); }
+
+hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
+    const int C = b.dims[0] * b.dims[1] * b.dims[2];
+    const int n = b.n;
+    hipError_t e;
+    if (b.use_box) {
+        geom_box_kernel<<<1, 64, 0, s>>>(b.box_lo[0], b.box_lo[1], b.box_lo[2], b.box_hi[0],
+                                         b.box_hi[1], b.box_hi[2], b.dims[0], b.dims[1],
+                                         b.dims[2], b.geom);
+    } else {
+        if ((e = hipMemsetAsync(b.bbox_words, 0, 8 * sizeof(unsigned), s)) != hipSuccess) return e;
+        const unsigned grid = std::max(1u, std::min(cdiv((size_t)n, 256 * 4), 1024u));
+        bbox_kernel<<<grid, 256, 0, s>>>(b.points, n, b.bbox_words);
+        geom_kernel<<<1, 64, 0, s>>>(b.bbox_words, b.dims[0], b.dims[1], b.dims[2], b.geom);
+    }
+    if ((e = hipMemsetAsync(b.cell_count, 0, (size_t)C * sizeof(int), s)) != hipSuccess) return e;
+    if (n > 0) count_kernel<<<cdiv(n, 256), 256, 0, s>>>(b.points, n, b.geom, b.cell_count, b.cell_rank);
+    const unsigned nb = (unsigned)scan_block_count(C);
+    scan_blocks_kernel<<<nb, 256, 0, s>>>(b.cell_count, C, b.cell_scan, b.block_sums);
+    scan_top_kernel<<<1, 1024, 0, s>>>(b.block_sums, (int)nb);
+    const size_t threads = std::max((size_t)n, (size_t)C + 1);
+    scatter_kernel<<<cdiv(threads, 256), 256, 0, s>>>(b.points, n, b.cell_rank, b.cell_scan,
+                                                      b.block_sums, C, b.cell_start, b.sorted,
+                                                      b.perm);
+    if (b.deterministic)
+        cell_sort_kernel<<<cdiv(C, 256), 256, 0, s>>>(b.cell_start, C, b.sorted, b.perm);
+    return hipGetLastError();
+}
+
+hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int hist_len,
+                             hipStream_t s) {
+    hipError_t e;
+    const int init[3] = {0x7fffffff, 0, 0};
+    (void)init;
+    if ((e = hipMemsetAsync(out, 0, (size_t)(3 + hist_len) * sizeof(int), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(out, 0x7f, sizeof(int), s)) != hipSuccess) return e;
+    if (num_cells > 0)
+        cell_stats_kernel<<<cdiv(num_cells, 256), 256, 0, s>>>(cell_start, num_cells, out, hist_len);
+    return hipGetLastError();
+}
+
+}  // namespace kn

@@ -1,0 +1,210 @@
+// api.cpp -- C API (knearests.h) on top of kn::Engine.
+// Reference: knearests.cu:235-466 (kn_prepare / kn_solve / kn_free / getters / stats).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+#include "../host/host.hpp"
+#include "knearests.h"
+
+namespace {
+thread_local std::string g_err;
+
+kn::Engine* eng(kn_problem* kn) { return kn ? static_cast<kn::Engine*>(kn->impl) : nullptr; }
+
+void sync_fields(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    kn->allocated_points = e->n();
+    kn->dimx = e->dims()[0];
+    kn->dimy = e->dims()[1];
+    kn->dimz = e->dims()[2];
+    kn->num_cell_offsets = 0;
+    kn->k = e->k();
+    kn->d_permutation = e->d_perm();
+    kn->d_cell_start = e->d_cell_start();
+    kn->d_stored_points = reinterpret_cast<float*>(e->d_sorted());
+    kn->d_knearests = nullptr;
+}
+
+kn::EngineConfig to_engine(const kn_config* c) {
+    kn::EngineConfig e;
+    if (!c) return e;
+    e.k = c->k > 0 ? c->k : KN_DEFAULT_K;
+    e.points_per_cell = c->points_per_cell;
+    for (int a = 0; a < 3; ++a) e.tile[a] = c->tile[a];
+    e.halo = c->halo;
+    e.deterministic = c->deterministic;
+    e.device = c->device;
+    e.verbose = c->verbose;
+    e.use_tiles = c->exact_only ? 0 : 1;
+    return e;
+}
+}  // namespace
+
+extern "C" {
+
+kn_config kn_default_config(void) {
+    kn_config c;
+    std::memset(&c, 0, sizeof(c));
+    c.k = KN_DEFAULT_K;
+    c.deterministic = 1;
+    c.verbose = 0;
+    return c;
+}
+
+const char* kn_last_error(void) { return g_err.c_str(); }
+
+kn_problem* kn_prepare_ex(const kn_float3* points, int numpoints, const kn_config* cfg) {
+    kn_config c = cfg ? *cfg : kn_default_config();
+    auto* e = new kn::Engine(to_engine(&c));
+    if (e->prepare_host(reinterpret_cast<const float*>(points), numpoints) != KN_OK) {
+        g_err = e->error();
+        delete e;
+        return nullptr;
+    }
+    auto* kn = static_cast<kn_problem*>(std::calloc(1, sizeof(kn_problem)));
+    kn->impl = e;
+    sync_fields(kn);
+    return kn;
+}
+
+kn_problem* kn_prepare(const kn_float3* points, int numpoints) {
+    kn_config c = kn_default_config();
+    c.verbose = 1;  // reference prints its timings (IF_VERBOSE, params.h:6)
+    if (const char* v = std::getenv("KN_VERBOSE")) c.verbose = std::atoi(v);
+    return kn_prepare_ex(points, numpoints, &c);
+}
+
+kn_status kn_solve_ex(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    if (!e) { g_err = "null problem"; return KN_ERR_INVALID_ARGUMENT; }
+    kn_status s = e->solve();
+    if (s != KN_OK) g_err = e->error();
+    return s;
+}
+
+void kn_solve(kn_problem* kn) { (void)kn_solve_ex(kn); }
+
+kn_status kn_set_k(kn_problem* kn, int k) {
+    kn::Engine* e = eng(kn);
+    if (!e) { g_err = "null problem"; return KN_ERR_INVALID_ARGUMENT; }
+    kn_status s = e->set_k(k);
+    if (s != KN_OK) g_err = e->error();
+    kn->k = e->k();
+    return s;
+}
+
+void kn_free(kn_problem** kn) {
+    if (!kn || !*kn) return;
+    delete eng(*kn);
+    std::free(*kn);
+    *kn = nullptr;  // reference knearests.cu:407
+}
+
+kn_float3* kn_get_points(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    if (!e) return nullptr;
+    float* p = e->get_points_sorted();
+    if (!p) g_err = e->error();
+    return reinterpret_cast<kn_float3*>(p);
+}
+
+unsigned int* kn_get_permutation(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    if (!e) return nullptr;
+    unsigned* p = e->get_permutation();
+    if (!p) g_err = e->error();
+    return p;
+}
+
+unsigned int* kn_get_knearests(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    if (!e) return nullptr;
+    unsigned* p = e->get_knearests_stored();
+    if (!p) g_err = e->error();
+    kn->d_knearests = e->d_knn_stored();
+    return p;
+}
+
+float* kn_get_distances(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    if (!e) return nullptr;
+    float* p = e->get_distances_stored();
+    if (!p) g_err = e->error();
+    return p;
+}
+
+unsigned int* kn_get_neighbors(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    if (!e) return nullptr;
+    unsigned* p = e->get_neighbors_original();
+    if (!p) g_err = e->error();
+    return p;
+}
+
+kn_status kn_get_stats(kn_problem* kn, kn_stats* out) {
+    kn::Engine* e = eng(kn);
+    if (!e || !out) { g_err = "null argument"; return KN_ERR_INVALID_ARGUMENT; }
+    kn_status s = e->stats(out, nullptr);
+    if (s != KN_OK) g_err = e->error();
+    return s;
+}
+
+void kn_print_stats(kn_problem* kn) {
+    kn::Engine* e = eng(kn);
+    if (!e) return;
+    kn_stats st;
+    std::vector<int> hist;
+    if (e->stats(&st, &hist) != KN_OK) { fprintf(stderr, "kn_print_stats: %s\n", e->error().c_str()); return; }
+    fprintf(stderr, "grid %dx%dx%d (%d cells), %d points, K=%d\n", st.dims[0], st.dims[1], st.dims[2],
+            st.num_cells, st.num_points, st.k);
+    fprintf(stderr, "points per cell: min %d, max %d, avg %.3f, empty cells %d\n", st.min_cell,
+            st.max_cell, st.avg_cell, st.empty_cells);
+    for (size_t i = 0; i < hist.size(); ++i)
+        if (hist[i]) fprintf(stderr, "  [%2zu%s] %d\n", i, i + 1 == hist.size() ? "+" : " ", hist[i]);
+    fprintf(stderr, "exact-path queries %d, uncertified %d, build %.3f ms, solve %.3f ms\n",
+            st.fallback_queries, st.uncertified_queries, st.ms_build, st.ms_solve);
+}
+
+kn_status kn_save(kn_problem* kn, const char* path) {
+    kn::Engine* e = eng(kn);
+    if (!e || !path) { g_err = "null argument"; return KN_ERR_INVALID_ARGUMENT; }
+    kn_status s = e->save(path);
+    if (s != KN_OK) g_err = e->error();
+    return s;
+}
+
+kn_problem* kn_load(const char* path, const kn_config* cfg) {
+    kn_config c = cfg ? *cfg : kn_default_config();
+    kn::EngineConfig ec = to_engine(&c);
+    if (!cfg) ec.k = 0;  // take K from the file
+    std::string err;
+    kn::Engine* e = kn::Engine::load(path, ec, &err);
+    if (!e) { g_err = err; return nullptr; }
+    auto* kn = static_cast<kn_problem*>(std::calloc(1, sizeof(kn_problem)));
+    kn->impl = e;
+    sync_fields(kn);
+    return kn;
+}
+
+kn_float3* kn_read_xyz(const char* path, int* n, int normalize) {
+    std::vector<float> xyz;
+    std::string err;
+    if (!path || !knh::read_xyz(path, xyz, normalize != 0, &err)) { g_err = err; if (n) *n = 0; return nullptr; }
+    const size_t cnt = xyz.size() / 3;
+    float* out = static_cast<float*>(std::malloc(std::max<size_t>(1, xyz.size()) * sizeof(float)));
+    std::memcpy(out, xyz.data(), xyz.size() * sizeof(float));
+    if (n) *n = (int)cnt;
+    return reinterpret_cast<kn_float3*>(out);
+}
+
+kn_status kn_write_xyz(const char* path, const kn_float3* pts, int n) {
+    std::string err;
+    if (!knh::write_xyz(path, reinterpret_cast<const float*>(pts), n, &err)) { g_err = err; return KN_ERR_IO; }
+    return KN_OK;
+}
+
+}  // extern "C"

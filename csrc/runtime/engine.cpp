@@ -1,0 +1,430 @@
+// engine.cpp -- single-GPU host runtime. See engine.hpp.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+
+namespace kn {
+
+namespace {
+constexpr size_t kAlign = 256;
+size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
+template <class T>
+T* carve(char*& p, size_t count) {
+    T* r = reinterpret_cast<T*>(p);
+    p += align_up(count * sizeof(T));
+    return r;
+}
+}  // namespace
+
+Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
+    if (cfg_.k <= 0) cfg_.k = KN_DEFAULT_K;
+}
+
+Engine::~Engine() { release(); }
+
+void Engine::release() {
+    if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    if (arena_) { (void)hipFree(arena_); arena_ = nullptr; }
+    if (out_idx_) { (void)hipFree(out_idx_); out_idx_ = nullptr; }
+    if (out_dist_) { (void)hipFree(out_dist_); out_dist_ = nullptr; }
+    if (inv_perm_) { (void)hipFree(inv_perm_); inv_perm_ = nullptr; }
+    if (knn_stored_) { (void)hipFree(knn_stored_); knn_stored_ = nullptr; }
+    if (dist_stored_) { (void)hipFree(dist_stored_); dist_stored_ = nullptr; }
+    for (auto& e : ev_) if (e) { (void)hipEventDestroy(e); e = nullptr; }  // reference leaks these (D6)
+    if (stream_) { (void)hipStreamDestroy(stream_); stream_ = nullptr; }
+}
+
+kn_status Engine::fail(kn_status s, const std::string& msg) {
+    err_ = msg;
+    if (cfg_.verbose) fprintf(stderr, "[knearests] error: %s\n", msg.c_str());
+    return s;
+}
+
+kn_status Engine::check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return KN_OK;
+    return fail(e == hipErrorOutOfMemory ? KN_ERR_OUT_OF_MEMORY : KN_ERR_DEVICE,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+kn_status Engine::allocate(int n, const int* dims_override) {
+    if (n < 0) return fail(KN_ERR_INVALID_ARGUMENT, "negative point count");
+    if (cfg_.k < 1 || cfg_.k > KN_MAX_K) return fail(KN_ERR_INVALID_ARGUMENT, "k out of range [1,128]");
+    kn_status st;
+    if ((st = check(hipSetDevice(cfg_.device), "hipSetDevice")) != KN_OK) return st;
+    if (!stream_) {
+        if ((st = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate")) != KN_OK) return st;
+        for (auto& e : ev_)
+            if ((st = check(hipEventCreate(&e), "hipEventCreate")) != KN_OK) return st;
+    }
+    ap_ = auto_params(n, cfg_.k, cfg_.points_per_cell, cfg_.tile, cfg_.halo, nullptr);
+    if (dims_override) {
+        for (int a = 0; a < 3; ++a) ap_.dims[a] = std::max(1, dims_override[a]);
+        const double ppc = (double)std::max(1, n) / ((double)ap_.dims[0] * ap_.dims[1] * ap_.dims[2]);
+        const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
+                              (ap_.tile[2] + 2 * ap_.halo) * ppc;
+        ap_.lds_capacity = lds_capacity_for(staged);
+        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, cap);
+    }
+    const int C = ap_.dims[0] * ap_.dims[1] * ap_.dims[2];
+    const size_t nb = scan_block_count(C) + 1;
+    size_t bytes = 0;
+    bytes += align_up((size_t)n * 3 * sizeof(float));
+    bytes += align_up(8 * sizeof(unsigned));
+    bytes += align_up(sizeof(GridGeom));
+    bytes += 3 * align_up((size_t)(C + 1) * sizeof(int));
+    bytes += align_up(nb * sizeof(int));
+    bytes += align_up((size_t)n * sizeof(int2));
+    bytes += align_up((size_t)n * sizeof(float4));
+    bytes += 2 * align_up((size_t)n * sizeof(unsigned));
+    bytes += align_up(4 * sizeof(unsigned));
+    if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    if (bytes > arena_bytes_) {
+        if (arena_) (void)hipFree(arena_);
+        arena_ = nullptr;
+        if ((st = check(hipMalloc(&arena_, bytes), "hipMalloc(arena)")) != KN_OK) return st;
+        arena_bytes_ = bytes;
+    }
+    char* p = arena_;
+    points_ = carve<float>(p, (size_t)n * 3);
+    bbox_ = carve<unsigned>(p, 8);
+    geom_ = carve<GridGeom>(p, 1);
+    cell_count_ = carve<int>(p, C + 1);
+    cell_scan_ = carve<int>(p, C + 1);
+    cell_start_ = carve<int>(p, C + 1);
+    block_sums_ = carve<int>(p, nb);
+    cell_rank_ = carve<int2>(p, n);
+    sorted_ = carve<float4>(p, n);
+    perm_ = carve<unsigned>(p, n);
+    fallback_ = carve<unsigned>(p, n);
+    counters_ = carve<unsigned>(p, 4);
+    // outputs
+    for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
+                     (void**)&dist_stored_})
+        if (*q) { (void)hipFree(*q); *q = nullptr; }
+    const size_t nk = std::max<size_t>(1, (size_t)n * cfg_.k);
+    if ((st = check(hipMalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
+    if (cfg_.with_distances &&
+        (st = check(hipMalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
+        return st;
+    n_ = n;
+    C_ = C;
+    built_ = solved_ = stored_valid_ = false;
+    if (cfg_.verbose)
+        fprintf(stderr, "[knearests] N=%d K=%d grid %dx%dx%d tile %dx%dx%d halo %d lds %zu B, GPU memory %.1f MB\n",
+                n, cfg_.k, ap_.dims[0], ap_.dims[1], ap_.dims[2], ap_.tile[0], ap_.tile[1],
+                ap_.tile[2], ap_.halo, ap_.lds_bytes,
+                (bytes + nk * (sizeof(unsigned) + (cfg_.with_distances ? 4 : 0))) / 1048576.0);
+    return KN_OK;
+}
+
+BuildBuffers Engine::build_buffers() const {
+    BuildBuffers b{};
+    b.points = points_;
+    b.n = n_;
+    for (int a = 0; a < 3; ++a) b.dims[a] = ap_.dims[a];
+    b.bbox_words = bbox_;
+    b.geom = geom_;
+    b.cell_count = cell_count_;
+    b.cell_scan = cell_scan_;
+    b.block_sums = block_sums_;
+    b.cell_start = cell_start_;
+    b.cell_rank = cell_rank_;
+    b.sorted = sorted_;
+    b.perm = perm_;
+    b.deterministic = cfg_.deterministic;
+    b.use_box = 0;
+    return b;
+}
+
+QueryBuffers Engine::query_buffers() const {
+    QueryBuffers q{};
+    q.sorted = sorted_;
+    q.cell_start = cell_start_;
+    q.perm = perm_;
+    q.geom = geom_;
+    q.n = n_;
+    for (int a = 0; a < 3; ++a) q.dims[a] = ap_.dims[a];
+    q.k = cfg_.k;
+    q.n_queries = n_;
+    q.id_map = nullptr;
+    for (int a = 0; a < 3; ++a) { q.complete.lo[a] = -INFINITY; q.complete.hi[a] = INFINITY; }
+    q.out_idx = out_idx_;
+    q.out_dist = out_dist_;
+    q.fallback_list = fallback_;
+    q.counters = counters_;
+    for (int a = 0; a < 3; ++a) q.tile[a] = ap_.tile[a];
+    q.halo = ap_.halo;
+    q.lds_capacity = ap_.lds_capacity;
+    q.use_tiles = cfg_.use_tiles;
+    return q;
+}
+
+kn_status Engine::build_async() { return check(launch_build(build_buffers(), stream_), "build"); }
+kn_status Engine::query_async() { return check(launch_query(query_buffers(), stream_), "query"); }
+
+kn_status Engine::prepare_host(const float* pts, int n) {
+    kn_status st;
+    if (!pts && n > 0) return fail(KN_ERR_INVALID_ARGUMENT, "null points");
+    if ((st = allocate(n)) != KN_OK) return st;
+    if (n > 0 && (st = check(hipMemcpyAsync(points_, pts, (size_t)n * 12, hipMemcpyHostToDevice, stream_),
+                             "H2D points")) != KN_OK)
+        return st;
+    (void)hipEventRecord(ev_[0], stream_);
+    if ((st = build_async()) != KN_OK) return st;
+    (void)hipEventRecord(ev_[1], stream_);
+    if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
+    (void)hipEventElapsedTime(&ms_build_, ev_[0], ev_[1]);
+    if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
+    built_ = true;
+    return KN_OK;
+}
+
+kn_status Engine::prepare_device(const float* d_pts, int n) {
+    kn_status st;
+    if ((st = allocate(n)) != KN_OK) return st;
+    if (n > 0 && (st = check(hipMemcpyAsync(points_, d_pts, (size_t)n * 12, hipMemcpyDeviceToDevice, stream_),
+                             "D2D points")) != KN_OK)
+        return st;
+    (void)hipEventRecord(ev_[0], stream_);
+    if ((st = build_async()) != KN_OK) return st;
+    (void)hipEventRecord(ev_[1], stream_);
+    if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
+    (void)hipEventElapsedTime(&ms_build_, ev_[0], ev_[1]);
+    built_ = true;
+    return KN_OK;
+}
+
+kn_status Engine::solve() {
+    if (!built_) return fail(KN_ERR_STATE, "solve() before prepare()");
+    kn_status st;
+    (void)hipEventRecord(ev_[2], stream_);
+    if ((st = query_async()) != KN_OK) return st;
+    (void)hipEventRecord(ev_[3], stream_);
+    if ((st = check(hipEventSynchronize(ev_[3]), "solve sync")) != KN_OK) return st;
+    (void)hipEventElapsedTime(&ms_solve_, ev_[2], ev_[3]);
+    if (cfg_.verbose) {
+        unsigned c[4] = {0, 0, 0, 0};
+        (void)hipMemcpy(c, counters_, sizeof(c), hipMemcpyDeviceToHost);
+        fprintf(stderr, "kn_solve: %.3f msec (exact-path queries %u, uncertified %u, dense tiles %u)\n",
+                ms_solve_, c[0], c[1], c[2]);
+    }
+    solved_ = true;
+    stored_valid_ = false;
+    return KN_OK;
+}
+
+kn_status Engine::set_k(int k) {
+    if (k < 1 || k > KN_MAX_K) return fail(KN_ERR_INVALID_ARGUMENT, "k out of range [1,128]");
+    if (!built_) return fail(KN_ERR_STATE, "set_k() before prepare()");
+    if (k == cfg_.k) return KN_OK;
+    cfg_.k = k;
+    // grid density stays; the halo/LDS plan follows K
+    const AutoParams np = auto_params(n_, k, cfg_.points_per_cell, cfg_.tile, cfg_.halo, nullptr);
+    ap_.tile[0] = np.tile[0]; ap_.tile[1] = np.tile[1]; ap_.tile[2] = np.tile[2];
+    ap_.halo = np.halo;
+    {
+        const double ppc = (double)n_ / std::max(1, C_);
+        const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
+                              (ap_.tile[2] + 2 * ap_.halo) * ppc;
+        ap_.lds_capacity = lds_capacity_for(staged);
+        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, cap);
+    }
+    for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_, (void**)&dist_stored_})
+        if (*q) { (void)hipFree(*q); *q = nullptr; }
+    const size_t nk = std::max<size_t>(1, (size_t)n_ * k);
+    kn_status st;
+    if ((st = check(hipMalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
+    if (cfg_.with_distances &&
+        (st = check(hipMalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
+        return st;
+    if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    solved_ = stored_valid_ = false;
+    return KN_OK;
+}
+
+kn_status Engine::run_graph(int iters, float* ms_per_iter) {
+    if (!built_) return fail(KN_ERR_STATE, "run_graph() before prepare()");
+    kn_status st;
+    if (!graph_) {
+        hipGraph_t g;
+        if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
+        kn_status s1 = build_async();
+        kn_status s2 = query_async();
+        hipError_t e = hipStreamEndCapture(stream_, &g);
+        if (s1 != KN_OK) return s1;
+        if (s2 != KN_OK) return s2;
+        if ((st = check(e, "end capture")) != KN_OK) return st;
+        e = hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if ((st = check(e, "graph instantiate")) != KN_OK) return st;
+    }
+    (void)hipEventRecord(ev_[0], stream_);
+    for (int i = 0; i < iters; ++i)
+        if ((st = check(hipGraphLaunch(graph_, stream_), "graph launch")) != KN_OK) return st;
+    (void)hipEventRecord(ev_[1], stream_);
+    if ((st = check(hipEventSynchronize(ev_[1]), "graph sync")) != KN_OK) return st;
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, ev_[0], ev_[1]);
+    if (ms_per_iter) *ms_per_iter = iters > 0 ? ms / iters : 0.f;
+    solved_ = true;
+    stored_valid_ = false;
+    return KN_OK;
+}
+
+unsigned* Engine::d_knn_stored() {
+    if (!solved_) return nullptr;
+    if (stored_valid_) return knn_stored_;
+    const size_t nk = std::max<size_t>(1, (size_t)n_ * cfg_.k);
+    if (!inv_perm_ && check(hipMalloc(&inv_perm_, std::max<size_t>(1, n_) * sizeof(unsigned)), "hipMalloc(inv)") != KN_OK)
+        return nullptr;
+    if (!knn_stored_ && check(hipMalloc(&knn_stored_, nk * sizeof(unsigned)), "hipMalloc(knn_stored)") != KN_OK)
+        return nullptr;
+    if (out_dist_ && !dist_stored_ && check(hipMalloc(&dist_stored_, nk * sizeof(float)), "hipMalloc(dist_stored)") != KN_OK)
+        return nullptr;
+    if (check(launch_invert_perm(perm_, n_, inv_perm_, stream_), "invert perm") != KN_OK) return nullptr;
+    if (check(launch_to_stored_space(out_idx_, perm_, inv_perm_, n_, cfg_.k, knn_stored_, out_dist_,
+                                     dist_stored_, stream_),
+              "to stored space") != KN_OK)
+        return nullptr;
+    if (check(hipStreamSynchronize(stream_), "sync") != KN_OK) return nullptr;
+    stored_valid_ = true;
+    return knn_stored_;
+}
+
+template <class T>
+static T* d2h(const T* d, size_t count, hipStream_t s) {
+    T* h = (T*)malloc(std::max<size_t>(1, count) * sizeof(T));
+    if (!h) return nullptr;
+    if (count && (hipMemcpyAsync(h, d, count * sizeof(T), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                  hipStreamSynchronize(s) != hipSuccess)) {
+        free(h);
+        return nullptr;
+    }
+    return h;
+}
+
+float* Engine::get_points_sorted() {
+    if (!built_) { fail(KN_ERR_STATE, "not prepared"); return nullptr; }
+    float4* tmp = d2h(sorted_, (size_t)n_, stream_);
+    if (!tmp) return nullptr;
+    float* out = (float*)malloc(std::max<size_t>(1, (size_t)n_ * 3) * sizeof(float));
+    for (int i = 0; i < n_; ++i) { out[3 * i] = tmp[i].x; out[3 * i + 1] = tmp[i].y; out[3 * i + 2] = tmp[i].z; }
+    free(tmp);
+    return out;
+}
+unsigned* Engine::get_permutation() {
+    if (!built_) { fail(KN_ERR_STATE, "not prepared"); return nullptr; }
+    return d2h(perm_, (size_t)n_, stream_);
+}
+unsigned* Engine::get_knearests_stored() {
+    unsigned* d = d_knn_stored();
+    if (!d) { if (err_.empty()) fail(KN_ERR_STATE, "not solved"); return nullptr; }
+    return d2h(d, (size_t)n_ * cfg_.k, stream_);
+}
+float* Engine::get_distances_stored() {
+    if (!out_dist_) { fail(KN_ERR_STATE, "distances disabled"); return nullptr; }
+    if (!d_knn_stored()) return nullptr;
+    return d2h(dist_stored_, (size_t)n_ * cfg_.k, stream_);
+}
+unsigned* Engine::get_neighbors_original() {
+    if (!solved_) { fail(KN_ERR_STATE, "not solved"); return nullptr; }
+    return d2h(out_idx_, (size_t)n_ * cfg_.k, stream_);
+}
+float* Engine::get_distances_original() {
+    if (!solved_ || !out_dist_) { fail(KN_ERR_STATE, "not solved / distances disabled"); return nullptr; }
+    return d2h(out_dist_, (size_t)n_ * cfg_.k, stream_);
+}
+
+kn_status Engine::stats(kn_stats* out, std::vector<int>* hist) {
+    if (!built_) return fail(KN_ERR_STATE, "not prepared");
+    constexpr int H = 64;
+    kn_status st;
+    if ((st = check(launch_cell_stats(cell_start_, C_, cell_count_, H, stream_), "cell stats")) != KN_OK) return st;
+    std::vector<int> v(3 + H);
+    if ((st = check(hipMemcpyAsync(v.data(), cell_count_, v.size() * sizeof(int), hipMemcpyDeviceToHost, stream_), "D2H")) != KN_OK) return st;
+    unsigned c[4] = {0, 0, 0, 0};
+    if ((st = check(hipMemcpyAsync(c, counters_, sizeof(c), hipMemcpyDeviceToHost, stream_), "D2H")) != KN_OK) return st;
+    if ((st = check(hipStreamSynchronize(stream_), "sync")) != KN_OK) return st;
+    std::memset(out, 0, sizeof(*out));
+    out->num_points = n_;
+    out->k = cfg_.k;
+    for (int a = 0; a < 3; ++a) out->dims[a] = ap_.dims[a];
+    out->num_cells = C_;
+    out->min_cell = C_ ? v[0] : 0;
+    out->max_cell = v[1];
+    out->avg_cell = C_ ? (float)n_ / C_ : 0.f;
+    out->empty_cells = v[2];
+    out->fallback_queries = solved_ ? (int)c[0] : 0;
+    out->uncertified_queries = solved_ ? (int)c[1] : 0;
+    out->ms_build = ms_build_;
+    out->ms_solve = ms_solve_;
+    if (hist) hist->assign(v.begin() + 3, v.end());
+    // the stats kernel used cell_count_ as scratch: it is rebuilt by every build
+    return KN_OK;
+}
+
+namespace {
+constexpr unsigned kMagic = 0x4b4e4731;  // "KNG1"
+}
+
+kn_status Engine::save(const char* path) {
+    if (!built_) return fail(KN_ERR_STATE, "not prepared");
+    std::ofstream f(path, std::ios::binary);
+    if (!f) return fail(KN_ERR_IO, std::string("cannot open ") + path);
+    GridGeom g;
+    kn_status st;
+    if ((st = check(hipMemcpy(&g, geom_, sizeof(g), hipMemcpyDeviceToHost), "D2H geom")) != KN_OK) return st;
+    std::vector<float4> s(n_);
+    std::vector<int> cs(C_ + 1);
+    if (n_ && (st = check(hipMemcpy(s.data(), sorted_, n_ * sizeof(float4), hipMemcpyDeviceToHost), "D2H")) != KN_OK) return st;
+    if ((st = check(hipMemcpy(cs.data(), cell_start_, (C_ + 1) * sizeof(int), hipMemcpyDeviceToHost), "D2H")) != KN_OK) return st;
+    const int hdr[6] = {(int)kMagic, n_, ap_.dims[0], ap_.dims[1], ap_.dims[2], cfg_.k};
+    f.write((const char*)hdr, sizeof(hdr));
+    f.write((const char*)&g, sizeof(g));
+    f.write((const char*)s.data(), s.size() * sizeof(float4));
+    f.write((const char*)cs.data(), cs.size() * sizeof(int));
+    return f ? KN_OK : fail(KN_ERR_IO, "write failed");
+}
+
+Engine* Engine::load(const char* path, const EngineConfig& cfg, std::string* err) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) { if (err) *err = std::string("cannot open ") + path; return nullptr; }
+    int hdr[6];
+    f.read((char*)hdr, sizeof(hdr));
+    if (!f || hdr[0] != (int)kMagic || hdr[1] < 0) { if (err) *err = "bad file header"; return nullptr; }
+    GridGeom g;
+    f.read((char*)&g, sizeof(g));
+    const int n = hdr[1];
+    std::vector<float4> s(n);
+    const long C = (long)hdr[2] * hdr[3] * hdr[4];
+    if (C <= 0 || C > 400000000L) { if (err) *err = "bad grid"; return nullptr; }
+    std::vector<int> cs(C + 1);
+    f.read((char*)s.data(), s.size() * sizeof(float4));
+    f.read((char*)cs.data(), cs.size() * sizeof(int));
+    if (!f) { if (err) *err = "truncated file"; return nullptr; }
+    EngineConfig c = cfg;
+    if (c.k <= 0) c.k = hdr[5];
+    Engine* e = new Engine(c);
+    const int dims[3] = {hdr[2], hdr[3], hdr[4]};
+    if (e->allocate(n, dims) != KN_OK) { if (err) *err = e->error(); delete e; return nullptr; }
+    std::vector<unsigned> perm(n);
+    for (int i = 0; i < n; ++i) {
+        unsigned u;
+        std::memcpy(&u, &s[i].w, 4);
+        perm[i] = u;
+    }
+    bool ok = hipMemcpy(e->geom_, &g, sizeof(g), hipMemcpyHostToDevice) == hipSuccess &&
+              (n == 0 || hipMemcpy(e->sorted_, s.data(), n * sizeof(float4), hipMemcpyHostToDevice) == hipSuccess) &&
+              (n == 0 || hipMemcpy(e->perm_, perm.data(), n * sizeof(unsigned), hipMemcpyHostToDevice) == hipSuccess) &&
+              hipMemcpy(e->cell_start_, cs.data(), (C + 1) * sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
+    if (!ok) { if (err) *err = "upload failed"; delete e; return nullptr; }
+    e->built_ = true;
+    return e;
+}
+
+}  // namespace kn

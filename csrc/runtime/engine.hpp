@@ -1,0 +1,115 @@
+// engine.hpp -- single-GPU host runtime (replaces reference knearests.cu:205-466).
+//
+// * One device arena sized up front (reference allocates 9 buffers with an over-allocation
+//   bug, knearests.cu:329-335 / defect D3).
+// * Stream-ordered, allocation-free build + solve; both can be captured once into a hipGraph
+//   and replayed (run_graph), which removes the per-launch host overhead of the ~8 kernels.
+// * Errors are returned as kn_status + message, never exit() (reference defect D7).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "knearests.h"
+#include "kn/kernels.h"
+
+namespace kn {
+
+struct EngineConfig {
+    int k = KN_DEFAULT_K;
+    float points_per_cell = 0.f;
+    int tile[3] = {0, 0, 0};
+    int halo = 0;
+    int deterministic = 1;
+    int device = 0;
+    int verbose = 0;
+    int use_tiles = 1;
+    int with_distances = 1;
+};
+
+class Engine {
+public:
+    explicit Engine(const EngineConfig& cfg);
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    // Upload host points (N x 3 floats) and build the grid.
+    kn_status prepare_host(const float* pts, int n);
+    // Build from device points already resident (N x 3 floats). The engine keeps a copy.
+    kn_status prepare_device(const float* d_pts, int n);
+    kn_status solve();
+    kn_status set_k(int k);
+    // Capture build+solve into a graph once, then replay it `iters` times (bench path).
+    kn_status run_graph(int iters, float* ms_per_iter);
+
+    // Host copies (caller frees with free()).
+    float* get_points_sorted();            // N x 3
+    unsigned* get_permutation();
+    unsigned* get_knearests_stored();      // N x K stored space (reference semantics)
+    float* get_distances_stored();
+    unsigned* get_neighbors_original();    // N x K original space
+    float* get_distances_original();
+    kn_status stats(kn_stats* out, std::vector<int>* hist);
+
+    kn_status save(const char* path);
+    static Engine* load(const char* path, const EngineConfig& cfg, std::string* err);
+
+    const std::string& error() const { return err_; }
+    int n() const { return n_; }
+    int k() const { return cfg_.k; }
+    const int* dims() const { return ap_.dims; }
+    int num_cells() const { return C_; }
+    float ms_build() const { return ms_build_; }
+    float ms_solve() const { return ms_solve_; }
+
+    // raw device pointers (C API struct fields)
+    float4* d_sorted() const { return sorted_; }
+    int* d_cell_start() const { return cell_start_; }
+    unsigned* d_perm() const { return perm_; }
+    unsigned* d_knn_stored();
+
+private:
+    kn_status fail(kn_status s, const std::string& msg);
+    kn_status check(hipError_t e, const char* what);
+    kn_status allocate(int n, const int* dims_override = nullptr);
+    kn_status build_async();
+    kn_status query_async();
+    QueryBuffers query_buffers() const;
+    BuildBuffers build_buffers() const;
+    void release();
+
+    EngineConfig cfg_;
+    AutoParams ap_{};
+    std::string err_;
+    hipStream_t stream_ = nullptr;
+    hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipGraphExec_t graph_ = nullptr;
+    int n_ = 0, C_ = 0;
+    size_t arena_bytes_ = 0;
+    char* arena_ = nullptr;
+    float* points_ = nullptr;
+    unsigned* bbox_ = nullptr;
+    GridGeom* geom_ = nullptr;
+    int* cell_count_ = nullptr;
+    int* cell_scan_ = nullptr;
+    int* block_sums_ = nullptr;
+    int* cell_start_ = nullptr;
+    int2* cell_rank_ = nullptr;
+    float4* sorted_ = nullptr;
+    unsigned* perm_ = nullptr;
+    unsigned* fallback_ = nullptr;
+    unsigned* counters_ = nullptr;
+    // outputs (re-allocated when K changes)
+    unsigned* out_idx_ = nullptr;
+    float* out_dist_ = nullptr;
+    unsigned* inv_perm_ = nullptr;
+    unsigned* knn_stored_ = nullptr;
+    float* dist_stored_ = nullptr;
+    bool built_ = false, solved_ = false, stored_valid_ = false;
+    float ms_build_ = 0.f, ms_solve_ = 0.f;
+};
+
+}  // namespace kn

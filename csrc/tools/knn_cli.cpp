@@ -1,0 +1,149 @@
+// knn_cli -- reference-equivalent driver (reference test_knearests.cu:117-235).
+//
+//   knn_cli points.xyz [options]          load + normalise like the reference
+//   knn_cli --uniform N | --blue N | --clustered N [options]
+// options: --k K  --ppc X  --tile a,b,c  --halo H  --exact  --nondet  --no-check  --json
+//          --save file.kng  --out neighbours.txt  --repeat R
+//
+// Flow: device report -> load -> kn_prepare_ex + kn_solve_ex (timed) -> kn_print_stats ->
+// stored-space getters -> remap to original ids (reference :155-160) -> permutation
+// bijection check -> duplicate check (fails, unlike the reference's :183) -> kd-tree
+// oracle -> distance-aware comparison. Exit code 0 only if everything matches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "knearests.h"
+#include "../host/host.hpp"
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static void device_report() {
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess) nd = 0;
+    fprintf(stderr, "HIP devices: %d\n", nd);
+    for (int d = 0; d < nd; ++d) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, d) != hipSuccess) continue;
+        fprintf(stderr, "  [%d] %s (%s): %d CUs, wave %d, LDS/WG %zu KiB, HBM %.1f GiB, clock %d MHz\n", d,
+                p.name, p.gcnArchName, p.multiProcessorCount, p.warpSize, p.sharedMemPerBlock / 1024,
+                p.totalGlobalMem / 1073741824.0, p.clockRate / 1000);
+    }
+}
+
+int main(int argc, char** argv) {
+    kn_config cfg = kn_default_config();
+    cfg.k = KN_DEFAULT_K;
+    cfg.verbose = 1;
+    std::string path, gen, save, out;
+    int gen_n = 0, repeat = 1;
+    bool check = true, json = false, exact = false;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> const char* {
+            if (i + 1 >= argc) { fprintf(stderr, "missing value for %s\n", a.c_str()); exit(2); }
+            return argv[++i];
+        };
+        if (a == "--k") cfg.k = atoi(next());
+        else if (a == "--ppc") cfg.points_per_cell = (float)atof(next());
+        else if (a == "--halo") cfg.halo = atoi(next());
+        else if (a == "--tile") { if (sscanf(next(), "%d,%d,%d", &cfg.tile[0], &cfg.tile[1], &cfg.tile[2]) != 3) return 2; }
+        else if (a == "--uniform" || a == "--blue" || a == "--clustered") { gen = a.substr(2); gen_n = atoi(next()); }
+        else if (a == "--exact") exact = true;
+        else if (a == "--nondet") cfg.deterministic = 0;
+        else if (a == "--no-check") check = false;
+        else if (a == "--json") json = true;
+        else if (a == "--save") save = next();
+        else if (a == "--out") out = next();
+        else if (a == "--repeat") repeat = std::max(1, atoi(next()));
+        else if (a == "-h" || a == "--help") {
+            fprintf(stderr, "usage: %s points.xyz | --uniform N | --blue N | --clustered N [--k K] [--ppc X] "
+                            "[--tile a,b,c] [--halo H] [--exact] [--nondet] [--no-check] [--json] [--save f] [--out f]\n", argv[0]);
+            return 0;
+        } else path = a;
+    }
+    device_report();
+
+    std::vector<float> pts;
+    if (!gen.empty()) {
+        if (gen == "uniform") knh::gen_uniform(gen_n, 1, pts);
+        else if (gen == "blue") knh::gen_blue(gen_n, 1, pts);
+        else knh::gen_clustered(gen_n, 1, pts);
+    } else {
+        if (path.empty()) { fprintf(stderr, "no input (see --help)\n"); return 2; }
+        std::string err;
+        if (!knh::read_xyz(path, pts, true, &err)) { fprintf(stderr, "load failed: %s\n", err.c_str()); return 1; }
+    }
+    const int n = (int)(pts.size() / 3);
+    const int K = cfg.k;
+    fprintf(stderr, "%d points, K=%d\n", n, K);
+    if (exact) cfg.exact_only = 1;
+
+    {   // context warm-up outside the timer (reference test_knearests.cu:138-146)
+        void* p = nullptr;
+        (void)hipMalloc(&p, 4);
+        (void)hipFree(p);
+    }
+    std::vector<uint32_t> neighbors((size_t)n * K);
+    double t0 = now_ms();
+    kn_problem* kn = kn_prepare_ex(reinterpret_cast<const kn_float3*>(pts.data()), n, &cfg);
+    if (!kn) { fprintf(stderr, "kn_prepare failed: %s\n", kn_last_error()); return 1; }
+    for (int r = 0; r < repeat; ++r)
+        if (kn_solve_ex(kn) != KN_OK) { fprintf(stderr, "kn_solve failed: %s\n", kn_last_error()); return 1; }
+    const double t1 = now_ms();
+    fprintf(stderr, "knn subgpu: %.3f ms (prepare + %d solve)\n", t1 - t0, repeat);
+    kn_print_stats(kn);
+    kn_stats st;
+    kn_get_stats(kn, &st);
+    unsigned* knn = kn_get_knearests(kn);
+    unsigned* perm = kn_get_permutation(kn);
+    if (!knn || !perm) { fprintf(stderr, "getter failed: %s\n", kn_last_error()); return 1; }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < K; ++j) {
+            const unsigned v = knn[(size_t)i * K + j];
+            neighbors[(size_t)perm[i] * K + j] = (v == 0xFFFFFFFFu) ? v : perm[v];
+        }
+    bool ok = true;
+    {   // permutation bijection (reference :162-168)
+        std::vector<unsigned> p(perm, perm + n);
+        std::sort(p.begin(), p.end());
+        for (int i = 0; i < n; ++i) if (p[i] != (unsigned)i) { ok = false; fprintf(stderr, "ERROR: permutation is not a bijection\n"); break; }
+    }
+    free(perm);
+    free(knn);
+    if (!save.empty() && kn_save(kn, save.c_str()) != KN_OK) fprintf(stderr, "save failed: %s\n", kn_last_error());
+    kn_free(&kn);
+    if (!out.empty()) {
+        FILE* f = fopen(out.c_str(), "w");
+        if (f) {
+            for (int i = 0; i < n; ++i) {
+                for (int j = 0; j < K; ++j) fprintf(f, "%d%c", (int)neighbors[(size_t)i * K + j], j + 1 == K ? '\n' : ' ');
+            }
+            fclose(f);
+        }
+    }
+    if (check) {
+        fprintf(stderr, "Querying the kd-tree oracle...");
+        std::vector<uint32_t> oi((size_t)n * K);
+        std::vector<float> od((size_t)n * K);
+        const double c0 = now_ms();
+        knh::kdtree_knn_all(pts.data(), n, K, oi.data(), od.data(), 0);
+        fprintf(stderr, " %.1f ms\n", now_ms() - c0);
+        const knh::CheckResult r = knh::check_knn(pts.data(), n, n, K, neighbors.data(), oi.data(), od.data());
+        fprintf(stderr, "Comparing GPU vs oracle: %ld / %ld rows differ (%s)\n", r.bad_rows, r.rows_checked, r.message.c_str());
+        ok = ok && r.bad_rows == 0;
+    }
+    if (json)
+        printf("{\"n\": %d, \"k\": %d, \"ms_build\": %.4f, \"ms_solve\": %.4f, \"exact_path\": %d, \"ok\": %s}\n", n, K,
+               st.ms_build, st.ms_solve, st.fallback_queries, ok ? "true" : "false");
+    fprintf(stderr, "%s\n", ok ? "ok" : "FAILED");
+    return ok ? 0 : 1;
+}

@@ -1,0 +1,268 @@
+// bindings.cpp -- PyTorch (ROCm) extension `cuda_knearests_amd._C`.
+//
+// Device ops run on the current PyTorch HIP stream with memory from the caching allocator,
+// so they compose with torch.cuda graphs and torch.distributed (RCCL) in the Python layer.
+// GPU ops throw if called on CPU tensors; there is no silent fallback.
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/extension.h>
+
+#include <cmath>
+#include <limits>
+#include <vector>
+
+#include "kn/kernels.h"
+#include "../host/host.hpp"
+
+namespace {
+
+#define KN_CHECK_HIP(expr)                                                                 \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        TORCH_CHECK(e_ == hipSuccess, "HIP error in ", #expr, ": ", hipGetErrorString(e_)); \
+    } while (0)
+
+void check_points(const torch::Tensor& p, bool cuda) {
+    TORCH_CHECK(p.dim() == 2 && p.size(1) == 3, "points must be (N, 3)");
+    TORCH_CHECK(p.scalar_type() == torch::kFloat32, "points must be float32");
+    TORCH_CHECK(p.is_contiguous(), "points must be contiguous");
+    if (cuda) {
+        TORCH_CHECK(p.is_cuda(), "points must be a GPU (HIP) tensor");
+    } else {
+        TORCH_CHECK(p.device().is_cpu(), "points must be a CPU tensor");
+    }
+}
+
+// geom tensor: 16 x int32 (64 bytes) holding a kn::GridGeom
+static_assert(sizeof(kn::GridGeom) <= 64, "GridGeom must fit in 64 bytes");
+
+std::vector<torch::Tensor> build(torch::Tensor points, std::vector<int64_t> dims, bool deterministic,
+                                 c10::optional<std::vector<double>> box) {
+    check_points(points, true);
+    TORCH_CHECK(dims.size() == 3 && dims[0] > 0 && dims[1] > 0 && dims[2] > 0, "dims must be 3 positive ints");
+    const c10::DeviceGuard guard(points.device());
+    const int n = (int)points.size(0);
+    const int64_t C = dims[0] * dims[1] * dims[2];
+    TORCH_CHECK(C < (1ll << 31) - 1, "too many cells");
+    auto i32 = points.options().dtype(torch::kInt32);
+    auto f32 = points.options().dtype(torch::kFloat32);
+    const int64_t nb = (int64_t)kn::scan_block_count((int)C) + 1;
+    // workspace (int32 words): bbox 8 | geom-pad 16 | cell_count C+1 | cell_scan C+1 | block_sums nb
+    //                          | (8-byte aligned) cell_rank 2N
+    int64_t rank_off = 8 + 16 + 2 * (C + 1) + nb;
+    rank_off = (rank_off + 1) & ~(int64_t)1;
+    auto ws = torch::empty({rank_off + 2 * (int64_t)n}, i32);
+    auto cell_start = torch::empty({C + 1}, i32);
+    auto sorted = torch::empty({(int64_t)n, 4}, f32);
+    auto perm = torch::empty({(int64_t)n}, i32);
+    auto geom = torch::empty({16}, i32);
+    int* w = ws.data_ptr<int>();
+    kn::BuildBuffers b{};
+    b.points = points.data_ptr<float>();
+    b.n = n;
+    for (int a = 0; a < 3; ++a) b.dims[a] = (int)dims[a];
+    b.bbox_words = reinterpret_cast<unsigned*>(w);
+    b.geom = reinterpret_cast<kn::GridGeom*>(geom.data_ptr<int>());
+    b.cell_count = w + 8 + 16;
+    b.cell_scan = b.cell_count + (C + 1);
+    b.block_sums = b.cell_scan + (C + 1);
+    b.cell_rank = reinterpret_cast<int2*>(w + rank_off);
+    b.cell_start = cell_start.data_ptr<int>();
+    b.sorted = reinterpret_cast<float4*>(sorted.data_ptr<float>());
+    b.perm = reinterpret_cast<unsigned*>(perm.data_ptr<int>());
+    b.deterministic = deterministic ? 1 : 0;
+    b.use_box = 0;
+    if (box.has_value()) {
+        TORCH_CHECK(box->size() == 6, "box must be [lox, loy, loz, hix, hiy, hiz]");
+        b.use_box = 1;
+        for (int a = 0; a < 3; ++a) { b.box_lo[a] = (float)(*box)[a]; b.box_hi[a] = (float)(*box)[3 + a]; }
+    }
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_build(b, s));
+    return {sorted, cell_start, perm, geom};
+}
+
+std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom,
+                                 std::vector<int64_t> dims, int64_t k, int64_t n_queries,
+                                 c10::optional<torch::Tensor> id_map, std::vector<double> complete,
+                                 std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
+                                 bool use_tiles, bool with_dist) {
+    TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
+                "sorted must be a (N,4) float32 GPU tensor");
+    TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
+    TORCH_CHECK(geom.is_cuda() && geom.numel() == 16, "geom must be a 16-int GPU tensor");
+    TORCH_CHECK(dims.size() == 3 && tile.size() == 3 && complete.size() == 6, "bad dims/tile/complete");
+    TORCH_CHECK(k >= 1 && k <= 128, "k must be in [1, 128]");
+    TORCH_CHECK(cell_start.numel() == dims[0] * dims[1] * dims[2] + 1, "cell_start size does not match dims");
+    const int n = (int)sorted.size(0);
+    TORCH_CHECK(n_queries >= 0 && n_queries <= n, "n_queries out of range");
+    const c10::DeviceGuard guard(sorted.device());
+    auto i32 = sorted.options().dtype(torch::kInt32);
+    auto out_idx = torch::empty({n_queries, k}, i32);
+    torch::Tensor out_dist;
+    if (with_dist) out_dist = torch::empty({n_queries, k}, sorted.options());
+    auto fallback = torch::empty({std::max(1, n)}, i32);
+    auto counters = torch::empty({4}, i32);
+    auto uncert = torch::empty({std::max<int64_t>(1, n_queries)}, i32);
+    kn::QueryBuffers q{};
+    q.sorted = reinterpret_cast<const float4*>(sorted.data_ptr<float>());
+    q.cell_start = cell_start.data_ptr<int>();
+    q.perm = nullptr;
+    q.geom = reinterpret_cast<const kn::GridGeom*>(geom.data_ptr<int>());
+    q.n = n;
+    for (int a = 0; a < 3; ++a) q.dims[a] = (int)dims[a];
+    q.k = (int)k;
+    q.n_queries = (int)n_queries;
+    if (id_map.has_value()) {
+        TORCH_CHECK(id_map->is_cuda() && id_map->scalar_type() == torch::kInt32 && id_map->numel() >= n,
+                    "id_map must be an int32 GPU tensor with >= N entries");
+        q.id_map = reinterpret_cast<const unsigned*>(id_map->data_ptr<int>());
+    }
+    for (int a = 0; a < 3; ++a) { q.complete.lo[a] = (float)complete[a]; q.complete.hi[a] = (float)complete[3 + a]; }
+    q.out_idx = reinterpret_cast<unsigned*>(out_idx.data_ptr<int>());
+    q.out_dist = with_dist ? out_dist.data_ptr<float>() : nullptr;
+    q.fallback_list = reinterpret_cast<unsigned*>(fallback.data_ptr<int>());
+    q.counters = reinterpret_cast<unsigned*>(counters.data_ptr<int>());
+    q.uncert_list = reinterpret_cast<unsigned*>(uncert.data_ptr<int>());
+    for (int a = 0; a < 3; ++a) q.tile[a] = (int)tile[a];
+    q.halo = (int)halo;
+    q.lds_capacity = (int)lds_capacity;
+    q.use_tiles = use_tiles ? 1 : 0;
+    TORCH_CHECK(lds_capacity >= 64 && (lds_capacity & (lds_capacity - 1)) == 0 && lds_capacity <= 8192,
+                "lds_capacity must be a power of two in [64, 8192]");
+    TORCH_CHECK(kn::query_lds_bytes(q.tile, q.halo, q.lds_capacity) <= 160 * 1024, "tile plan exceeds 160 KiB LDS");
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_query(q, s));
+    if (!with_dist) out_dist = torch::empty({0}, sorted.options());
+    return {out_idx, out_dist, counters, uncert};
+}
+
+py::dict auto_params(int64_t n, int64_t k, double ppc, std::vector<int64_t> tile, int64_t halo,
+                     c10::optional<std::vector<double>> extent) {
+    int th[3] = {0, 0, 0};
+    for (size_t a = 0; a < tile.size() && a < 3; ++a) th[a] = (int)tile[a];
+    float ext[3];
+    const float* pe = nullptr;
+    if (extent.has_value() && extent->size() == 3) {
+        for (int a = 0; a < 3; ++a) ext[a] = (float)(*extent)[a];
+        pe = ext;
+    }
+    const kn::AutoParams p = kn::auto_params((int)n, (int)k, (float)ppc, th, (int)halo, pe);
+    py::dict d;
+    d["dims"] = std::vector<int>{p.dims[0], p.dims[1], p.dims[2]};
+    d["tile"] = std::vector<int>{p.tile[0], p.tile[1], p.tile[2]};
+    d["halo"] = p.halo;
+    d["lds_capacity"] = p.lds_capacity;
+    d["lds_bytes"] = (int64_t)p.lds_bytes;
+    return d;
+}
+
+torch::Tensor to_stored_space(torch::Tensor out_orig, torch::Tensor perm) {
+    TORCH_CHECK(out_orig.is_cuda() && perm.is_cuda(), "GPU tensors expected");
+    const c10::DeviceGuard guard(out_orig.device());
+    const int n = (int)perm.numel();
+    const int k = (int)out_orig.size(1);
+    auto inv = torch::empty({std::max(1, n)}, perm.options());
+    auto out = torch::empty_like(out_orig);
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_invert_perm(reinterpret_cast<const unsigned*>(perm.data_ptr<int>()), n,
+                                        reinterpret_cast<unsigned*>(inv.data_ptr<int>()), s));
+    KN_CHECK_HIP(kn::launch_to_stored_space(reinterpret_cast<const unsigned*>(out_orig.data_ptr<int>()),
+                                            reinterpret_cast<const unsigned*>(perm.data_ptr<int>()),
+                                            reinterpret_cast<const unsigned*>(inv.data_ptr<int>()), n, k,
+                                            reinterpret_cast<unsigned*>(out.data_ptr<int>()), nullptr,
+                                            nullptr, s));
+    return out;
+}
+
+// ---- CPU (host) components ----------------------------------------------------------
+std::vector<torch::Tensor> kdtree_knn(torch::Tensor points, int64_t k, int64_t threads) {
+    check_points(points, false);
+    const int n = (int)points.size(0);
+    auto idx = torch::empty({n, k}, torch::kInt32);
+    auto d2 = torch::empty({n, k}, torch::kFloat32);
+    {
+        py::gil_scoped_release nogil;
+        knh::kdtree_knn_all(points.data_ptr<float>(), n, (int)k, reinterpret_cast<uint32_t*>(idx.data_ptr<int>()),
+                            d2.data_ptr<float>(), (int)threads);
+    }
+    return {idx, d2};
+}
+
+std::vector<torch::Tensor> brute_knn(torch::Tensor points, int64_t k, int64_t threads) {
+    check_points(points, false);
+    const int n = (int)points.size(0);
+    auto idx = torch::empty({n, k}, torch::kInt32);
+    auto d2 = torch::empty({n, k}, torch::kFloat32);
+    {
+        py::gil_scoped_release nogil;
+        knh::brute_knn_all(points.data_ptr<float>(), n, (int)k, reinterpret_cast<uint32_t*>(idx.data_ptr<int>()),
+                           d2.data_ptr<float>(), (int)threads);
+    }
+    return {idx, d2};
+}
+
+std::vector<torch::Tensor> grid_knn_cpu(torch::Tensor points, int64_t n_queries, int64_t k, double ppc,
+                                        std::vector<double> complete, int64_t threads) {
+    check_points(points, false);
+    TORCH_CHECK(complete.size() == 6, "complete must have 6 entries");
+    const int n = (int)points.size(0);
+    TORCH_CHECK(n_queries >= 0 && n_queries <= n, "n_queries out of range");
+    auto idx = torch::empty({n_queries, k}, torch::kInt32);
+    auto d2 = torch::empty({n_queries, k}, torch::kFloat32);
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) { lo[a] = (float)complete[a]; hi[a] = (float)complete[3 + a]; }
+    std::vector<uint32_t> unc;
+    {
+        py::gil_scoped_release nogil;
+        knh::grid_knn_cpu(points.data_ptr<float>(), n, (int)n_queries, (int)k, (float)ppc, lo, hi,
+                          reinterpret_cast<uint32_t*>(idx.data_ptr<int>()), d2.data_ptr<float>(), &unc,
+                          (int)threads);
+    }
+    auto u = torch::empty({(int64_t)unc.size()}, torch::kInt32);
+    for (size_t i = 0; i < unc.size(); ++i) u[i] = (int)unc[i];
+    return {idx, d2, u};
+}
+
+torch::Tensor read_xyz(const std::string& path, bool normalize) {
+    std::vector<float> xyz;
+    std::string err;
+    TORCH_CHECK(knh::read_xyz(path, xyz, normalize, &err), err);
+    auto t = torch::empty({(int64_t)(xyz.size() / 3), 3}, torch::kFloat32);
+    std::memcpy(t.data_ptr<float>(), xyz.data(), xyz.size() * sizeof(float));
+    return t;
+}
+
+void write_xyz(const std::string& path, torch::Tensor points) {
+    check_points(points, false);
+    std::string err;
+    TORCH_CHECK(knh::write_xyz(path, points.data_ptr<float>(), (int)points.size(0), &err), err);
+}
+
+torch::Tensor normalize_1000(torch::Tensor points) {
+    check_points(points, false);
+    std::vector<float> xyz(points.data_ptr<float>(), points.data_ptr<float>() + points.numel());
+    knh::normalize_1000(xyz);
+    auto t = torch::empty_like(points);
+    std::memcpy(t.data_ptr<float>(), xyz.data(), xyz.size() * sizeof(float));
+    return t;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.doc() = "MI355X-native k-nearest-neighbour kernels (gfx950 HIP) and CPU oracles";
+    m.def("build", &build, "bin points into the grid (GPU)", py::arg("points"), py::arg("dims"),
+          py::arg("deterministic") = true, py::arg("box") = py::none());
+    m.def("query", &query, "k-nearest-neighbour queries on a built grid (GPU)");
+    m.def("auto_params", &auto_params, "grid / tile plan");
+    m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
+    m.def("kdtree_knn", &kdtree_knn, "CPU kd-tree oracle", py::arg("points"), py::arg("k"), py::arg("threads") = 0);
+    m.def("brute_knn", &brute_knn, "CPU brute-force oracle", py::arg("points"), py::arg("k"), py::arg("threads") = 0);
+    m.def("grid_knn_cpu", &grid_knn_cpu, "CPU grid kNN (engine algorithm on the host)");
+    m.def("read_xyz", &read_xyz, "read a .xyz file", py::arg("path"), py::arg("normalize") = false);
+    m.def("write_xyz", &write_xyz, "write a .xyz file");
+    m.def("normalize_1000", &normalize_1000, "map a cloud into [0,1000]^3 (reference normalisation)");
+    m.attr("SENTINEL") = py::int_(-1);
+    m.attr("MAX_K") = py::int_(128);
+}

@@ -1,0 +1,91 @@
+"""Spatial domain decomposition of the point grid across ranks (NEW: the reference is single-GPU).
+
+World sizes factor into a px x py x pz box grid (2 -> 2x1x1, 4 -> 2x2x1, 8 -> 2x2x2, any N by
+balanced factorisation, largest factor on the longest axis). Each rank owns one box; a point
+belongs to the box containing it. With 2x2x2 every rank neighbours all 7 others, so the halo
+all-to-all uses every point-to-point xGMI link of an MI355X node.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Sequence
+
+import torch
+
+
+def factor3(world: int, extent: Sequence[float] = (1.0, 1.0, 1.0)) -> tuple:
+    """Balanced 3-factorisation of ``world`` (minimises the surface of the rank boxes)."""
+    best, best_cost = (world, 1, 1), math.inf
+    for a in range(1, world + 1):
+        if world % a:
+            continue
+        for b in range(1, world // a + 1):
+            if (world // a) % b:
+                continue
+            c = world // a // b
+            f = (a, b, c)
+            # surface of one box for the given domain extent
+            bx, by, bz = (extent[i] / f[i] for i in range(3))
+            cost = bx * by + by * bz + bx * bz
+            if cost < best_cost - 1e-12:
+                best, best_cost = f, cost
+    return best
+
+
+@dataclass
+class SpatialDecomposition:
+    world: int
+    lo: tuple  # global domain
+    hi: tuple
+    grid: tuple = None  # (px, py, pz)
+
+    def __post_init__(self):
+        ext = tuple(max(self.hi[a] - self.lo[a], 1e-30) for a in range(3))
+        if self.grid is None:
+            self.grid = factor3(self.world, ext)
+        assert self.grid[0] * self.grid[1] * self.grid[2] == self.world
+
+    def coords(self, rank: int) -> tuple:
+        px, py, _ = self.grid
+        return rank % px, (rank // px) % py, rank // (px * py)
+
+    def rank_box(self, rank: int) -> tuple:
+        c = self.coords(rank)
+        lo, hi = [], []
+        for a in range(3):
+            w = (self.hi[a] - self.lo[a]) / self.grid[a]
+            lo.append(self.lo[a] + c[a] * w)
+            hi.append(self.hi[a] if c[a] == self.grid[a] - 1 else self.lo[a] + (c[a] + 1) * w)
+        return tuple(lo), tuple(hi)
+
+    def owner(self, points: torch.Tensor) -> torch.Tensor:
+        """Owning rank of each point (int64). Points outside the domain clamp to edge boxes."""
+        dev = points.device
+        lo = torch.tensor(self.lo, dtype=torch.float32, device=dev)
+        hi = torch.tensor(self.hi, dtype=torch.float32, device=dev)
+        g = torch.tensor(self.grid, dtype=torch.float32, device=dev)
+        f = (points - lo) / (hi - lo).clamp(min=1e-30) * g
+        c = torch.floor(f).clamp(min=0)
+        c = torch.minimum(c, g - 1).long()
+        return c[:, 0] + self.grid[0] * (c[:, 1] + self.grid[1] * c[:, 2])
+
+    def complete_box(self, rank: int, h: float) -> list:
+        """Box in which a rank holding its points + an h-halo has the complete cloud: its own box
+        grown by h, unbounded on the faces that lie on the global domain boundary."""
+        lo, hi = self.rank_box(rank)
+        c = self.coords(rank)
+        out_lo, out_hi = [], []
+        for a in range(3):
+            out_lo.append(-math.inf if c[a] == 0 else lo[a] - h)
+            out_hi.append(math.inf if c[a] == self.grid[a] - 1 else hi[a] + h)
+        return out_lo + out_hi
+
+    def box_dist2(self, points: torch.Tensor, rank: int) -> torch.Tensor:
+        """Squared distance from each point to rank's box (0 inside)."""
+        lo, hi = self.rank_box(rank)
+        dev = points.device
+        lo_t = torch.tensor(lo, dtype=torch.float32, device=dev)
+        hi_t = torch.tensor(hi, dtype=torch.float32, device=dev)
+        d = torch.clamp(lo_t - points, min=0) + torch.clamp(points - hi_t, min=0)
+        return (d * d).sum(1)

@@ -1,0 +1,118 @@
+"""CPU-only tests: oracles, CPU grid solver, .xyz I/O, C++ unit binary."""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import cuda_knearests_amd as kn
+from cuda_knearests_amd.utils import REPO, blue_cloud, clustered_cloud, dataset, uniform_cloud
+
+
+def _same_up_to_ties(i1, d1, i2, d2):
+    assert torch.equal(d1, d2)
+    same = (i1 == i2) | (d1.unsqueeze(-1) == d2.unsqueeze(-2)).any(-1)
+    assert bool(same.all())
+
+
+@pytest.mark.parametrize("k", [1, 8, 16, 50])
+@pytest.mark.parametrize("gen", ["uniform", "blue", "clustered", "dupes"])
+def test_oracles_agree(k, gen):
+    if gen == "uniform":
+        p = uniform_cloud(4000, 1)
+    elif gen == "blue":
+        p = blue_cloud(4000, 2)
+    elif gen == "clustered":
+        p = clustered_cloud(4000, 3)
+    else:
+        p = uniform_cloud(2000, 4)
+        p = torch.cat([p, p])
+    bi, bd = kn.knn_cpu(p, k, "brute")
+    ki, kd = kn.knn_cpu(p, k, "kdtree")
+    gi, gd, unc = kn.knn_cpu(p, k, "grid")
+    assert unc.numel() == 0
+    _same_up_to_ties(ki, kd, bi, bd)
+    _same_up_to_ties(gi, gd, bi, bd)
+    # ascending, no self
+    assert bool((bd[:, 1:] >= bd[:, :-1]).all())
+    assert not bool((bi == torch.arange(p.size(0)).unsqueeze(1)).any())
+
+
+def test_self_excluded_by_index_with_duplicates():
+    # the reference oracle drops neighbour 0 assuming it is the query (test_knearests.cu:210);
+    # with exact duplicates the twin must stay in the result at distance 0.
+    p = torch.tensor([[0, 0, 0], [0, 0, 0], [1, 0, 0], [5, 5, 5]], dtype=torch.float32)
+    i, d = kn.knn_cpu(p, 2, "kdtree")
+    assert i[0, 0] == 1 and d[0, 0] == 0 and i[1, 0] == 0
+
+
+def test_small_n_fills_sentinel():
+    p = torch.tensor([[0, 0, 0], [1, 0, 0], [0, 3, 0]], dtype=torch.float32)
+    for m in ("brute", "kdtree"):
+        i, d = kn.knn_cpu(p, 4, m)
+        assert i[0].tolist() == [1, 2, -1, -1]
+        assert math.isinf(d[0, 2].item())
+    i, d, _ = kn.knn_cpu(p, 4, "grid")
+    assert i[0].tolist() == [1, 2, -1, -1]
+
+
+def test_pts20k_reference_dataset_k8():
+    # BASELINE config 1: pts20K.xyz, k=8, CPU kd_tree path (plumbing, no GPU)
+    p = kn.read_xyz(str(dataset("pts20K.xyz")), normalize=True)
+    assert p.shape == (20626, 3)
+    assert 0.0 < float(p.min()) and float(p.max()) < 1000.0
+    ki, kd = kn.knn_cpu(p, 8, "kdtree")
+    gi, gd, unc = kn.knn_cpu(p, 8, "grid")
+    _same_up_to_ties(gi, gd, ki, kd)
+    # blue noise: min NN spacing ~25 after x1000
+    nn = kd[:, 0].sqrt()
+    assert 20.0 < float(nn.min()) < 30.0
+
+
+def test_xyz_roundtrip(tmp_path):
+    p = uniform_cloud(1000, 5)
+    f = tmp_path / "a.xyz"
+    kn.write_xyz(str(f), p)
+    q = kn.read_xyz(str(f))
+    assert torch.equal(p, q)
+    lines = f.read_text().splitlines()
+    assert lines[0] == "1000"
+    with pytest.raises(RuntimeError):
+        bad = tmp_path / "b.xyz"
+        bad.write_text("5\n1 2 3\n")
+        kn.read_xyz(str(bad))
+
+
+def test_normalize_matches_reference_rule():
+    p = torch.tensor([[0, 0, 0], [2, 1, 0.5], [1, 1, 1]], dtype=torch.float32)
+    q = kn.normalize_1000(p)
+    # bbox inflated by 0.1% of the max side, uniform scale by the inflated max side
+    d = 0.002
+    side = 2 + 2 * d
+    ref = (p - torch.tensor([-d, -d, -d])) * (1000.0 / side)
+    assert torch.allclose(q, ref, rtol=1e-5, atol=1e-3)
+
+
+def test_plan_auto_reference_density():
+    p = kn.Plan.auto(900_000, 16)
+    # ~3.1 points per cell (reference knearests.cu:249): (900000/3.1)^(1/3) = 66.2
+    assert p.dims == [66, 66, 66]
+    assert p.halo >= 1 and p.lds_capacity >= 1024 and p.lds_bytes <= 160 * 1024
+
+
+def test_cpp_unit_cpu():
+    exe = REPO / "bin" / "knn_unit"
+    if not exe.exists():
+        from cuda_knearests_amd import _build
+
+        _build.build(verbose=False)
+    r = subprocess.run([str(exe), "cpu"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_cli_help():
+    r = subprocess.run([str(REPO / "bin" / "knn_cli"), "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0
+    assert "usage" in r.stderr

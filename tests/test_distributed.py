@@ -1,0 +1,112 @@
+"""Multi-process distributed path on CPU ranks (gloo) -- SURVEY §4.2 item 3.
+
+Each rank gets an arbitrary share of a global cloud; DistributedKNearests redistributes,
+exchanges halos and solves locally. The union of the per-rank results must equal the
+single-process oracle for every point (global ids, distance-aware).
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, k, gen, partitioned, halo_factor, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from cuda_knearests_amd.parallel import DistributedKNearests, SpatialDecomposition
+    from cuda_knearests_amd.utils import clustered_cloud, uniform_cloud
+
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 6000
+    cloud = uniform_cloud(n, 42) if gen == "uniform" else clustered_cloud(n, 43)
+    ids = torch.arange(n, dtype=torch.int32)
+    if partitioned:
+        lo, hi = tuple(cloud.min(0).values.tolist()), tuple(cloud.max(0).values.tolist())
+        dec = SpatialDecomposition(world, lo, hi)
+        mine = dec.owner(cloud) == rank
+    else:
+        mine = (torch.arange(n) % world) == rank  # scattered, not spatial
+    dk = DistributedKNearests(k=k, halo_factor=halo_factor)
+    res = dk.solve(cloud[mine].contiguous(), ids[mine].contiguous(), partitioned=partitioned)
+    # numpy copies travel by value (tensors would go through fds that die with the worker)
+    q.put((rank, res.ids.numpy().copy(), res.neighbors.numpy().copy(), res.d2.numpy().copy(), res.stats))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(world, k, gen="uniform", partitioned=False, halo_factor=1.6):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, gen, partitioned, halo_factor, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return [(r, torch.from_numpy(i), torch.from_numpy(nb), torch.from_numpy(d), s) for r, i, nb, d, s in out]
+
+
+@pytest.mark.parametrize("world,k,gen,partitioned", [
+    (2, 8, "uniform", False),
+    (2, 16, "uniform", True),
+    (4, 16, "clustered", False),
+])
+def test_distributed_matches_single(world, k, gen, partitioned):
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.utils import clustered_cloud, uniform_cloud
+
+    out = _run(world, k, gen, partitioned)
+    n = 6000
+    cloud = uniform_cloud(n, 42) if gen == "uniform" else clustered_cloud(n, 43)
+    oi, od = kn.knn_cpu(cloud, k, "kdtree")
+    seen = torch.zeros(n, dtype=torch.bool)
+    for rank, ids, nb, d2, stats in out:
+        ids = ids.long()
+        assert not bool(seen[ids].any()), "a point is owned by two ranks"
+        seen[ids] = True
+        assert torch.equal(d2, od[ids]), f"rank {rank}: distances differ"
+        same = (nb.long() == oi[ids].long()) | (d2.unsqueeze(-1) == od[ids].unsqueeze(-2)).any(-1)
+        assert bool(same.all())
+    assert bool(seen.all()), "some points were lost in redistribution"
+
+
+def test_halo_growth_round():
+    # a deliberately tiny halo forces uncertified queries -> the halo doubles until certified
+    out = _run(2, 16, "uniform", False, halo_factor=0.05)
+    assert max(s["rounds"] for *_, s in out) > 1
+
+
+def test_decomposition_factors():
+    from cuda_knearests_amd.parallel import SpatialDecomposition, factor3
+
+    assert sorted(factor3(2)) == [1, 1, 2]
+    assert sorted(factor3(4)) == [1, 2, 2]
+    assert factor3(8) == (2, 2, 2)
+    assert sorted(factor3(6)) == [1, 2, 3]
+    d = SpatialDecomposition(8, (0, 0, 0), (1000, 1000, 1000))
+    pts = torch.rand(10000, 3) * 1000
+    o = d.owner(pts)
+    for r in range(8):
+        lo, hi = d.rank_box(r)
+        m = o == r
+        assert bool(((pts[m] >= torch.tensor(lo)) & (pts[m] <= torch.tensor(hi))).all())
+    cb = d.complete_box(0, 10.0)
+    assert cb[0] == float("-inf") and cb[3] == 510.0

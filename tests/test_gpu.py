@@ -1,0 +1,152 @@
+"""GPU tests (MI355X): HIP kernels vs the CPU oracles.
+
+Every comparison is distance-aware: squared distances must equal the kd-tree oracle's bit for
+bit (same fp32 fma chain), ids may differ only inside runs of equal distance.
+"""
+import subprocess
+
+import pytest
+import torch
+
+import cuda_knearests_amd as kn
+from cuda_knearests_amd.utils import REPO, blue_cloud, clustered_cloud, dataset, uniform_cloud
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_matches_oracle(p, idx, d2, k):
+    oi, od = kn.knn_cpu(p.cpu(), k, "kdtree")
+    idx, d2 = idx.cpu(), d2.cpu()
+    assert idx.shape == oi.shape
+    mism = (d2 != od).any(1)
+    assert int(mism.sum()) == 0, f"{int(mism.sum())} rows differ; first {int(mism.nonzero()[0, 0])}"
+    same = (idx == oi) | (d2.unsqueeze(-1) == od.unsqueeze(-2)).any(-1)
+    assert bool(same.all())
+
+
+def test_native_extension_loaded(cuda, ext):
+    import cuda_knearests_amd._C as C
+
+    assert C.__file__.startswith(str(REPO))
+
+
+@pytest.mark.parametrize("k", [1, 4, 8, 16, 32, 50, 64])
+def test_uniform_tile_vs_oracle(cuda, k):
+    p = uniform_cloud(30000, seed=k, device=cuda)
+    idx, d2 = kn.knn(p, k)
+    _assert_matches_oracle(p, idx, d2, k)
+
+
+@pytest.mark.parametrize("k", [8, 16, 96, 128])
+def test_exact_path_vs_oracle(cuda, k):
+    p = uniform_cloud(20000, seed=100 + k, device=cuda)
+    idx, d2 = kn.knn(p, k, use_tiles=False)
+    _assert_matches_oracle(p, idx, d2, k)
+
+
+@pytest.mark.parametrize("gen", ["blue", "clustered"])
+def test_distributions(cuda, gen):
+    p = (blue_cloud if gen == "blue" else clustered_cloud)(40000, seed=7).to(cuda)
+    idx, d2 = kn.knn(p, 16)
+    _assert_matches_oracle(p, idx, d2, 16)
+
+
+def test_duplicates_and_tiny(cuda):
+    p = uniform_cloud(3000, seed=9)
+    p = torch.cat([p, p]).to(cuda)
+    idx, d2 = kn.knn(p, 8)
+    _assert_matches_oracle(p, idx, d2, 8)
+    for n in (1, 2, 3, 9, 17, 65):
+        p = uniform_cloud(n, seed=n, device=cuda)
+        idx, d2 = kn.knn(p, 8)
+        _assert_matches_oracle(p, idx, d2, 8)
+
+
+def test_pts20k_reference_dataset(cuda):
+    p = kn.read_xyz(str(dataset("pts20K.xyz")), normalize=True).to(cuda)
+    for k in (8, 50):
+        idx, d2 = kn.knn(p, k)
+        _assert_matches_oracle(p, idx, d2, k)
+
+
+def test_engine_reference_semantics(cuda):
+    p = uniform_cloud(25000, seed=11, device=cuda)
+    e = kn.KNearests(k=16, device=cuda).prepare(p).solve()
+    knn_s = e.get_knearests().cpu().long()
+    perm = e.get_permutation().cpu().long()
+    assert torch.equal(torch.sort(perm).values, torch.arange(p.size(0)))
+    # stored-space rows remapped through the permutation == original-space result
+    remap = torch.full_like(knn_s, -1)
+    valid = knn_s >= 0
+    remap[valid] = perm[knn_s[valid]]
+    orig = torch.empty_like(remap)
+    orig[perm] = remap
+    assert torch.equal(orig, e.neighbors.cpu().long())
+    sp = e.get_points().cpu()
+    assert torch.equal(sp, p.cpu()[perm])
+    s = e.stats()
+    assert s["num_cells"] == 29 ** 3 or s["num_cells"] > 0
+    assert s["min_cell"] >= 0 and s["max_cell"] >= s["avg_cell"]
+
+
+def test_graph_replay_matches_eager(cuda):
+    p = uniform_cloud(50000, seed=12, device=cuda)
+    e = kn.KNearests(k=16, device=cuda).prepare(p).solve()
+    ref_i, ref_d = e.neighbors.clone(), e.distances.clone()
+    g = kn.KNearests(k=16, device=cuda)
+    g.points = p
+    for _ in range(3):
+        g.step(p, capture=True)
+    torch.cuda.synchronize()
+    assert torch.equal(g.neighbors, ref_i) and torch.equal(g.distances, ref_d)
+    # new data through the same graph
+    q = uniform_cloud(50000, seed=13, device=cuda)
+    g.step(q, capture=True)
+    torch.cuda.synchronize()
+    i2, d2 = kn.knn(q, 16)
+    assert torch.equal(g.neighbors, i2) and torch.equal(g.distances, d2)
+
+
+def test_deterministic_reruns(cuda):
+    p = uniform_cloud(100000, seed=14, device=cuda)
+    a = kn.knn(p, 16)
+    b = kn.knn(p, 16)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_set_k_and_save_load(cuda, tmp_path):
+    p = uniform_cloud(20000, seed=15, device=cuda)
+    e = kn.KNearests(k=8, device=cuda).prepare(p).solve()
+    e.set_k(24).solve()
+    _assert_matches_oracle(p, e.neighbors, e.distances, 24)
+    f = tmp_path / "g.pt"
+    e.save(str(f))
+    e2 = kn.KNearests.load(str(f), device=cuda).solve()
+    assert torch.equal(e2.neighbors, e.neighbors)
+
+
+def test_large_uniform_subset(cuda):
+    # 900K: the headline config (subset vs brute force on the GPU)
+    p = uniform_cloud(900_000, seed=16, device=cuda)
+    idx, d2, info = kn.query(kn.build_grid(p, 16), 16, return_info=True)
+    sel = torch.randperm(p.size(0), device=cuda)[:1024]
+    dd = torch.cdist(p[sel], p).pow(2)
+    dd[torch.arange(1024, device=cuda), sel] = float("inf")
+    ref = torch.topk(dd, 16, largest=False).values
+    assert torch.allclose(d2[sel], ref, rtol=1e-4, atol=1e-2)
+    c = info["counters"].cpu()
+    assert int(c[1]) == 0  # nothing uncertified on a single GPU
+    assert int(c[0]) < 0.01 * p.size(0), f"exact-path fraction too high: {int(c[0])}"
+
+
+def test_cpp_unit_gpu(cuda):
+    r = subprocess.run([str(REPO / "bin" / "knn_unit"), "gpu"], capture_output=True, text=True, timeout=900)
+    print(r.stderr[-4000:])
+    assert r.returncode == 0, r.stderr[-4000:]
+
+
+def test_cli_reference_flow(cuda):
+    r = subprocess.run([str(REPO / "bin" / "knn_cli"), str(dataset("pts20K.xyz")), "--k", "50", "--json"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert '"ok": true' in r.stdout
