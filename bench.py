@@ -57,6 +57,13 @@ def brute_check(points: torch.Tensor, idx: torch.Tensor, d2: torch.Tensor, k: in
     return {"checked": int(sel.numel()), "bad_rows": bad}
 
 
+T_START = time.perf_counter()
+
+
+def log(msg: str) -> None:
+    print(f"[bench {time.perf_counter() - T_START:8.2f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def run_single(args) -> dict:
     from cuda_knearests_amd import KNearests
     from cuda_knearests_amd.utils import uniform_cloud
@@ -65,19 +72,24 @@ def run_single(args) -> dict:
     torch.cuda.set_device(dev)
     pts = uniform_cloud(args.n, seed=args.seed, device=dev)
     kn = KNearests(k=args.k, device=dev, deterministic=not args.nondet)
+    log("eager prepare+solve")
     kn.prepare(pts)
     kn.solve()  # eager pass: plan + per-phase device timings + counters
     ms_build, ms_solve = kn.timings["ms_build"], kn.timings["ms_solve"]
     info = dict(kn.info)
+    log(f"eager done: build {ms_build:.3f} ms solve {ms_solve:.3f} ms {info}")
     for _ in range(args.warmup):
         kn.step(pts, capture=not args.no_graph)
     torch.cuda.synchronize()
+    log("warmup done")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         kn.step(pts, capture=not args.no_graph)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
     chk = brute_check(pts, kn.neighbors, kn.distances, args.k) if not args.no_check else {}
+    log(f"check {chk}")
     # per-phase device times, median of a few eager runs
     bts, sts = [], []
     for _ in range(5):
@@ -150,6 +162,10 @@ def main() -> int:
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--nondet", action="store_true")
     args = ap.parse_args()
+    if os.environ.get("KN_BENCH_WATCHDOG"):
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["KN_BENCH_WATCHDOG"]), exit=True)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world_env == 1:
         # convenience: relaunch under torch.distributed.run (before any GPU init)

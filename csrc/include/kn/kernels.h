@@ -105,6 +105,11 @@ struct AutoParams {
 };
 AutoParams auto_params(int n, int k, float points_per_cell, const int* tile_hint, int halo_hint,
                        const float* extent /* nullable: cubic grid */);
+// Checked builds only (KN_CHECKED): first out-of-bounds report of each kernel file
+// {site code, index, limit, index high word}; all 0xFFFFFFFF in release builds.
+hipError_t debug_words_build(unsigned out[4], bool reset);
+hipError_t debug_words_query(unsigned out[4], bool reset);
+
 size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity);
 int lds_capacity_for(double staged_points);
 

@@ -7,6 +7,46 @@
 
 namespace kn {
 
+// ---- checked builds (-DKN_CHECKED=1): bounds-checked indexing --------------------------
+// Every wrapped index is tested against its buffer's extent; a violation is recorded in a
+// per-translation-unit device word (first failing site code, index, limit) and the access is
+// redirected to element 0, so a bug shows up as a report instead of a GPU memory fault.
+// The release build compiles the macro away.
+#if defined(KN_CHECKED) && KN_CHECKED
+static __device__ unsigned kn_dbg_words[4];
+__device__ __noinline__ long long kn_dbg_fail(unsigned code, long long i, long long n) {
+    if (atomicCAS(&kn_dbg_words[0], 0u, code) == 0u) {
+        kn_dbg_words[1] = (unsigned)i;
+        kn_dbg_words[2] = (unsigned)n;
+        kn_dbg_words[3] = (unsigned)(i >> 32);
+    }
+    return 0;
+}
+#define KN_IDX(i, n, code) \
+    (((unsigned long long)(long long)(i) < (unsigned long long)(long long)(n)) \
+         ? (i)                                                                 \
+         : (__decltype_nr(i))kn_dbg_fail((code), (long long)(i), (long long)(n)))
+template <class T> struct kn_nr { using type = T; };
+template <class T> struct kn_nr<T&> { using type = T; };
+#define __decltype_nr(x) typename kn::kn_nr<decltype(x)>::type
+#define KN_DEFINE_DEBUG_READER(NAME)                                                     \
+    hipError_t NAME(unsigned out[4], bool reset) {                                        \
+        hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(kn_dbg_words), 16, 0, hipMemcpyDeviceToHost); \
+        if (e == hipSuccess && reset) {                                                   \
+            const unsigned z[4] = {0, 0, 0, 0};                                           \
+            e = hipMemcpyToSymbol(HIP_SYMBOL(kn_dbg_words), z, 16, 0, hipMemcpyHostToDevice); \
+        }                                                                                 \
+        return e;                                                                         \
+    }
+#else
+#define KN_IDX(i, n, code) (i)
+#define KN_DEFINE_DEBUG_READER(NAME)                       \
+    hipError_t NAME(unsigned out[4], bool) {               \
+        out[0] = out[1] = out[2] = out[3] = 0xFFFFFFFFu;   \
+        return hipSuccess;                                 \
+    }
+#endif
+
 // DPP controls (gfx9 encoding)
 #define KN_DPP_QUAD_1032 0xB1
 #define KN_DPP_QUAD_2301 0x4E

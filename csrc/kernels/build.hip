@@ -109,6 +109,7 @@ __global__ __launch_bounds__(256) void count_kernel(const float* __restrict__ pt
     const int c = cell_of(*g, p);
     const int r = atomicAdd(cell_count + c, 1);
     cell_rank[i] = make_int2(c, r);
+    (void)KN_IDX(c, g->dims[0] * g->dims[1] * g->dims[2], 101);
 }
 
 // Block-local exclusive scan of kScanItems ints (256 threads x 16 items), block total out.
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(256) void scatter_kernel(
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         const int2 cr = cell_rank[i];
-        const int pos = cell_scan[cr.x] + block_sums[cr.x / kScanItems] + cr.y;
+        const int pos = KN_IDX(cell_scan[KN_IDX(cr.x, num_cells, 103)] + block_sums[cr.x / kScanItems] + cr.y, n, 102);
         sorted[pos] = make_float4(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], __uint_as_float((unsigned)i));
         perm[pos] = (unsigned)i;
     }
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(256) void cell_sort_kernel(const int* __restrict__ 
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= num_cells) return;
     const int a = cell_start[c], b = cell_start[c + 1];
+    (void)KN_IDX(b, a + 100000000, 105);
     for (int i = a + 1; i < b; ++i) {
         const float4 v = sorted[i];
         const unsigned key = __float_as_uint(v.w);
@@ -262,6 +264,8 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         cell_sort_kernel<<<cdiv(C, 256), 256, 0, s>>>(b.cell_start, C, b.sorted, b.perm);
     return hipGetLastError();
 }
+
+KN_DEFINE_DEBUG_READER(debug_words_build)
 
 hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int hist_len,
                              hipStream_t s) {

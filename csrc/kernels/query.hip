@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     for (int t = threadIdx.x; t < nrows * cbs; t += kWG) {
         const int r = t / cbs, i = t - r * cbs;
         const int y = sy0 + r % nys, z = sz0 + r / nys;
-        cb[r * cbs + i] = a.cell_start[(z * a.Y + y) * a.X + sx0 + i];
+        cb[r * cbs + i] = a.cell_start[KN_IDX((z * a.Y + y) * a.X + sx0 + i, a.X * a.Y * a.Z + 1, 201)];
     }
     __syncthreads();
     // ---- 2. row prefix (LDS offsets) and tile-row query prefix (wave 0) ----------------
@@ -152,10 +152,10 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (qpref[mid] <= t) lo = mid; else hi = mid - 1; }
             const int r = (ty0 - sy0 + lo % ntry) + nys * (tz0 - sz0 + lo / ntry);
             const unsigned sidx = (unsigned)(cb[r * cbs + hx] + (t - qpref[lo]));
-            const unsigned orig = __float_as_uint(a.sorted[sidx].w);
+            const unsigned orig = __float_as_uint(a.sorted[KN_IDX(sidx, (unsigned)a.n, 204)].w);
             if ((int)orig < a.n_queries) {
                 const unsigned pos = atomicAdd(a.counters + 0, 1u);
-                a.fallback_list[pos] = sidx;
+                a.fallback_list[KN_IDX(pos, (unsigned)a.n, 205)] = sidx;
             }
         }
         if (threadIdx.x == 0) atomicAdd(a.counters + 2, 1u);
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     for (int s = threadIdx.x; s < S; s += kWG) {
         int lo = 0, hi = nrows - 1;
         while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rowbase[mid] <= s) lo = mid; else hi = mid - 1; }
-        pts[s] = a.sorted[cb[lo * cbs] + (s - rowbase[lo])];
+        pts[KN_IDX(s, a.cap, 203)] = a.sorted[KN_IDX(cb[lo * cbs] + (s - rowbase[lo]), a.n, 202)];
     }
     __syncthreads();
     (void)misc;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             qslot = rowbase[r] + off;
             qsidx = (unsigned)(cb[r * cbs] + off);
         }
-        const float4 qp = pts[qslot];
+        const float4 qp = pts[KN_IDX(qslot, S, 206)];
         const unsigned qorig = __float_as_uint(qp.w);
         active = active && ((int)qorig < a.n_queries);
         const float qx = qp.x, qy = qp.y, qz = qp.z;
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 const int r = y + nys * z;
                 const int rb = rowbase[r] - cb[r * cbs];
                 const int s0 = rb + cb[r * cbs + X0];
-                const int s1 = rb + cb[r * cbs + X1 + 1];
+                const int s1 = KN_IDX(rb + cb[r * cbs + X1 + 1], S + 1, 207);
                 for (int s = s0; s < s1; ++s) {
                     const float4 p = pts[s];
                     const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
             if (keys[j] != SENT) {
-                const float4 p = pts[keys[j] & MASK];
+                const float4 p = pts[KN_IDX(keys[j] & MASK, (unsigned)S, 208)];
                 const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
                 dd[j] = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
                 ii[j] = __float_as_uint(p.w);
@@ -318,13 +318,14 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
                 if (j < k) {
-                    a.out_idx[row + j] = a.id_map ? a.id_map[ii[j]] : ii[j];
-                    if (a.out_dist) a.out_dist[row + j] = dd[j];
+                    const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 209);
+                    a.out_idx[o] = a.id_map ? a.id_map[KN_IDX(ii[j], (unsigned)a.n, 211)] : ii[j];
+                    if (a.out_dist) a.out_dist[o] = dd[j];
                 }
             }
         } else {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
-            a.fallback_list[pos] = qsidx;
+            a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx;
         }
     }
 }
@@ -347,96 +348,164 @@ struct ExactArgs {
     unsigned* uncert_list;     // optional: original indices of uncertified queries
 };
 
+// Top-K storage policies for the exact kernel: registers (K <= 64: static-index insertion
+// network, no scratch) or a per-lane column in LDS (K > 64: keeps the register file free;
+// layout [slot][lane] so a wave's accesses to one slot hit 64 consecutive dwords).
+template <int KT>
+struct RegTopK {
+    float dd[KT];
+    unsigned ii[KT];
+    __device__ __forceinline__ void init(unsigned char*) {
+#pragma unroll
+        for (int j = 0; j < KT; ++j) { dd[j] = INFINITY; ii[j] = SENT; }
+    }
+    __device__ __forceinline__ bool improves(float d2, unsigned id) const { return pair_less(d2, id, dd[KT - 1], ii[KT - 1]); }
+    __device__ __forceinline__ void insert(float d2, unsigned id) {
+#pragma unroll
+        for (int j = KT - 1; j > 0; --j) {
+            const bool before_prev = pair_less(d2, id, dd[j - 1], ii[j - 1]);
+            const bool before_cur = pair_less(d2, id, dd[j], ii[j]);
+            const float nd = before_prev ? dd[j - 1] : (before_cur ? d2 : dd[j]);
+            const unsigned ni = before_prev ? ii[j - 1] : (before_cur ? id : ii[j]);
+            dd[j] = nd; ii[j] = ni;
+        }
+        if (pair_less(d2, id, dd[0], ii[0])) { dd[0] = d2; ii[0] = id; }
+    }
+    __device__ __forceinline__ float dist(int k) const {
+        float r = INFINITY;
+#pragma unroll
+        for (int j = 0; j < KT; ++j) if (j == k) r = dd[j];
+        return r;
+    }
+    template <class F>
+    __device__ __forceinline__ void emit(int k, F&& f) const {
+#pragma unroll
+        for (int j = 0; j < KT; ++j) if (j < k) f(j, dd[j], ii[j]);
+    }
+};
+
+template <int KT>
+struct LdsTopK {
+    float* dd;
+    unsigned* ii;
+    float worst_d;
+    unsigned worst_i;
+    __device__ __forceinline__ void init(unsigned char* smem) {
+        const int lane = threadIdx.x;
+        dd = reinterpret_cast<float*>(smem) + lane;
+        ii = reinterpret_cast<unsigned*>(smem + (size_t)KT * 64 * sizeof(float)) + lane;
+        for (int j = 0; j < KT; ++j) { dd[j * 64] = INFINITY; ii[j * 64] = SENT; }
+        worst_d = INFINITY;
+        worst_i = SENT;
+    }
+    __device__ __forceinline__ bool improves(float d2, unsigned id) const { return pair_less(d2, id, worst_d, worst_i); }
+    __device__ __forceinline__ void insert(float d2, unsigned id) {
+        int j = KT - 1;
+        while (j > 0) {
+            const float pd = dd[(j - 1) * 64];
+            const unsigned pi = ii[(j - 1) * 64];
+            if (!pair_less(d2, id, pd, pi)) break;
+            dd[j * 64] = pd; ii[j * 64] = pi;
+            --j;
+        }
+        dd[j * 64] = d2; ii[j * 64] = id;
+        worst_d = dd[(KT - 1) * 64];
+        worst_i = ii[(KT - 1) * 64];
+    }
+    __device__ __forceinline__ float dist(int k) const { return (k >= 0 && k < KT) ? dd[k * 64] : INFINITY; }
+    template <class F>
+    __device__ __forceinline__ void emit(int k, F&& f) const {
+        for (int j = 0; j < k && j < KT; ++j) f(j, dd[j * 64], ii[j * 64]);
+    }
+};
+
+template <class Top>
+__device__ __forceinline__ void exact_query(const ExactArgs& a, const GridGeom& g, unsigned sidx, Top& top) {
+    const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 302)];
+    const unsigned qorig = __float_as_uint(qp.w);
+    if ((int)qorig >= a.n_queries) return;
+    const float qx = qp.x, qy = qp.y, qz = qp.z;
+    const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
+    const int k = a.k;
+    const int rmax = max(max(max(cx, a.X - 1 - cx), max(cy, a.Y - 1 - cy)), max(cz, a.Z - 1 - cz));
+    bool certified = false;
+    for (int r = 0; r <= rmax; ++r) {
+        const int z0 = max(0, cz - r), z1 = min(a.Z - 1, cz + r);
+        const int y0 = max(0, cy - r), y1 = min(a.Y - 1, cy + r);
+        for (int z = z0; z <= z1; ++z) {
+            for (int y = y0; y <= y1; ++y) {
+                const bool shell = (z == cz - r) || (z == cz + r) || (y == cy - r) || (y == cy + r);
+                const int rowc = (z * a.Y + y) * a.X;
+                // the shell row is one contiguous x range; interior rows contribute 2 cells
+                for (int part = 0; part < (shell ? 1 : 2); ++part) {
+                    int xa, xb;
+                    if (shell) { xa = max(0, cx - r); xb = min(a.X - 1, cx + r); }
+                    else if (part == 0) { xa = cx - r; xb = cx - r; }
+                    else { xa = cx + r; xb = cx + r; }
+                    if (xa < 0 || xb > a.X - 1 || xa > xb) continue;
+                    const int p0 = a.cell_start[KN_IDX(rowc + xa, a.X * a.Y * a.Z + 1, 303)];
+                    const int p1 = a.cell_start[KN_IDX(rowc + xb + 1, a.X * a.Y * a.Z + 1, 303)];
+                    for (int p = p0; p < p1; ++p) {
+                        if ((unsigned)p == sidx) continue;
+                        const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
+                        const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
+                        const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                        const unsigned id = __float_as_uint(c.w);
+                        if (top.improves(d2, id)) top.insert(d2, id);
+                    }
+                }
+            }
+        }
+        // stopping rule: distance from q to the outside of the scanned block
+        float m = INFINITY;
+        if (cx - r > 0) m = fminf(m, qx - (g.origin[0] + (cx - r) * g.cell[0]));
+        if (cx + r < a.X - 1) m = fminf(m, g.origin[0] + (cx + r + 1) * g.cell[0] - qx);
+        if (cy - r > 0) m = fminf(m, qy - (g.origin[1] + (cy - r) * g.cell[1]));
+        if (cy + r < a.Y - 1) m = fminf(m, g.origin[1] + (cy + r + 1) * g.cell[1] - qy);
+        if (cz - r > 0) m = fminf(m, qz - (g.origin[2] + (cz - r) * g.cell[2]));
+        if (cz + r < a.Z - 1) m = fminf(m, g.origin[2] + (cz + r + 1) * g.cell[2] - qz);
+        m -= g.eps;
+        const float dK2 = top.dist(k - 1);
+        if (m == INFINITY || (m > 0.f && dK2 <= m * m)) { certified = true; break; }
+    }
+    // the complete box (multi-GPU): the K-th distance must stay inside it
+    const float dK2 = top.dist(k - 1);
+    const float m = fminf(fminf(complete_margin(a.complete, qx, 0), complete_margin(a.complete, qy, 1)),
+                          complete_margin(a.complete, qz, 2)) - g.eps;
+    if (!(m == INFINITY || (m > 0.f && dK2 <= m * m))) certified = false;
+    if (!certified) {
+        const unsigned pos = atomicAdd(a.counters + 1, 1u);
+        if (a.uncert_list) a.uncert_list[KN_IDX(pos, (unsigned)a.n_queries, 306)] = qorig;
+    }
+    const size_t row = (size_t)qorig * (size_t)k;
+    top.emit(k, [&](int j, float d, unsigned i) {
+        const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 305);
+        a.out_idx[o] = (i == SENT) ? SENT : (a.id_map ? a.id_map[KN_IDX(i, (unsigned)a.n, 307)] : i);
+        if (a.out_dist) a.out_dist[o] = d;
+    });
+}
+
 template <int KT>
 __global__ __launch_bounds__(256) void knn_exact_kernel(ExactArgs a) {
     const GridGeom g = *a.geom;
     const int total = a.list ? (int)*a.list_count : a.n;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        const unsigned sidx = a.list ? a.list[t] : (unsigned)t;
-        const float4 qp = a.sorted[sidx];
-        const unsigned qorig = __float_as_uint(qp.w);
-        if ((int)qorig >= a.n_queries) continue;
-        const float qx = qp.x, qy = qp.y, qz = qp.z;
-        const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
-        float dd[KT];
-        unsigned ii[KT];
-#pragma unroll
-        for (int j = 0; j < KT; ++j) { dd[j] = INFINITY; ii[j] = SENT; }
-        const int k = a.k;
-        const int rmax = max(max(max(cx, a.X - 1 - cx), max(cy, a.Y - 1 - cy)), max(cz, a.Z - 1 - cz));
-        bool certified = false;
-        for (int r = 0; r <= rmax; ++r) {
-            const int z0 = max(0, cz - r), z1 = min(a.Z - 1, cz + r);
-            const int y0 = max(0, cy - r), y1 = min(a.Y - 1, cy + r);
-            for (int z = z0; z <= z1; ++z) {
-                for (int y = y0; y <= y1; ++y) {
-                    const bool shell = (z == cz - r) || (z == cz + r) || (y == cy - r) || (y == cy + r);
-                    const int rowc = (z * a.Y + y) * a.X;
-                    // up to two contiguous x ranges
-                    for (int part = 0; part < (shell ? 1 : 2); ++part) {
-                        int xa, xb;
-                        if (shell) { xa = max(0, cx - r); xb = min(a.X - 1, cx + r); }
-                        else if (part == 0) { xa = cx - r; xb = cx - r; }
-                        else { xa = cx + r; xb = cx + r; }
-                        if (xa < 0 || xb > a.X - 1 || xa > xb) continue;
-                        if (!shell && r == 0) continue;
-                        const int p0 = a.cell_start[rowc + xa], p1 = a.cell_start[rowc + xb + 1];
-                        for (int p = p0; p < p1; ++p) {
-                            if ((unsigned)p == sidx) continue;
-                            const float4 c = a.sorted[p];
-                            const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
-                            const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                            const unsigned id = __float_as_uint(c.w);
-                            if (pair_less(d2, id, dd[KT - 1], ii[KT - 1])) {
-#pragma unroll
-                                for (int j = KT - 1; j > 0; --j) {
-                                    const bool before_prev = pair_less(d2, id, dd[j - 1], ii[j - 1]);
-                                    const bool before_cur = pair_less(d2, id, dd[j], ii[j]);
-                                    const float nd = before_prev ? dd[j - 1] : (before_cur ? d2 : dd[j]);
-                                    const unsigned ni = before_prev ? ii[j - 1] : (before_cur ? id : ii[j]);
-                                    dd[j] = nd; ii[j] = ni;
-                                }
-                                if (pair_less(d2, id, dd[0], ii[0])) { dd[0] = d2; ii[0] = id; }
-                            }
-                        }
-                    }
-                }
-            }
-            // stopping rule: distance from q to the outside of the scanned block
-            float m = INFINITY;
-            if (cx - r > 0) m = fminf(m, qx - (g.origin[0] + (cx - r) * g.cell[0]));
-            if (cx + r < a.X - 1) m = fminf(m, g.origin[0] + (cx + r + 1) * g.cell[0] - qx);
-            if (cy - r > 0) m = fminf(m, qy - (g.origin[1] + (cy - r) * g.cell[1]));
-            if (cy + r < a.Y - 1) m = fminf(m, g.origin[1] + (cy + r + 1) * g.cell[1] - qy);
-            if (cz - r > 0) m = fminf(m, qz - (g.origin[2] + (cz - r) * g.cell[2]));
-            if (cz + r < a.Z - 1) m = fminf(m, g.origin[2] + (cz + r + 1) * g.cell[2] - qz);
-            m -= g.eps;
-            float dK2 = INFINITY;
-#pragma unroll
-            for (int j = 0; j < KT; ++j) if (j == k - 1) dK2 = dd[j];
-            if (m == INFINITY || (m > 0.f && dK2 <= m * m)) { certified = true; break; }
-        }
-        // the complete box (multi-GPU): the K-th distance must stay inside it
-        {
-            float dK2 = INFINITY;
-#pragma unroll
-            for (int j = 0; j < KT; ++j) if (j == k - 1) dK2 = dd[j];
-            float m = fminf(fminf(complete_margin(a.complete, qx, 0), complete_margin(a.complete, qy, 1)),
-                            complete_margin(a.complete, qz, 2)) - g.eps;
-            if (!(m == INFINITY || (m > 0.f && dK2 <= m * m))) certified = false;
-            if (!certified) {
-                const unsigned pos = atomicAdd(a.counters + 1, 1u);
-                if (a.uncert_list) a.uncert_list[pos] = qorig;
-            }
-        }
-        const size_t row = (size_t)qorig * (size_t)k;
-#pragma unroll
-        for (int j = 0; j < KT; ++j) {
-            if (j < k) {
-                a.out_idx[row + j] = (ii[j] == SENT) ? SENT : (a.id_map ? a.id_map[ii[j]] : ii[j]);
-                if (a.out_dist) a.out_dist[row + j] = dd[j];
-            }
-        }
+        RegTopK<KT> top;
+        top.init(nullptr);
+        exact_query(a, g, a.list ? a.list[KN_IDX(t, a.n, 301)] : (unsigned)t, top);
+    }
+}
+
+// K > 64: 64-thread workgroups, top-K columns in LDS (KT * 64 * 8 bytes).
+template <int KT>
+__global__ __launch_bounds__(64) void knn_exact_lds_kernel(ExactArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const GridGeom g = *a.geom;
+    const int total = a.list ? (int)*a.list_count : a.n;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        LdsTopK<KT> top;
+        top.init(smem);
+        exact_query(a, g, a.list ? a.list[KN_IDX(t, a.n, 301)] : (unsigned)t, top);
     }
 }
 
@@ -487,8 +556,8 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         static bool attr_set = false;
         if (!attr_set) {
             if constexpr (KT <= 64)
-                hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr_set = true;
         }
         const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
@@ -503,8 +572,14 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     b.list_count = q.counters + 0;
     b.counters = q.counters;
     b.uncert_list = q.uncert_list;
-    const unsigned grid = tiles ? 512u : std::max(1u, std::min(cdiv(q.n, 256), 65535u));
-    knn_exact_kernel<KT><<<grid, 256, 0, s>>>(b);
+    if constexpr (KT <= 64) {
+        const unsigned grid = tiles ? 512u : std::max(1u, std::min(cdiv(q.n, 256), 65535u));
+        knn_exact_kernel<KT><<<grid, 256, 0, s>>>(b);
+    } else {
+        const unsigned grid = tiles ? 2048u : std::max(1u, std::min(cdiv(q.n, 64), 65535u));
+        const size_t lds = (size_t)KT * 64 * 8;
+        knn_exact_lds_kernel<KT><<<grid, 64, lds, s>>>(b);
+    }
     return hipGetLastError();
 }
 
@@ -520,6 +595,8 @@ size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity) {
     b += 16;
     return (b + 15) & ~(size_t)15;
 }
+
+KN_DEFINE_DEBUG_READER(debug_words_query)
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t s) {
     const int k = q.k;
@@ -588,7 +665,7 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
     const double staged = (double)(p.tile[0] + 2 * p.halo) * (p.tile[1] + 2 * p.halo) *
                           (p.tile[2] + 2 * p.halo) * ppc;
     p.lds_capacity = lds_capacity_for(staged);
-    p.lds_bytes = query_lds_bytes(p.tile, p.halo, cap);
+    p.lds_bytes = query_lds_bytes(p.tile, p.halo, p.lds_capacity);
     return p;
 }
 

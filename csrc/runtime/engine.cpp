@@ -68,7 +68,7 @@ kn_status Engine::allocate(int n, const int* dims_override) {
         const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
                               (ap_.tile[2] + 2 * ap_.halo) * ppc;
         ap_.lds_capacity = lds_capacity_for(staged);
-        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, cap);
+        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity);
     }
     const int C = ap_.dims[0] * ap_.dims[1] * ap_.dims[2];
     const size_t nb = scan_block_count(C) + 1;
@@ -232,7 +232,7 @@ kn_status Engine::set_k(int k) {
         const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
                               (ap_.tile[2] + 2 * ap_.halo) * ppc;
         ap_.lds_capacity = lds_capacity_for(staged);
-        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, cap);
+        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity);
     }
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_, (void**)&dist_stored_})
         if (*q) { (void)hipFree(*q); *q = nullptr; }
@@ -274,6 +274,49 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     solved_ = true;
     stored_valid_ = false;
     return KN_OK;
+}
+
+kn_status Engine::launch_graph(int iters) {
+    if (!built_) return fail(KN_ERR_STATE, "launch_graph() before prepare()");
+    kn_status st;
+    if (!graph_) {
+        hipGraph_t g;
+        if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
+        kn_status s1 = build_async();
+        kn_status s2 = query_async();
+        hipError_t e = hipStreamEndCapture(stream_, &g);
+        if (s1 != KN_OK) return s1;
+        if (s2 != KN_OK) return s2;
+        if ((st = check(e, "end capture")) != KN_OK) return st;
+        e = hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if ((st = check(e, "graph instantiate")) != KN_OK) return st;
+    }
+    for (int i = 0; i < iters; ++i)
+        if ((st = check(hipGraphLaunch(graph_, stream_), "graph launch")) != KN_OK) return st;
+    solved_ = true;
+    stored_valid_ = false;
+    return KN_OK;
+}
+
+kn_status Engine::sync() { return check(hipStreamSynchronize(stream_), "stream sync"); }
+
+kn_status Engine::copy_results(unsigned* d_idx, float* d_dist) {
+    if (!solved_) return fail(KN_ERR_STATE, "not solved");
+    const size_t nk = (size_t)n_ * cfg_.k;
+    kn_status st;
+    if (d_idx && nk && (st = check(hipMemcpyAsync(d_idx, out_idx_, nk * 4, hipMemcpyDeviceToDevice, stream_), "D2D idx")) != KN_OK)
+        return st;
+    if (d_dist && out_dist_ && nk &&
+        (st = check(hipMemcpyAsync(d_dist, out_dist_, nk * 4, hipMemcpyDeviceToDevice, stream_), "D2D dist")) != KN_OK)
+        return st;
+    return sync();
+}
+
+kn_status Engine::counters(unsigned out[4]) {
+    kn_status st;
+    if ((st = check(hipMemcpyAsync(out, counters_, 16, hipMemcpyDeviceToHost, stream_), "D2H counters")) != KN_OK) return st;
+    return sync();
 }
 
 unsigned* Engine::d_knn_stored() {

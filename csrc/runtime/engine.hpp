@@ -44,6 +44,12 @@ public:
     kn_status set_k(int k);
     // Capture build+solve into a graph once, then replay it `iters` times (bench path).
     kn_status run_graph(int iters, float* ms_per_iter);
+    // Enqueue `iters` graph replays without waiting (capturing on first use); sync() waits.
+    kn_status launch_graph(int iters);
+    kn_status sync();
+    // Device-to-device copy of the original-space results into caller buffers.
+    kn_status copy_results(unsigned* d_idx, float* d_dist);
+    kn_status counters(unsigned out[4]);
 
     // Host copies (caller frees with free()).
     float* get_points_sorted();            // N x 3

@@ -13,6 +13,9 @@
 
 #include "kn/kernels.h"
 #include "../host/host.hpp"
+#include "../runtime/engine.hpp"
+
+#include <memory>
 
 namespace {
 
@@ -175,6 +178,67 @@ torch::Tensor to_stored_space(torch::Tensor out_orig, torch::Tensor perm) {
     return out;
 }
 
+// ---- native engine (own arena + own stream + hipGraph), the C API's runtime ------------
+class PyEngine {
+public:
+    PyEngine(int64_t k, double ppc, std::vector<int64_t> tile, int64_t halo, bool deterministic, bool use_tiles,
+             bool with_dist, int64_t device) {
+        kn::EngineConfig c;
+        c.k = (int)k;
+        c.points_per_cell = (float)ppc;
+        for (size_t a = 0; a < 3 && a < tile.size(); ++a) c.tile[a] = (int)tile[a];
+        c.halo = (int)halo;
+        c.deterministic = deterministic ? 1 : 0;
+        c.use_tiles = use_tiles ? 1 : 0;
+        c.with_distances = with_dist ? 1 : 0;
+        c.device = (int)device;
+        e_ = std::make_unique<kn::Engine>(c);
+    }
+    void prepare(torch::Tensor points) {
+        check_points(points, true);
+        const c10::DeviceGuard guard(points.device());
+        // the engine's own stream must see the producer's writes
+        KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+        TORCH_CHECK(e_->prepare_device(points.data_ptr<float>(), (int)points.size(0)) == KN_OK, e_->error());
+    }
+    void solve() { TORCH_CHECK(e_->solve() == KN_OK, e_->error()); }
+    void launch_graph(int64_t iters) { TORCH_CHECK(e_->launch_graph((int)iters) == KN_OK, e_->error()); }
+    void sync() { TORCH_CHECK(e_->sync() == KN_OK, e_->error()); }
+    std::vector<torch::Tensor> results(torch::Device dev) {
+        const int64_t n = e_->n(), k = e_->k();
+        auto opt = torch::TensorOptions().device(dev);
+        auto idx = torch::empty({n, k}, opt.dtype(torch::kInt32));
+        auto d2 = torch::empty({n, k}, opt.dtype(torch::kFloat32));
+        TORCH_CHECK(e_->copy_results(reinterpret_cast<unsigned*>(idx.data_ptr<int>()), d2.data_ptr<float>()) == KN_OK,
+                    e_->error());
+        return {idx, d2};
+    }
+    std::vector<int64_t> counters() {
+        unsigned c[4];
+        TORCH_CHECK(e_->counters(c) == KN_OK, e_->error());
+        return {c[0], c[1], c[2], c[3]};
+    }
+    py::dict info() {
+        py::dict d;
+        d["n"] = e_->n();
+        d["k"] = e_->k();
+        d["dims"] = std::vector<int>{e_->dims()[0], e_->dims()[1], e_->dims()[2]};
+        d["ms_build"] = e_->ms_build();
+        d["ms_solve"] = e_->ms_solve();
+        return d;
+    }
+
+private:
+    std::unique_ptr<kn::Engine> e_;
+};
+
+std::vector<int64_t> debug_words(bool reset) {
+    unsigned b[4], q[4];
+    KN_CHECK_HIP(kn::debug_words_build(b, reset));
+    KN_CHECK_HIP(kn::debug_words_query(q, reset));
+    return {b[0], b[1], b[2], b[3], q[0], q[1], q[2], q[3]};
+}
+
 // ---- CPU (host) components ----------------------------------------------------------
 std::vector<torch::Tensor> kdtree_knn(torch::Tensor points, int64_t k, int64_t threads) {
     check_points(points, false);
@@ -257,6 +321,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("query", &query, "k-nearest-neighbour queries on a built grid (GPU)");
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
+    py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")
+        .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t>(), py::arg("k") = 16,
+             py::arg("points_per_cell") = 0.0, py::arg("tile") = std::vector<int64_t>{}, py::arg("halo") = 0,
+             py::arg("deterministic") = true, py::arg("use_tiles") = true, py::arg("with_dist") = true,
+             py::arg("device") = 0)
+        .def("prepare", &PyEngine::prepare)
+        .def("solve", &PyEngine::solve)
+        .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
+        .def("sync", &PyEngine::sync)
+        .def("results", &PyEngine::results)
+        .def("counters", &PyEngine::counters)
+        .def("info", &PyEngine::info);
+    m.def("debug_words", &debug_words, "checked builds: first OOB report {code, index, limit, hi} of build and query kernels",
+          py::arg("reset") = false);
+#if defined(KN_CHECKED) && KN_CHECKED
+    m.attr("CHECKED") = true;
+#else
+    m.attr("CHECKED") = false;
+#endif
     m.def("kdtree_knn", &kdtree_knn, "CPU kd-tree oracle", py::arg("points"), py::arg("k"), py::arg("threads") = 0);
     m.def("brute_knn", &brute_knn, "CPU brute-force oracle", py::arg("points"), py::arg("k"), py::arg("threads") = 0);
     m.def("grid_knn_cpu", &grid_knn_cpu, "CPU grid kNN (engine algorithm on the host)");

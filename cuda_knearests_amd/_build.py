@@ -100,15 +100,22 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
         futs = {}
         for k in KERNELS:
             futs[ex.submit(_compile, k, HIPFLAGS, "hip", force)] = ("kern", k)
+            # bounds-checked variant (KN_CHECKED=1 -> cuda_knearests_amd._C_checked)
+            futs[ex.submit(_compile, k, HIPFLAGS + ["-DKN_CHECKED=1"], "hipchk", force)] = ("kernchk", k)
         for h in HOST:
             futs[ex.submit(_compile, h, HOSTFLAGS, "host", force)] = ("host", h)
         for r in RUNTIME:
             futs[ex.submit(_compile, r, HOSTFLAGS, "rt", force)] = ("rt", r)
         futs[ex.submit(_compile, "torch/bindings.cpp", HOSTFLAGS + tflags + ["-Wno-unused-function"],
                        "torch", force)] = ("torch", "bindings")
+        chk_tflags = [f for f in tflags if not f.startswith("-DTORCH_EXTENSION_NAME")]
+        futs[ex.submit(_compile, "torch/bindings.cpp", HOSTFLAGS + chk_tflags +
+                       ["-Wno-unused-function", "-DTORCH_EXTENSION_NAME=_C_checked", "-DKN_CHECKED=1"],
+                       "torchchk", force)] = ("torchchk", "bindings")
         futs[ex.submit(_compile, "tools/knn_cli.cpp", HOSTFLAGS, "tool", force)] = ("tool", "cli")
         futs[ex.submit(_compile, "tools/knn_unit.cpp", HOSTFLAGS, "tool", force)] = ("tool", "unit")
-        objs: dict[str, list[Path]] = {"kern": [], "host": [], "rt": [], "torch": [], "tool": []}
+        objs: dict[str, list[Path]] = {"kern": [], "kernchk": [], "host": [], "rt": [], "torch": [],
+                                       "torchchk": [], "tool": []}
         tools: dict[str, Path] = {}
         for f in cf.as_completed(futs):
             kind, name = futs[f]
@@ -125,7 +132,10 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
     hiplink = [f"--offload-arch={ARCH}", "-fopenmp", f"-L{ROCM}/lib", "-lamdhip64"]
     _run([HIPCC, "-shared", "-o", str(lib)] + [str(o) for o in kern + host + rt] + hiplink)
     cext = PKG / f"_C{ext}"
-    _run([HIPCC, "-shared", "-o", str(cext)] + [str(o) for o in kern + host + objs["torch"]] + hiplink + tld)
+    _run([HIPCC, "-shared", "-o", str(cext)] + [str(o) for o in kern + host + rt + objs["torch"]] + hiplink + tld)
+    cchk = PKG / f"_C_checked{ext}"
+    _run([HIPCC, "-shared", "-o", str(cchk)] + [str(o) for o in sorted(objs["kernchk"]) + host + rt + objs["torchchk"]]
+         + hiplink + tld)
     bindir = ROOT / "bin"
     bindir.mkdir(exist_ok=True)
     exes = {}
@@ -134,7 +144,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
         _run([HIPCC, "-o", str(exe), str(o), str(lib), f"-Wl,-rpath,{libdir}", f"-Wl,-rpath,$ORIGIN/../cuda_knearests_amd/lib"]
              + hiplink)
         exes[name] = exe
-    res = {"ext": cext, "lib": lib, **{f"bin_{k}": v for k, v in exes.items()}}
+    res = {"ext": cext, "ext_checked": cchk, "lib": lib, **{f"bin_{k}": v for k, v in exes.items()}}
     if verbose:
         for k, v in res.items():
             print(f"[build] {k}: {v}")

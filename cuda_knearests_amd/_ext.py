@@ -23,14 +23,15 @@ def load():
         return _C
     import torch  # noqa: F401  (libtorch / torch's HIP runtime must be loaded first)
 
+    name = "cuda_knearests_amd._C_checked" if os.environ.get("KN_CHECKED") == "1" else "cuda_knearests_amd._C"
     try:
-        _C = importlib.import_module("cuda_knearests_amd._C")
+        _C = importlib.import_module(name)
     except ImportError as e:  # pragma: no cover - exercised only without a build
         if os.environ.get("KN_AUTOBUILD", "1") == "1":
             from . import _build
 
             _build.build(verbose=False)
-            _C = importlib.import_module("cuda_knearests_amd._C")
+            _C = importlib.import_module(name)
         else:
             _ERR = e
             raise RuntimeError(
