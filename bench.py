@@ -64,12 +64,49 @@ def log(msg: str) -> None:
     print(f"[bench {time.perf_counter() - T_START:8.2f}s] {msg}", file=sys.stderr, flush=True)
 
 
+def run_native(args) -> dict:
+    """1 GPU through the native C++ runtime (kn::Engine: own arena, own stream, hipGraph)."""
+    from cuda_knearests_amd._ext import load
+    from cuda_knearests_amd.utils import uniform_cloud
+
+    C = load()
+    dev = torch.device("cuda", 0)
+    pts = uniform_cloud(args.n, seed=args.seed, device=dev)
+    e = C.Engine(args.k, deterministic=not args.nondet)
+    log("native eager prepare+solve")
+    e.prepare(pts)
+    e.solve()
+    info0 = e.info()
+    cnt = e.counters()
+    log(f"eager done: {info0} counters {cnt}")
+    e.launch_graph(args.warmup)
+    e.sync()
+    log("warmup done")
+    t0 = time.perf_counter()
+    e.launch_graph(args.steps)
+    e.sync()
+    dt = time.perf_counter() - t0
+    log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
+    idx, d2 = e.results(dev)
+    chk = brute_check(pts, idx, d2, args.k) if not args.no_check else {}
+    log(f"check {chk}")
+    bts, sts = [], []
+    for _ in range(5):
+        e.prepare(pts)
+        e.solve()
+        i = e.info()
+        bts.append(i["ms_build"])
+        sts.append(i["ms_solve"])
+    bts.sort(), sts.sort()
+    return {"t": dt, "ms_build": bts[2], "ms_solve": sts[2], "info": {"exact_path": cnt[0], "uncertified": cnt[1]},
+            "check": chk, "n_total": args.n}
+
+
 def run_single(args) -> dict:
     from cuda_knearests_amd import KNearests
     from cuda_knearests_amd.utils import uniform_cloud
 
     dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
     pts = uniform_cloud(args.n, seed=args.seed, device=dev)
     kn = KNearests(k=args.k, device=dev, deterministic=not args.nondet)
     log("eager prepare+solve")
@@ -159,6 +196,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--layout", choices=["scattered", "partitioned"], default="scattered")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--path", choices=["native", "torch"], default="native",
+                    help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--nondet", action="store_true")
     args = ap.parse_args()
@@ -182,10 +221,10 @@ def main() -> int:
         extra = {"halo_width": r["stats"].get("halo_width"), "n_halo_rank0": r["stats"].get("n_halo"),
                  "rounds": r["stats"].get("rounds"), "rank_grid": r["stats"].get("grid"), "layout": args.layout}
     else:
-        r = run_single(args)
+        r = run_native(args) if args.path == "native" else run_single(args)
         n_gpus = 1
         extra = {"ms_build": round(r["ms_build"], 4), "ms_solve": round(r["ms_solve"], 4),
-                 "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph}
+                 "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph, "path": args.path}
     ms = r["t"] / args.steps * 1e3
     qps = r["n_total"] * args.steps / r["t"]
     line = {

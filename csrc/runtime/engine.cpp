@@ -199,6 +199,18 @@ kn_status Engine::prepare_device(const float* d_pts, int n) {
     return KN_OK;
 }
 
+kn_status Engine::upload_device(const float* d_pts, int n) {
+    kn_status st;
+    if (!arena_ || n != n_) {
+        if ((st = allocate(n)) != KN_OK) return st;
+    }
+    if (n > 0 && (st = check(hipMemcpyAsync(points_, d_pts, (size_t)n * 12, hipMemcpyDeviceToDevice, stream_),
+                             "D2D points")) != KN_OK)
+        return st;
+    built_ = true;  // the next launch_graph() (or solve after a build) owns the grid
+    return KN_OK;
+}
+
 kn_status Engine::solve() {
     if (!built_) return fail(KN_ERR_STATE, "solve() before prepare()");
     kn_status st;

@@ -40,6 +40,9 @@ public:
     kn_status prepare_host(const float* pts, int n);
     // Build from device points already resident (N x 3 floats). The engine keeps a copy.
     kn_status prepare_device(const float* d_pts, int n);
+    // Copy device points into the arena WITHOUT building (for graph replay: the captured graph
+    // rebuilds the grid itself). Re-plans (and drops the graph) only when n changes.
+    kn_status upload_device(const float* d_pts, int n);
     kn_status solve();
     kn_status set_k(int k);
     // Capture build+solve into a graph once, then replay it `iters` times (bench path).

@@ -201,6 +201,12 @@ public:
         KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
         TORCH_CHECK(e_->prepare_device(points.data_ptr<float>(), (int)points.size(0)) == KN_OK, e_->error());
     }
+    void prepare_async(torch::Tensor points) {
+        check_points(points, true);
+        const c10::DeviceGuard guard(points.device());
+        KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+        TORCH_CHECK(e_->upload_device(points.data_ptr<float>(), (int)points.size(0)) == KN_OK, e_->error());
+    }
     void solve() { TORCH_CHECK(e_->solve() == KN_OK, e_->error()); }
     void launch_graph(int64_t iters) { TORCH_CHECK(e_->launch_graph((int)iters) == KN_OK, e_->error()); }
     void sync() { TORCH_CHECK(e_->sync() == KN_OK, e_->error()); }
@@ -327,6 +333,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              py::arg("deterministic") = true, py::arg("use_tiles") = true, py::arg("with_dist") = true,
              py::arg("device") = 0)
         .def("prepare", &PyEngine::prepare)
+        .def("prepare_async", &PyEngine::prepare_async)
         .def("solve", &PyEngine::solve)
         .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
         .def("sync", &PyEngine::sync)

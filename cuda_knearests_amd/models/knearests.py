@@ -50,7 +50,8 @@ class KNearests:
         self.distances: Optional[torch.Tensor] = None
         self.info: dict = {}
         self.timings = {"ms_build": 0.0, "ms_solve": 0.0}
-        self._graph = None
+        self._graph = None  # native engine (hipGraph) used by step(capture=True)
+        self._graph_n = -1
         self._static = None
 
     # ------------------------------------------------------------------ lifecycle ----
@@ -125,37 +126,33 @@ class KNearests:
 
     # ------------------------------------------------------------- bench fast path ---
     def step(self, points: Optional[torch.Tensor] = None, capture: bool = True):
-        """build + solve on the current stream; with ``capture`` the pair is recorded into a
-        HIP graph on first use and replayed (static input buffer, see ``static_input``)."""
+        """build + solve of the whole cloud.
+
+        ``capture=False``: eager torch ops on the current stream. ``capture=True``: the native
+        C++ runtime (``kn::Engine``: own device arena and stream); build + solve are captured
+        into one hipGraph on first use and replayed on every later call, so a step costs one
+        graph launch instead of ~10 kernel launches. Results land in ``neighbors``/``distances``.
+        """
         if self.device.type == "cpu":
             if points is not None:
                 self.prepare(points)
             return self.solve()
+        pts = self.points if points is None else points
         if not capture:
-            pts = self.points if points is None else points
             g = ops.build_grid(pts, self.k, plan=self.plan(pts.size(0)), deterministic=self.deterministic)
             self.neighbors, self.distances = ops.query(g, self.k, use_tiles=self.use_tiles,
                                                        with_dist=self.with_distances)
             self.grid = g
             return self
-        if self._graph is None:
-            src = self.points if points is None else points
-            self._static = src.clone()
-            plan = self.plan(src.size(0))
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):  # warm-up outside capture (allocator pools)
-                g = ops.build_grid(self._static, self.k, plan=plan, deterministic=self.deterministic)
-                ops.query(g, self.k, use_tiles=self.use_tiles, with_dist=self.with_distances)
-            torch.cuda.current_stream().wait_stream(s)
-            self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph):
-                g = ops.build_grid(self._static, self.k, plan=plan, deterministic=self.deterministic)
-                idx, d2 = ops.query(g, self.k, use_tiles=self.use_tiles, with_dist=self.with_distances)
-            self.grid, self.neighbors, self.distances = g, idx, d2
-        if points is not None and points.data_ptr() != self._static.data_ptr():
-            self._static.copy_(points)
-        self._graph.replay()
+        if self._graph is None or self._graph_n != pts.size(0):
+            self._graph = load().Engine(self.k, self.points_per_cell, list(self.tile), self.halo,
+                                        self.deterministic, self.use_tiles, True, self.device.index or 0)
+            self._graph_n = pts.size(0)
+        # the engine keeps its own copy of the input, so every step re-uploads (D2D) + replays
+        self._graph.prepare_async(pts)
+        self._graph.launch_graph(1)
+        self._graph.sync()
+        self.neighbors, self.distances = self._graph.results(self.device)
         return self
 
     # ------------------------------------------------------------------ getters ------
