@@ -78,6 +78,32 @@ KN_WAVE_REDUCE(wave_max_u32, unsigned, kn_umax)
 KN_WAVE_REDUCE(wave_min_i32, int, kn_imin)
 KN_WAVE_REDUCE(wave_max_i32, int, kn_imax)
 
+// Wave-wide (min(mn), max(mx)) of small ints (|v| < 32767; INT_MAX / INT_MIN sentinels
+// saturate) in ONE reduction: (-mn, mx) packed as two int16 and reduced with v_pk_max_i16.
+// Result is wave-uniform (scalar registers).
+__device__ __forceinline__ unsigned pk_max_i16(unsigned a, unsigned b) {
+    unsigned r;
+    asm("v_pk_max_i16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ int2 wave_minmax_i32(int mn, int mx) {
+    mn = mn < -32767 ? -32767 : (mn > 32767 ? 32767 : mn);
+    mx = mx < -32768 ? -32768 : (mx > 32767 ? 32767 : mx);
+    unsigned v = ((unsigned)(-mn) & 0xFFFFu) | ((unsigned)mx << 16);
+    v = pk_max_i16(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, KN_DPP_QUAD_1032, 0xF, 0xF, false));
+    v = pk_max_i16(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, KN_DPP_QUAD_2301, 0xF, 0xF, false));
+    v = pk_max_i16(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false));
+    v = pk_max_i16(v, (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, KN_DPP_ROW_MIRROR, 0xF, 0xF, false));
+    int lo = -32768, hi = -32768;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const unsigned u = (unsigned)__builtin_amdgcn_readlane((int)v, 16 * r);
+        lo = max(lo, (int)(short)(u & 0xFFFFu));
+        hi = max(hi, (int)(short)(u >> 16));
+    }
+    return make_int2(-lo, hi);
+}
+
 // Inclusive prefix sum over the 64 lanes.
 __device__ __forceinline__ int wave_inclusive_scan_add(int v) {
     const int lane = threadIdx.x & 63;

@@ -83,6 +83,28 @@ __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Packed 32-bit key of one candidate: squared-distance float bits with the low SB mantissa
+// bits replaced by the candidate's LDS slot; the query itself maps to SENT.
+__device__ __forceinline__ unsigned cand_key(const float4& p, float qx, float qy, float qz, unsigned himask,
+                                             int s, int qslot) {
+    const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    const unsigned key = (__float_as_uint(d2) & himask) | (unsigned)s;
+    return (s == qslot) ? SENT : key;
+}
+
+// Sorted-array insertion of `key` into keys[0..KM) (ascending), dropping the largest:
+// new[j] = med3(old[j-1], key, old[j]) -- one v_med3_u32 per slot, all independent. Skipped
+// (uniform branch) when no lane of the wave improves; a non-improving key is a no-op anyway.
+template <int KM>
+__device__ __forceinline__ void topk_push(unsigned (&keys)[KM], unsigned key) {
+    if (__builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
+#pragma unroll
+        for (int j = KM - 1; j > 0; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
+        keys[0] = min(keys[0], key);
+    }
+}
+
 template <int KT, int M>
 __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     constexpr int KM = KT + M;
@@ -174,39 +196,39 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     const unsigned HIMASK = ~MASK;
 
     // ---- 4. query chunks: 64 queries per wave ------------------------------------------
+    // Lanes past the tile's last query duplicate that query (identical candidate tests, so
+    // they never add work to the uniform stream); only lanes < Q are written back.
     for (int chunk = wid; chunk * 64 < Q; chunk += kWaves) {
-        const int qi = chunk * 64 + lane;
-        bool active = qi < Q;
-        int qslot = 0;
-        unsigned qsidx = 0;
-        if (active) {
-            int lo = 0, hi = ntr - 1;
-            while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (qpref[mid] <= qi) lo = mid; else hi = mid - 1; }
-            const int r = (ty0 - sy0 + lo % ntry) + nys * (tz0 - sz0 + lo / ntry);
-            const int off = cb[r * cbs + hx] - cb[r * cbs] + (qi - qpref[lo]);
-            qslot = rowbase[r] + off;
-            qsidx = (unsigned)(cb[r * cbs] + off);
-        }
+        const int qi_raw = chunk * 64 + lane;
+        const bool in_range = qi_raw < Q;
+        const int qi = in_range ? qi_raw : Q - 1;
+        int lo = 0, hi = ntr - 1;
+        while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (qpref[mid] <= qi) lo = mid; else hi = mid - 1; }
+        const int qrow = (ty0 - sy0 + lo % ntry) + nys * (tz0 - sz0 + lo / ntry);
+        const int qoff = cb[qrow * cbs + hx] - cb[qrow * cbs] + (qi - qpref[lo]);
+        const int qslot = rowbase[qrow] + qoff;
+        const unsigned qsidx = (unsigned)(cb[qrow * cbs] + qoff);
         const float4 qp = pts[KN_IDX(qslot, S, 206)];
         const unsigned qorig = __float_as_uint(qp.w);
-        active = active && ((int)qorig < a.n_queries);
+        const bool live = (int)qorig < a.n_queries;  // halo points of a multi-GPU rank are not queries
         const float qx = qp.x, qy = qp.y, qz = qp.z;
         const int cx = cell_coord(g, 0, qx) - sx0;
         const int cy = cell_coord(g, 1, qy) - sy0;
         const int cz = cell_coord(g, 2, qz) - sz0;
-        const int bx0 = wave_min_i32(active ? cx : INT_MAX), bx1 = wave_max_i32(active ? cx : INT_MIN);
-        if (bx0 > bx1) continue;  // no live query in this chunk (uniform)
-        const int by0 = wave_min_i32(active ? cy : INT_MAX), by1 = wave_max_i32(active ? cy : INT_MIN);
-        const int bz0 = wave_min_i32(active ? cz : INT_MAX), bz1 = wave_max_i32(active ? cz : INT_MIN);
-        const int rx0 = max(0, bx0 - a.H), rx1 = min(nxs - 1, bx1 + a.H);
-        const int ry0 = max(0, by0 - a.H), ry1 = min(nys - 1, by1 + a.H);
-        const int rz0 = max(0, bz0 - a.H), rz1 = min(nzs - 1, bz1 + a.H);
+        // wave bounding box of the live queries' cells: 3 packed (-min, max) reductions
+        const int2 bx = wave_minmax_i32(live ? cx : INT_MAX, live ? cx : INT_MIN);
+        if (bx.x > bx.y) continue;  // no live query in this chunk (uniform)
+        const int2 by = wave_minmax_i32(live ? cy : INT_MAX, live ? cy : INT_MIN);
+        const int2 bz = wave_minmax_i32(live ? cz : INT_MAX, live ? cz : INT_MIN);
+        const int rx0 = max(0, bx.x - a.H), rx1 = min(nxs - 1, bx.y + a.H);
+        const int ry0 = max(0, by.x - a.H), ry1 = min(nys - 1, by.y + a.H);
+        const int rz0 = max(0, bz.x - a.H), rz1 = min(nzs - 1, bz.y + a.H);
 
         unsigned keys[KM];
 #pragma unroll
         for (int j = 0; j < KM; ++j) keys[j] = SENT;
 
-        const int zc = (bz0 + bz1) >> 1, yc = (by0 + by1) >> 1;
+        const int zc = (bz.x + bz.y) >> 1, yc = (by.x + by.y) >> 1;
         const int nzt = 2 * max(zc - rz0, rz1 - zc) + 1;
         const int nyt = 2 * max(yc - ry0, ry1 - yc) + 1;
         for (int tz_ = 0; tz_ < nzt; ++tz_) {
@@ -220,69 +242,68 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
                 const float dyz2 = fmaf(dyb, dyb, dz2);
                 const unsigned last = keys[KM - 1];
+                // x-range of cells this lane still needs in row (y,z): |x - qx|^2 < tau - dyz2
                 int lx0 = INT_MAX, lx1 = INT_MIN;
-                if (active) {
-                    if (last == SENT) {
-                        lx0 = rx0; lx1 = rx1;
-                    } else {
-                        const float tau = __uint_as_float(last | MASK);
-                        if (dyz2 <= tau) {
-                            const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
-                            lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
-                            lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
-                        }
+                if (last == SENT) {
+                    lx0 = rx0; lx1 = rx1;
+                } else {
+                    const float tau = __uint_as_float(last | MASK);
+                    if (dyz2 <= tau) {
+                        const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                        lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
+                        lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
                     }
                 }
-                const int X0 = wave_min_i32(lx0);
-                const int X1 = wave_max_i32(lx1);
-                if (X0 > X1) continue;
+                if (!live) { lx0 = INT_MAX; lx1 = INT_MIN; }
+                const int2 X = wave_minmax_i32(lx0, lx1);
+                if (X.x > X.y) continue;
                 const int r = y + nys * z;
                 const int rb = rowbase[r] - cb[r * cbs];
-                const int s0 = rb + cb[r * cbs + X0];
-                const int s1 = KN_IDX(rb + cb[r * cbs + X1 + 1], S + 1, 207);
-                for (int s = s0; s < s1; ++s) {
-                    const float4 p = pts[s];
-                    const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
-                    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                    unsigned key = (__float_as_uint(d2) & HIMASK) | (unsigned)s;
-                    key = (active && s != qslot) ? key : SENT;
-                    if (__builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
-#pragma unroll
-                        for (int j = KM - 1; j > 0; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
-                        keys[0] = min(keys[0], key);
-                    }
+                // uniform bounds -> scalar loop control
+                const int s0 = __builtin_amdgcn_readfirstlane(rb + cb[r * cbs + X.x]);
+                const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + cb[r * cbs + X.y + 1], S + 1, 207));
+                int s = s0;
+                // 4 broadcast LDS reads in flight, then 4 key tests / insertions
+                for (; s + 4 <= s1; s += 4) {
+                    const float4 p0 = pts[s], p1 = pts[s + 1], p2 = pts[s + 2], p3 = pts[s + 3];
+                    const unsigned k0 = cand_key(p0, qx, qy, qz, HIMASK, s, qslot);
+                    const unsigned k1 = cand_key(p1, qx, qy, qz, HIMASK, s + 1, qslot);
+                    const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, s + 2, qslot);
+                    const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, s + 3, qslot);
+                    topk_push<KM>(keys, k0);
+                    topk_push<KM>(keys, k1);
+                    topk_push<KM>(keys, k2);
+                    topk_push<KM>(keys, k3);
                 }
+                for (; s < s1; ++s) topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
             }
         }
-        if (!active) continue;
+        if (!(in_range && live)) continue;
 
-        // ---- exact re-rank of the K+M kept candidates -----------------------------------
+        // ---- exact re-rank of the K+M kept candidates (branch-free) ----------------------
         float dd[KM];
         unsigned ii[KM];
         int nfound = 0;
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
-            if (keys[j] != SENT) {
-                const float4 p = pts[KN_IDX(keys[j] & MASK, (unsigned)S, 208)];
-                const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
-                dd[j] = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                ii[j] = __float_as_uint(p.w);
-                ++nfound;
-            } else {
-                dd[j] = INFINITY;
-                ii[j] = SENT;
-            }
+            const bool valid = keys[j] != SENT;
+            const float4 p = pts[KN_IDX(valid ? (keys[j] & MASK) : 0u, (unsigned)S, 208)];
+            const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+            const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+            dd[j] = valid ? d : INFINITY;
+            ii[j] = valid ? __float_as_uint(p.w) : SENT;
+            nfound += valid ? 1 : 0;
         }
-        // keys are sorted by truncated distance; exact order differs only inside equal
-        // truncation buckets -> two odd-even passes, then verify.
+        // keys are sorted by truncated distance; the exact order differs only inside equal
+        // truncation buckets -> two odd-even passes, then verify (else: exact path).
 #pragma unroll
         for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
             for (int j = pass; j + 1 < KM; j += 2) {
-                if (pair_less(dd[j + 1], ii[j + 1], dd[j], ii[j])) {
-                    const float td = dd[j]; dd[j] = dd[j + 1]; dd[j + 1] = td;
-                    const unsigned ti = ii[j]; ii[j] = ii[j + 1]; ii[j + 1] = ti;
-                }
+                const bool sw = pair_less(dd[j + 1], ii[j + 1], dd[j], ii[j]);
+                const float d0 = sw ? dd[j + 1] : dd[j], d1 = sw ? dd[j] : dd[j + 1];
+                const unsigned i0 = sw ? ii[j + 1] : ii[j], i1 = sw ? ii[j] : ii[j + 1];
+                dd[j] = d0; dd[j + 1] = d1; ii[j] = i0; ii[j + 1] = i1;
             }
         }
         bool ok = true;
@@ -294,7 +315,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 #pragma unroll
         for (int j = 0; j < KM; ++j) if (j == k - 1) dK2 = dd[j];
         const unsigned last = keys[KM - 1];
-        if (last != SENT) ok = ok && (dK2 <= __uint_as_float(last & HIMASK));
+        const bool trunc_ok = (last == SENT) || (dK2 <= __uint_as_float(last & HIMASK));
         // distance to the boundary of the scanned region (grid faces do not count: no points
         // exist beyond the grid) and to the complete box (multi-GPU halo limit)
         float m = INFINITY;
@@ -312,8 +333,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             m = fminf(m, complete_margin(a.complete, qz, 2));
             m -= g.eps;
         }
-        ok = ok && (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
-        if (ok) {
+        const bool geo_ok = (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
+        if (ok && trunc_ok && geo_ok) {
             const size_t row = (size_t)qorig * (size_t)k;
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
@@ -326,6 +347,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         } else {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
             a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx;
+            if (!(ok && trunc_ok)) atomicAdd(a.counters + 3, 1u);  // precision (not geometry) misses
         }
     }
 }
