@@ -35,6 +35,13 @@ struct CompleteBox {
 
 constexpr int kScanItems = 4096;  // elements per scan block (256 threads x 16)
 
+// Query counters (device, zeroed by every launch_query):
+//  [0] queries sent to the exact kernel   [1] uncertified (multi-GPU: K-th leaves complete box)
+//  [2] LDS-overflow (dense) tiles         [3] in-wave exact re-scans (truncation near-ties)
+//  [4] rows streamed (per wave)           [5] candidates streamed (per wave)
+//  [6] insertion networks executed        [7] query chunks (waves x chunk iterations)
+constexpr int kNumCounters = 8;
+
 struct BuildBuffers {
     // inputs
     const float* points;      // N x 3 floats (AoS, 12-byte stride)
@@ -73,12 +80,13 @@ struct QueryBuffers {
     unsigned* out_idx;        // n_queries x k   (row = original index), UINT_MAX = empty
     float* out_dist;          // optional n_queries x k squared distances
     unsigned* fallback_list;  // n   (stored indices of queries needing the exact path)
-    unsigned* counters;       // 4 words: [0] fallback count, [1] uncertified, [2] tile overflow, [3] spare
+    unsigned* counters;       // kNumCounters words, see below
     unsigned* uncert_list;    // optional n_queries: original indices of uncertified queries
     int tile[3];
     int halo;
     int lds_capacity;         // points staged per workgroup (power of two)
     int use_tiles;            // 0: exact ring walk for every query (debug / reference path)
+    int flags;                // 1: force the tile kernel's exact re-scan for every query (tests)
 };
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);

@@ -66,7 +66,10 @@ struct TileArgs {
     int ntx, nty, ntz;
     int cb_stride;  // max staged cells per row + 1
     int max_rows;
+    int flags;      // kQueryForceRescan: every query takes the exact re-scan (tests)
 };
+
+constexpr int kQueryForceRescan = 1;
 
 __device__ __forceinline__ float complete_margin(const CompleteBox& cb, float q, int a) {
     return fminf(q - cb.lo[a], cb.hi[a] - q);
@@ -97,12 +100,14 @@ __device__ __forceinline__ unsigned cand_key(const float4& p, float qx, float qy
 // new[j] = med3(old[j-1], key, old[j]) -- one v_med3_u32 per slot, all independent. Skipped
 // (uniform branch) when no lane of the wave improves; a non-improving key is a no-op anyway.
 template <int KM>
-__device__ __forceinline__ void topk_push(unsigned (&keys)[KM], unsigned key) {
+__device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key) {
     if (__builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
 #pragma unroll
         for (int j = KM - 1; j > 0; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
         keys[0] = min(keys[0], key);
+        return 1u;
     }
+    return 0u;
 }
 
 template <int KT, int M>
@@ -224,45 +229,58 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         const int ry0 = max(0, by.x - a.H), ry1 = min(nys - 1, by.y + a.H);
         const int rz0 = max(0, bz.x - a.H), rz1 = min(nzs - 1, bz.y + a.H);
 
-        unsigned keys[KM];
-#pragma unroll
-        for (int j = 0; j < KM; ++j) keys[j] = SENT;
-
+        // Visit the region's rows centre-out; for each row every live lane derives the x-range of
+        // cells its current bound `tau` still needs (|x - qx|^2 <= tau - dyz^2), the wave takes
+        // the union, and `body(s0, s1)` streams the uniform LDS slot range [s0, s1).
         const int zc = (bz.x + bz.y) >> 1, yc = (by.x + by.y) >> 1;
         const int nzt = 2 * max(zc - rz0, rz1 - zc) + 1;
         const int nyt = 2 * max(yc - ry0, ry1 - yc) + 1;
-        for (int tz_ = 0; tz_ < nzt; ++tz_) {
-            const int z = zc + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
-            if (z < rz0 || z > rz1) continue;
-            const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
-            const float dz2 = dzb * dzb;
-            for (int ty_ = 0; ty_ < nyt; ++ty_) {
-                const int y = yc + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
-                if (y < ry0 || y > ry1) continue;
-                const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
-                const float dyz2 = fmaf(dyb, dyb, dz2);
-                const unsigned last = keys[KM - 1];
-                // x-range of cells this lane still needs in row (y,z): |x - qx|^2 < tau - dyz2
-                int lx0 = INT_MAX, lx1 = INT_MIN;
-                if (last == SENT) {
-                    lx0 = rx0; lx1 = rx1;
-                } else {
-                    const float tau = __uint_as_float(last | MASK);
-                    if (dyz2 <= tau) {
+        auto scan_region = [&](auto&& lane_tau, auto&& body) {
+            for (int tz_ = 0; tz_ < nzt; ++tz_) {
+                const int z = zc + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
+                if (z < rz0 || z > rz1) continue;
+                const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
+                const float dz2 = dzb * dzb;
+                for (int ty_ = 0; ty_ < nyt; ++ty_) {
+                    const int y = yc + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
+                    if (y < ry0 || y > ry1) continue;
+                    const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
+                    const float dyz2 = fmaf(dyb, dyb, dz2);
+                    const float tau = lane_tau();
+                    int lx0 = INT_MAX, lx1 = INT_MIN;
+                    if (tau == INFINITY) {
+                        lx0 = rx0; lx1 = rx1;
+                    } else if (dyz2 <= tau) {
                         const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
                         lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
                         lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
                     }
+                    if (!live) { lx0 = INT_MAX; lx1 = INT_MIN; }
+                    const int2 X = wave_minmax_i32(lx0, lx1);
+                    if (X.x > X.y) continue;
+                    const int r = y + nys * z;
+                    const int rb = rowbase[r] - cb[r * cbs];
+                    // uniform bounds -> scalar loop control
+                    const int s0 = __builtin_amdgcn_readfirstlane(rb + cb[r * cbs + X.x]);
+                    const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + cb[r * cbs + X.y + 1], S + 1, 207));
+                    body(s0, s1);
                 }
-                if (!live) { lx0 = INT_MAX; lx1 = INT_MIN; }
-                const int2 X = wave_minmax_i32(lx0, lx1);
-                if (X.x > X.y) continue;
-                const int r = y + nys * z;
-                const int rb = rowbase[r] - cb[r * cbs];
-                // uniform bounds -> scalar loop control
-                const int s0 = __builtin_amdgcn_readfirstlane(rb + cb[r * cbs + X.x]);
-                const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + cb[r * cbs + X.y + 1], S + 1, 207));
+            }
+        };
+
+        unsigned keys[KM];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) keys[j] = SENT;
+        unsigned st_rows = 0, st_cand = 0, st_ins = 0;  // uniform per-chunk statistics
+        scan_region(
+            [&]() {
+                const unsigned last = keys[KM - 1];
+                return last == SENT ? INFINITY : __uint_as_float(last | MASK);
+            },
+            [&](int s0, int s1) {
                 int s = s0;
+                st_rows += 1u;
+                st_cand += (unsigned)(s1 - s0);
                 // 4 broadcast LDS reads in flight, then 4 key tests / insertions
                 for (; s + 4 <= s1; s += 4) {
                     const float4 p0 = pts[s], p1 = pts[s + 1], p2 = pts[s + 2], p3 = pts[s + 3];
@@ -270,20 +288,23 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const unsigned k1 = cand_key(p1, qx, qy, qz, HIMASK, s + 1, qslot);
                     const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, s + 2, qslot);
                     const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, s + 3, qslot);
-                    topk_push<KM>(keys, k0);
-                    topk_push<KM>(keys, k1);
-                    topk_push<KM>(keys, k2);
-                    topk_push<KM>(keys, k3);
+                    st_ins += topk_push<KM>(keys, k0);
+                    st_ins += topk_push<KM>(keys, k1);
+                    st_ins += topk_push<KM>(keys, k2);
+                    st_ins += topk_push<KM>(keys, k3);
                 }
-                for (; s < s1; ++s) topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
-            }
+                for (; s < s1; ++s) st_ins += topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
+            });
+        if (lane == 0) {  // wave-uniform work statistics (4 atomics per chunk)
+            atomicAdd(a.counters + 4, st_rows);
+            atomicAdd(a.counters + 5, st_cand);
+            atomicAdd(a.counters + 6, st_ins);
+            atomicAdd(a.counters + 7, 1u);
         }
-        if (!(in_range && live)) continue;
 
         // ---- exact re-rank of the K+M kept candidates (branch-free) ----------------------
         float dd[KM];
         unsigned ii[KM];
-        int nfound = 0;
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
             const bool valid = keys[j] != SENT;
@@ -292,30 +313,83 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
             dd[j] = valid ? d : INFINITY;
             ii[j] = valid ? __float_as_uint(p.w) : SENT;
-            nfound += valid ? 1 : 0;
         }
         // keys are sorted by truncated distance; the exact order differs only inside equal
-        // truncation buckets -> two odd-even passes, then verify (else: exact path).
+        // truncation buckets (near-ties: clouds can hold several candidates within 2^-12 of
+        // each other) -> odd-even transposition rounds until no lane of the wave swaps
+        // (almost always one round; bounded by KM, after which the order is exact).
+        for (int round = 0; round < (KM + 1) / 2; ++round) {
+            bool swapped = false;
 #pragma unroll
-        for (int pass = 0; pass < 2; ++pass) {
+            for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-            for (int j = pass; j + 1 < KM; j += 2) {
-                const bool sw = pair_less(dd[j + 1], ii[j + 1], dd[j], ii[j]);
-                const float d0 = sw ? dd[j + 1] : dd[j], d1 = sw ? dd[j] : dd[j + 1];
-                const unsigned i0 = sw ? ii[j + 1] : ii[j], i1 = sw ? ii[j] : ii[j + 1];
-                dd[j] = d0; dd[j + 1] = d1; ii[j] = i0; ii[j + 1] = i1;
+                for (int j = pass; j + 1 < KM; j += 2) {
+                    const bool sw = pair_less(dd[j + 1], ii[j + 1], dd[j], ii[j]);
+                    const float d0 = sw ? dd[j + 1] : dd[j], d1 = sw ? dd[j] : dd[j + 1];
+                    const unsigned i0 = sw ? ii[j + 1] : ii[j], i1 = sw ? ii[j] : ii[j + 1];
+                    dd[j] = d0; dd[j + 1] = d1; ii[j] = i0; ii[j + 1] = i1;
+                    swapped |= sw;
+                }
             }
+            if (!__builtin_amdgcn_ballot_w64(swapped)) break;
         }
-        bool ok = true;
-#pragma unroll
-        for (int j = 0; j + 1 < KM; ++j) ok = ok && !pair_less(dd[j + 1], ii[j + 1], dd[j], ii[j]);
 
         const int k = a.k;
-        float dK2 = INFINITY;
+        auto kth = [&]() {
+            float v = INFINITY;
 #pragma unroll
-        for (int j = 0; j < KM; ++j) if (j == k - 1) dK2 = dd[j];
+            for (int j = 0; j < KM; ++j) if (j == k - 1) v = dd[j];
+            return v;
+        };
+        float dK2 = kth();
+        // Precision check: everything truncated away has key >= last, i.e. exact d2 >= the
+        // floor of last's bucket. If the K-th exact distance reaches into that bucket (K-th and
+        // (K+M)-th candidates within one truncation ulp), redo this query exactly: a second,
+        // uniform pass over the same region with full (d2, id) insertion, bounded by the exact
+        // K-th distance found so far (an upper bound of the true one). Rare: only waves with
+        // such a lane pay for it, instead of a trip through the latency-bound exact kernel.
         const unsigned last = keys[KM - 1];
-        const bool trunc_ok = (last == SENT) || (dK2 <= __uint_as_float(last & HIMASK));
+        const bool need = live && ((last != SENT && !(dK2 <= __uint_as_float(last & HIMASK))) ||
+                                   (a.flags & kQueryForceRescan));
+        if (__builtin_amdgcn_ballot_w64(need)) {
+            const float thr = need ? ((a.flags & kQueryForceRescan) ? INFINITY : dK2) : -1.f;
+            // only the lanes that need it start over; the others keep their (final) lists
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                dd[j] = need ? INFINITY : dd[j];
+                ii[j] = need ? SENT : ii[j];
+            }
+            scan_region([&]() { return thr; },
+                        [&](int s0, int s1) {
+                            for (int s = s0; s < s1; ++s) {
+                                const float4 p = pts[s];
+                                const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+                                const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                                const unsigned id = __float_as_uint(p.w);
+                                const bool take = s != qslot && d2 <= thr && pair_less(d2, id, dd[KM - 1], ii[KM - 1]);
+                                if (__builtin_amdgcn_ballot_w64(take)) {
+                                    if (take) {
+#pragma unroll
+                                        for (int j = KM - 1; j > 0; --j) {
+                                            const bool bp = pair_less(d2, id, dd[j - 1], ii[j - 1]);
+                                            const bool bc = pair_less(d2, id, dd[j], ii[j]);
+                                            const float nd = bp ? dd[j - 1] : (bc ? d2 : dd[j]);
+                                            const unsigned ni = bp ? ii[j - 1] : (bc ? id : ii[j]);
+                                            dd[j] = nd; ii[j] = ni;
+                                        }
+                                        if (pair_less(d2, id, dd[0], ii[0])) { dd[0] = d2; ii[0] = id; }
+                                    }
+                                }
+                            }
+                        });
+            if (need && in_range) atomicAdd(a.counters + 3, 1u);  // precision re-scans (diagnostic)
+            dK2 = kth();
+        }
+        int nfound = 0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) nfound += (ii[j] != SENT) ? 1 : 0;
+        if (!(in_range && live)) continue;
+
         // distance to the boundary of the scanned region (grid faces do not count: no points
         // exist beyond the grid) and to the complete box (multi-GPU halo limit)
         float m = INFINITY;
@@ -334,7 +408,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             m -= g.eps;
         }
         const bool geo_ok = (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
-        if (ok && trunc_ok && geo_ok) {
+        if (geo_ok) {
             const size_t row = (size_t)qorig * (size_t)k;
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
@@ -347,7 +421,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         } else {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
             a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx;
-            if (!(ok && trunc_ok)) atomicAdd(a.counters + 3, 1u);  // precision (not geometry) misses
         }
     }
 }
@@ -553,9 +626,11 @@ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 template <int KT>
 hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
+    // margin slots beyond K: a query is lost to the exact path only if the K-th and (K+M)-th
+    // distances collide within one truncation ulp (~2^-(23-SB)); M=3 makes that ~1e-7/query.
     constexpr int M = 2;
     const int X = q.dims[0], Y = q.dims[1], Z = q.dims[2];
-    hipError_t e = hipMemsetAsync(q.counters, 0, 4 * sizeof(unsigned), s);
+    hipError_t e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     if (q.n == 0 || q.n_queries == 0) return hipSuccess;
     // the register-resident tile path covers K <= 64; larger K use the exact ring walk
@@ -568,6 +643,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.fallback_list = q.fallback_list; a.counters = q.counters;
         a.TX = q.tile[0]; a.TY = q.tile[1]; a.TZ = q.tile[2]; a.H = q.halo;
         a.cap = q.lds_capacity;
+        a.flags = q.flags;
         int sb = 0;
         while ((1 << sb) < q.lds_capacity) ++sb;
         a.slot_bits = sb;

@@ -81,7 +81,7 @@ kn_status Engine::allocate(int n, const int* dims_override) {
     bytes += align_up((size_t)n * sizeof(int2));
     bytes += align_up((size_t)n * sizeof(float4));
     bytes += 2 * align_up((size_t)n * sizeof(unsigned));
-    bytes += align_up(4 * sizeof(unsigned));
+    bytes += align_up(kNumCounters * sizeof(unsigned));
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (bytes > arena_bytes_) {
         if (arena_) (void)hipFree(arena_);
@@ -101,7 +101,7 @@ kn_status Engine::allocate(int n, const int* dims_override) {
     sorted_ = carve<float4>(p, n);
     perm_ = carve<unsigned>(p, n);
     fallback_ = carve<unsigned>(p, n);
-    counters_ = carve<unsigned>(p, 4);
+    counters_ = carve<unsigned>(p, kNumCounters);
     // outputs
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
                      (void**)&dist_stored_})
@@ -220,7 +220,7 @@ kn_status Engine::solve() {
     if ((st = check(hipEventSynchronize(ev_[3]), "solve sync")) != KN_OK) return st;
     (void)hipEventElapsedTime(&ms_solve_, ev_[2], ev_[3]);
     if (cfg_.verbose) {
-        unsigned c[4] = {0, 0, 0, 0};
+        unsigned c[kNumCounters] = {0};
         (void)hipMemcpy(c, counters_, sizeof(c), hipMemcpyDeviceToHost);
         fprintf(stderr, "kn_solve: %.3f msec (exact-path queries %u, uncertified %u, dense tiles %u)\n",
                 ms_solve_, c[0], c[1], c[2]);
@@ -325,9 +325,9 @@ kn_status Engine::copy_results(unsigned* d_idx, float* d_dist) {
     return sync();
 }
 
-kn_status Engine::counters(unsigned out[4]) {
+kn_status Engine::counters(unsigned out[kNumCounters]) {
     kn_status st;
-    if ((st = check(hipMemcpyAsync(out, counters_, 16, hipMemcpyDeviceToHost, stream_), "D2H counters")) != KN_OK) return st;
+    if ((st = check(hipMemcpyAsync(out, counters_, kNumCounters * sizeof(unsigned), hipMemcpyDeviceToHost, stream_), "D2H counters")) != KN_OK) return st;
     return sync();
 }
 
@@ -402,7 +402,7 @@ kn_status Engine::stats(kn_stats* out, std::vector<int>* hist) {
     if ((st = check(launch_cell_stats(cell_start_, C_, cell_count_, H, stream_), "cell stats")) != KN_OK) return st;
     std::vector<int> v(3 + H);
     if ((st = check(hipMemcpyAsync(v.data(), cell_count_, v.size() * sizeof(int), hipMemcpyDeviceToHost, stream_), "D2H")) != KN_OK) return st;
-    unsigned c[4] = {0, 0, 0, 0};
+    unsigned c[kNumCounters] = {0};
     if ((st = check(hipMemcpyAsync(c, counters_, sizeof(c), hipMemcpyDeviceToHost, stream_), "D2H")) != KN_OK) return st;
     if ((st = check(hipStreamSynchronize(stream_), "sync")) != KN_OK) return st;
     std::memset(out, 0, sizeof(*out));

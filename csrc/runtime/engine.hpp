@@ -52,7 +52,7 @@ public:
     kn_status sync();
     // Device-to-device copy of the original-space results into caller buffers.
     kn_status copy_results(unsigned* d_idx, float* d_dist);
-    kn_status counters(unsigned out[4]);
+    kn_status counters(unsigned out[kNumCounters]);
 
     // Host copies (caller frees with free()).
     float* get_points_sorted();            // N x 3

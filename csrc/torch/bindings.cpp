@@ -89,7 +89,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                                  std::vector<int64_t> dims, int64_t k, int64_t n_queries,
                                  c10::optional<torch::Tensor> id_map, std::vector<double> complete,
                                  std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
-                                 bool use_tiles, bool with_dist) {
+                                 bool use_tiles, bool with_dist, int64_t flags) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
@@ -105,7 +105,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     torch::Tensor out_dist;
     if (with_dist) out_dist = torch::empty({n_queries, k}, sorted.options());
     auto fallback = torch::empty({std::max(1, n)}, i32);
-    auto counters = torch::empty({4}, i32);
+    auto counters = torch::empty({kn::kNumCounters}, i32);
     auto uncert = torch::empty({std::max<int64_t>(1, n_queries)}, i32);
     kn::QueryBuffers q{};
     q.sorted = reinterpret_cast<const float4*>(sorted.data_ptr<float>());
@@ -131,13 +131,14 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     q.halo = (int)halo;
     q.lds_capacity = (int)lds_capacity;
     q.use_tiles = use_tiles ? 1 : 0;
+    q.flags = (int)flags;
     TORCH_CHECK(lds_capacity >= 64 && (lds_capacity & (lds_capacity - 1)) == 0 && lds_capacity <= 8192,
                 "lds_capacity must be a power of two in [64, 8192]");
     TORCH_CHECK(kn::query_lds_bytes(q.tile, q.halo, q.lds_capacity) <= 160 * 1024, "tile plan exceeds 160 KiB LDS");
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_query(q, s));
     if (!with_dist) out_dist = torch::empty({0}, sorted.options());
-    return {out_idx, out_dist, counters, uncert};
+    return {out_idx, out_dist, counters, uncert, fallback};
 }
 
 py::dict auto_params(int64_t n, int64_t k, double ppc, std::vector<int64_t> tile, int64_t halo,
@@ -220,9 +221,9 @@ public:
         return {idx, d2};
     }
     std::vector<int64_t> counters() {
-        unsigned c[4];
+        unsigned c[kn::kNumCounters];
         TORCH_CHECK(e_->counters(c) == KN_OK, e_->error());
-        return {c[0], c[1], c[2], c[3]};
+        return std::vector<int64_t>(c, c + kn::kNumCounters);
     }
     py::dict info() {
         py::dict d;
@@ -324,7 +325,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X-native k-nearest-neighbour kernels (gfx950 HIP) and CPU oracles";
     m.def("build", &build, "bin points into the grid (GPU)", py::arg("points"), py::arg("dims"),
           py::arg("deterministic") = true, py::arg("box") = py::none());
-    m.def("query", &query, "k-nearest-neighbour queries on a built grid (GPU)");
+    m.def("query", &query, "k-nearest-neighbour queries on a built grid (GPU)", py::arg("sorted"),
+          py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("k"), py::arg("n_queries"),
+          py::arg("id_map"), py::arg("complete"), py::arg("tile"), py::arg("halo"), py::arg("lds_capacity"),
+          py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")

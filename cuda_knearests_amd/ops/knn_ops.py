@@ -83,7 +83,7 @@ def build_grid(points: torch.Tensor, k: int = 16, plan: Optional[Plan] = None,
 
 def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[torch.Tensor] = None,
           complete: Optional[Sequence[float]] = None, use_tiles: bool = True, with_dist: bool = True,
-          return_info: bool = False):
+          return_info: bool = False, flags: int = 0):
     """kNN of the grid's points (original index < n_queries) against all grid points.
 
     Returns ``(idx, d2)`` (+ ``info`` dict with the device counters and the uncertified
@@ -95,11 +95,12 @@ def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[
     comp = list(complete) if complete is not None else [-INF, -INF, -INF, INF, INF, INF]
     p = grid.plan
     halo, cap = p.halo, p.lds_capacity
-    idx, d2, counters, uncert = load().query(grid.sorted, grid.cell_start, grid.geom, list(p.dims), int(k), nq,
+    idx, d2, counters, uncert, fallback = load().query(grid.sorted, grid.cell_start, grid.geom, list(p.dims), int(k), nq,
                                              id_map, comp, list(p.tile), int(halo), int(cap), bool(use_tiles),
-                                             bool(with_dist))
+                                             bool(with_dist), int(flags))
     if return_info:
-        return idx, (d2 if with_dist else None), {"counters": counters, "uncertified": uncert}
+        return idx, (d2 if with_dist else None), {"counters": counters, "uncertified": uncert,
+                                                  "exact_path": fallback}
     return idx, (d2 if with_dist else None)
 
 

@@ -37,6 +37,17 @@ def test_uniform_tile_vs_oracle(cuda, k):
     _assert_matches_oracle(p, idx, d2, k)
 
 
+@pytest.mark.parametrize("k", [1, 16, 50])
+def test_forced_exact_rescan(cuda, k):
+    # the in-wave exact re-scan normally runs only for truncation near-ties; force it for every
+    # query so the branch is covered (rare data-dependent branches need their test)
+    p = uniform_cloud(20000, seed=200 + k, device=cuda)
+    g = kn.build_grid(p, k)
+    idx, d2, info = kn.query(g, k, return_info=True, flags=1)
+    assert int(info["counters"][3]) == p.size(0)
+    _assert_matches_oracle(p, idx, d2, k)
+
+
 @pytest.mark.parametrize("k", [8, 16, 96, 128])
 def test_exact_path_vs_oracle(cuda, k):
     p = uniform_cloud(20000, seed=100 + k, device=cuda)
