@@ -70,6 +70,11 @@ struct TileArgs {
 };
 
 constexpr int kQueryForceRescan = 1;
+#if defined(KN_CHECKED) && KN_CHECKED
+constexpr bool kStats = true;
+#else
+constexpr bool kStats = false;
+#endif
 
 __device__ __forceinline__ float complete_margin(const CompleteBox& cb, float q, int a) {
     return fminf(q - cb.lo[a], cb.hi[a] - q);
@@ -271,7 +276,9 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         unsigned keys[KM];
 #pragma unroll
         for (int j = 0; j < KM; ++j) keys[j] = SENT;
-        unsigned st_rows = 0, st_cand = 0, st_ins = 0;  // uniform per-chunk statistics
+        // uniform per-chunk work statistics: diagnostics builds only (KN_CHECKED), they cost
+        // SGPRs in the hot loop
+        unsigned st_rows = 0, st_cand = 0, st_ins = 0;
         scan_region(
             [&]() {
                 const unsigned last = keys[KM - 1];
@@ -279,8 +286,10 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             },
             [&](int s0, int s1) {
                 int s = s0;
-                st_rows += 1u;
-                st_cand += (unsigned)(s1 - s0);
+                if constexpr (kStats) {
+                    st_rows += 1u;
+                    st_cand += (unsigned)(s1 - s0);
+                }
                 // 4 broadcast LDS reads in flight, then 4 key tests / insertions
                 for (; s + 4 <= s1; s += 4) {
                     const float4 p0 = pts[s], p1 = pts[s + 1], p2 = pts[s + 2], p3 = pts[s + 3];
@@ -288,14 +297,18 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const unsigned k1 = cand_key(p1, qx, qy, qz, HIMASK, s + 1, qslot);
                     const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, s + 2, qslot);
                     const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, s + 3, qslot);
-                    st_ins += topk_push<KM>(keys, k0);
-                    st_ins += topk_push<KM>(keys, k1);
-                    st_ins += topk_push<KM>(keys, k2);
-                    st_ins += topk_push<KM>(keys, k3);
+                    const unsigned i0 = topk_push<KM>(keys, k0);
+                    const unsigned i1 = topk_push<KM>(keys, k1);
+                    const unsigned i2 = topk_push<KM>(keys, k2);
+                    const unsigned i3 = topk_push<KM>(keys, k3);
+                    if constexpr (kStats) st_ins += i0 + i1 + i2 + i3;
                 }
-                for (; s < s1; ++s) st_ins += topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
+                for (; s < s1; ++s) {
+                    const unsigned i0 = topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
+                    if constexpr (kStats) st_ins += i0;
+                }
             });
-        if (lane == 0) {  // wave-uniform work statistics (4 atomics per chunk)
+        if (kStats && lane == 0) {  // wave-uniform work statistics (4 atomics per chunk)
             atomicAdd(a.counters + 4, st_rows);
             atomicAdd(a.counters + 5, st_cand);
             atomicAdd(a.counters + 6, st_ins);
@@ -604,6 +617,151 @@ __global__ __launch_bounds__(64) void knn_exact_lds_kernel(ExactArgs a) {
     }
 }
 
+// ---- wave-per-query exact kernel (fallback list, K <= 64) ---------------------------------
+// A single lane walking rings issues its global loads one dependent row at a time, so even a
+// handful of fallback queries cost ~200 us of latency (measured). Here one WAVE serves one
+// query: the rows of each Chebyshev shell are dealt to the 64 lanes, every lane keeps a
+// private sorted (d2, id) list of its own candidates, and the wave decides certification by
+// COUNTING (sum over lanes of entries within the scanned-block margin >= K, i.e. the K-th
+// distance is inside). The final K are selected by a wave-wide binary search on the 64-bit
+// (d2 bits, id) key, compacted through LDS and ordered by a 64-lane bitonic sort.
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned x) {
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_ROW_MIRROR, 0xF, 0xF, false);
+    return (unsigned)__builtin_amdgcn_readlane((int)x, 0) + (unsigned)__builtin_amdgcn_readlane((int)x, 16) +
+           (unsigned)__builtin_amdgcn_readlane((int)x, 32) + (unsigned)__builtin_amdgcn_readlane((int)x, 48);
+}
+
+__device__ __forceinline__ unsigned long long pack_key64(float d, unsigned id) {
+    return ((unsigned long long)__float_as_uint(d) << 32) | id;
+}
+
+template <int KT>
+__global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
+    __shared__ unsigned long long s_sel[4][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const GridGeom g = *a.geom;
+    const int total = a.list ? (int)*a.list_count : a.n;
+    const int k = a.k;
+    for (int t = blockIdx.x * 4 + wid; t < total; t += gridDim.x * 4) {
+        const unsigned sidx = (unsigned)__builtin_amdgcn_readfirstlane(
+            (int)(a.list ? a.list[KN_IDX(t, a.n, 301)] : (unsigned)t));
+        const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 302)];
+        const unsigned qorig = __float_as_uint(qp.w);
+        if ((int)qorig >= a.n_queries) continue;
+        const float qx = qp.x, qy = qp.y, qz = qp.z;
+        const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
+        RegTopK<KT> top;
+        top.init(nullptr);
+        const int rmax = max(max(max(cx, a.X - 1 - cx), max(cy, a.Y - 1 - cy)), max(cz, a.Z - 1 - cz));
+        bool certified = false;
+        for (int r = 0; r <= rmax; ++r) {
+            const int z0 = max(0, cz - r), z1 = min(a.Z - 1, cz + r);
+            const int y0 = max(0, cy - r), y1 = min(a.Y - 1, cy + r);
+            const int ny = y1 - y0 + 1, nrows = (z1 - z0 + 1) * ny;
+            for (int tr = lane; tr < nrows; tr += 64) {  // rows of the block dealt to the lanes
+                const int z = z0 + tr / ny, y = y0 + tr % ny;
+                const bool shell = (z == cz - r) || (z == cz + r) || (y == cy - r) || (y == cy + r);
+                const int rowc = (z * a.Y + y) * a.X;
+                for (int part = 0; part < (shell ? 1 : 2); ++part) {
+                    int xa, xb;
+                    if (shell) { xa = max(0, cx - r); xb = min(a.X - 1, cx + r); }
+                    else if (part == 0) { xa = cx - r; xb = cx - r; }
+                    else { xa = cx + r; xb = cx + r; }
+                    if (xa < 0 || xb > a.X - 1 || xa > xb) continue;
+                    const int p0 = a.cell_start[KN_IDX(rowc + xa, a.X * a.Y * a.Z + 1, 303)];
+                    const int p1 = a.cell_start[KN_IDX(rowc + xb + 1, a.X * a.Y * a.Z + 1, 303)];
+                    for (int p = p0; p < p1; ++p) {
+                        if ((unsigned)p == sidx) continue;
+                        const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
+                        const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
+                        const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                        const unsigned id = __float_as_uint(c.w);
+                        if (top.improves(d2, id)) top.insert(d2, id);
+                    }
+                }
+            }
+            float m = INFINITY;
+            if (cx - r > 0) m = fminf(m, qx - (g.origin[0] + (cx - r) * g.cell[0]));
+            if (cx + r < a.X - 1) m = fminf(m, g.origin[0] + (cx + r + 1) * g.cell[0] - qx);
+            if (cy - r > 0) m = fminf(m, qy - (g.origin[1] + (cy - r) * g.cell[1]));
+            if (cy + r < a.Y - 1) m = fminf(m, g.origin[1] + (cy + r + 1) * g.cell[1] - qy);
+            if (cz - r > 0) m = fminf(m, qz - (g.origin[2] + (cz - r) * g.cell[2]));
+            if (cz + r < a.Z - 1) m = fminf(m, g.origin[2] + (cz + r + 1) * g.cell[2] - qz);
+            m -= g.eps;
+            if (m == INFINITY) { certified = true; break; }  // the block covers the whole grid
+            if (m > 0.f) {
+                const float m2 = m * m;
+                unsigned c = 0;
+#pragma unroll
+                for (int j = 0; j < KT; ++j) c += (top.dd[j] <= m2) ? 1u : 0u;
+                if ((int)wave_sum_u32(c) >= k) { certified = true; break; }
+            }
+        }
+        // wave-wide k-th smallest 64-bit key: binary search on the key value
+        unsigned long long lo = 0, hi = ~0ull;
+        unsigned have = 0;
+#pragma unroll
+        for (int j = 0; j < KT; ++j) have += (top.ii[j] != SENT) ? 1u : 0u;
+        const unsigned avail = wave_sum_u32(have);
+        {
+            const unsigned want = min((unsigned)k, avail);
+            if (want == 0) hi = 0;
+            while (lo < hi) {
+                const unsigned long long mid = lo + ((hi - lo) >> 1);
+                unsigned c = 0;
+#pragma unroll
+                for (int j = 0; j < KT; ++j) c += (pack_key64(top.dd[j], top.ii[j]) <= mid) ? 1u : 0u;
+                if (wave_sum_u32(c) >= want) hi = mid; else lo = mid + 1;
+            }
+        }
+        const unsigned long long kth = lo;
+        // compaction: every lane's entries <= kth go to LDS (<= k <= 64 of them in total)
+        unsigned mine = 0;
+#pragma unroll
+        for (int j = 0; j < KT; ++j) mine += (top.ii[j] != SENT && pack_key64(top.dd[j], top.ii[j]) <= kth) ? 1u : 0u;
+        const unsigned incl = (unsigned)wave_inclusive_scan_add((int)mine);
+        const unsigned base = incl - mine;
+        s_sel[wid][lane] = ~0ull;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < KT; ++j)
+            if ((unsigned)j < mine) s_sel[wid][KN_IDX(base + j, 64u, 308)] = pack_key64(top.dd[j], top.ii[j]);
+        __builtin_amdgcn_wave_barrier();
+        unsigned long long v = s_sel[wid][lane];
+        // 64-lane bitonic sort (ascending)
+        for (int size = 2; size <= 64; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const unsigned lo32 = (unsigned)__shfl_xor((int)(unsigned)v, stride, 64);
+                const unsigned hi32 = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), stride, 64);
+                const unsigned long long o = ((unsigned long long)hi32 << 32) | lo32;
+                const bool up = (lane & size) == 0;
+                const bool lower = (lane & stride) == 0;
+                const unsigned long long mn = v < o ? v : o, mx = v < o ? o : v;
+                v = (up == lower) ? mn : mx;
+            }
+        }
+        // certification against the rank's complete box (multi-GPU); needs the k-th distance
+        const float dk = ((int)avail < k) ? INFINITY : __uint_as_float((unsigned)(kth >> 32));
+        const float mc = fminf(fminf(complete_margin(a.complete, qx, 0), complete_margin(a.complete, qy, 1)),
+                               complete_margin(a.complete, qz, 2)) - g.eps;
+        const bool cert = certified && (mc == INFINITY || (mc > 0.f && dk <= mc * mc));
+        if (!cert && lane == 0) {
+            const unsigned pos = atomicAdd(a.counters + 1, 1u);
+            if (a.uncert_list) a.uncert_list[KN_IDX(pos, (unsigned)a.n_queries, 306)] = qorig;
+        }
+        if (lane < k) {
+            const size_t o = KN_IDX((size_t)qorig * (size_t)k + lane, (size_t)a.n_queries * k, 305);
+            const unsigned id = (unsigned)v;
+            const bool empty = (v == ~0ull);
+            a.out_idx[o] = empty ? SENT : (a.id_map ? a.id_map[KN_IDX(id, (unsigned)a.n, 307)] : id);
+            if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
+        }
+    }
+}
+
 __global__ void invert_perm_kernel(const unsigned* __restrict__ perm, int n, unsigned* __restrict__ inv) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) inv[perm[i]] = (unsigned)i;
@@ -671,8 +829,9 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     b.counters = q.counters;
     b.uncert_list = q.uncert_list;
     if constexpr (KT <= 64) {
-        const unsigned grid = tiles ? 512u : std::max(1u, std::min(cdiv(q.n, 256), 65535u));
-        knn_exact_kernel<KT><<<grid, 256, 0, s>>>(b);
+        // one wave per query; the fallback list is short, so 256 workgroups (1024 waves) suffice
+        const unsigned grid = tiles ? 256u : std::max(1u, std::min(cdiv(q.n, 4), 16384u));
+        knn_exact_wave_kernel<KT><<<grid, 256, 0, s>>>(b);
     } else {
         const unsigned grid = tiles ? 2048u : std::max(1u, std::min(cdiv(q.n, 64), 65535u));
         const size_t lds = (size_t)KT * 64 * 8;
