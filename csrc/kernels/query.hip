@@ -92,13 +92,15 @@ __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
 }
 
 // Packed 32-bit key of one candidate: squared-distance float bits with the low SB mantissa
-// bits replaced by the candidate's LDS slot; the query itself maps to SENT.
+// bits replaced by the candidate's LDS slot (one v_bfi_b32).
 __device__ __forceinline__ unsigned cand_key(const float4& p, float qx, float qy, float qz, unsigned himask,
-                                             int s, int qslot) {
+                                             int s, int /*qslot*/) {
     const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
     const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-    const unsigned key = (__float_as_uint(d2) & himask) | (unsigned)s;
-    return (s == qslot) ? SENT : key;
+    unsigned key;
+    // VOP3 reads at most one SGPR on gfx9: keep the (loop-invariant) mask in a VGPR
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(key) : "v"(himask), "v"(__float_as_uint(d2)), "s"((unsigned)s));
+    return key;
 }
 
 // Sorted-array insertion of `key` into keys[0..KM) (ascending), dropping the largest:
@@ -117,7 +119,9 @@ __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key
 
 template <int KT, int M>
 __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
-    constexpr int KM = KT + M;
+    // K + M margin slots + 1: the query itself is not filtered in the hot loop (that cost 3
+    // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
+    constexpr int KM = KT + M + 1;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* pts = reinterpret_cast<float4*>(smem);
     int* cb = reinterpret_cast<int*>(smem + (size_t)a.cap * sizeof(float4));
@@ -297,6 +301,9 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const unsigned k1 = cand_key(p1, qx, qy, qz, HIMASK, s + 1, qslot);
                     const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, s + 2, qslot);
                     const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, s + 3, qslot);
+                    // materialise all four keys before the first (uniform) insertion branch so
+                    // their dependent chains overlap instead of being sunk into the branches
+                    asm volatile("" ::"v"(k0), "v"(k1), "v"(k2), "v"(k3));
                     const unsigned i0 = topk_push<KM>(keys, k0);
                     const unsigned i1 = topk_push<KM>(keys, k1);
                     const unsigned i2 = topk_push<KM>(keys, k2);
@@ -320,7 +327,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         unsigned ii[KM];
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
-            const bool valid = keys[j] != SENT;
+            const bool valid = keys[j] != SENT && (keys[j] & MASK) != (unsigned)qslot;
             const float4 p = pts[KN_IDX(valid ? (keys[j] & MASK) : 0u, (unsigned)S, 208)];
             const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
             const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
