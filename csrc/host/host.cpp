@@ -152,7 +152,7 @@ void grid_knn_cpu(const float* pts, int n, int n_queries, int k, float ppc, cons
                   const float chi[3], uint32_t* idx, float* d2, std::vector<uint32_t>* uncert,
                   int threads) {
     if (n_queries <= 0) return;
-    if (!(ppc > 0.f)) ppc = std::max(3.1f, 0.2f * k);
+    if (!(ppc > 0.f)) ppc = 3.1f;  // same default grid density as the GPU engine
     float lo[3], hi[3];
     for (int a = 0; a < 3; ++a) { lo[a] = std::numeric_limits<float>::infinity(); hi[a] = -lo[a]; }
     for (int i = 0; i < n; ++i)

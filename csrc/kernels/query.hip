@@ -61,7 +61,7 @@ struct TileArgs {
     unsigned* fallback_list;
     unsigned* counters;
     int TX, TY, TZ, H;
-    int cap;        // LDS point capacity (power of two)
+    int cap;        // LDS point capacity (multiple of 64)
     int slot_bits;  // log2(cap)
     int ntx, nty, ntz;
     int cb_stride;  // max staged cells per row + 1
@@ -106,9 +106,12 @@ __device__ __forceinline__ unsigned cand_key(const float4& p, float qx, float qy
 // Sorted-array insertion of `key` into keys[0..KM) (ascending), dropping the largest:
 // new[j] = med3(old[j-1], key, old[j]) -- one v_med3_u32 per slot, all independent. Skipped
 // (uniform branch) when no lane of the wave improves; a non-improving key is a no-op anyway.
+#ifndef KN_BRANCHFREE_INSERT
+#define KN_BRANCHFREE_INSERT 0
+#endif
 template <int KM>
 __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key) {
-    if (__builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
+    if (KN_BRANCHFREE_INSERT || __builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
 #pragma unroll
         for (int j = KM - 1; j > 0; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
         keys[0] = min(keys[0], key);
@@ -893,19 +896,23 @@ hipError_t launch_to_stored_space(const unsigned* out_orig, const unsigned* perm
     return hipGetLastError();
 }
 
-// Expected staged points -> LDS slot capacity (power of two). The staged count of a tile is
-// ~Poisson with mean `staged`; 12% headroom + 64 keeps overflow (-> exact path) negligible for
-// near-uniform clouds while leaving room for 4 workgroups per CU.
+// Expected staged points -> LDS slot capacity (multiple of 64, not necessarily a power of two:
+// the key's slot field is ceil(log2(cap)) bits either way). The staged count of a tile is
+// ~Poisson(staged) (sd = sqrt(staged)); staged + 5 sd + 64 makes an overflow (-> exact path)
+// negligible for near-uniform clouds while keeping the 4x4x4/H2 plan at ~31 KB per workgroup,
+// i.e. 5 workgroups (20 waves) per CU instead of 4 with a power-of-two 2048.
 int lds_capacity_for(double staged) {
-    int cap = 256;
-    while (cap < staged * 1.12 + 64 && cap < 8192) cap <<= 1;
-    return cap;
+    double c = staged + 5.0 * std::sqrt(std::max(staged, 1.0)) + 64.0;
+    int cap = ((int)std::ceil(c) + 63) & ~63;
+    return std::max(128, std::min(cap, 8192));
 }
 
 AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_hint,
                        const float* extent) {
     AutoParams p;
-    if (!(ppc > 0.f)) ppc = std::max(3.1f, 0.2f * (float)k);  // reference density 3.1 (knearests.cu:249)
+    // reference density 3.1 points per cell (knearests.cu:249): measured best for K = 16 and 50
+    // on MI355X (scripts/sweep_tiles.py); larger K widen the halo instead of the cells
+    if (!(ppc > 0.f)) ppc = 3.1f;
     const double cells = std::max(1.0, (double)n / ppc);
     if (extent && extent[0] > 0 && extent[1] > 0 && extent[2] > 0) {
         const double vol = (double)extent[0] * extent[1] * extent[2];

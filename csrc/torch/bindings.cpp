@@ -132,8 +132,8 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     q.lds_capacity = (int)lds_capacity;
     q.use_tiles = use_tiles ? 1 : 0;
     q.flags = (int)flags;
-    TORCH_CHECK(lds_capacity >= 64 && (lds_capacity & (lds_capacity - 1)) == 0 && lds_capacity <= 8192,
-                "lds_capacity must be a power of two in [64, 8192]");
+    TORCH_CHECK(lds_capacity >= 64 && lds_capacity % 64 == 0 && lds_capacity <= 8192,
+                "lds_capacity must be a multiple of 64 in [64, 8192]");
     TORCH_CHECK(kn::query_lds_bytes(q.tile, q.halo, q.lds_capacity) <= 160 * 1024, "tile plan exceeds 160 KiB LDS");
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_query(q, s));

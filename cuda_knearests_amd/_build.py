@@ -151,6 +151,25 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
     return res
 
 
+def build_variant(name: str, hip_flags: list[str], jobs: int = 8) -> Path:
+    """Extension ``cuda_knearests_amd._C_<name>`` with extra kernel compile flags, for in-process
+    A/B timing of kernel variants (scripts/ab_variant.py)."""
+    tflags, tld, ext = _torch_flags()
+    tag = "var_" + name
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        kf = [ex.submit(_compile, k, HIPFLAGS + hip_flags, tag, False) for k in KERNELS]
+        hf = [ex.submit(_compile, h, HOSTFLAGS, "host", False) for h in HOST]
+        rf = [ex.submit(_compile, r, HOSTFLAGS, "rt", False) for r in RUNTIME]
+        base = [f for f in tflags if not f.startswith("-DTORCH_EXTENSION_NAME")]
+        bf = ex.submit(_compile, "torch/bindings.cpp",
+                       HOSTFLAGS + base + ["-Wno-unused-function", f"-DTORCH_EXTENSION_NAME=_C_{name}"], tag, False)
+        objs = [f.result() for f in kf + hf + rf] + [bf.result()]
+    out = PKG / f"_C_{name}{ext}"
+    hiplink = [f"--offload-arch={ARCH}", "-fopenmp", f"-L{ROCM}/lib", "-lamdhip64"]
+    _run([HIPCC, "-shared", "-o", str(out)] + [str(o) for o in objs] + hiplink + tld)
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
