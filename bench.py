@@ -148,6 +148,8 @@ def run_dist(args) -> dict:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+        os.environ.setdefault(key, val)  # --dist without a launcher: a world of one
     dist.init_process_group("nccl", device_id=dev)
     rank, world = dist.get_rank(), dist.get_world_size()
     pts = uniform_cloud(args.n, seed=args.seed + 7919 * rank, device=dev)
@@ -199,6 +201,8 @@ def main() -> int:
     ap.add_argument("--path", choices=["native", "torch"], default="native",
                     help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--dist", action="store_true",
+                    help="use the distributed (routing + RCCL) path even at world size 1")
     ap.add_argument("--nondet", action="store_true")
     args = ap.parse_args()
     if os.environ.get("KN_BENCH_WATCHDOG"):
@@ -213,7 +217,7 @@ def main() -> int:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
                "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29517")] + sys.argv
         return subprocess.call(cmd)
-    if world_env > 1:
+    if world_env > 1 or args.dist:
         r = run_dist(args)
         if r["rank"] != 0:
             return 0

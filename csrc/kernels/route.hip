@@ -1,0 +1,232 @@
+// route.hip -- multi-GPU point routing on gfx950: owner + halo destinations in ONE exchange.
+//
+// NEW component (the reference is single-GPU, knearests.cu has no partitioning). A rank's
+// points go, in one all-to-all-v over RCCL/xGMI, to
+//   * their OWNER (the rank box of the px*py*pz spatial decomposition that contains them), and
+//   * every other rank whose box lies within the halo width h (HALO copies),
+// so redistribution and halo exchange cost a single collective per solve. The send buffer is
+// laid out per destination d as [owned rows for d][halo rows for d], rows are float4
+// {x, y, z, bits(global id)} (16-B aligned, one dwordx4 per row on both sides of the copy).
+//
+// Order is deterministic and stable (by input index) -- no atomics decide positions:
+//   route_count_kernel   : per-block counts of every (destination, kind) column (LDS atomics)
+//   route_scan_kernel    : one workgroup per column, exclusive scan over blocks + column total
+//   route_scatter_kernel : per-wave ballots give in-wave ranks, LDS gives wave offsets
+//   route_unpack_kernel  : received [owned|halo] segments of every source -> owned points first
+//                          (queries), halo after, as (N,3) points + int32 global ids
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kn/route.h"
+#include "kn/wave.h"
+
+namespace kn {
+
+namespace {
+
+constexpr int kRT = 256;                      // threads per routing block
+constexpr int kRounds = kRouteItems / kRT;    // points per thread
+
+__device__ __forceinline__ int route_owner(const RouteParams& p, float x, float y, float z) {
+    const float v[3] = {x, y, z};
+    int c[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        // same operation order as SpatialDecomposition.owner: (p - lo) / ext * g
+        const float f = __fmul_rn(__fdiv_rn(__fsub_rn(v[a], p.lo[a]), p.ext[a]), p.g[a]);
+        int i = (int)floorf(f);
+        i = i < 0 ? 0 : i;
+        c[a] = i > p.grid[a] - 1 ? p.grid[a] - 1 : i;
+    }
+    return c[0] + p.grid[0] * (c[1] + p.grid[1] * c[2]);
+}
+
+// Bit r set: point must be sent to rank r as halo (r != owner, squared distance to r's box
+// within h2). Un-fused arithmetic, same order as SpatialDecomposition.box_dist2.
+__device__ __forceinline__ unsigned long long route_halo(const RouteParams& p, float x, float y, float z,
+                                                         int owner) {
+    unsigned long long m = 0;
+    for (int r = 0; r < p.world; ++r) {
+        if (r == owner) continue;
+        const float dx = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[r][0], x), 0.f), fmaxf(__fsub_rn(x, p.box_hi[r][0]), 0.f));
+        const float dy = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[r][1], y), 0.f), fmaxf(__fsub_rn(y, p.box_hi[r][1]), 0.f));
+        const float dz = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[r][2], z), 0.f), fmaxf(__fsub_rn(z, p.box_hi[r][2]), 0.f));
+        const float d2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+        if (d2 <= p.h2) m |= 1ull << r;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(kRT) void route_count_kernel(const float* __restrict__ pts, int n, RouteParams p,
+                                                          int* __restrict__ block_counts, int nb) {
+    __shared__ int cnt[2 * kRouteMaxWorld];
+    const int cols = 2 * p.world;
+    for (int c = threadIdx.x; c < cols; c += kRT) cnt[c] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
+        if (i < n) {
+            const float x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
+            const int o = route_owner(p, x, y, z);
+            atomicAdd(&cnt[2 * o], 1);
+            unsigned long long m = route_halo(p, x, y, z, o);
+            while (m) {
+                const int d = __builtin_ctzll(m);
+                m &= m - 1;
+                atomicAdd(&cnt[2 * d + 1], 1);
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < cols; c += kRT) block_counts[(size_t)c * nb + blockIdx.x] = cnt[c];
+}
+
+// One workgroup per column: exclusive scan of the column's nb block counts; total -> totals[c].
+__global__ __launch_bounds__(kRT) void route_scan_kernel(int* __restrict__ block_counts, int nb,
+                                                         int* __restrict__ totals) {
+    __shared__ int wsum[kRT / 64];
+    __shared__ int carry_s;
+    int* col = block_counts + (size_t)blockIdx.x * nb;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    for (int base = 0; base < nb; base += kRT) {
+        const int i = base + threadIdx.x;
+        const int v = (i < nb) ? col[i] : 0;
+        const int incl = wave_inclusive_scan_add(v);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        int woff = 0;
+        for (int w = 0; w < wid; ++w) woff += wsum[w];
+        const int carry = carry_s;
+        if (i < nb) col[i] = carry + woff + incl - v;
+        __syncthreads();
+        if (threadIdx.x == kRT - 1) carry_s = carry + woff + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = carry_s;
+}
+
+__global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restrict__ pts,
+                                                            const int* __restrict__ ids, int n, RouteParams p,
+                                                            const int* __restrict__ block_offsets, int nb,
+                                                            const int* __restrict__ totals,
+                                                            float4* __restrict__ send, int send_rows) {
+    __shared__ int base[2 * kRouteMaxWorld];            // block's next row of every column
+    __shared__ int wcnt[kRT / 64][2 * kRouteMaxWorld];  // per-wave counts of the current round
+    const int cols = 2 * p.world;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        int seg = 0;
+        for (int d = 0; d < p.world; ++d) {
+            const int own = totals[2 * d], halo = totals[2 * d + 1];
+            base[2 * d] = seg + block_offsets[(size_t)(2 * d) * nb + blockIdx.x];
+            base[2 * d + 1] = seg + own + block_offsets[(size_t)(2 * d + 1) * nb + blockIdx.x];
+            seg += own + halo;
+        }
+    }
+    __syncthreads();
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int r = 0; r < kRounds; ++r) {
+        const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
+        const bool valid = i < n;
+        float x = 0.f, y = 0.f, z = 0.f;
+        int o = -1;
+        unsigned long long m = 0;
+        if (valid) {
+            x = pts[3 * i]; y = pts[3 * i + 1]; z = pts[3 * i + 2];
+            o = route_owner(p, x, y, z);
+            m = route_halo(p, x, y, z, o);
+        }
+        // phase A: per-wave column counts
+        for (int d = 0; d < p.world; ++d) {
+            const unsigned long long bo = __builtin_amdgcn_ballot_w64(o == d);
+            const unsigned long long bh = __builtin_amdgcn_ballot_w64((m >> d) & 1ull);
+            if (lane == 0) {
+                wcnt[wid][2 * d] = __builtin_popcountll(bo);
+                wcnt[wid][2 * d + 1] = __builtin_popcountll(bh);
+            }
+        }
+        __syncthreads();
+        // phase B: rows (in-wave rank from the ballot, earlier waves from LDS)
+        if (__builtin_amdgcn_ballot_w64(valid)) {
+            const float4 row = make_float4(x, y, z, __int_as_float(valid ? ids[i] : 0));
+            for (int d = 0; d < p.world; ++d) {
+                const bool po = o == d, ph = (m >> d) & 1ull;
+                const unsigned long long bo = __builtin_amdgcn_ballot_w64(po);
+                const unsigned long long bh = __builtin_amdgcn_ballot_w64(ph);
+                if (po || ph) {
+                    const int c = 2 * d + (po ? 0 : 1);
+                    int off = base[c];
+                    for (int w = 0; w < wid; ++w) off += wcnt[w][c];
+                    off += __builtin_popcountll((po ? bo : bh) & lt);
+                    send[KN_IDX(off, send_rows, 401)] = row;
+                }
+            }
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < cols; c += kRT) {
+            int s = 0;
+            for (int w = 0; w < kRT / 64; ++w) s += wcnt[w][c];
+            base[c] += s;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restrict__ recv, int rows, UnpackTable t,
+                                                           float* __restrict__ pts, int* __restrict__ gids) {
+    const int j = blockIdx.x * kRT + threadIdx.x;
+    if (j >= rows) return;
+    int lo = 0, hi = t.world - 1;  // last source whose segment starts at or before j
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (t.seg[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    const int o = j - t.seg[lo];
+    const int out = (o < t.own[lo]) ? t.own_pref[lo] + o : t.n_own + t.halo_pref[lo] + (o - t.own[lo]);
+    const float4 v = recv[j];
+    const int oo = KN_IDX(out, rows, 402);
+    pts[3 * oo] = v.x;
+    pts[3 * oo + 1] = v.y;
+    pts[3 * oo + 2] = v.z;
+    gids[oo] = __float_as_int(v.w);
+}
+
+inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+
+}  // namespace
+
+int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
+
+hipError_t launch_route_count(const float* pts, int n, const RouteParams& p, int* block_counts, int* totals,
+                              hipStream_t s) {
+    if (p.world < 1 || p.world > kRouteMaxWorld) return hipErrorInvalidValue;
+    const int nb = route_block_count(n);
+    route_count_kernel<<<nb, kRT, 0, s>>>(pts, n, p, block_counts, nb);
+    route_scan_kernel<<<2 * p.world, kRT, 0, s>>>(block_counts, nb, totals);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams& p,
+                                const int* block_offsets, const int* totals, float4* send, int send_rows,
+                                hipStream_t s) {
+    if (p.world < 1 || p.world > kRouteMaxWorld) return hipErrorInvalidValue;
+    const int nb = route_block_count(n);
+    if (n > 0)
+        route_scatter_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, block_offsets, nb, totals, send, send_rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_unpack(const float4* recv, int rows, const UnpackTable& t, float* pts, int* gids,
+                               hipStream_t s) {
+    if (t.world < 1 || t.world > kRouteMaxWorld) return hipErrorInvalidValue;
+    if (rows > 0) route_unpack_kernel<<<cdiv(rows, kRT), kRT, 0, s>>>(recv, rows, t, pts, gids);
+    return hipGetLastError();
+}
+
+KN_DEFINE_DEBUG_READER(debug_words_route)
+
+}  // namespace kn

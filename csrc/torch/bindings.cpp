@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "kn/kernels.h"
+#include "kn/route.h"
 #include "../host/host.hpp"
 #include "../runtime/engine.hpp"
 
@@ -179,6 +180,102 @@ torch::Tensor to_stored_space(torch::Tensor out_orig, torch::Tensor perm) {
     return out;
 }
 
+// ---- multi-GPU routing (csrc/kernels/route.hip) -------------------------------------
+kn::RouteParams route_params(const std::vector<double>& lo, const std::vector<double>& hi,
+                             const std::vector<int64_t>& grid, const std::vector<double>& boxes, double h) {
+    TORCH_CHECK(lo.size() == 3 && hi.size() == 3 && grid.size() == 3, "lo/hi/grid must have 3 entries");
+    const int64_t world = grid[0] * grid[1] * grid[2];
+    TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld, "world size must be in [1, 64]");
+    TORCH_CHECK((int64_t)boxes.size() == 6 * world, "boxes must hold 6 floats per rank");
+    kn::RouteParams p{};
+    for (int a = 0; a < 3; ++a) {
+        // float32 arithmetic, exactly as SpatialDecomposition.owner evaluates it
+        const float l = (float)lo[a], u = (float)hi[a];
+        p.lo[a] = l;
+        p.ext[a] = std::max(u - l, 1e-30f);
+        p.g[a] = (float)grid[a];
+        p.grid[a] = (int)grid[a];
+    }
+    p.world = (int)world;
+    const float hf = (float)h;
+    p.h2 = hf * hf;
+    for (int r = 0; r < world; ++r)
+        for (int a = 0; a < 3; ++a) {
+            p.box_lo[r][a] = (float)boxes[6 * r + a];
+            p.box_hi[r][a] = (float)boxes[6 * r + 3 + a];
+        }
+    return p;
+}
+
+// -> (scanned block counts, totals (world, 2) = owned / halo rows per destination)
+std::vector<torch::Tensor> route_count(torch::Tensor points, std::vector<double> lo, std::vector<double> hi,
+                                       std::vector<int64_t> grid, std::vector<double> boxes, double h) {
+    check_points(points, true);
+    const c10::DeviceGuard guard(points.device());
+    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h);
+    const int n = (int)points.size(0);
+    const int nb = kn::route_block_count(n);
+    auto i32 = points.options().dtype(torch::kInt32);
+    auto bc = torch::empty({2 * (int64_t)p.world * nb}, i32);
+    auto totals = torch::empty({(int64_t)p.world, 2}, i32);
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, p, bc.data_ptr<int>(), totals.data_ptr<int>(), s));
+    return {bc, totals};
+}
+
+torch::Tensor route_scatter(torch::Tensor points, torch::Tensor ids, std::vector<double> lo, std::vector<double> hi,
+                            std::vector<int64_t> grid, std::vector<double> boxes, double h, torch::Tensor block_offsets,
+                            torch::Tensor totals, int64_t rows) {
+    check_points(points, true);
+    const c10::DeviceGuard guard(points.device());
+    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h);
+    const int n = (int)points.size(0);
+    TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == torch::kInt32 && ids.numel() == n && ids.is_contiguous(),
+                "ids must be a contiguous int32 GPU tensor of N entries");
+    TORCH_CHECK(block_offsets.numel() == 2 * (int64_t)p.world * kn::route_block_count(n) &&
+                    totals.numel() == 2 * (int64_t)p.world,
+                "block_offsets / totals do not match route_count's output");
+    TORCH_CHECK(rows >= 0, "rows must be >= 0");
+    auto send = torch::empty({rows, 4}, points.options());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), ids.data_ptr<int>(), n, p,
+                                          block_offsets.data_ptr<int>(), totals.data_ptr<int>(),
+                                          reinterpret_cast<float4*>(send.data_ptr<float>()), (int)rows, s));
+    return send;
+}
+
+// recv: rows received from every source, source s = [recv_own[s] owned | recv_halo[s] halo].
+// -> (points (rows, 3): owned of all sources first, then halo; global ids (rows,))
+std::vector<torch::Tensor> route_unpack(torch::Tensor recv, std::vector<int64_t> recv_own, std::vector<int64_t> recv_halo) {
+    TORCH_CHECK(recv.is_cuda() && recv.dim() == 2 && recv.size(1) == 4 && recv.scalar_type() == torch::kFloat32 &&
+                    recv.is_contiguous(),
+                "recv must be a contiguous (R, 4) float32 GPU tensor");
+    const int world = (int)recv_own.size();
+    TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld && (int)recv_halo.size() == world, "bad source table");
+    const c10::DeviceGuard guard(recv.device());
+    kn::UnpackTable t{};
+    t.world = world;
+    int64_t seg = 0, own = 0, halo = 0;
+    for (int s = 0; s < world; ++s) {
+        TORCH_CHECK(recv_own[s] >= 0 && recv_halo[s] >= 0, "negative counts");
+        t.seg[s] = (int)seg;
+        t.own[s] = (int)recv_own[s];
+        t.own_pref[s] = (int)own;
+        t.halo_pref[s] = (int)halo;
+        seg += recv_own[s] + recv_halo[s];
+        own += recv_own[s];
+        halo += recv_halo[s];
+    }
+    t.n_own = (int)own;
+    TORCH_CHECK(seg == recv.size(0), "source table does not add up to the received rows");
+    auto pts = torch::empty({seg, 3}, recv.options());
+    auto gids = torch::empty({seg}, recv.options().dtype(torch::kInt32));
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_unpack(reinterpret_cast<const float4*>(recv.data_ptr<float>()), (int)seg, t,
+                                         pts.data_ptr<float>(), gids.data_ptr<int>(), s));
+    return {pts, gids};
+}
+
 // ---- native engine (own arena + own stream + hipGraph), the C API's runtime ------------
 class PyEngine {
 public:
@@ -240,10 +337,11 @@ private:
 };
 
 std::vector<int64_t> debug_words(bool reset) {
-    unsigned b[4], q[4];
+    unsigned b[4], q[4], r[4];
     KN_CHECK_HIP(kn::debug_words_build(b, reset));
     KN_CHECK_HIP(kn::debug_words_query(q, reset));
-    return {b[0], b[1], b[2], b[3], q[0], q[1], q[2], q[3]};
+    KN_CHECK_HIP(kn::debug_words_route(r, reset));
+    return {b[0], b[1], b[2], b[3], q[0], q[1], q[2], q[3], r[0], r[1], r[2], r[3]};
 }
 
 // ---- CPU (host) components ----------------------------------------------------------
@@ -331,6 +429,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
+    m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts");
+    m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");
+    m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")
         .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t>(), py::arg("k") = 16,
              py::arg("points_per_cell") = 0.0, py::arg("tile") = std::vector<int64_t>{}, py::arg("halo") = 0,

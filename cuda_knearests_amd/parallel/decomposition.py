@@ -88,4 +88,14 @@ class SpatialDecomposition:
         lo_t = torch.tensor(lo, dtype=torch.float32, device=dev)
         hi_t = torch.tensor(hi, dtype=torch.float32, device=dev)
         d = torch.clamp(lo_t - points, min=0) + torch.clamp(points - hi_t, min=0)
-        return (d * d).sum(1)
+        dd = d * d
+        # fixed summation order ((x + y) + z): the native router (route.hip) uses the same
+        return (dd[:, 0] + dd[:, 1]) + dd[:, 2]
+
+    def boxes(self) -> list:
+        """All rank boxes flattened [lo0, lo1, lo2, hi0, hi1, hi2] * world (router input)."""
+        out = []
+        for r in range(self.world):
+            lo, hi = self.rank_box(r)
+            out += list(lo) + list(hi)
+        return out

@@ -1,22 +1,28 @@
-"""Multi-GPU k-nearest neighbours: spatial split + halo exchange over RCCL (NEW component).
+"""Multi-GPU k-nearest neighbours: spatial split + ONE routing all-to-all over RCCL (NEW component).
 
-One process per GPU, ``torch.distributed`` with backend ``"nccl"`` (= RCCL over xGMI on
+The reference is single-GPU (knearests.cu has no streams, devices or collectives).
+Here: one process per GPU, ``torch.distributed`` with backend ``"nccl"`` (= RCCL over xGMI on
 ROCm) or ``"gloo"`` (CPU ranks, used by the tests). Per solve:
 
-1. global domain: one all-reduce of the local bounding boxes (min/max packed in 6 floats);
-2. redistribution: every point goes to the rank whose box contains it -- ONE
-   ``all_to_all_single`` of packed float4 {x, y, z, bits(global id)} rows (counts first);
-3. halo: each owned point within ``h`` of another rank's box is sent to that rank -- ONE
-   more ``all_to_all_single``. ``h`` starts at ``halo_factor`` x the expected K-th neighbour
-   radius of the cloud;
-4. local solve on owned + halo points (GPU: the LDS-tiled HIP kernel; CPU: native grid
-   solver), queries = owned points, ids remapped to global ids on the device, certification
-   against the rank's *complete box* (own box grown by h, unbounded at the domain boundary);
-5. if any rank has an uncertified query (its K-th distance leaves the complete box) the halo
-   is doubled and steps 3-4 are repeated (an all-reduce decides; rare).
+1. **meta** -- one ``all_gather`` of {local bbox, point count} (8 doubles per rank) gives the
+   global domain, the total N (halo width) and every rank's id offset; one host sync.
+2. **route** -- every point is sent to its OWNER rank (the box of a px*py*pz decomposition that
+   contains it) and, as a HALO copy, to every rank whose box is within ``h`` of it, in ONE
+   ``all_to_all_single`` of float4 rows {x, y, z, bits(global id)}. GPU ranks build the send
+   buffer with the native router (``csrc/kernels/route.hip``: per-block counts -> scan ->
+   ballot-ranked scatter, deterministic order); the (owned, halo) counts per destination are
+   exchanged first (a tiny all-to-all, one host sync for both directions' split sizes).
+   ``h`` = ``halo_factor`` x the expected K-th neighbour radius of the whole cloud.
+3. **local solve** on owned + halo points (GPU: grid build over the rank's box + the LDS-tiled
+   HIP query kernel; CPU: the native grid solver). Queries = owned points; neighbour ids are
+   mapped to global ids on the device; every query is certified against the rank's *complete
+   box* (own box grown by h, unbounded on domain faces).
+4. **growth round** (rare): if any rank has an uncertified query (its K-th distance reaches past
+   the complete box) one all-reduce says so, ``h`` doubles and the halo is re-routed.
 
-Messages are few and large (two all-to-alls per solve): xGMI is point-to-point, so one
-all-to-all-v of the whole payload keeps all 7 links of a 2x2x2 decomposition busy at once.
+xGMI is point-to-point: with 2x2x2 ranks every rank neighbours all 7 others, so the single
+all-to-all-v keeps all 7 links busy at once; per step there are 3 small host syncs (meta,
+counts, certification flag) and one bulk collective.
 """
 from __future__ import annotations
 
@@ -25,10 +31,10 @@ from dataclasses import dataclass
 from typing import Optional
 
 import torch
-import torch.distributed as dist
 
 from ..ops import knn_ops as ops
 from .decomposition import SpatialDecomposition
+from .transport import TorchDistTransport
 
 INF = math.inf
 
@@ -41,6 +47,30 @@ def _unpack(rows: torch.Tensor):
     return rows[:, :3].contiguous(), rows[:, 3].contiguous().view(torch.int32)
 
 
+def halo_send_width(h: float, lo, hi) -> float:
+    """Halo width used for SENDING: h plus a slack far above fp32 rounding of the box / distance
+    arithmetic, so every point the receiver's certification (which uses h) relies on is sent."""
+    scale = max(max(abs(v) for v in lo), max(abs(v) for v in hi), max(hi[a] - lo[a] for a in range(3)))
+    return h * (1.0 + 1e-5) + 1e-5 * scale
+
+
+def route_rows_torch(dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor, h_send: float):
+    """Reference router (any device): send rows [owned | halo] per destination + (world, 2) counts.
+    Same decisions and same stable order as the native router (route.hip)."""
+    owner = dec.owner(points)
+    rows = _pack(points, ids)
+    hf = torch.tensor(h_send, dtype=torch.float32, device=points.device)
+    h2 = hf * hf  # fp32 square, as the native router computes it
+    parts, counts = [], []
+    for d in range(dec.world):
+        own_m = owner == d
+        halo_m = (~own_m) & (dec.box_dist2(points, d) <= h2)
+        parts += [rows[own_m], rows[halo_m]]
+        counts.append([int(own_m.sum()), int(halo_m.sum())])
+    send = torch.cat(parts) if parts else rows[:0]
+    return send, torch.tensor(counts, dtype=torch.int32, device=points.device)
+
+
 @dataclass
 class DistResult:
     ids: torch.Tensor        # (n_owned,) global ids of this rank's query points
@@ -51,119 +81,141 @@ class DistResult:
 
 class DistributedKNearests:
     def __init__(self, k: int = 16, group=None, halo_factor: float = 1.6, points_per_cell: float = 0.0,
-                 deterministic: bool = True, max_rounds: int = 8):
+                 deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
+                 transport=None):
         self.k = int(k)
         self.group = group
         self.halo_factor = float(halo_factor)
         self.points_per_cell = float(points_per_cell)
         self.deterministic = deterministic
         self.max_rounds = max_rounds
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        self.native_route = native_route  # None: native router on GPU tensors, torch router on CPU
+        self.comm = transport if transport is not None else TorchDistTransport(group)
+        self.rank = self.comm.rank
+        self.world = self.comm.world
 
     # ------------------------------------------------------------------ helpers ------
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
         out = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
-        dist.all_to_all_single(out, send, recv_counts, send_counts, group=self.group)
+        self.comm.all_to_all_single(out, send, recv_counts, send_counts)
         return out
 
-    def _counts(self, send_counts: torch.Tensor) -> list:
-        recv = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv, send_counts, group=self.group)
-        return recv.tolist()
+    def meta(self, points: torch.Tensor):
+        """One all-gather: global domain (lo, hi) and every rank's point count."""
+        dev = points.device
+        v = torch.empty(8, dtype=torch.float64, device=dev)
+        if points.numel():
+            mn, mx = torch.aminmax(points, dim=0)
+            v[0:3] = mn.double()
+            v[3:6] = mx.double()
+        else:
+            v[0:3] = INF
+            v[3:6] = -INF
+        v[6] = points.size(0)
+        v[7] = 0.0
+        m = torch.stack(self.comm.all_gather(v)).cpu()  # host sync 1
+        lo = tuple(float(x) for x in m[:, 0:3].min(0).values)
+        hi = tuple(float(x) for x in m[:, 3:6].max(0).values)
+        if not all(math.isfinite(x) for x in lo + hi):
+            lo, hi = (0.0, 0.0, 0.0), (1.0, 1.0, 1.0)  # empty global cloud
+        counts = [int(x) for x in m[:, 6]]
+        return lo, hi, counts
 
     def domain(self, points: torch.Tensor):
-        if points.numel():
-            lo, hi = points.min(0).values, points.max(0).values
-        else:
-            lo = torch.full((3,), INF, device=points.device)
-            hi = torch.full((3,), -INF, device=points.device)
-        v = torch.cat([-lo, hi]).float()
-        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=self.group)
-        v = v.tolist()
-        lo = tuple(-x for x in v[:3])
-        hi = tuple(v[3:])
+        lo, hi, _ = self.meta(points)
         return lo, hi
 
-    # ------------------------------------------------------------------- phases ------
-    def redistribute(self, dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor):
-        owner = dec.owner(points)
-        order = torch.argsort(owner, stable=True)
-        counts = torch.bincount(owner, minlength=self.world)
-        rows = _pack(points, ids)[order]
-        recv = self._counts(counts)
-        got = self._a2a(rows, counts.tolist(), recv)
-        return _unpack(got)
+    def _use_native(self, points: torch.Tensor) -> bool:
+        return points.is_cuda if self.native_route is None else bool(self.native_route)
 
-    def halo(self, dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor, h: float):
-        sel, counts = [], []
-        h2 = h * h
-        for r in range(self.world):
-            if r == self.rank:
-                counts.append(0)
-                continue
-            m = torch.nonzero(dec.box_dist2(points, r) <= h2).squeeze(1)
-            sel.append(m)
-            counts.append(int(m.numel()))
-        idx = torch.cat(sel) if sel else torch.empty(0, dtype=torch.long, device=points.device)
-        rows = _pack(points, ids)[idx]
-        recv = self._counts(torch.tensor(counts, dtype=torch.long, device=points.device))
-        got = self._a2a(rows, counts, recv)
-        return _unpack(got)
+    def exchange(self, dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor, h_send: float):
+        """Route points to owner + halo ranks in one all-to-all.
+        Returns (points (n,3) owned-first, global ids (n,), n_owned)."""
+        ids = ids.to(torch.int32).contiguous()
+        if self._use_native(points):
+            C = ops.load()
+            lo, hi = list(dec.lo), list(dec.hi)
+            boxes = dec.boxes()
+            bc, totals = C.route_count(points, lo, hi, list(dec.grid), boxes, float(h_send))
+            recv_tot = torch.empty_like(totals)
+            self.comm.all_to_all_single(recv_tot, totals)
+            both = torch.cat([totals, recv_tot]).cpu()  # host sync 2 (send + receive splits)
+            send_counts = [int(a + b) for a, b in both[: self.world].tolist()]
+            recv_own = [int(a) for a, _ in both[self.world:].tolist()]
+            recv_halo = [int(b) for _, b in both[self.world:].tolist()]
+            send = C.route_scatter(points, ids, lo, hi, list(dec.grid), boxes, float(h_send), bc, totals,
+                                   sum(send_counts))
+            recv = self._a2a(send, send_counts, [a + b for a, b in zip(recv_own, recv_halo)])
+            pts, gids = C.route_unpack(recv, recv_own, recv_halo)
+            return pts, gids, sum(recv_own)
+        send, totals = route_rows_torch(dec, points, ids, h_send)
+        recv_tot = torch.empty_like(totals)
+        self.comm.all_to_all_single(recv_tot, totals)
+        st, rt = totals.tolist(), recv_tot.tolist()
+        recv = self._a2a(send, [a + b for a, b in st], [a + b for a, b in rt])
+        own_parts, halo_parts, off = [], [], 0
+        for a, b in rt:
+            own_parts.append(recv[off:off + a])
+            halo_parts.append(recv[off + a:off + a + b])
+            off += a + b
+        rows = torch.cat(own_parts + halo_parts) if rt else recv
+        pts, gids = _unpack(rows)
+        return pts, gids, sum(a for a, _ in rt)
 
-    def local_solve(self, pts: torch.Tensor, gids: torch.Tensor, n_owned: int, complete: list):
+    def local_solve(self, pts: torch.Tensor, gids: torch.Tensor, n_owned: int, complete: list, box: list):
         if pts.is_cuda:
-            g = ops.build_grid(pts, self.k, points_per_cell=self.points_per_cell,
-                               deterministic=self.deterministic)
+            ext = [box[3] - box[0], box[4] - box[1], box[5] - box[2]]
+            plan = ops.Plan.auto(pts.size(0), self.k, self.points_per_cell, extent=ext)
+            g = ops.build_grid(pts, self.k, plan=plan, deterministic=self.deterministic, box=box)
             idx, d2, info = ops.query(g, self.k, n_queries=n_owned, id_map=gids, complete=complete,
                                       return_info=True)
-            n_unc = int(info["counters"][1].item())
-            return idx, d2, n_unc
+            return idx, d2, info["counters"][1:2].long()
         idx, d2, unc = ops.knn_cpu(pts, self.k, "grid", n_queries=n_owned, complete=complete,
                                    points_per_cell=self.points_per_cell)
         gl = gids.long()
         mapped = torch.where(idx >= 0, gl[idx.clamp(min=0).long()], torch.full_like(gl[:1], -1)).to(torch.int32)
-        return mapped, d2, int(unc.numel())
+        return mapped, d2, torch.tensor([unc.numel()], dtype=torch.long)
 
     # -------------------------------------------------------------------- solve ------
     def solve(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None,
               partitioned: bool = False, domain=None) -> DistResult:
         """kNN of the distributed cloud. ``points``: this rank's (N_r, 3) float32 share (any
-        distribution; ``partitioned=True`` promises they already lie in this rank's box).
-        ``ids``: their global ids (int32); default = rank offset + arange."""
+        distribution; ``partitioned`` is accepted for API compatibility -- points already in
+        this rank's box simply route to itself). ``ids``: their global ids (int32); default =
+        rank offset + arange."""
         points = points.contiguous().float()
         dev = points.device
+        lo, hi, counts = self.meta(points)
+        if domain is not None:
+            lo, hi = tuple(domain[0]), tuple(domain[1])
         if ids is None:
-            n_all = torch.tensor([points.size(0)], dtype=torch.long, device=dev)
-            sizes = [torch.zeros_like(n_all) for _ in range(self.world)]
-            dist.all_gather(sizes, n_all, group=self.group)
-            off = int(sum(int(s.item()) for s in sizes[: self.rank]))
+            off = sum(counts[: self.rank])
             ids = torch.arange(off, off + points.size(0), dtype=torch.int32, device=dev)
-        lo, hi = domain if domain is not None else self.domain(points)
         dec = SpatialDecomposition(self.world, lo, hi)
-        if partitioned:
-            own_pts, own_ids = points, ids.to(torch.int32)
-        else:
-            own_pts, own_ids = self.redistribute(dec, points, ids)
-        n_owned = own_pts.size(0)
-        n_tot = torch.tensor([n_owned], dtype=torch.long, device=dev)
-        dist.all_reduce(n_tot, group=self.group)
+        n_total = sum(counts)
         vol = max(1e-30, (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]))
-        h = self.halo_factor * ops.expected_kth_radius(int(n_tot.item()), self.k, vol)
+        h = self.halo_factor * ops.expected_kth_radius(n_total, self.k, vol)
         diag = math.sqrt(sum((hi[a] - lo[a]) ** 2 for a in range(3)))
+        blo, bhi = dec.rank_box(self.rank)
         rounds = 0
+        src_pts, src_ids = points, ids
         while True:
             rounds += 1
-            hp, hid = self.halo(dec, own_pts, own_ids, h)
-            pts = torch.cat([own_pts, hp])
-            gids = torch.cat([own_ids, hid])
-            complete = dec.complete_box(self.rank, h) if h < diag else [-INF] * 3 + [INF] * 3
-            idx, d2, n_unc = self.local_solve(pts, gids, n_owned, complete)
-            flag = torch.tensor([n_unc], dtype=torch.long, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
-            if int(flag.item()) == 0 or h >= diag or rounds >= self.max_rounds:
+            full = h >= diag
+            hs = halo_send_width(h, lo, hi) if not full else 2.0 * diag + 1.0
+            pts, gids, n_owned = self.exchange(dec, src_pts, src_ids, hs)
+            if rounds == 1:
+                own_pts, own_ids = pts[:n_owned], gids[:n_owned]
+            complete = dec.complete_box(self.rank, h) if not full else [-INF] * 3 + [INF] * 3
+            box = [max(lo[a], blo[a] - hs) for a in range(3)] + [min(hi[a], bhi[a] + hs) for a in range(3)]
+            idx, d2, n_unc = self.local_solve(pts, gids, n_owned, complete, box)
+            flag = n_unc.to(dev) if dev.type != "cpu" else n_unc
+            self.comm.all_reduce_max(flag)
+            if int(flag.item()) == 0 or full or rounds >= self.max_rounds:  # host sync 3
                 break
             h *= 2.0
-        stats = {"n_owned": n_owned, "n_halo": int(hp.size(0)), "halo_width": h, "rounds": rounds,
+            # owned points are in place: re-route them (owner = this rank) for the wider halo
+            src_pts, src_ids = own_pts, own_ids
+        stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
                  "grid": dec.grid}
         return DistResult(own_ids, idx, d2, stats)

@@ -110,3 +110,44 @@ def test_decomposition_factors():
         assert bool(((pts[m] >= torch.tensor(lo)) & (pts[m] <= torch.tensor(hi))).all())
     cb = d.complete_box(0, 10.0)
     assert cb[0] == float("-inf") and cb[3] == 510.0
+
+
+def _loopback_check(world, k, gen, device, native, n=6000, halo_factor=1.6, scatter="mod"):
+    """Run the distributed solve on `world` virtual ranks (threads, LoopbackTransport) and
+    compare the union of the per-rank results with the single-process kd-tree oracle."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+    from cuda_knearests_amd.utils import clustered_cloud, uniform_cloud
+
+    cloud = uniform_cloud(n, 42) if gen == "uniform" else clustered_cloud(n, 43)
+    ids = torch.arange(n, dtype=torch.int32)
+    owner = torch.arange(n) % world if scatter == "mod" else torch.randint(0, world, (n,), generator=torch.Generator().manual_seed(5))
+
+    def fn(t):
+        m = owner == t.rank
+        dk = DistributedKNearests(k=k, halo_factor=halo_factor, transport=t, native_route=native)
+        r = dk.solve(cloud[m].contiguous().to(device), ids[m].contiguous().to(device))
+        return r.ids.cpu(), r.neighbors.cpu(), r.d2.cpu(), r.stats
+
+    out = run_loopback(world, fn)
+    oi, od = kn.knn_cpu(cloud, k, "kdtree")
+    seen = torch.zeros(n, dtype=torch.bool)
+    for ids_r, nb, d2, stats in out:
+        ids_r = ids_r.long()
+        assert not bool(seen[ids_r].any()), "a point is owned by two ranks"
+        seen[ids_r] = True
+        assert torch.equal(d2, od[ids_r]), "distances differ from the oracle"
+        same = (nb.long() == oi[ids_r].long()) | (d2.unsqueeze(-1) == od[ids_r].unsqueeze(-2)).any(-1)
+        assert bool(same.all())
+    assert bool(seen.all()), "some points were lost in routing"
+    return out
+
+
+@pytest.mark.parametrize("world,gen", [(3, "uniform"), (8, "clustered")])
+def test_loopback_cpu_matches_single(world, gen):
+    _loopback_check(world, 8, gen, "cpu", native=False)
+
+
+def test_loopback_cpu_growth_round():
+    out = _loopback_check(4, 16, "uniform", "cpu", native=False, halo_factor=0.05)
+    assert max(s["rounds"] for *_, s in out) > 1

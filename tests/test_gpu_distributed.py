@@ -1,0 +1,78 @@
+"""GPU tests of the multi-GPU path on ONE device:
+* the native router (route.hip) against the torch reference router, bit for bit;
+* the full distributed solve on 2/4/8 virtual ranks (LoopbackTransport threads) with the native
+  router + HIP kernels, against the kd-tree oracle;
+* the RCCL path itself (torch.distributed "nccl", world 1) end to end.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+from cuda_knearests_amd.parallel import SpatialDecomposition, halo_send_width, route_rows_torch
+from cuda_knearests_amd.utils import uniform_cloud
+
+from test_distributed import _loopback_check
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("world,h", [(1, 30.0), (2, 25.0), (8, 40.0), (12, 15.0)])
+def test_native_router_matches_torch(cuda, ext, world, h):
+    n = 50_000
+    p = uniform_cloud(n, seed=world, device=cuda)
+    ids = torch.arange(n, dtype=torch.int32, device=cuda) * 3 + 7
+    lo, hi = (0.0, 0.0, 0.0), (1000.0, 1000.0, 1000.0)
+    dec = SpatialDecomposition(world, lo, hi)
+    hs = halo_send_width(h, lo, hi)
+    ref, cnt = route_rows_torch(dec, p, ids, hs)
+    bc, totals = ext.route_count(p, list(lo), list(hi), list(dec.grid), dec.boxes(), hs)
+    assert torch.equal(totals, cnt)
+    send = ext.route_scatter(p, ids, list(lo), list(hi), list(dec.grid), dec.boxes(), hs, bc, totals, ref.size(0))
+    assert torch.equal(send.view(torch.int32), ref.view(torch.int32))
+    # unpack as if every source sent this buffer: owned rows of all sources first, then halo
+    c = cnt.tolist()
+    own = [a for a, _ in c]
+    halo = [b for _, b in c]
+    pts, gids = ext.route_unpack(send, own, halo)
+    segs, o = [], 0
+    for a, b in c:
+        segs.append((send[o:o + a], send[o + a:o + a + b]))
+        o += a + b
+    exp = torch.cat([s[0] for s in segs] + [s[1] for s in segs])
+    assert torch.equal(pts, exp[:, :3].contiguous())
+    assert torch.equal(gids, exp[:, 3].contiguous().view(torch.int32))
+
+
+@pytest.mark.parametrize("world,k,gen", [(2, 16, "uniform"), (4, 8, "clustered"), (8, 16, "uniform"), (8, 50, "uniform")])
+def test_loopback_gpu_matches_single(cuda, world, k, gen):
+    _loopback_check(world, k, gen, cuda, native=True, n=30000, scatter="random")
+
+
+def test_loopback_gpu_growth_round(cuda):
+    out = _loopback_check(8, 16, "uniform", cuda, native=True, n=20000, halo_factor=0.05)
+    assert max(s["rounds"] for *_, s in out) > 1
+
+
+def test_rccl_world1_end_to_end(cuda):
+    import torch.distributed as dist
+
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    store = dist.TCPStore("127.0.0.1", port, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=cuda)
+    try:
+        p = uniform_cloud(40000, seed=77, device=cuda)
+        r = DistributedKNearests(k=16).solve(p)
+        i, d = kn.knn(p, 16)
+        assert torch.equal(r.ids.long().cpu(), torch.arange(p.size(0)))
+        assert torch.equal(r.d2, d)
+        assert torch.equal(r.neighbors, i)
+    finally:
+        dist.destroy_process_group()
