@@ -7,10 +7,14 @@
 One *step* = the reference's kn_prepare + kn_solve on device-resident points (knearests.cu
 :235-392): bounding box, binning (count/scan/scatter), LDS-tiled kNN of EVERY point,
 exact-path fallback, results in original order with squared distances. On 1 GPU the step
-is replayed from a HIP graph. On N GPUs (weak scaling: N x 900K points, uniform in the
-shared [0,1000]^3 cube, generated independently per rank, i.e. NOT pre-partitioned) a
-step additionally redistributes the points to their spatial owner and exchanges halos with
-RCCL all-to-alls (see cuda_knearests_amd/parallel/distributed.py).
+is replayed from a HIP graph. On N GPUs (weak scaling: N x 900K points, a globally uniform
+cloud of the [0,1000]^3 cube) the BASELINE config is "spatial split + RCCL halo all-to-all":
+with ``--layout partitioned`` (default) rank r holds the uniform points of its own box of the
+decomposition; every step re-derives the global domain (all-gather), classifies EVERY point
+(owner + halo destinations, native router kernel), moves them with one RCCL all-to-all-v,
+then bins and solves owned + halo points. ``--layout scattered`` gives every rank a uniform
+sample of the WHOLE cube instead, so each step also redistributes (N-1)/N of all points
+(see cuda_knearests_amd/parallel/distributed.py).
 
 Timing: W untimed steps, barrier + synchronize, K timed steps, synchronize + barrier; the
 per-rank time is MAX-reduced; rank 0 prints one JSON line. Correctness is spot-checked
@@ -39,19 +43,21 @@ def brute_check(points: torch.Tensor, idx: torch.Tensor, d2: torch.Tensor, k: in
     sel = torch.randperm(nq, generator=g)[: min(nsample, nq)].to(points.device)
     q = (queries if queries is not None else points)[sel]
     bad = 0
-    for c0 in range(0, sel.numel(), 256):
-        qs = q[c0:c0 + 256]
+    # bound the (rows x N) temporaries to ~2e8 elements (multi-GPU clouds reach 10^8 points)
+    step = max(1, min(256, int(2e8) // max(1, points.size(0))))
+    for c0 in range(0, sel.numel(), step):
+        qs = q[c0:c0 + step]
         dx = points[None, :, 0] - qs[:, None, 0]
         dy = points[None, :, 1] - qs[:, None, 1]
         dz = points[None, :, 2] - qs[:, None, 2]
         dd = torch.addcmul(torch.addcmul(dx * dx, dy, dy), dz, dz)
-        self_idx = sel[c0:c0 + 256] if queries is None else None
+        self_idx = sel[c0:c0 + step] if queries is None else None
         if self_idx is not None:
             dd[torch.arange(qs.size(0), device=dd.device), self_idx] = float("inf")
         else:
             dd[dd == 0] = float("inf")  # distributed: exclude self by zero distance (ids differ)
         ref = torch.topk(dd, k, dim=1, largest=False).values
-        got = d2[sel[c0:c0 + 256]]
+        got = d2[sel[c0:c0 + step]]
         # brute force rounds without fma: allow 1e-5 relative
         bad += int(((got - ref).abs() > 1e-5 * ref.abs().clamp(min=1e-6)).any(1).sum())
     return {"checked": int(sel.numel()), "bad_rows": bad}
@@ -152,7 +158,17 @@ def run_dist(args) -> dict:
         os.environ.setdefault(key, val)  # --dist without a launcher: a world of one
     dist.init_process_group("nccl", device_id=dev)
     rank, world = dist.get_rank(), dist.get_world_size()
-    pts = uniform_cloud(args.n, seed=args.seed + 7919 * rank, device=dev)
+    if args.layout == "partitioned":
+        # spatial split: rank r holds a uniform sample of ITS box of the [0,1000]^3 cube (the
+        # decomposition the engine itself derives), i.e. a globally uniform cloud of N x 900K
+        from cuda_knearests_amd.parallel import SpatialDecomposition
+
+        blo, bhi = SpatialDecomposition(world, (0.0,) * 3, (1000.0,) * 3).rank_box(rank)
+        u = uniform_cloud(args.n, seed=args.seed + 7919 * rank, device=dev, lo=0.0, hi=1.0)
+        pts = (u * torch.tensor([bhi[a] - blo[a] for a in range(3)], device=dev)
+               + torch.tensor(blo, device=dev)).contiguous()
+    else:
+        pts = uniform_cloud(args.n, seed=args.seed + 7919 * rank, device=dev)
     dk = DistributedKNearests(k=args.k)
     res = None
     for _ in range(args.warmup):
@@ -196,7 +212,7 @@ def main() -> int:
     ap.add_argument("--n", type=int, default=900_000, help="points per GPU")
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--layout", choices=["scattered", "partitioned"], default="scattered")
+    ap.add_argument("--layout", choices=["scattered", "partitioned"], default="partitioned")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--path", choices=["native", "torch"], default="native",
                     help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
@@ -234,7 +250,8 @@ def main() -> int:
     line = {
         "metric": METRIC, "value": qps, "unit": "queries/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic uniform random [0,1000]^3 (seeded per rank)",
+        "vs_baseline": None, "dtype": "fp32", "data": ("synthetic uniform random [0,1000]^3 (seeded per rank" +
+                 (f", {args.layout} layout)" if n_gpus > 1 or args.dist else ")")),
         "config": {"model": f"uniform-grid kNN, {args.n} pts/GPU, k={args.k}", "global_batch": r["n_total"],
                    "seq_len": args.k, "parallelism": f"spatial{n_gpus}" if n_gpus > 1 else "single"},
         "vs_cpu_oracle": qps / CPU_ORACLE_QPS, "check": r.get("check", {}), **extra,

@@ -44,6 +44,9 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
                                 hipStream_t s);
 hipError_t launch_route_unpack(const float4* recv, int rows, const UnpackTable& t, float* pts, int* gids,
                                hipStream_t s);
+// Local meta of a rank's share: out = {lo[3], hi[3], n, 0} (doubles; +-inf box when n == 0).
+// words: 8 scratch words. One all_gather of `out` gives the global domain and the id offsets.
+hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* out, hipStream_t s);
 hipError_t debug_words_route(unsigned out[4], bool reset);
 
 }  // namespace kn

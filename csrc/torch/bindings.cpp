@@ -276,6 +276,18 @@ std::vector<torch::Tensor> route_unpack(torch::Tensor recv, std::vector<int64_t>
     return {pts, gids};
 }
 
+// -> (8,) float64 {lo[3], hi[3], n, 0} of this rank's points (one kernel pass, no host sync)
+torch::Tensor local_meta(torch::Tensor points) {
+    check_points(points, true);
+    const c10::DeviceGuard guard(points.device());
+    auto words = torch::empty({8}, points.options().dtype(torch::kInt32));
+    auto out = torch::empty({8}, points.options().dtype(torch::kFloat64));
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_local_meta(points.data_ptr<float>(), (int)points.size(0),
+                                       reinterpret_cast<unsigned*>(words.data_ptr<int>()), out.data_ptr<double>(), s));
+    return out;
+}
+
 // ---- native engine (own arena + own stream + hipGraph), the C API's runtime ------------
 class PyEngine {
 public:
@@ -429,6 +441,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
+    m.def("local_meta", &local_meta, "multi-GPU: {lo[3], hi[3], n, 0} of the local points (float64, on device)");
     m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");

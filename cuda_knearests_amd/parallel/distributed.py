@@ -102,17 +102,19 @@ class DistributedKNearests:
 
     def meta(self, points: torch.Tensor):
         """One all-gather: global domain (lo, hi) and every rank's point count."""
-        dev = points.device
-        v = torch.empty(8, dtype=torch.float64, device=dev)
-        if points.numel():
-            mn, mx = torch.aminmax(points, dim=0)
-            v[0:3] = mn.double()
-            v[3:6] = mx.double()
+        if points.is_cuda:
+            v = ops.load().local_meta(points)  # native bbox pass, stays on the device
         else:
-            v[0:3] = INF
-            v[3:6] = -INF
-        v[6] = points.size(0)
-        v[7] = 0.0
+            v = torch.empty(8, dtype=torch.float64)
+            if points.numel():
+                mn, mx = torch.aminmax(points, dim=0)
+                v[0:3] = mn.double()
+                v[3:6] = mx.double()
+            else:
+                v[0:3] = INF
+                v[3:6] = -INF
+            v[6] = points.size(0)
+            v[7] = 0.0
         m = torch.stack(self.comm.all_gather(v)).cpu()  # host sync 1
         lo = tuple(float(x) for x in m[:, 0:3].min(0).values)
         hi = tuple(float(x) for x in m[:, 3:6].max(0).values)

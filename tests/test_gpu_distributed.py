@@ -76,3 +76,17 @@ def test_rccl_world1_end_to_end(cuda):
         assert torch.equal(r.neighbors, i)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [0, 1, 777, 300_000])
+def test_local_meta_matches_torch(cuda, ext, n):
+    p = uniform_cloud(n, seed=n, device=cuda, lo=-250.0, hi=640.0)
+    v = ext.local_meta(p).cpu()
+    assert v.dtype == torch.float64 and v.numel() == 8
+    assert v[6].item() == n and v[7].item() == 0.0
+    if n == 0:
+        assert torch.isinf(v[:3]).all() and (v[:3] > 0).all() and (v[3:6] < 0).all()
+        return
+    mn, mx = torch.aminmax(p, dim=0)
+    assert torch.equal(v[:3], mn.double().cpu())
+    assert torch.equal(v[3:6], mx.double().cpu())
