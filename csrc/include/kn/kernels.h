@@ -86,7 +86,8 @@ struct QueryBuffers {
     int halo;
     int lds_capacity;         // points staged per workgroup (power of two)
     int use_tiles;            // 0: exact ring walk for every query (debug / reference path)
-    int flags;                // 1: force the tile kernel's exact re-scan for every query (tests)
+    int flags;                // 1: force the exact re-scan for every query (tests); 2: stream kernel;
+                              // 4: LDS-staged tile kernel (neither: env KN_QUERY_ALGO / default)
 };
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);

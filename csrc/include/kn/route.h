@@ -19,9 +19,15 @@ struct RouteParams {
     int grid[3];
     int world;      // px * py * pz <= kRouteMaxWorld
     float h2;       // squared halo send width
-    float box_lo[kRouteMaxWorld][3];  // rank boxes (host-computed, same as SpatialDecomposition)
+    int id_offset;  // global id of this rank's first point (route_scatter with ids == nullptr)
+    float box_lo[kRouteMaxWorld][3];  // rank boxes (same formula as SpatialDecomposition.rank_box)
     float box_hi[kRouteMaxWorld][3];
 };
+
+// Device-side plan header (doubles) written by launch_route_plan for the host's one sync:
+constexpr int kPlanHdr = 16;
+// [0..2] global lo  [3..5] global hi  [6] h (certification halo)  [7] h_send  [8] n_total
+// [9] id offset of this rank  [10] 1 if the halo covers the whole domain  [11] domain diagonal
 
 // Receive-side table: source s's segment starts at seg[s], holds own[s] owned rows then its
 // halo rows; owned rows of all sources go first (own_pref), then halo rows (halo_pref).
@@ -35,15 +41,24 @@ struct UnpackTable {
 };
 
 int route_block_count(int n);
+// Every launcher reads the routing parameters from DEVICE memory (`p`), so the whole
+// meta -> plan -> count chain is enqueued without a host round trip. `world` = p->world.
 // block_counts: 2*world*route_block_count(n) ints (column-major, scanned in place);
 // totals: 2*world ints = (owned, halo) rows per destination.
-hipError_t launch_route_count(const float* pts, int n, const RouteParams& p, int* block_counts, int* totals,
-                              hipStream_t s);
-hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams& p,
+hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int world, int* block_counts,
+                              int* totals, hipStream_t s);
+// ids == nullptr: global id = p->id_offset + local index
+hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams* p, int world,
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
                                 hipStream_t s);
 hipError_t launch_route_unpack(const float4* recv, int rows, const UnpackTable& t, float* pts, int* gids,
                                hipStream_t s);
+// metas: world x 8 doubles (every rank's launch_local_meta output, all-gathered on device).
+// Writes the RouteParams for decomposition `grid` (px*py*pz == world) and the plan header:
+// global domain, h = halo_factor x expected K-th neighbour radius of the whole cloud, the
+// send width (h plus rounding slack; the whole domain once h reaches its diagonal), id offset.
+hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
+                             double halo_factor, RouteParams* p, double* hdr, hipStream_t s);
 // Local meta of a rank's share: out = {lo[3], hi[3], n, 0} (doubles; +-inf box when n == 0).
 // words: 8 scratch words. One all_gather of `out` gives the global domain and the id offsets.
 hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* out, hipStream_t s);

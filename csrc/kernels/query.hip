@@ -34,6 +34,8 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 
 #include "kn/kernels.h"
 #include "kn/wave.h"
@@ -69,7 +71,18 @@ struct TileArgs {
     int flags;      // kQueryForceRescan: every query takes the exact re-scan (tests)
 };
 
+#ifndef KN_STAGE_ROWS
+#define KN_STAGE_ROWS 0
+#endif
+#ifndef KN_YPRUNE
+#define KN_YPRUNE 1
+#endif
+#ifndef KN_LDS_PIPE
+#define KN_LDS_PIPE 1
+#endif
 constexpr int kQueryForceRescan = 1;
+constexpr int kQueryAlgoStream = 2;
+constexpr int kQueryAlgoTile = 4;
 #if defined(KN_CHECKED) && KN_CHECKED
 constexpr bool kStats = true;
 #else
@@ -200,12 +213,38 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         if (threadIdx.x == 0) atomicAdd(a.counters + 2, 1u);
         return;
     }
+#if KN_STAGE_ROWS
+    // ---- 3. stage the points: rows round-robin over the waves, lanes = points of a row,
+    //         4 rows' 16-B loads in flight per wave (no per-point row search) -------------
+    for (int r0 = wid; r0 < nrows; r0 += 4 * kWaves) {
+        float4 v[4];
+        int dst[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int r = r0 + u * kWaves;
+            const int len = r < nrows ? rowbase[r + 1] - rowbase[r] : 0;
+            dst[u] = lane < len ? rowbase[r] + lane : -1;
+            if (dst[u] >= 0) v[u] = a.sorted[KN_IDX(cb[r * cbs] + lane, a.n, 202)];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (dst[u] >= 0) pts[KN_IDX(dst[u], a.cap, 203)] = v[u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // rows longer than a wave (dense tiles)
+            const int r = r0 + u * kWaves;
+            const int len = r < nrows ? rowbase[r + 1] - rowbase[r] : 0;
+            for (int i = lane + 64; i < len; i += 64)
+                pts[KN_IDX(rowbase[r] + i, a.cap, 203)] = a.sorted[KN_IDX(cb[r * cbs] + i, a.n, 202)];
+        }
+    }
+#else
     // ---- 3. stage the points (16-B coalesced loads, row found by binary search) --------
     for (int s = threadIdx.x; s < S; s += kWG) {
         int lo = 0, hi = nrows - 1;
         while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rowbase[mid] <= s) lo = mid; else hi = mid - 1; }
         pts[KN_IDX(s, a.cap, 203)] = a.sorted[KN_IDX(cb[lo * cbs] + (s - rowbase[lo]), a.n, 202)];
     }
+#endif
     __syncthreads();
     (void)misc;
 
@@ -253,9 +292,30 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 if (z < rz0 || z > rz1) continue;
                 const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
                 const float dz2 = dzb * dzb;
+#if KN_YPRUNE
+                // rows of this slab any live lane can still need (bound at slab start: superset)
+                int yl0 = ry0, yl1 = ry1;
+                {
+                    const float tz = lane_tau();
+                    int ly0 = INT_MAX, ly1 = INT_MIN;
+                    if (tz == INFINITY) {
+                        ly0 = ry0; ly1 = ry1;
+                    } else if (dz2 <= tz) {
+                        const float rr = sqrtf(tz - dz2) * 1.000001f + g.eps;
+                        ly0 = max(ry0, cell_coord(g, 1, qy - rr) - sy0);
+                        ly1 = min(ry1, cell_coord(g, 1, qy + rr) - sy0);
+                    }
+                    if (!live) { ly0 = INT_MAX; ly1 = INT_MIN; }
+                    const int2 Yr = wave_minmax_i32(ly0, ly1);
+                    if (Yr.x > Yr.y) continue;
+                    yl0 = Yr.x; yl1 = Yr.y;
+                }
+#else
+                const int yl0 = ry0, yl1 = ry1;
+#endif
                 for (int ty_ = 0; ty_ < nyt; ++ty_) {
                     const int y = yc + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
-                    if (y < ry0 || y > ry1) continue;
+                    if (y < yl0 || y > yl1) continue;
                     const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
                     const float dyz2 = fmaf(dyb, dyb, dz2);
                     const float tau = lane_tau();
@@ -297,6 +357,36 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     st_rows += 1u;
                     st_cand += (unsigned)(s1 - s0);
                 }
+#if KN_LDS_PIPE
+                // software-pipelined: the next 4 broadcast reads are issued before the current 4
+                // candidates are scored (two register sets, no loop-carried copies); reads past
+                // s1 stay inside the workgroup's LDS and are never scored
+                if (s + 4 <= s1) {
+                    float4 a0 = pts[s], a1 = pts[s + 1], a2 = pts[s + 2], a3 = pts[s + 3];
+                    auto score4 = [&](const float4& p0, const float4& p1, const float4& p2, const float4& p3, int sb) {
+                        const unsigned k0 = cand_key(p0, qx, qy, qz, HIMASK, sb, qslot);
+                        const unsigned k1 = cand_key(p1, qx, qy, qz, HIMASK, sb + 1, qslot);
+                        const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, sb + 2, qslot);
+                        const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, sb + 3, qslot);
+                        asm volatile("" ::"v"(k0), "v"(k1), "v"(k2), "v"(k3));
+                        const unsigned i0 = topk_push<KM>(keys, k0);
+                        const unsigned i1 = topk_push<KM>(keys, k1);
+                        const unsigned i2 = topk_push<KM>(keys, k2);
+                        const unsigned i3 = topk_push<KM>(keys, k3);
+                        if constexpr (kStats) st_ins += i0 + i1 + i2 + i3;
+                    };
+                    while (true) {
+                        const float4 b0 = pts[s + 4], b1 = pts[s + 5], b2 = pts[s + 6], b3 = pts[s + 7];
+                        score4(a0, a1, a2, a3, s);
+                        s += 4;
+                        if (s + 4 > s1) break;
+                        a0 = pts[s + 4]; a1 = pts[s + 5]; a2 = pts[s + 6]; a3 = pts[s + 7];
+                        score4(b0, b1, b2, b3, s);
+                        s += 4;
+                        if (s + 4 > s1) break;
+                    }
+                }
+#else
                 // 4 broadcast LDS reads in flight, then 4 key tests / insertions
                 for (; s + 4 <= s1; s += 4) {
                     const float4 p0 = pts[s], p1 = pts[s + 1], p2 = pts[s + 2], p3 = pts[s + 3];
@@ -313,6 +403,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const unsigned i3 = topk_push<KM>(keys, k3);
                     if constexpr (kStats) st_ins += i0 + i1 + i2 + i3;
                 }
+#endif
                 for (; s < s1; ++s) {
                     const unsigned i0 = topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
                     if constexpr (kStats) st_ins += i0;
@@ -444,6 +535,362 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         } else {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
             a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// knn_stream_kernel -- the tile kernel's algorithm (one workgroup per cell tile, 64 queries
+// per wave, wave-uniform candidate stream, med3 top-K, exact re-rank, certification) WITHOUT
+// the workgroup-wide LDS staging of the tile + halo points. Each wave streams the cell rows
+// it needs straight from the cell-sorted array (L2-resident; one point per lane, 16-B
+// coalesced), ONE ROW AHEAD: the next row's extent is derived with the current (stale, hence
+// conservative) bound and its load is in flight while the current row is scored. A 64-entry
+// wave-private LDS ring turns the per-lane loads into broadcast reads for the hot loop.
+//   * no staging phase, no per-tile LDS capacity (dense tiles no longer spill to the exact
+//     kernel), ~11 KB of LDS per workgroup -> occupancy is set by VGPRs, and waves of a
+//     workgroup run independently (a wave without a chunk exits at once);
+//   * top-K keys carry the candidate's STREAM POSITION in their low SB bits; a per-wave row
+//     table {position of the row's first candidate, its stored index} maps a kept key back to
+//     its point at the re-rank (binary lifting, all K+M keys in lockstep).
+// PMC that motivated it (900K, k=16, tile kernel): SQ_WAIT_ANY 35 % of wave cycles (staging
+// loads + barriers), ~2.6 resident waves/SIMD of the 5 the LDS budget allows.
+constexpr int kRing = 64;
+constexpr int kMaxRowsPerChunk = 128;
+constexpr int kStreamSlotBits = 11;  // stream positions per chunk: 2048
+
+// Occupancy target: the scheduler otherwise trades waves for ILP (unconstrained: 112-187
+// VGPRs = 2-4 waves/SIMD); 5 waves/SIMD fits in 94 VGPRs without spills.
+#ifndef KN_STREAM_WPE
+#define KN_STREAM_WPE 5
+#endif
+template <int KT, int M>
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_WPE, 8))) void knn_stream_kernel(
+    TileArgs a) {
+    constexpr int KM = KT + M + 1;
+    constexpr unsigned MASK = (1u << kStreamSlotBits) - 1u;
+    constexpr unsigned HIMASK = ~MASK;
+    __shared__ __attribute__((aligned(16))) float4 ring_all[kWaves][kRing];
+    __shared__ int rpos_all[kWaves][kMaxRowsPerChunk];
+    __shared__ int rsid_all[kWaves][kMaxRowsPerChunk];
+    extern __shared__ __attribute__((aligned(16))) int dyn[];
+    int* cb = dyn;
+    int* qpref = cb + a.max_rows * a.cb_stride;  // TY*TZ + 1 entries
+
+    const GridGeom g = *a.geom;
+    const int ntiles = a.ntx * a.nty * a.ntz;
+    const int tile = xcd_remap(blockIdx.x, ntiles);
+    const int tx = tile % a.ntx, ty = (tile / a.ntx) % a.nty, tz = tile / (a.ntx * a.nty);
+    const int tx0 = tx * a.TX, ty0 = ty * a.TY, tz0 = tz * a.TZ;
+    const int tx1 = min(a.X, tx0 + a.TX), ty1 = min(a.Y, ty0 + a.TY), tz1 = min(a.Z, tz0 + a.TZ);
+    const int sx0 = max(0, tx0 - a.H), sx1 = min(a.X, tx1 + a.H);
+    const int sy0 = max(0, ty0 - a.H), sy1 = min(a.Y, ty1 + a.H);
+    const int sz0 = max(0, tz0 - a.H), sz1 = min(a.Z, tz1 + a.H);
+    const int nxs = sx1 - sx0, nys = sy1 - sy0, nzs = sz1 - sz0;
+    const int nrows = nys * nzs;
+    const int cbs = nxs + 1;
+    const int ntry = ty1 - ty0, ntrz = tz1 - tz0, ntr = ntry * ntrz;
+    const int hx = tx0 - sx0;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    float4* ring = ring_all[wid];
+    int* rpos = rpos_all[wid];
+    int* rsid = rsid_all[wid];
+
+    // ---- 1. cell boundaries of every row of the tile + halo box (as knn_tile_kernel) ----
+    for (int t = threadIdx.x; t < nrows * cbs; t += kWG) {
+        const int r = t / cbs, i = t - r * cbs;
+        const int y = sy0 + r % nys, z = sz0 + r / nys;
+        cb[r * cbs + i] = a.cell_start[KN_IDX((z * a.Y + y) * a.X + sx0 + i, a.X * a.Y * a.Z + 1, 221)];
+    }
+    __syncthreads();
+    // ---- 2. query prefix over the tile's rows (wave 0) ----------------------------------
+    if (wid == 0) {
+        int qc = 0;
+        for (int base = 0; base < ntr; base += 64) {
+            const int t = base + lane;
+            int len = 0;
+            if (t < ntr) {
+                const int r = (ty0 - sy0 + t % ntry) + nys * (tz0 - sz0 + t / ntry);
+                len = cb[r * cbs + hx + (tx1 - tx0)] - cb[r * cbs + hx];
+            }
+            const int incl = wave_inclusive_scan_add(len);
+            if (t < ntr) qpref[t] = qc + incl - len;
+            qc += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) qpref[ntr] = qc;
+    }
+    __syncthreads();
+    const int Q = qpref[ntr];
+
+    // ---- 3. query chunks: 64 queries per wave -------------------------------------------
+    for (int chunk = wid; chunk * 64 < Q; chunk += kWaves) {
+        const int qi_raw = chunk * 64 + lane;
+        const bool in_range = qi_raw < Q;
+        const int qi = in_range ? qi_raw : Q - 1;
+        int lo = 0, hi = ntr - 1;
+        while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (qpref[mid] <= qi) lo = mid; else hi = mid - 1; }
+        const int qrow = (ty0 - sy0 + lo % ntry) + nys * (tz0 - sz0 + lo / ntry);
+        const unsigned qsidx = (unsigned)(cb[qrow * cbs + hx] + (qi - qpref[lo]));
+        const float4 qp = a.sorted[KN_IDX(qsidx, (unsigned)a.n, 222)];
+        const unsigned qorig = __float_as_uint(qp.w);
+        const bool live = (int)qorig < a.n_queries;
+        const float qx = qp.x, qy = qp.y, qz = qp.z;
+        const int cx = cell_coord(g, 0, qx) - sx0;
+        const int cy = cell_coord(g, 1, qy) - sy0;
+        const int cz = cell_coord(g, 2, qz) - sz0;
+        const int2 bx = wave_minmax_i32(live ? cx : INT_MAX, live ? cx : INT_MIN);
+        if (bx.x > bx.y) continue;  // no live query in this chunk (uniform)
+        const int2 by = wave_minmax_i32(live ? cy : INT_MAX, live ? cy : INT_MIN);
+        const int2 bz = wave_minmax_i32(live ? cz : INT_MAX, live ? cz : INT_MIN);
+        const int rx0 = max(0, bx.x - a.H), rx1 = min(nxs - 1, bx.y + a.H);
+        const int ry0 = max(0, by.x - a.H), ry1 = min(nys - 1, by.y + a.H);
+        const int rz0 = max(0, bz.x - a.H), rz1 = min(nzs - 1, bz.y + a.H);
+        const int zc = (bz.x + bz.y) >> 1, yc = (by.x + by.y) >> 1;
+        const int nzt = 2 * max(zc - rz0, rz1 - zc) + 1;
+        const int nyt = 2 * max(yc - ry0, ry1 - yc) + 1;
+        const int nit = nzt * nyt;
+
+        // union x-range (local cells) of the row visited at iteration `it` under bound `tau`;
+        // returns false (uniform) when the row lies outside the region or no lane needs it
+        auto row_range = [&](int it, float tau, int& r, int& X0, int& X1) -> bool {
+            const int tz_ = it / nyt, ty_ = it - tz_ * nyt;
+            const int z = zc + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
+            const int y = yc + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
+            if (z < rz0 || z > rz1 || y < ry0 || y > ry1) return false;
+            const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
+            const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
+            const float dyz2 = fmaf(dyb, dyb, dzb * dzb);
+            int lx0 = INT_MAX, lx1 = INT_MIN;
+            if (tau == INFINITY) {
+                lx0 = rx0; lx1 = rx1;
+            } else if (dyz2 <= tau) {
+                const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
+                lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
+            }
+            if (!live) { lx0 = INT_MAX; lx1 = INT_MIN; }
+            const int2 X = wave_minmax_i32(lx0, lx1);
+            r = y + nys * z;
+            X0 = X.x; X1 = X.y;
+            return X.x <= X.y;
+        };
+
+        unsigned keys[KM];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) keys[j] = SENT;
+        auto lane_tau = [&]() {
+            const unsigned last = keys[KM - 1];
+            return last == SENT ? INFINITY : __uint_as_float(last | MASK);
+        };
+
+        // prefetch state: the next non-empty row (iteration, staged-row, stored range)
+        int it = 0;
+        int pf_it = -1, pf_r = 0, pf_p0 = 0, pf_p1 = 0;
+        float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto prefetch_next = [&]() {
+            const float tau = lane_tau();
+            pf_it = -1;
+            for (; it < nit; ++it) {
+                int r, X0, X1;
+                if (row_range(it, tau, r, X0, X1)) {
+                    pf_it = it; pf_r = r;
+                    pf_p0 = __builtin_amdgcn_readfirstlane(cb[r * cbs + X0]);
+                    pf_p1 = __builtin_amdgcn_readfirstlane(cb[r * cbs + X1 + 1]);
+                    if (lane < pf_p1 - pf_p0) pf = a.sorted[KN_IDX(pf_p0 + lane, a.n, 223)];
+                    ++it;
+                    return;
+                }
+            }
+        };
+
+        int nrow = 0;         // rows recorded in the row table (uniform)
+        unsigned pos = 0;     // stream position of the next candidate (uniform)
+        bool overflow = false;
+        prefetch_next();
+        while (pf_it >= 0) {
+            const int cur_it = pf_it, cur_r = pf_r, cur_p0 = pf_p0, cur_p1 = pf_p1;
+            if (lane < cur_p1 - cur_p0) ring[lane] = pf;
+            prefetch_next();  // next row's load overlaps this row's scoring
+            int r, X0, X1;
+            if (!row_range(cur_it, lane_tau(), r, X0, X1)) continue;  // bound shrank past it
+            const int s0 = __builtin_amdgcn_readfirstlane(cb[cur_r * cbs + X0]);
+            const int s1 = __builtin_amdgcn_readfirstlane(cb[cur_r * cbs + X1 + 1]);
+            if (s0 >= s1) continue;
+            if (nrow >= kMaxRowsPerChunk || pos + (unsigned)(s1 - s0) > MASK + 1u) { overflow = true; break; }
+            if (lane == 0) { rpos[nrow] = (int)pos; rsid[nrow] = s0; }
+            ++nrow;
+            // rows longer than the ring are scored in 64-point pieces (the first is prefetched)
+            for (int base = cur_p0; base < s1; base += kRing) {
+                if (base != cur_p0) {
+                    const int len = min(kRing, cur_p1 - base);
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (lane < len) v = a.sorted[KN_IDX(base + lane, a.n, 224)];
+                    if (lane < len) ring[lane] = v;
+                }
+                const int i0 = max(s0, base) - base, i1 = min(s1, base + kRing) - base;
+                if (i0 >= i1) continue;
+                unsigned pp = pos + (unsigned)(base + i0 - s0);
+                int i = i0;
+                for (; i + 4 <= i1; i += 4, pp += 4) {
+                    const float4 p0 = ring[i], p1 = ring[i + 1], p2 = ring[i + 2], p3 = ring[i + 3];
+                    const unsigned k0 = cand_key(p0, qx, qy, qz, HIMASK, (int)pp, 0);
+                    const unsigned k1 = cand_key(p1, qx, qy, qz, HIMASK, (int)pp + 1, 0);
+                    const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, (int)pp + 2, 0);
+                    const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, (int)pp + 3, 0);
+                    asm volatile("" ::"v"(k0), "v"(k1), "v"(k2), "v"(k3));
+                    topk_push<KM>(keys, k0);
+                    topk_push<KM>(keys, k1);
+                    topk_push<KM>(keys, k2);
+                    topk_push<KM>(keys, k3);
+                }
+                for (; i < i1; ++i, ++pp) topk_push<KM>(keys, cand_key(ring[i], qx, qy, qz, HIMASK, (int)pp, 0));
+            }
+            pos += (unsigned)(s1 - s0);
+        }
+        if (overflow) {
+            // stream too long for the key's slot bits / row table: the chunk's live queries
+            // take the exact kernel (drain the prefetch first)
+            if (live && in_range) {
+                const unsigned p = atomicAdd(a.counters + 0, 1u);
+                a.fallback_list[KN_IDX(p, (unsigned)a.n, 225)] = qsidx;
+            }
+            if (lane == 0) atomicAdd(a.counters + 2, 1u);
+            continue;
+        }
+
+        // ---- exact re-rank: slot -> stored index via the row table (binary lifting) ------
+        const unsigned last_key = keys[KM - 1];
+        int rl[KM];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            keys[j] = keys[j] == SENT ? SENT : (keys[j] & MASK);  // slot (SENT stays)
+            rl[j] = 0;
+        }
+#pragma unroll 1
+        for (int st = kMaxRowsPerChunk / 2; st > 0; st >>= 1) {
+            if (st >= nrow) continue;  // uniform
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                const int c = min(rl[j] + st, kMaxRowsPerChunk - 1);
+                if (rl[j] + st < nrow && rpos[c] <= (int)keys[j]) rl[j] = c;
+                if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const unsigned sidx = (unsigned)(rsid[rl[j]] + ((int)keys[j] - rpos[rl[j]]));
+            rl[j] = (keys[j] != SENT && sidx != qsidx) ? (int)sidx : -1;  // stored index or -1
+        }
+        float dd[KM];
+        unsigned ii[KM];
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const unsigned sidx = (unsigned)rl[j];
+            const bool valid = rl[j] >= 0;
+            const float4 p = a.sorted[KN_IDX(valid ? sidx : qsidx, (unsigned)a.n, 226)];
+            const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+            const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+            dd[j] = valid ? d : INFINITY;
+            ii[j] = valid ? __float_as_uint(p.w) : SENT;
+            // at most 4 gathers in flight: 19 float4 loads hoisted together cost 76 VGPRs
+            if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+        const unsigned last = last_key;
+        for (int round = 0; round < (KM + 1) / 2; ++round) {
+            bool swapped = false;
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+                for (int j = pass; j + 1 < KM; j += 2) {
+                    const bool sw = pair_less(dd[j + 1], ii[j + 1], dd[j], ii[j]);
+                    const float d0 = sw ? dd[j + 1] : dd[j], d1 = sw ? dd[j] : dd[j + 1];
+                    const unsigned i0 = sw ? ii[j + 1] : ii[j], i1 = sw ? ii[j] : ii[j + 1];
+                    dd[j] = d0; dd[j + 1] = d1; ii[j] = i0; ii[j + 1] = i1;
+                    swapped |= sw;
+                }
+            }
+            if (!__builtin_amdgcn_ballot_w64(swapped)) break;
+        }
+        const int k = a.k;
+        auto kth = [&]() {
+            float v = INFINITY;
+#pragma unroll
+            for (int j = 0; j < KM; ++j) if (j == k - 1) v = dd[j];
+            return v;
+        };
+        float dK2 = kth();
+        const bool need = live && ((last != SENT && !(dK2 <= __uint_as_float(last & HIMASK))) ||
+                                   (a.flags & kQueryForceRescan));
+        if (__builtin_amdgcn_ballot_w64(need)) {
+            // truncation near-tie (rare): exact (d2, id) re-scan of the region, from global
+            const float thr = need ? ((a.flags & kQueryForceRescan) ? INFINITY : dK2) : -1.f;
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                dd[j] = need ? INFINITY : dd[j];
+                ii[j] = need ? SENT : ii[j];
+            }
+            for (int it2 = 0; it2 < nit; ++it2) {
+                int r, X0, X1;
+                if (!row_range(it2, need ? thr : -1.f, r, X0, X1)) continue;
+                const int s0 = __builtin_amdgcn_readfirstlane(cb[r * cbs + X0]);
+                const int s1 = __builtin_amdgcn_readfirstlane(cb[r * cbs + X1 + 1]);
+                for (int s = s0; s < s1; ++s) {
+                    const float4 p = a.sorted[KN_IDX(s, a.n, 227)];
+                    const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+                    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                    const unsigned id = __float_as_uint(p.w);
+                    const bool take = (unsigned)s != qsidx && d2 <= thr && pair_less(d2, id, dd[KM - 1], ii[KM - 1]);
+                    if (__builtin_amdgcn_ballot_w64(take)) {
+                        if (take) {
+#pragma unroll
+                            for (int j = KM - 1; j > 0; --j) {
+                                const bool bp = pair_less(d2, id, dd[j - 1], ii[j - 1]);
+                                const bool bc = pair_less(d2, id, dd[j], ii[j]);
+                                const float nd = bp ? dd[j - 1] : (bc ? d2 : dd[j]);
+                                const unsigned ni = bp ? ii[j - 1] : (bc ? id : ii[j]);
+                                dd[j] = nd; ii[j] = ni;
+                            }
+                            if (pair_less(d2, id, dd[0], ii[0])) { dd[0] = d2; ii[0] = id; }
+                        }
+                    }
+                }
+            }
+            if (need && in_range) atomicAdd(a.counters + 3, 1u);
+            dK2 = kth();
+        }
+        int nfound = 0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) nfound += (ii[j] != SENT) ? 1 : 0;
+        if (!(in_range && live)) continue;
+        float m = INFINITY;
+        {
+            const int gx0 = sx0 + rx0, gx1 = sx0 + rx1, gy0 = sy0 + ry0, gy1 = sy0 + ry1;
+            const int gz0 = sz0 + rz0, gz1 = sz0 + rz1;
+            if (gx0 > 0) m = fminf(m, qx - (g.origin[0] + gx0 * g.cell[0]));
+            if (gx1 < a.X - 1) m = fminf(m, g.origin[0] + (gx1 + 1) * g.cell[0] - qx);
+            if (gy0 > 0) m = fminf(m, qy - (g.origin[1] + gy0 * g.cell[1]));
+            if (gy1 < a.Y - 1) m = fminf(m, g.origin[1] + (gy1 + 1) * g.cell[1] - qy);
+            if (gz0 > 0) m = fminf(m, qz - (g.origin[2] + gz0 * g.cell[2]));
+            if (gz1 < a.Z - 1) m = fminf(m, g.origin[2] + (gz1 + 1) * g.cell[2] - qz);
+            m = fminf(m, complete_margin(a.complete, qx, 0));
+            m = fminf(m, complete_margin(a.complete, qy, 1));
+            m = fminf(m, complete_margin(a.complete, qz, 2));
+            m -= g.eps;
+        }
+        const bool geo_ok = (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
+        if (geo_ok) {
+            const size_t row = (size_t)qorig * (size_t)k;
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                if (j < k) {
+                    const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 228);
+                    a.out_idx[o] = a.id_map ? a.id_map[KN_IDX(ii[j], (unsigned)a.n, 229)] : ii[j];
+                    if (a.out_dist) a.out_dist[o] = dd[j];
+                }
+            }
+        } else {
+            const unsigned p = atomicAdd(a.counters + 0, 1u);
+            a.fallback_list[KN_IDX(p, (unsigned)a.n, 230)] = qsidx;
         }
     }
 }
@@ -792,6 +1239,22 @@ __global__ void to_stored_kernel(const unsigned* __restrict__ out_orig, const un
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
+// Query algorithm: flags bit 1 -> stream kernel, bit 2 -> LDS-staged tile kernel; neither ->
+// the process default (env KN_QUERY_ALGO = "tile" | "stream", else kDefaultAlgo).
+constexpr int kAlgoTile = 1, kAlgoStream = 2;
+constexpr int kDefaultAlgo = kAlgoTile;
+inline int query_algo(int flags) {
+    if (flags & kQueryAlgoStream) return kAlgoStream;
+    if (flags & kQueryAlgoTile) return kAlgoTile;
+    static const int def = [] {
+        const char* e = std::getenv("KN_QUERY_ALGO");
+        if (e && std::strcmp(e, "stream") == 0) return kAlgoStream;
+        if (e && std::strcmp(e, "tile") == 0) return kAlgoTile;
+        return kDefaultAlgo;
+    }();
+    return def;
+}
+
 template <int KT>
 hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     // margin slots beyond K: a query is lost to the exact path only if the K-th and (K+M)-th
@@ -818,6 +1281,12 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.ntx = (X + a.TX - 1) / a.TX; a.nty = (Y + a.TY - 1) / a.TY; a.ntz = (Z + a.TZ - 1) / a.TZ;
         a.cb_stride = std::min(X, a.TX + 2 * a.H) + 1;
         a.max_rows = std::min(Y, a.TY + 2 * a.H) * std::min(Z, a.TZ + 2 * a.H);
+        const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
+        if (query_algo(q.flags) == kAlgoStream) {
+            a.flags = q.flags & kQueryForceRescan;
+            const size_t dyn = ((size_t)a.max_rows * a.cb_stride + (size_t)a.TY * a.TZ + 1) * sizeof(int);
+            if constexpr (KT <= 64) knn_stream_kernel<KT, M><<<nt, kWG, dyn, s>>>(a);
+        } else {
         const size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity);
         static bool attr_set = false;
         if (!attr_set) {
@@ -826,8 +1295,8 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             attr_set = true;
         }
-        const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
         if constexpr (KT <= 64) knn_tile_kernel<KT, M><<<nt, kWG, lds, s>>>(a);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     ExactArgs b;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 
 #include "kn/route.h"
 #include "kn/wave.h"
@@ -58,8 +59,10 @@ __device__ __forceinline__ unsigned long long route_halo(const RouteParams& p, f
     return m;
 }
 
-__global__ __launch_bounds__(kRT) void route_count_kernel(const float* __restrict__ pts, int n, RouteParams p,
+__global__ __launch_bounds__(kRT) void route_count_kernel(const float* __restrict__ pts, int n,
+                                                          const RouteParams* __restrict__ pp,
                                                           int* __restrict__ block_counts, int nb) {
+    const RouteParams& p = *pp;
     __shared__ int cnt[2 * kRouteMaxWorld];
     const int cols = 2 * p.world;
     for (int c = threadIdx.x; c < cols; c += kRT) cnt[c] = 0;
@@ -110,12 +113,14 @@ __global__ __launch_bounds__(kRT) void route_scan_kernel(int* __restrict__ block
 }
 
 __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restrict__ pts,
-                                                            const int* __restrict__ ids, int n, RouteParams p,
+                                                            const int* __restrict__ ids, int n,
+                                                            const RouteParams* __restrict__ pp,
                                                             const int* __restrict__ block_offsets, int nb,
                                                             const int* __restrict__ totals,
                                                             float4* __restrict__ send, int send_rows) {
     __shared__ int base[2 * kRouteMaxWorld];            // block's next row of every column
     __shared__ int wcnt[kRT / 64][2 * kRouteMaxWorld];  // per-wave counts of the current round
+    const RouteParams& p = *pp;
     const int cols = 2 * p.world;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) {
@@ -152,7 +157,8 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
         __syncthreads();
         // phase B: rows (in-wave rank from the ballot, earlier waves from LDS)
         if (__builtin_amdgcn_ballot_w64(valid)) {
-            const float4 row = make_float4(x, y, z, __int_as_float(valid ? ids[i] : 0));
+            const int gid = valid ? (ids ? ids[i] : p.id_offset + i) : 0;
+            const float4 row = make_float4(x, y, z, __int_as_float(gid));
             for (int d = 0; d < p.world; ++d) {
                 const bool po = o == d, ph = (m >> d) & 1ull;
                 const unsigned long long bo = __builtin_amdgcn_ballot_w64(po);
@@ -193,6 +199,71 @@ __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restr
     pts[3 * oo + 1] = v.y;
     pts[3 * oo + 2] = v.z;
     gids[oo] = __float_as_int(v.w);
+}
+
+
+// One thread: global domain, halo width, rank boxes and id offset from the gathered metas.
+// Formulas follow SpatialDecomposition / DistributedKNearests (parallel/*.py) in double.
+__global__ void route_plan_kernel(const double* __restrict__ metas, int world, int rank, int gx, int gy, int gz,
+                                  int k, double halo_factor, RouteParams* __restrict__ p,
+                                  double* __restrict__ hdr) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double lo[3], hi[3];
+    double ntot = 0.0, off = 0.0;
+    for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+    for (int r = 0; r < world; ++r) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fmin(lo[a], metas[8 * r + a]);
+            hi[a] = fmax(hi[a], metas[8 * r + 3 + a]);
+        }
+        if (r < rank) off += metas[8 * r + 6];
+        ntot += metas[8 * r + 6];
+    }
+    bool finite = true;
+    for (int a = 0; a < 3; ++a) finite = finite && isfinite(lo[a]) && isfinite(hi[a]);
+    if (!finite)
+        for (int a = 0; a < 3; ++a) { lo[a] = 0.0; hi[a] = 1.0; }  // empty global cloud
+    double vol = 1.0, diag2 = 0.0, scale = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        const double e = hi[a] - lo[a];
+        vol *= e;
+        diag2 += e * e;
+        scale = fmax(scale, fmax(fabs(lo[a]), fmax(fabs(hi[a]), e)));
+    }
+    vol = fmax(vol, 1e-30);
+    const double rk = cbrt(3.0 * (k + 1) * vol / (4.0 * M_PI * fmax(1.0, ntot)));
+    const double h = halo_factor * rk;
+    const double diag = sqrt(diag2);
+    const bool full = h >= diag;
+    const double hs = full ? 2.0 * diag + 1.0 : h * (1.0 + 1e-5) + 1e-5 * scale;
+    const int g[3] = {gx, gy, gz};
+    for (int a = 0; a < 3; ++a) {
+        const float l = (float)lo[a], u = (float)hi[a];
+        p->lo[a] = l;
+        p->ext[a] = fmaxf(u - l, 1e-30f);
+        p->g[a] = (float)g[a];
+        p->grid[a] = g[a];
+    }
+    p->world = world;
+    const float hf = (float)hs;
+    p->h2 = hf * hf;
+    p->id_offset = (int)off;
+    for (int r = 0; r < world; ++r) {
+        const int c[3] = {r % gx, (r / gx) % gy, r / (gx * gy)};
+        for (int a = 0; a < 3; ++a) {
+            const double w = (hi[a] - lo[a]) / g[a];
+            p->box_lo[r][a] = (float)__dadd_rn(lo[a], __dmul_rn((double)c[a], w));
+            p->box_hi[r][a] = (float)(c[a] == g[a] - 1 ? hi[a] : __dadd_rn(lo[a], __dmul_rn((double)(c[a] + 1), w)));
+        }
+    }
+    for (int a = 0; a < 3; ++a) { hdr[a] = lo[a]; hdr[3 + a] = hi[a]; }
+    hdr[6] = h;
+    hdr[7] = hs;
+    hdr[8] = ntot;
+    hdr[9] = off;
+    hdr[10] = full ? 1.0 : 0.0;
+    hdr[11] = diag;
+    for (int i = 12; i < kPlanHdr; ++i) hdr[i] = 0.0;
 }
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
@@ -251,22 +322,30 @@ __global__ void meta_finalize_kernel(const unsigned* __restrict__ words, int n, 
 
 int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
 
-hipError_t launch_route_count(const float* pts, int n, const RouteParams& p, int* block_counts, int* totals,
-                              hipStream_t s) {
-    if (p.world < 1 || p.world > kRouteMaxWorld) return hipErrorInvalidValue;
+hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int world, int* block_counts,
+                              int* totals, hipStream_t s) {
+    if (world < 1 || world > kRouteMaxWorld) return hipErrorInvalidValue;
     const int nb = route_block_count(n);
     route_count_kernel<<<nb, kRT, 0, s>>>(pts, n, p, block_counts, nb);
-    route_scan_kernel<<<2 * p.world, kRT, 0, s>>>(block_counts, nb, totals);
+    route_scan_kernel<<<2 * world, kRT, 0, s>>>(block_counts, nb, totals);
     return hipGetLastError();
 }
 
-hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams& p,
+hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams* p, int world,
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
                                 hipStream_t s) {
-    if (p.world < 1 || p.world > kRouteMaxWorld) return hipErrorInvalidValue;
+    if (world < 1 || world > kRouteMaxWorld) return hipErrorInvalidValue;
     const int nb = route_block_count(n);
     if (n > 0)
         route_scatter_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, block_offsets, nb, totals, send, send_rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
+                             double halo_factor, RouteParams* p, double* hdr, hipStream_t s) {
+    if (world < 1 || world > kRouteMaxWorld || grid[0] * grid[1] * grid[2] != world || rank < 0 || rank >= world)
+        return hipErrorInvalidValue;
+    route_plan_kernel<<<1, 64, 0, s>>>(metas, world, rank, grid[0], grid[1], grid[2], k, halo_factor, p, hdr);
     return hipGetLastError();
 }
 

@@ -8,6 +8,7 @@
 #include <torch/extension.h>
 
 #include <cmath>
+#include <cstring>
 #include <limits>
 #include <vector>
 
@@ -207,20 +208,60 @@ kn::RouteParams route_params(const std::vector<double>& lo, const std::vector<do
     return p;
 }
 
+// RouteParams on the device (the route kernels read their parameters from device memory)
+torch::Tensor upload_params(const kn::RouteParams& p, const torch::Device& dev) {
+    auto h = torch::empty({(int64_t)sizeof(kn::RouteParams)}, torch::TensorOptions().dtype(torch::kUInt8));
+    std::memcpy(h.data_ptr<uint8_t>(), &p, sizeof(p));
+    return h.to(dev, /*non_blocking=*/false);
+}
+
+const kn::RouteParams* params_ptr(const torch::Tensor& plan) {
+    TORCH_CHECK(plan.is_cuda() && plan.scalar_type() == torch::kUInt8 && plan.numel() == (int64_t)sizeof(kn::RouteParams),
+                "plan must be the uint8 device tensor returned by route_plan");
+    return reinterpret_cast<const kn::RouteParams*>(plan.data_ptr<uint8_t>());
+}
+
+std::vector<torch::Tensor> route_count_impl(const torch::Tensor& points, const kn::RouteParams* p, int world) {
+    const int n = (int)points.size(0);
+    const int nb = kn::route_block_count(n);
+    auto i32 = points.options().dtype(torch::kInt32);
+    auto bc = torch::empty({2 * (int64_t)world * nb}, i32);
+    auto totals = torch::empty({(int64_t)world, 2}, i32);
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, p, world, bc.data_ptr<int>(), totals.data_ptr<int>(), s));
+    return {bc, totals};
+}
+
+torch::Tensor route_scatter_impl(const torch::Tensor& points, const c10::optional<torch::Tensor>& ids,
+                                 const kn::RouteParams* p, int world, const torch::Tensor& block_offsets,
+                                 const torch::Tensor& totals, int64_t rows) {
+    const int n = (int)points.size(0);
+    const int* idp = nullptr;
+    if (ids.has_value()) {
+        TORCH_CHECK(ids->is_cuda() && ids->scalar_type() == torch::kInt32 && ids->numel() == n && ids->is_contiguous(),
+                    "ids must be a contiguous int32 GPU tensor of N entries");
+        idp = ids->data_ptr<int>();
+    }
+    TORCH_CHECK(block_offsets.numel() == 2 * (int64_t)world * kn::route_block_count(n) &&
+                    totals.numel() == 2 * (int64_t)world,
+                "block_offsets / totals do not match route_count's output");
+    TORCH_CHECK(rows >= 0, "rows must be >= 0");
+    auto send = torch::empty({rows, 4}, points.options());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, p, world, block_offsets.data_ptr<int>(),
+                                          totals.data_ptr<int>(), reinterpret_cast<float4*>(send.data_ptr<float>()),
+                                          (int)rows, s));
+    return send;
+}
+
 // -> (scanned block counts, totals (world, 2) = owned / halo rows per destination)
 std::vector<torch::Tensor> route_count(torch::Tensor points, std::vector<double> lo, std::vector<double> hi,
                                        std::vector<int64_t> grid, std::vector<double> boxes, double h) {
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
     const kn::RouteParams p = route_params(lo, hi, grid, boxes, h);
-    const int n = (int)points.size(0);
-    const int nb = kn::route_block_count(n);
-    auto i32 = points.options().dtype(torch::kInt32);
-    auto bc = torch::empty({2 * (int64_t)p.world * nb}, i32);
-    auto totals = torch::empty({(int64_t)p.world, 2}, i32);
-    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-    KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, p, bc.data_ptr<int>(), totals.data_ptr<int>(), s));
-    return {bc, totals};
+    auto dp = upload_params(p, points.device());
+    return route_count_impl(points, params_ptr(dp), p.world);
 }
 
 torch::Tensor route_scatter(torch::Tensor points, torch::Tensor ids, std::vector<double> lo, std::vector<double> hi,
@@ -229,19 +270,43 @@ torch::Tensor route_scatter(torch::Tensor points, torch::Tensor ids, std::vector
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
     const kn::RouteParams p = route_params(lo, hi, grid, boxes, h);
-    const int n = (int)points.size(0);
-    TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == torch::kInt32 && ids.numel() == n && ids.is_contiguous(),
-                "ids must be a contiguous int32 GPU tensor of N entries");
-    TORCH_CHECK(block_offsets.numel() == 2 * (int64_t)p.world * kn::route_block_count(n) &&
-                    totals.numel() == 2 * (int64_t)p.world,
-                "block_offsets / totals do not match route_count's output");
-    TORCH_CHECK(rows >= 0, "rows must be >= 0");
-    auto send = torch::empty({rows, 4}, points.options());
+    auto dp = upload_params(p, points.device());
+    return route_scatter_impl(points, ids, params_ptr(dp), p.world, block_offsets, totals, rows);
+}
+
+// Device-side plan from the all-gathered metas (world x 8 float64, on device): no host sync.
+// -> (plan (uint8 RouteParams on device), header (16,) float64 on device, see kn::kPlanHdr)
+std::vector<torch::Tensor> route_plan(torch::Tensor metas, int64_t rank, std::vector<int64_t> grid, int64_t k,
+                                      double halo_factor) {
+    TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
+                    metas.numel() % 8 == 0,
+                "metas must be a contiguous (world*8,) float64 GPU tensor");
+    TORCH_CHECK(grid.size() == 3, "grid must have 3 entries");
+    const int world = (int)(metas.numel() / 8);
+    const c10::DeviceGuard guard(metas.device());
+    auto plan = torch::empty({(int64_t)sizeof(kn::RouteParams)}, metas.options().dtype(torch::kUInt8));
+    auto hdr = torch::empty({kn::kPlanHdr}, metas.options());
+    const int g[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-    KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), ids.data_ptr<int>(), n, p,
-                                          block_offsets.data_ptr<int>(), totals.data_ptr<int>(),
-                                          reinterpret_cast<float4*>(send.data_ptr<float>()), (int)rows, s));
-    return send;
+    KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor,
+                                       reinterpret_cast<kn::RouteParams*>(plan.data_ptr<uint8_t>()),
+                                       hdr.data_ptr<double>(), s));
+    return {plan, hdr};
+}
+
+std::vector<torch::Tensor> route_count_dev(torch::Tensor points, torch::Tensor plan, int64_t world) {
+    check_points(points, true);
+    const c10::DeviceGuard guard(points.device());
+    TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld, "world size must be in [1, 64]");
+    return route_count_impl(points, params_ptr(plan), (int)world);
+}
+
+torch::Tensor route_scatter_dev(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor plan,
+                                int64_t world, torch::Tensor block_offsets, torch::Tensor totals, int64_t rows) {
+    check_points(points, true);
+    const c10::DeviceGuard guard(points.device());
+    TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld, "world size must be in [1, 64]");
+    return route_scatter_impl(points, ids, params_ptr(plan), (int)world, block_offsets, totals, rows);
 }
 
 // recv: rows received from every source, source s = [recv_own[s] owned | recv_halo[s] halo].
@@ -443,6 +508,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     m.def("local_meta", &local_meta, "multi-GPU: {lo[3], hi[3], n, 0} of the local points (float64, on device)");
     m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts");
+    m.def("route_plan", &route_plan, "multi-GPU: device-side routing plan from the gathered metas (no host sync)");
+    m.def("route_count_dev", &route_count_dev, "multi-GPU: route_count with the device plan");
+    m.def("route_scatter_dev", &route_scatter_dev, "multi-GPU: route_scatter with the device plan (ids=None: offset + i)",
+          py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("world"), py::arg("block_offsets"),
+          py::arg("totals"), py::arg("rows"));
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")

@@ -33,7 +33,7 @@ from typing import Optional
 import torch
 
 from ..ops import knn_ops as ops
-from .decomposition import SpatialDecomposition
+from .decomposition import SpatialDecomposition, factor3
 from .transport import TorchDistTransport
 
 INF = math.inf
@@ -82,7 +82,7 @@ class DistResult:
 class DistributedKNearests:
     def __init__(self, k: int = 16, group=None, halo_factor: float = 1.6, points_per_cell: float = 0.0,
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
-                 transport=None):
+                 transport=None, device_plan: bool = True):
         self.k = int(k)
         self.group = group
         self.halo_factor = float(halo_factor)
@@ -93,6 +93,8 @@ class DistributedKNearests:
         self.comm = transport if transport is not None else TorchDistTransport(group)
         self.rank = self.comm.rank
         self.world = self.comm.world
+        self.device_plan = device_plan  # GPU: plan the routing on the device (1 host sync, not 2)
+        self._grid = None
 
     # ------------------------------------------------------------------ helpers ------
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
@@ -178,6 +180,63 @@ class DistributedKNearests:
         mapped = torch.where(idx >= 0, gl[idx.clamp(min=0).long()], torch.full_like(gl[:1], -1)).to(torch.int32)
         return mapped, d2, torch.tensor([unc.numel()], dtype=torch.long)
 
+    # ------------------------------------------------------- native (GPU) fast path ------
+    def _solve_native(self, points: torch.Tensor, ids: Optional[torch.Tensor]) -> DistResult:
+        """Device-planned solve: local meta -> all-gather -> route plan -> route counts ->
+        counts all-to-all are enqueued back to back and read with ONE host sync (the split
+        sizes the payload all-to-all needs); the certification flag is the second. The
+        decomposition grid is cached across calls and re-planned if the domain's shape asks
+        for another one."""
+        C = ops.load()
+        world, rank = self.world, self.rank
+        metas = self.comm.all_gather_cat(C.local_meta(points))  # (world*8,) f64, on device
+        grid = self._grid or factor3(world, (1.0, 1.0, 1.0))
+        hf = self.halo_factor
+        src_pts, src_ids = points, (ids.to(torch.int32).contiguous() if ids is not None else None)
+        rounds = 0
+        own_pts = own_ids = None
+        while True:
+            rounds += 1
+            while True:
+                plan, hdr = C.route_plan(metas, rank, list(grid), self.k, hf)
+                bc, totals = C.route_count_dev(src_pts, plan, world)
+                recv_tot = torch.empty_like(totals)
+                self.comm.all_to_all_single(recv_tot, totals)
+                host = torch.cat([hdr, totals.flatten().double(), recv_tot.flatten().double()]).cpu()  # sync 1
+                hv = host.tolist()
+                lo, hi = tuple(hv[0:3]), tuple(hv[3:6])
+                want = factor3(world, tuple(max(hi[a] - lo[a], 1e-30) for a in range(3)))
+                if want == tuple(grid):
+                    break
+                grid = want  # domain shape changed: re-plan with the matching decomposition
+            self._grid = tuple(grid)
+            h, hs, full = hv[6], hv[7], hv[10] != 0.0
+            tot = [int(x) for x in hv[16:16 + 2 * world]]
+            rtot = [int(x) for x in hv[16 + 2 * world:16 + 4 * world]]
+            send_counts = [tot[2 * d] + tot[2 * d + 1] for d in range(world)]
+            recv_own = [rtot[2 * d] for d in range(world)]
+            recv_halo = [rtot[2 * d + 1] for d in range(world)]
+            send = C.route_scatter_dev(src_pts, src_ids, plan, world, bc, totals, sum(send_counts))
+            recv = self._a2a(send, send_counts, [a + b for a, b in zip(recv_own, recv_halo)])
+            pts, gids = C.route_unpack(recv, recv_own, recv_halo)
+            n_owned = sum(recv_own)
+            if rounds == 1:
+                own_pts, own_ids = pts[:n_owned], gids[:n_owned]
+            dec = SpatialDecomposition(world, lo, hi, tuple(grid))
+            blo, bhi = dec.rank_box(rank)
+            complete = dec.complete_box(rank, h) if not full else [-INF] * 3 + [INF] * 3
+            box = [max(lo[a], blo[a] - hs) for a in range(3)] + [min(hi[a], bhi[a] + hs) for a in range(3)]
+            idx, d2, n_unc = self.local_solve(pts, gids, n_owned, complete, box)
+            flag = n_unc.to(points.device)
+            self.comm.all_reduce_max(flag)
+            if int(flag.item()) == 0 or full or rounds >= self.max_rounds:  # sync 2
+                break
+            hf *= 2.0
+            src_pts, src_ids = own_pts, own_ids
+        stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
+                 "grid": tuple(grid)}
+        return DistResult(own_ids, idx, d2, stats)
+
     # -------------------------------------------------------------------- solve ------
     def solve(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None,
               partitioned: bool = False, domain=None) -> DistResult:
@@ -186,6 +245,8 @@ class DistributedKNearests:
         this rank's box simply route to itself). ``ids``: their global ids (int32); default =
         rank offset + arange."""
         points = points.contiguous().float()
+        if domain is None and self._use_native(points) and self.device_plan:
+            return self._solve_native(points, ids)
         dev = points.device
         lo, hi, counts = self.meta(points)
         if domain is not None:

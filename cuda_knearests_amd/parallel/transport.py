@@ -31,6 +31,12 @@ class TorchDistTransport:
         dist.all_gather(parts, t, group=self.group)
         return parts
 
+    def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
+        """All ranks' ``t`` concatenated (rank order), left on the device (no host sync)."""
+        out = t.new_empty((self.world * t.numel(),))
+        dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=self.group)
+        return out
+
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> None:
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
@@ -63,6 +69,9 @@ class LoopbackTransport:
 
     def all_gather(self, t: torch.Tensor) -> List[torch.Tensor]:
         return [x.clone() for x in self._exchange(t)]
+
+    def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
+        return torch.cat([x.reshape(-1) for x in self._exchange(t)])
 
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> None:
         n = inp.size(0)

@@ -20,6 +20,8 @@ ref = A.query(*args())
 out = B.query(*args())
 torch.cuda.synchronize()
 print("identical:", torch.equal(ref[0], out[0]) and torch.equal(ref[1], out[1]), flush=True)
+if "chk" in var:
+    print("debug_words:", B.debug_words(False), flush=True)
 ta, tb = [], []
 ev = lambda: torch.cuda.Event(enable_timing=True)
 for r in range(rounds):

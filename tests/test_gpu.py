@@ -48,6 +48,28 @@ def test_forced_exact_rescan(cuda, k):
     _assert_matches_oracle(p, idx, d2, k)
 
 
+@pytest.mark.parametrize("k,gen", [(1, "uniform"), (16, "uniform"), (50, "uniform"), (64, "uniform"),
+                                   (16, "clustered"), (8, "blue")])
+def test_stream_kernel_vs_oracle(cuda, k, gen):
+    # staging-free stream kernel (query flags bit 1): same certification, rows read from global
+    mk = {"uniform": uniform_cloud, "clustered": clustered_cloud, "blue": blue_cloud}[gen]
+    p = mk(25000, seed=300 + k).to(cuda)
+    g = kn.build_grid(p, k)
+    idx, d2 = kn.query(g, k, flags=2)
+    _assert_matches_oracle(p, idx, d2, k)
+    # and it agrees with the LDS-staged tile kernel bit for bit
+    i2, e2 = kn.query(g, k, flags=4)
+    assert torch.equal(idx, i2) and torch.equal(d2, e2)
+
+
+def test_stream_kernel_forced_rescan(cuda):
+    p = uniform_cloud(20000, seed=401, device=cuda)
+    g = kn.build_grid(p, 16)
+    idx, d2, info = kn.query(g, 16, return_info=True, flags=1 | 2)
+    assert int(info["counters"][3]) == p.size(0)
+    _assert_matches_oracle(p, idx, d2, 16)
+
+
 @pytest.mark.parametrize("k", [8, 16, 96, 128])
 def test_exact_path_vs_oracle(cuda, k):
     p = uniform_cloud(20000, seed=100 + k, device=cuda)

@@ -90,3 +90,54 @@ def test_local_meta_matches_torch(cuda, ext, n):
     mn, mx = torch.aminmax(p, dim=0)
     assert torch.equal(v[:3], mn.double().cpu())
     assert torch.equal(v[3:6], mx.double().cpu())
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_device_plan_matches_host_plan(cuda, world):
+    """Device-planned routing (one host sync) == host-planned routing, bit for bit."""
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+
+    n = 40000
+    cloud = uniform_cloud(n, seed=90 + world)
+    owner = torch.randint(0, world, (n,), generator=torch.Generator().manual_seed(world))
+
+    def fn(device_plan):
+        def body(t):
+            m = owner == t.rank
+            dk = DistributedKNearests(k=16, transport=t, device_plan=device_plan)
+            ids = torch.nonzero(m).flatten().to(torch.int32)
+            r = dk.solve(cloud[m].contiguous().to(cuda), ids.to(cuda))
+            return r.ids.cpu(), r.neighbors.cpu(), r.d2.cpu(), r.stats
+        return run_loopback(world, body)
+
+    a, b = fn(True), fn(False)
+    for (ia, na, da, sa), (ib, nb, db, sb) in zip(a, b):
+        assert torch.equal(ia, ib) and torch.equal(na, nb) and torch.equal(da, db)
+        assert sa["halo_width"] == pytest.approx(sb["halo_width"], rel=1e-12)
+
+
+def test_device_plan_default_ids(cuda):
+    """ids=None: global id = rank offset + local index, generated inside route_scatter."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+
+    world, n, k = 4, 30000, 8
+    cloud = uniform_cloud(n, seed=123)
+    owner = torch.randint(0, world, (n,), generator=torch.Generator().manual_seed(1))
+    parts = [cloud[owner == r].contiguous() for r in range(world)]
+    cat = torch.cat(parts)
+
+    def body(t):
+        r = DistributedKNearests(k=k, transport=t).solve(parts[t.rank].to(cuda))
+        return r.ids.cpu(), r.neighbors.cpu(), r.d2.cpu()
+
+    out = run_loopback(world, body)
+    oi, od = kn.knn_cpu(cat, k, "kdtree")
+    seen = torch.zeros(n, dtype=torch.bool)
+    for ids_r, nb, d2 in out:
+        ids_r = ids_r.long()
+        seen[ids_r] = True
+        assert torch.equal(d2, od[ids_r])
+        same = (nb.long() == oi[ids_r].long()) | (d2.unsqueeze(-1) == od[ids_r].unsqueeze(-2)).any(-1)
+        assert bool(same.all())
+    assert bool(seen.all())
