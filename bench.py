@@ -63,6 +63,22 @@ def brute_check(points: torch.Tensor, idx: torch.Tensor, d2: torch.Tensor, k: in
     return {"checked": int(sel.numel()), "bad_rows": bad}
 
 
+def make_cloud(args, dev, seed_offset: int = 0) -> torch.Tensor:
+    """Synthetic cloud of args.n points: uniform (headline), blue-noise stand-in for the
+    reference's missing *_blue_cube.xyz, clustered, or a .xyz file (--xyz, normalised)."""
+    from cuda_knearests_amd import read_xyz
+    from cuda_knearests_amd.utils import blue_cloud, clustered_cloud, uniform_cloud
+
+    if args.xyz:
+        return read_xyz(args.xyz, normalize=True).to(dev)
+    seed = args.seed + seed_offset
+    if args.gen == "blue":
+        return blue_cloud(args.n, seed=seed, device=dev)
+    if args.gen == "clustered":
+        return clustered_cloud(args.n, seed=seed, device=dev)
+    return uniform_cloud(args.n, seed=seed, device=dev)
+
+
 T_START = time.perf_counter()
 
 
@@ -77,7 +93,8 @@ def run_native(args) -> dict:
 
     C = load()
     dev = torch.device("cuda", 0)
-    pts = uniform_cloud(args.n, seed=args.seed, device=dev)
+    pts = make_cloud(args, dev)
+    args.n = pts.size(0)
     e = C.Engine(args.k, deterministic=not args.nondet)
     log("native eager prepare+solve")
     e.prepare(pts)
@@ -113,7 +130,8 @@ def run_single(args) -> dict:
     from cuda_knearests_amd.utils import uniform_cloud
 
     dev = torch.device("cuda", 0)
-    pts = uniform_cloud(args.n, seed=args.seed, device=dev)
+    pts = make_cloud(args, dev)
+    args.n = pts.size(0)
     kn = KNearests(k=args.k, device=dev, deterministic=not args.nondet)
     log("eager prepare+solve")
     kn.prepare(pts)
@@ -168,7 +186,7 @@ def run_dist(args) -> dict:
         pts = (u * torch.tensor([bhi[a] - blo[a] for a in range(3)], device=dev)
                + torch.tensor(blo, device=dev)).contiguous()
     else:
-        pts = uniform_cloud(args.n, seed=args.seed + 7919 * rank, device=dev)
+        pts = make_cloud(args, dev, 7919 * rank)
     dk = DistributedKNearests(k=args.k)
     res = None
     for _ in range(args.warmup):
@@ -204,6 +222,69 @@ def run_dist(args) -> dict:
     return out
 
 
+def run_loopback_bench(args) -> dict:
+    """W virtual ranks (threads) on ONE GPU, each holding n points of its own box (partitioned
+    layout): the full multi-rank algorithm (device-planned routing, halo exchange through the
+    loopback transport, per-rank build + solve) for clouds of W x n points -- e.g. the 100M / 8
+    configuration on a single device. Time = wall time of a whole W-rank step."""
+    from cuda_knearests_amd.parallel import DistributedKNearests, SpatialDecomposition, run_loopback
+    from cuda_knearests_amd.utils import uniform_cloud
+
+    dev = torch.device("cuda", 0)
+    W = args.loopback
+    shares = []
+    for r in range(W):
+        blo, bhi = SpatialDecomposition(W, (0.0,) * 3, (1000.0,) * 3).rank_box(r)
+        u = uniform_cloud(args.n, seed=args.seed + 7919 * r, device=dev, lo=0.0, hi=1.0)
+        shares.append((u * torch.tensor([bhi[a] - blo[a] for a in range(3)], device=dev)
+                       + torch.tensor(blo, device=dev)).contiguous())
+    log(f"loopback: {W} ranks x {args.n} points")
+    times = []
+
+    def body(t):
+        dk = DistributedKNearests(k=args.k, transport=t)
+        res = None
+        for i in range(args.warmup + args.steps):
+            if i == args.warmup and t.rank == 0:
+                torch.cuda.synchronize()
+                times.append(time.perf_counter())
+            res = dk.solve(shares[t.rank])
+        torch.cuda.synchronize()
+        return res
+
+    out = run_loopback(W, body, timeout=1800)
+    dt = time.perf_counter() - times[0]
+    log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
+    chk = {}
+    if not args.no_check:
+        cloud = torch.cat(shares)
+        bad = checked = 0
+        for res in out[:2]:
+            c = brute_check(cloud, res.neighbors, res.d2, args.k, nsample=128, queries=cloud[res.ids.long()])
+            bad += c["bad_rows"]
+            checked += c["checked"]
+        chk = {"checked": checked, "bad_rows": bad}
+    st = out[0].stats
+    return {"t": dt, "n_total": args.n * W, "check": chk,
+            "stats": {k: st[k] for k in ("n_halo", "halo_width", "rounds", "grid")}}
+
+
+def run_cpu_oracle(args) -> dict:
+    """BASELINE config 1: the CPU kd-tree path (reference kd_tree.cpp semantics, our C++)."""
+    from cuda_knearests_amd import knn_cpu
+    from cuda_knearests_amd.utils import dataset
+
+    if not args.xyz:
+        args.xyz = str(dataset("pts20K.xyz"))
+    pts = make_cloud(args, "cpu")
+    knn_cpu(pts, args.k, "kdtree")  # warm-up (threads, pages)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        knn_cpu(pts, args.k, "kdtree")
+    dt = time.perf_counter() - t0
+    return {"t": dt, "n_total": pts.size(0), "check": {}}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,6 +301,12 @@ def main() -> int:
     ap.add_argument("--dist", action="store_true",
                     help="use the distributed (routing + RCCL) path even at world size 1")
     ap.add_argument("--nondet", action="store_true")
+    ap.add_argument("--gen", choices=["uniform", "blue", "clustered"], default="uniform",
+                    help="synthetic distribution (blue: stand-in for the reference's *_blue_cube.xyz)")
+    ap.add_argument("--xyz", default="", help="read points from a reference-format .xyz file instead")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="W virtual ranks on one GPU (multi-rank algorithm at W x n points)")
+    ap.add_argument("--cpu-oracle", action="store_true", help="time the CPU kd-tree path (BASELINE config 1)")
     args = ap.parse_args()
     if os.environ.get("KN_BENCH_WATCHDOG"):
         import faulthandler
@@ -233,6 +320,19 @@ def main() -> int:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
                "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29517")] + sys.argv
         return subprocess.call(cmd)
+    if args.cpu_oracle or args.loopback:
+        r = run_cpu_oracle(args) if args.cpu_oracle else run_loopback_bench(args)
+        ms = r["t"] / args.steps * 1e3
+        qps = r["n_total"] * args.steps / r["t"]
+        kind = "cpu kd-tree" if args.cpu_oracle else f"loopback{args.loopback}"
+        line = {"metric": "queries/sec", "value": qps, "unit": "queries/s", "n_gpus": 0 if args.cpu_oracle else 1,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+                "dtype": "fp32", "data": args.xyz or f"synthetic {args.gen}",
+                "config": {"model": f"{kind} kNN, {r['n_total']} pts, k={args.k}", "global_batch": r["n_total"],
+                           "seq_len": args.k, "parallelism": "cpu" if args.cpu_oracle else kind},
+                "check": r.get("check", {}), **({"stats": r["stats"]} if "stats" in r else {})}
+        print(json.dumps(line), flush=True)
+        return 0
     if world_env > 1 or args.dist:
         r = run_dist(args)
         if r["rank"] != 0:
@@ -250,8 +350,9 @@ def main() -> int:
     line = {
         "metric": METRIC, "value": qps, "unit": "queries/s", "n_gpus": n_gpus, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": ("synthetic uniform random [0,1000]^3 (seeded per rank" +
-                 (f", {args.layout} layout)" if n_gpus > 1 or args.dist else ")")),
+        "vs_baseline": None, "dtype": "fp32",
+        "data": args.xyz or (f"synthetic {args.gen} random [0,1000]^3 (seeded per rank" +
+                             (f", {args.layout} layout)" if n_gpus > 1 or args.dist else ")")),
         "config": {"model": f"uniform-grid kNN, {args.n} pts/GPU, k={args.k}", "global_batch": r["n_total"],
                    "seq_len": args.k, "parallelism": f"spatial{n_gpus}" if n_gpus > 1 else "single"},
         "vs_cpu_oracle": qps / CPU_ORACLE_QPS, "check": r.get("check", {}), **extra,

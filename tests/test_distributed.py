@@ -151,3 +151,45 @@ def test_loopback_cpu_matches_single(world, gen):
 def test_loopback_cpu_growth_round():
     out = _loopback_check(4, 16, "uniform", "cpu", native=False, halo_factor=0.05)
     assert max(s["rounds"] for *_, s in out) > 1
+
+
+def _transport_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from cuda_knearests_amd.parallel import TorchDistTransport
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    t = TorchDistTransport()
+    cat = t.all_gather_cat(torch.arange(8, dtype=torch.float64) + 100 * rank)
+    # uneven all-to-all: rank r sends (d + 1) rows of value 10 r + d to rank d
+    send = torch.cat([torch.full((d + 1, 4), float(10 * rank + d)) for d in range(world)])
+    out = torch.empty(sum(rank + 1 for _ in range(world)), 4)
+    t.all_to_all_single(out, send, [rank + 1] * world, [d + 1 for d in range(world)])
+    m = torch.tensor([float(rank * 3 % 5)])
+    t.all_reduce_max(m)
+    q.put((rank, cat.numpy().copy(), out.numpy().copy(), float(m.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_torch_transport_collectives():
+    """TorchDistTransport (the RCCL path's collectives) on gloo CPU ranks."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transport_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    exp_cat = torch.cat([torch.arange(8, dtype=torch.float64) + 100 * r for r in range(world)])
+    for rank, cat, recv, m in out:
+        assert torch.equal(torch.from_numpy(cat), exp_cat)
+        exp = torch.cat([torch.full((rank + 1, 4), float(10 * s + rank)) for s in range(world)])
+        assert torch.equal(torch.from_numpy(recv), exp)
+        assert m == max(float(r * 3 % 5) for r in range(world))
