@@ -1381,7 +1381,10 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
     AutoParams p;
     // reference density 3.1 points per cell (knearests.cu:249): measured best for K = 16 and 50
     // on MI355X (scripts/sweep_tiles.py); larger K widen the halo instead of the cells
-    if (!(ppc > 0.f)) ppc = 3.1f;
+    // grid density by K (900K uniform sweep, profiles/sweep_r1_tiles.txt): 3.1 (the reference's
+    // density, knearests.cu:249) is best up to K~24; K=32 prefers 4.0 (-12 %); K=50 prefers 2.5
+    // with the 3-ring halo it implies (-2 %, and no exact-path queries instead of 379)
+    if (!(ppc > 0.f)) ppc = k <= 24 ? 3.1f : (k <= 40 ? 4.0f : 2.5f);
     const double cells = std::max(1.0, (double)n / ppc);
     if (extent && extent[0] > 0 && extent[1] > 0 && extent[2] > 0) {
         const double vol = (double)extent[0] * extent[1] * extent[2];

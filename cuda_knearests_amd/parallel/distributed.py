@@ -80,7 +80,11 @@ class DistResult:
 
 
 class DistributedKNearests:
-    def __init__(self, k: int = 16, group=None, halo_factor: float = 1.6, points_per_cell: float = 0.0,
+    # halo_factor: h = halo_factor x the cloud's mean K-th neighbour radius. Queries on an edge of
+    # the global domain see a quarter ball (radius x 4^(1/3) ~ 1.59); at 1.6 a 100M / 8-rank run
+    # needed a growth round (profiles/bench_suite_r1.jsonl). 2.5 keeps even those at a Poisson
+    # tail ~1e-13 per query for +4 % halo points per rank.
+    def __init__(self, k: int = 16, group=None, halo_factor: float = 2.5, points_per_cell: float = 0.0,
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
                  transport=None, device_plan: bool = True):
         self.k = int(k)
