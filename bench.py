@@ -67,7 +67,7 @@ def make_cloud(args, dev, seed_offset: int = 0) -> torch.Tensor:
     """Synthetic cloud of args.n points: uniform (headline), blue-noise stand-in for the
     reference's missing *_blue_cube.xyz, clustered, or a .xyz file (--xyz, normalised)."""
     from cuda_knearests_amd import read_xyz
-    from cuda_knearests_amd.utils import blue_cloud, clustered_cloud, uniform_cloud
+    from cuda_knearests_amd.utils import blue_cloud, clustered_cloud, surface_cloud, uniform_cloud
 
     if args.xyz:
         return read_xyz(args.xyz, normalize=True).to(dev)
@@ -76,6 +76,8 @@ def make_cloud(args, dev, seed_offset: int = 0) -> torch.Tensor:
         return blue_cloud(args.n, seed=seed, device=dev)
     if args.gen == "clustered":
         return clustered_cloud(args.n, seed=seed, device=dev)
+    if args.gen == "surface":
+        return surface_cloud(args.n, seed=seed, device=dev)
     return uniform_cloud(args.n, seed=seed, device=dev)
 
 
@@ -95,7 +97,7 @@ def run_native(args) -> dict:
     dev = torch.device("cuda", 0)
     pts = make_cloud(args, dev)
     args.n = pts.size(0)
-    e = C.Engine(args.k, deterministic=not args.nondet)
+    e = C.Engine(args.k, deterministic=not args.nondet, adaptive=not args.fixed_grid)
     log("native eager prepare+solve")
     e.prepare(pts)
     e.solve()
@@ -122,7 +124,7 @@ def run_native(args) -> dict:
         sts.append(i["ms_solve"])
     bts.sort(), sts.sort()
     return {"t": dt, "ms_build": bts[2], "ms_solve": sts[2], "info": {"exact_path": cnt[0], "uncertified": cnt[1]},
-            "check": chk, "n_total": args.n}
+            "check": chk, "n_total": args.n, "dims": info0.get("dims")}
 
 
 def run_single(args) -> dict:
@@ -301,9 +303,11 @@ def main() -> int:
     ap.add_argument("--dist", action="store_true",
                     help="use the distributed (routing + RCCL) path even at world size 1")
     ap.add_argument("--nondet", action="store_true")
-    ap.add_argument("--gen", choices=["uniform", "blue", "clustered"], default="uniform",
+    ap.add_argument("--gen", choices=["uniform", "blue", "clustered", "surface"], default="uniform",
                     help="synthetic distribution (blue: stand-in for the reference's *_blue_cube.xyz)")
     ap.add_argument("--xyz", default="", help="read points from a reference-format .xyz file instead")
+    ap.add_argument("--fixed-grid", action="store_true",
+                    help="1 GPU: no occupancy refinement of the grid (the reference's fixed 3.1 pts/cell)")
     ap.add_argument("--loopback", type=int, default=0,
                     help="W virtual ranks on one GPU (multi-rank algorithm at W x n points)")
     ap.add_argument("--cpu-oracle", action="store_true", help="time the CPU kd-tree path (BASELINE config 1)")
@@ -344,6 +348,7 @@ def main() -> int:
         r = run_native(args) if args.path == "native" else run_single(args)
         n_gpus = 1
         extra = {"ms_build": round(r["ms_build"], 4), "ms_solve": round(r["ms_solve"], 4),
+                 "grid": r.get("dims"),
                  "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph, "path": args.path}
     ms = r["t"] / args.steps * 1e3
     qps = r["n_total"] * args.steps / r["t"]

@@ -101,6 +101,14 @@ hipError_t launch_invert_perm(const unsigned* perm, int n, unsigned* inv, hipStr
 
 // Grid-occupancy statistics (reference kn_print_stats, knearests.cu:440-466):
 // out[0]=min, out[1]=max, out[2]=empty cells, out[3..3+hist_len) = histogram of counts.
+// Occupancy-adaptive grid: out[0] = sum over cells of count^2 (= N x the mean occupancy of a
+// point's own cell; a Poisson(l) grid gives N (1 + l)). Clustered clouds and points on surfaces
+// give far more; refine_dims then proposes finer dims (see query.hip).
+hipError_t launch_cell_occupancy(const int* cell_start, int num_cells, unsigned long long* out,
+                                 hipStream_t stream);
+// Finer dims for an over-occupied grid (w = sum count^2 / N), or false if the grid is fine.
+bool refine_dims(const int dims[3], double w, int k, float points_per_cell, int n, int out[3]);
+float default_points_per_cell(int k);
 hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int hist_len,
                              hipStream_t stream);
 

@@ -61,6 +61,7 @@ typedef struct {
     int device;              /* HIP device ordinal                                        */
     int verbose;             /* 0 silent, 1 timings (reference IF_VERBOSE), 2 debug        */
     int exact_only;          /* 1 -> skip the LDS tile kernel (exact ring walk for all)      */
+    int fixed_grid;          /* 1 -> no occupancy refinement of the grid (clusters/surfaces) */
 } kn_config;
 
 /* Per-solve statistics (reference kn_print_stats + cell_max, knearests.cu:378-466). */

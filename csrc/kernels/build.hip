@@ -219,6 +219,22 @@ __global__ __launch_bounds__(256) void cell_sort_kernel(const int* __restrict__ 
     }
 }
 
+__global__ __launch_bounds__(256) void cell_occupancy_kernel(const int* __restrict__ cell_start, int num_cells,
+                                                             unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0;
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < num_cells; c += gridDim.x * blockDim.x) {
+        const unsigned long long cnt = (unsigned long long)(cell_start[c + 1] - cell_start[c]);
+        acc += cnt * cnt;
+    }
+    // wave reduction (two 32-bit halves through DPP-free shuffles), then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)acc, off, 64);
+        const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(acc >> 32), off, 64);
+        acc += ((unsigned long long)hi << 32) | lo;
+    }
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
 __global__ __launch_bounds__(256) void cell_stats_kernel(const int* __restrict__ cell_start,
                                                          int num_cells, int* __restrict__ out,
                                                          int hist_len) {
@@ -266,6 +282,16 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
 }
 
 KN_DEFINE_DEBUG_READER(debug_words_build)
+
+hipError_t launch_cell_occupancy(const int* cell_start, int num_cells, unsigned long long* out, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(out, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+    if (num_cells > 0) {
+        const unsigned grid = std::max(1u, std::min(cdiv(num_cells, 256 * 8), 2048u));
+        cell_occupancy_kernel<<<grid, 256, 0, s>>>(cell_start, num_cells, out);
+    }
+    return hipGetLastError();
+}
 
 hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int hist_len,
                              hipStream_t s) {

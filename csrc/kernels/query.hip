@@ -1376,6 +1376,21 @@ int lds_capacity_for(double staged) {
     return std::max(128, std::min(cap, 8192));
 }
 
+float default_points_per_cell(int k) { return k <= 24 ? 3.1f : (k <= 40 ? 4.0f : 2.5f); }
+
+bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3]) {
+    if (!(ppc > 0.f)) ppc = default_points_per_cell(k);
+    const double wt = 1.0 + ppc;  // a Poisson grid at the target density
+    if (!(w > 2.0 * wt) || n <= 0) return false;
+    double f = std::cbrt(w / wt);
+    const double c0 = (double)dims[0] * dims[1] * dims[2];
+    const double cmax = std::min(4.0e8, std::max(16.0 * n, 1048576.0));  // cell_start <= 64 B/point
+    if (c0 * f * f * f > cmax) f = std::cbrt(cmax / c0);
+    if (f < 1.2) return false;
+    for (int a = 0; a < 3; ++a) out[a] = std::max(1, (int)std::ceil(dims[a] * f));
+    return true;
+}
+
 AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_hint,
                        const float* extent) {
     AutoParams p;
@@ -1384,7 +1399,7 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
     // grid density by K (900K uniform sweep, profiles/sweep_r1_tiles.txt): 3.1 (the reference's
     // density, knearests.cu:249) is best up to K~24; K=32 prefers 4.0 (-12 %); K=50 prefers 2.5
     // with the 3-ring halo it implies (-2 %, and no exact-path queries instead of 379)
-    if (!(ppc > 0.f)) ppc = k <= 24 ? 3.1f : (k <= 40 ? 4.0f : 2.5f);
+    if (!(ppc > 0.f)) ppc = default_points_per_cell(k);
     const double cells = std::max(1.0, (double)n / ppc);
     if (extent && extent[0] > 0 && extent[1] > 0 && extent[2] > 0) {
         const double vol = (double)extent[0] * extent[1] * extent[2];

@@ -51,7 +51,7 @@ kn_status Engine::check(hipError_t e, const char* what) {
                 std::string(what) + ": " + hipGetErrorString(e));
 }
 
-kn_status Engine::allocate(int n, const int* dims_override) {
+kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
     if (n < 0) return fail(KN_ERR_INVALID_ARGUMENT, "negative point count");
     if (cfg_.k < 1 || cfg_.k > KN_MAX_K) return fail(KN_ERR_INVALID_ARGUMENT, "k out of range [1,128]");
     kn_status st;
@@ -62,7 +62,11 @@ kn_status Engine::allocate(int n, const int* dims_override) {
             if ((st = check(hipEventCreate(&e), "hipEventCreate")) != KN_OK) return st;
     }
     ap_ = auto_params(n, cfg_.k, cfg_.points_per_cell, cfg_.tile, cfg_.halo, nullptr);
-    if (dims_override) {
+    if (dims_override && refined) {
+        // occupancy refinement: finer cells, same tile / halo / LDS plan (occupied cells keep
+        // about the target density)
+        for (int a = 0; a < 3; ++a) ap_.dims[a] = std::max(1, dims_override[a]);
+    } else if (dims_override) {
         for (int a = 0; a < 3; ++a) ap_.dims[a] = std::max(1, dims_override[a]);
         const double ppc = (double)std::max(1, n) / ((double)ap_.dims[0] * ap_.dims[1] * ap_.dims[2]);
         const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
@@ -82,6 +86,7 @@ kn_status Engine::allocate(int n, const int* dims_override) {
     bytes += align_up((size_t)n * sizeof(float4));
     bytes += 2 * align_up((size_t)n * sizeof(unsigned));
     bytes += align_up(kNumCounters * sizeof(unsigned));
+    bytes += align_up(sizeof(unsigned long long));
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (bytes > arena_bytes_) {
         if (arena_) (void)hipFree(arena_);
@@ -102,6 +107,7 @@ kn_status Engine::allocate(int n, const int* dims_override) {
     perm_ = carve<unsigned>(p, n);
     fallback_ = carve<unsigned>(p, n);
     counters_ = carve<unsigned>(p, kNumCounters);
+    occ_ = carve<unsigned long long>(p, 1);
     // outputs
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
                      (void**)&dist_stored_})
@@ -167,37 +173,48 @@ QueryBuffers Engine::query_buffers() const {
 kn_status Engine::build_async() { return check(launch_build(build_buffers(), stream_), "build"); }
 kn_status Engine::query_async() { return check(launch_query(query_buffers(), stream_), "query"); }
 
-kn_status Engine::prepare_host(const float* pts, int n) {
+kn_status Engine::occupancy(double* w) {
+    unsigned long long s = 0;
     kn_status st;
-    if (!pts && n > 0) return fail(KN_ERR_INVALID_ARGUMENT, "null points");
-    if ((st = allocate(n)) != KN_OK) return st;
-    if (n > 0 && (st = check(hipMemcpyAsync(points_, pts, (size_t)n * 12, hipMemcpyHostToDevice, stream_),
-                             "H2D points")) != KN_OK)
+    if ((st = check(launch_cell_occupancy(cell_start_, C_, occ_, stream_), "occupancy")) != KN_OK) return st;
+    if ((st = check(hipMemcpyAsync(&s, occ_, sizeof(s), hipMemcpyDeviceToHost, stream_), "D2H occupancy")) != KN_OK)
         return st;
-    (void)hipEventRecord(ev_[0], stream_);
-    if ((st = build_async()) != KN_OK) return st;
-    (void)hipEventRecord(ev_[1], stream_);
-    if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
-    (void)hipEventElapsedTime(&ms_build_, ev_[0], ev_[1]);
+    if ((st = check(hipStreamSynchronize(stream_), "occupancy sync")) != KN_OK) return st;
+    *w = n_ > 0 ? (double)s / n_ : 0.0;
+    return KN_OK;
+}
+
+// Upload + build; with cfg_.adaptive, re-bin with finer cells while the mean occupancy of a
+// point's cell is far above a Poisson grid's (at most 3 refinements, cell_start <= 64 B/point).
+kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
+    kn_status st;
+    if (!src && n > 0) return fail(KN_ERR_INVALID_ARGUMENT, "null points");
+    if ((st = allocate(n)) != KN_OK) return st;
+    for (int round = 0;; ++round) {
+        if (n > 0 && (st = check(hipMemcpyAsync(points_, src, (size_t)n * 12, kind, stream_), "copy points")) != KN_OK)
+            return st;
+        (void)hipEventRecord(ev_[0], stream_);
+        if ((st = build_async()) != KN_OK) return st;
+        (void)hipEventRecord(ev_[1], stream_);
+        if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
+        (void)hipEventElapsedTime(&ms_build_, ev_[0], ev_[1]);
+        if (!cfg_.adaptive || round == 3 || n == 0) break;
+        double w = 0.0;
+        if ((st = occupancy(&w)) != KN_OK) return st;
+        int nd[3];
+        if (!refine_dims(ap_.dims, w, cfg_.k, cfg_.points_per_cell, n, nd)) break;
+        if (cfg_.verbose)
+            fprintf(stderr, "kn: cell occupancy %.1f -> grid %dx%dx%d\n", w, nd[0], nd[1], nd[2]);
+        if ((st = allocate(n, nd, true)) != KN_OK) return st;
+    }
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
     built_ = true;
     return KN_OK;
 }
 
-kn_status Engine::prepare_device(const float* d_pts, int n) {
-    kn_status st;
-    if ((st = allocate(n)) != KN_OK) return st;
-    if (n > 0 && (st = check(hipMemcpyAsync(points_, d_pts, (size_t)n * 12, hipMemcpyDeviceToDevice, stream_),
-                             "D2D points")) != KN_OK)
-        return st;
-    (void)hipEventRecord(ev_[0], stream_);
-    if ((st = build_async()) != KN_OK) return st;
-    (void)hipEventRecord(ev_[1], stream_);
-    if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
-    (void)hipEventElapsedTime(&ms_build_, ev_[0], ev_[1]);
-    built_ = true;
-    return KN_OK;
-}
+kn_status Engine::prepare_host(const float* pts, int n) { return prepare_from(pts, n, hipMemcpyHostToDevice); }
+
+kn_status Engine::prepare_device(const float* d_pts, int n) { return prepare_from(d_pts, n, hipMemcpyDeviceToDevice); }
 
 kn_status Engine::upload_device(const float* d_pts, int n) {
     kn_status st;
@@ -240,7 +257,10 @@ kn_status Engine::set_k(int k) {
     ap_.tile[0] = np.tile[0]; ap_.tile[1] = np.tile[1]; ap_.tile[2] = np.tile[2];
     ap_.halo = np.halo;
     {
-        const double ppc = (double)n_ / std::max(1, C_);
+        // occupied cells hold about the target density (refined grids have many empty cells)
+        const double ppc = std::max((double)n_ / std::max(1, C_),
+                                    (double)(cfg_.points_per_cell > 0.f ? cfg_.points_per_cell
+                                                                        : default_points_per_cell(k)));
         const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
                               (ap_.tile[2] + 2 * ap_.halo) * ppc;
         ap_.lds_capacity = lds_capacity_for(staged);

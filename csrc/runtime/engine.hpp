@@ -27,6 +27,7 @@ struct EngineConfig {
     int verbose = 0;
     int use_tiles = 1;
     int with_distances = 1;
+    int adaptive = 1;  // refine the grid when cells are over-occupied (clusters, surfaces)
 };
 
 class Engine {
@@ -83,7 +84,9 @@ public:
 private:
     kn_status fail(kn_status s, const std::string& msg);
     kn_status check(hipError_t e, const char* what);
-    kn_status allocate(int n, const int* dims_override = nullptr);
+    kn_status allocate(int n, const int* dims_override = nullptr, bool refined = false);
+    kn_status prepare_from(const float* src, int n, hipMemcpyKind kind);
+    kn_status occupancy(double* w);
     kn_status build_async();
     kn_status query_async();
     QueryBuffers query_buffers() const;
@@ -111,6 +114,7 @@ private:
     unsigned* perm_ = nullptr;
     unsigned* fallback_ = nullptr;
     unsigned* counters_ = nullptr;
+    unsigned long long* occ_ = nullptr;
     // outputs (re-allocated when K changes)
     unsigned* out_idx_ = nullptr;
     float* out_dist_ = nullptr;

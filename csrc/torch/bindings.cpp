@@ -341,6 +341,27 @@ std::vector<torch::Tensor> route_unpack(torch::Tensor recv, std::vector<int64_t>
     return {pts, gids};
 }
 
+// occupancy-adaptive grid: sum over cells of count^2 (int64, on device, no sync)
+torch::Tensor occupancy(torch::Tensor cell_start) {
+    TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32 && cell_start.is_contiguous() &&
+                    cell_start.numel() >= 1,
+                "cell_start must be a contiguous int32 GPU tensor of C + 1 entries");
+    const c10::DeviceGuard guard(cell_start.device());
+    auto out = torch::empty({1}, cell_start.options().dtype(torch::kInt64));
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_cell_occupancy(cell_start.data_ptr<int>(), (int)cell_start.numel() - 1,
+                                           reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), s));
+    return out;
+}
+
+py::object refine_dims(std::vector<int64_t> dims, double w, int64_t k, double ppc, int64_t n) {
+    TORCH_CHECK(dims.size() == 3, "dims must have 3 entries");
+    const int d[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
+    int out[3];
+    if (!kn::refine_dims(d, w, (int)k, (float)ppc, (int)n, out)) return py::none();
+    return py::cast(std::vector<int64_t>{out[0], out[1], out[2]});
+}
+
 // -> (8,) float64 {lo[3], hi[3], n, 0} of this rank's points (one kernel pass, no host sync)
 torch::Tensor local_meta(torch::Tensor points) {
     check_points(points, true);
@@ -357,7 +378,7 @@ torch::Tensor local_meta(torch::Tensor points) {
 class PyEngine {
 public:
     PyEngine(int64_t k, double ppc, std::vector<int64_t> tile, int64_t halo, bool deterministic, bool use_tiles,
-             bool with_dist, int64_t device) {
+             bool with_dist, int64_t device, bool adaptive) {
         kn::EngineConfig c;
         c.k = (int)k;
         c.points_per_cell = (float)ppc;
@@ -365,6 +386,7 @@ public:
         c.halo = (int)halo;
         c.deterministic = deterministic ? 1 : 0;
         c.use_tiles = use_tiles ? 1 : 0;
+        c.adaptive = adaptive ? 1 : 0;
         c.with_distances = with_dist ? 1 : 0;
         c.device = (int)device;
         e_ = std::make_unique<kn::Engine>(c);
@@ -506,6 +528,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
+    m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");
+    m.def("refine_dims", &refine_dims, "finer grid dims for an over-occupied grid, or None");
     m.def("local_meta", &local_meta, "multi-GPU: {lo[3], hi[3], n, 0} of the local points (float64, on device)");
     m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts");
     m.def("route_plan", &route_plan, "multi-GPU: device-side routing plan from the gathered metas (no host sync)");
@@ -516,10 +540,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")
-        .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t>(), py::arg("k") = 16,
-             py::arg("points_per_cell") = 0.0, py::arg("tile") = std::vector<int64_t>{}, py::arg("halo") = 0,
-             py::arg("deterministic") = true, py::arg("use_tiles") = true, py::arg("with_dist") = true,
-             py::arg("device") = 0)
+        .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t, bool>(),
+             py::arg("k") = 16, py::arg("points_per_cell") = 0.0, py::arg("tile") = std::vector<int64_t>{},
+             py::arg("halo") = 0, py::arg("deterministic") = true, py::arg("use_tiles") = true,
+             py::arg("with_dist") = true, py::arg("device") = 0, py::arg("adaptive") = true)
         .def("prepare", &PyEngine::prepare)
         .def("prepare_async", &PyEngine::prepare_async)
         .def("solve", &PyEngine::solve)

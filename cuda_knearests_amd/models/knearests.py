@@ -77,7 +77,7 @@ class KNearests:
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
         self.grid = ops.build_grid(self.points, self.k, plan=self.plan(self.points.size(0)),
-                                   deterministic=self.deterministic)
+                                   deterministic=self.deterministic, adaptive=True)
         t1.record()
         t1.synchronize()
         self.timings["ms_build"] = t0.elapsed_time(t1)
@@ -148,6 +148,7 @@ class KNearests:
             self._graph = load().Engine(self.k, self.points_per_cell, list(self.tile), self.halo,
                                         self.deterministic, self.use_tiles, True, self.device.index or 0)
             self._graph_n = pts.size(0)
+            self._graph.prepare(pts)  # eager first build: decides the (occupancy-adaptive) grid
         # the engine keeps its own copy of the input, so every step re-uploads (D2D) + replays
         self._graph.prepare_async(pts)
         self._graph.launch_graph(1)

@@ -67,8 +67,13 @@ def _check_gpu_points(points: torch.Tensor) -> torch.Tensor:
 
 def build_grid(points: torch.Tensor, k: int = 16, plan: Optional[Plan] = None,
                points_per_cell: float = 0.0, deterministic: bool = True,
-               box: Optional[Sequence[float]] = None) -> Grid:
-    """Bin ``points`` (N,3 float32, GPU) into a uniform grid (bbox, count, scan, scatter)."""
+               box: Optional[Sequence[float]] = None, adaptive: bool = False) -> Grid:
+    """Bin ``points`` (N,3 float32, GPU) into a uniform grid (bbox, count, scan, scatter).
+
+    ``adaptive``: measure the mean occupancy of a point's cell (one small reduction + one host
+    sync) and re-bin with finer cells while it is far above a Poisson grid's (clustered clouds,
+    points on surfaces); tile / halo / LDS plan stay those of the target density. Not for use
+    inside graph capture (it synchronises)."""
     points = _check_gpu_points(points)
     n = points.size(0)
     if plan is None:
@@ -76,8 +81,16 @@ def build_grid(points: torch.Tensor, k: int = 16, plan: Optional[Plan] = None,
         if box is not None:
             extent = [box[3] - box[0], box[4] - box[1], box[5] - box[2]]
         plan = Plan.auto(n, k, points_per_cell, extent=extent)
-    s, cs, perm, geom = load().build(points, list(plan.dims), bool(deterministic),
-                                     list(map(float, box)) if box is not None else None)
+    C = load()
+    bx = list(map(float, box)) if box is not None else None
+    s, cs, perm, geom = C.build(points, list(plan.dims), bool(deterministic), bx)
+    for _ in range(3 if adaptive and n > 0 else 0):
+        w = int(C.occupancy(cs).item()) / n
+        dims = C.refine_dims(list(plan.dims), w, int(k), float(points_per_cell), n)
+        if dims is None:
+            break
+        plan = Plan(list(dims), list(plan.tile), plan.halo, plan.lds_capacity, plan.lds_bytes)
+        s, cs, perm, geom = C.build(points, list(plan.dims), bool(deterministic), bx)
     return Grid(s, cs, perm, geom, plan, n)
 
 
@@ -105,9 +118,9 @@ def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[
 
 
 def knn(points: torch.Tensor, k: int = 16, points_per_cell: float = 0.0, deterministic: bool = True,
-        use_tiles: bool = True, with_dist: bool = True):
+        use_tiles: bool = True, with_dist: bool = True, adaptive: bool = True):
     """All-points k-nearest neighbours on the GPU. Returns ``(idx int32 (N,k), d2 float32 (N,k))``."""
-    g = build_grid(points, k, points_per_cell=points_per_cell, deterministic=deterministic)
+    g = build_grid(points, k, points_per_cell=points_per_cell, deterministic=deterministic, adaptive=adaptive)
     return query(g, k, use_tiles=use_tiles, with_dist=with_dist)
 
 

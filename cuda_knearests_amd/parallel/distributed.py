@@ -206,8 +206,10 @@ class DistributedKNearests:
                 bc, totals = C.route_count_dev(src_pts, plan, world)
                 recv_tot = torch.empty_like(totals)
                 self.comm.all_to_all_single(recv_tot, totals)
-                host = torch.cat([hdr, totals.flatten().double(), recv_tot.flatten().double()]).cpu()  # sync 1
-                hv = host.tolist()
+                # sync 1: plan header (f64 viewed as int32 pairs) + both count tables, one copy
+                host = torch.cat([hdr.view(torch.int32), totals.flatten(), recv_tot.flatten()]).cpu()
+                nh = 2 * hdr.numel()
+                hv = host[:nh].view(torch.float64).tolist() + host[nh:].tolist()
                 lo, hi = tuple(hv[0:3]), tuple(hv[3:6])
                 want = factor3(world, tuple(max(hi[a] - lo[a], 1e-30) for a in range(3)))
                 if want == tuple(grid):

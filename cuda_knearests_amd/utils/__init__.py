@@ -52,6 +52,20 @@ def clustered_cloud(n: int, seed: int = 0, device="cpu") -> torch.Tensor:
     return pts.clamp(0, 1000).to(device)
 
 
+def surface_cloud(n: int, seed: int = 0, device="cpu") -> torch.Tensor:
+    """Points on 2-D surfaces in the [0,1000]^3 cube (a sphere and a tilted plane), the shape of
+    scanned / meshed data: a uniform 3-D grid over the bbox puts tens of points in every
+    occupied cell (the occupancy-adaptive grid refines it)."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    ns = n * 2 // 3
+    v = torch.randn((ns, 3), generator=g)
+    sphere = 500 + 400 * v / v.norm(dim=1, keepdim=True)
+    uv = torch.rand((n - ns, 2), generator=g) * 1000
+    plane = torch.stack([uv[:, 0], uv[:, 1], 200 + 0.3 * uv[:, 0] + 0.1 * uv[:, 1]], 1)
+    return torch.cat([sphere, plane]).clamp(0, 1000).to(device)
+
+
 class Stopwatch:
     """RAII wall-clock timer (reference stopwatch.h:11-43, but monotonic and sub-ms):
     prints ``task...`` on entry and ``task: X ms`` on exit; ``tick()`` prints deltas."""

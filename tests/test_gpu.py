@@ -185,3 +185,76 @@ def test_cli_reference_flow(cuda):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert '"ok": true' in r.stdout
+
+
+@pytest.mark.parametrize("k", [16, 50])
+def test_halo1_certification_and_fallback(cuda, k):
+    """force a 1-ring halo -> many tile queries cannot be certified and must be
+    finished by the exact kernel; results stay exact."""
+    p = uniform_cloud(30000, seed=500 + k, device=cuda)
+    plan = kn.Plan.auto(p.size(0), k, halo=1)
+    assert plan.halo == 1
+    g = kn.build_grid(p, k, plan=plan)
+    idx, d2, info = kn.query(g, k, return_info=True)
+    assert int(info["counters"][0]) > 0, "expected exact-path queries with a 1-ring halo"
+    _assert_matches_oracle(p, idx, d2, k)
+
+
+def test_grid_layout_and_cell_mapping(cuda):
+    """Binning invariants: cell_start is an exclusive scan of per-cell counts (monotone, ends at
+    N), perm is a bijection, every stored point lies in the cell range its coordinates map to
+    (same fp32 arithmetic as the kernels), cells are ordered by original index (deterministic),
+    and points exactly on the bounding box land in valid edge cells."""
+    n = 50000
+    p = uniform_cloud(n, seed=5, device=cuda)
+    p[0] = torch.tensor([0.0, 0.0, 0.0], device=cuda)
+    p[1] = torch.tensor([1000.0, 1000.0, 1000.0], device=cuda)
+    p[2] = torch.tensor([0.0, 1000.0, 500.0], device=cuda)
+    g = kn.build_grid(p, 16)
+    cs = g.cell_start.cpu().long()
+    assert cs[0] == 0 and cs[-1] == n and bool((cs[1:] >= cs[:-1]).all())
+    perm = g.perm.cpu().long()
+    assert torch.equal(torch.sort(perm).values, torch.arange(n))
+    srt = g.sorted.cpu()
+    assert torch.equal(srt[:, :3], p.cpu()[perm])
+    assert torch.equal(srt[:, 3].contiguous().view(torch.int32).long(), perm)
+    geom = g.geom.cpu()
+    f = geom.view(torch.float32)
+    origin, inv = f[0:3], f[6:9]
+    dims = geom[10:13].long()
+    c = torch.floor(torch.minimum(torch.maximum((srt[:, :3] - origin) * inv, torch.tensor(-1.0)), dims.float()))
+    c = torch.minimum(torch.maximum(c.long(), torch.zeros(3, dtype=torch.long)), dims - 1)
+    cell = c[:, 0] + dims[0] * (c[:, 1] + dims[1] * c[:, 2])
+    pos = torch.arange(n)
+    assert bool(((cs[cell] <= pos) & (pos < cs[cell + 1])).all()), "stored point outside its cell range"
+    same = cell[1:] == cell[:-1]
+    assert bool((perm[1:][same] > perm[:-1][same]).all()), "cells not ordered by original index"
+
+
+@pytest.mark.parametrize("gen", ["surface", "clustered"])
+def test_occupancy_adaptive_grid(cuda, ext, gen):
+    """Over-occupied grids (points on surfaces, dense clusters) are re-binned with finer cells;
+    results stay exact and far fewer queries spill to the exact kernel."""
+    from cuda_knearests_amd.utils import surface_cloud
+
+    mk = surface_cloud if gen == "surface" else clustered_cloud
+    p = mk(60000, seed=11).to(cuda)
+    g0 = kn.build_grid(p, 16)
+    g1 = kn.build_grid(p, 16, adaptive=True)
+    w0 = int(ext.occupancy(g0.cell_start).item()) / p.size(0)
+    w1 = int(ext.occupancy(g1.cell_start).item()) / p.size(0)
+    c0 = g0.plan.dims[0] * g0.plan.dims[1] * g0.plan.dims[2]
+    c1 = g1.plan.dims[0] * g1.plan.dims[1] * g1.plan.dims[2]
+    assert c1 > c0 and w1 < w0, (g0.plan.dims, g1.plan.dims, w0, w1)
+    i0, d0, info0 = kn.query(g0, 16, return_info=True)
+    i1, d1, info1 = kn.query(g1, 16, return_info=True)
+    assert int(info1["counters"][0]) < int(info0["counters"][0])
+    _assert_matches_oracle(p, i1, d1, 16)
+    assert torch.equal(d0, d1)
+
+
+def test_uniform_grid_not_refined(cuda):
+    p = uniform_cloud(100000, seed=3, device=cuda)
+    g0 = kn.build_grid(p, 16)
+    g1 = kn.build_grid(p, 16, adaptive=True)
+    assert g0.plan.dims == g1.plan.dims

@@ -1,0 +1,14 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp PYTHONPATH=$PWD
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; grep -E "FAIL|Error|assert" gpurun_out/pytest_gpu.log | head -20; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+: > gpurun_out/adapt.jsonl
+for g in surface clustered; do
+  for f in "" "--fixed-grid"; do
+    timeout -k 10 300 python bench.py --gen $g --n 900000 --k 16 --steps 10 --warmup 2 $f > gpurun_out/_a.json 2> gpurun_out/adapt.err || { echo BENCH_FAIL $g $f; tail -5 gpurun_out/adapt.err; exit 1; }
+    tail -1 gpurun_out/_a.json >> gpurun_out/adapt.jsonl
+  done
+done
+cut -c1-400 gpurun_out/adapt.jsonl
