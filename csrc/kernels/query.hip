@@ -1114,31 +1114,59 @@ __global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
         top.init(nullptr);
         const int rmax = max(max(max(cx, a.X - 1 - cx), max(cy, a.Y - 1 - cy)), max(cz, a.Z - 1 - cz));
         bool certified = false;
+        bool dense = true;  // ring 0 is one row: candidate-parallel
         for (int r = 0; r <= rmax; ++r) {
             const int z0 = max(0, cz - r), z1 = min(a.Z - 1, cz + r);
             const int y0 = max(0, cy - r), y1 = min(a.Y - 1, cy + r);
             const int ny = y1 - y0 + 1, nrows = (z1 - z0 + 1) * ny;
-            for (int tr = lane; tr < nrows; tr += 64) {  // rows of the block dealt to the lanes
+            // stored range of part `part` of shell row `tr` (rows on the shell's y/z faces are
+            // whole x-runs, interior rows contribute their two x-end cells)
+            auto seg = [&](int tr, int part, int& p0, int& p1) -> bool {
                 const int z = z0 + tr / ny, y = y0 + tr % ny;
                 const bool shell = (z == cz - r) || (z == cz + r) || (y == cy - r) || (y == cy + r);
+                if (!shell && part == 1 && r == 0) return false;
+                if (shell && part == 1) return false;
+                int xa, xb;
+                if (shell) { xa = max(0, cx - r); xb = min(a.X - 1, cx + r); }
+                else if (part == 0) { xa = cx - r; xb = cx - r; }
+                else { xa = cx + r; xb = cx + r; }
+                if (xa < 0 || xb > a.X - 1 || xa > xb) return false;
                 const int rowc = (z * a.Y + y) * a.X;
-                for (int part = 0; part < (shell ? 1 : 2); ++part) {
-                    int xa, xb;
-                    if (shell) { xa = max(0, cx - r); xb = min(a.X - 1, cx + r); }
-                    else if (part == 0) { xa = cx - r; xb = cx - r; }
-                    else { xa = cx + r; xb = cx + r; }
-                    if (xa < 0 || xb > a.X - 1 || xa > xb) continue;
-                    const int p0 = a.cell_start[KN_IDX(rowc + xa, a.X * a.Y * a.Z + 1, 303)];
-                    const int p1 = a.cell_start[KN_IDX(rowc + xb + 1, a.X * a.Y * a.Z + 1, 303)];
-                    for (int p = p0; p < p1; ++p) {
-                        if ((unsigned)p == sidx) continue;
-                        const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
-                        const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
-                        const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                        const unsigned id = __float_as_uint(c.w);
-                        if (top.improves(d2, id)) top.insert(d2, id);
+                p0 = a.cell_start[KN_IDX(rowc + xa, a.X * a.Y * a.Z + 1, 303)];
+                p1 = a.cell_start[KN_IDX(rowc + xb + 1, a.X * a.Y * a.Z + 1, 303)];
+                return p0 < p1;
+            };
+            auto test = [&](int p) {
+                if ((unsigned)p == sidx) return;
+                const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
+                const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
+                const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                const unsigned id = __float_as_uint(c.w);
+                if (top.improves(d2, id)) top.insert(d2, id);
+            };
+            if (dense) {
+                // dense shells (clusters; always ring 0, a single row): candidate-parallel --
+                // each row's points are dealt to the 64 lanes (coalesced) instead of one lane
+                // walking a long row while the others idle
+                unsigned pts = 0;
+                for (int tr = 0; tr < nrows; ++tr)
+                    for (int part = 0; part < 2; ++part) {
+                        int p0, p1;
+                        if (!seg(tr, part, p0, p1)) continue;
+                        pts += (unsigned)(p1 - p0);
+                        for (int p = p0 + lane; p < p1; p += 64) test(p);
                     }
-                }
+                dense = pts > 32u * (unsigned)nrows;  // the next shell is probably alike
+            } else {
+                unsigned pts = 0;  // rows of the shell dealt to the lanes
+                for (int tr = lane; tr < nrows; tr += 64)
+                    for (int part = 0; part < 2; ++part) {
+                        int p0, p1;
+                        if (!seg(tr, part, p0, p1)) continue;
+                        pts += (unsigned)(p1 - p0);
+                        for (int p = p0; p < p1; ++p) test(p);
+                    }
+                dense = wave_sum_u32(pts) > 32u * (unsigned)nrows;
             }
             float m = INFINITY;
             if (cx - r > 0) m = fminf(m, qx - (g.origin[0] + (cx - r) * g.cell[0]));
