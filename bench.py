@@ -97,7 +97,7 @@ def run_native(args) -> dict:
     dev = torch.device("cuda", 0)
     pts = make_cloud(args, dev)
     args.n = pts.size(0)
-    e = C.Engine(args.k, deterministic=not args.nondet, adaptive=not args.fixed_grid)
+    e = C.Engine(args.k, deterministic=args.deterministic, adaptive=not args.fixed_grid)
     log("native eager prepare+solve")
     e.prepare(pts)
     e.solve()
@@ -134,7 +134,7 @@ def run_single(args) -> dict:
     dev = torch.device("cuda", 0)
     pts = make_cloud(args, dev)
     args.n = pts.size(0)
-    kn = KNearests(k=args.k, device=dev, deterministic=not args.nondet)
+    kn = KNearests(k=args.k, device=dev, deterministic=args.deterministic)
     log("eager prepare+solve")
     kn.prepare(pts)
     kn.solve()  # eager pass: plan + per-phase device timings + counters
@@ -189,7 +189,7 @@ def run_dist(args) -> dict:
                + torch.tensor(blo, device=dev)).contiguous()
     else:
         pts = make_cloud(args, dev, 7919 * rank)
-    dk = DistributedKNearests(k=args.k)
+    dk = DistributedKNearests(k=args.k, deterministic=args.deterministic)
     res = None
     for _ in range(args.warmup):
         res = dk.solve(pts, partitioned=args.layout == "partitioned")
@@ -302,7 +302,10 @@ def main() -> int:
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--dist", action="store_true",
                     help="use the distributed (routing + RCCL) path even at world size 1")
-    ap.add_argument("--nondet", action="store_true")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="sort every cell by original index: reproducible STORED order (reference-API "
+                         "getters); original-space results are bit-identical either way "
+                         "(tests/test_gpu.py::test_in_cell_order_does_not_change_results)")
     ap.add_argument("--gen", choices=["uniform", "blue", "clustered", "surface"], default="uniform",
                     help="synthetic distribution (blue: stand-in for the reference's *_blue_cube.xyz)")
     ap.add_argument("--xyz", default="", help="read points from a reference-format .xyz file instead")
@@ -360,7 +363,8 @@ def main() -> int:
                              (f", {args.layout} layout)" if n_gpus > 1 or args.dist else ")")),
         "config": {"model": f"uniform-grid kNN, {args.n} pts/GPU, k={args.k}", "global_batch": r["n_total"],
                    "seq_len": args.k, "parallelism": f"spatial{n_gpus}" if n_gpus > 1 else "single"},
-        "vs_cpu_oracle": qps / CPU_ORACLE_QPS, "check": r.get("check", {}), **extra,
+        "vs_cpu_oracle": qps / CPU_ORACLE_QPS, "check": r.get("check", {}), "in_cell_sort": args.deterministic,
+        **extra,
     }
     print(json.dumps(line), flush=True)
     return 0

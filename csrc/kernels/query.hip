@@ -1404,7 +1404,11 @@ int lds_capacity_for(double staged) {
     return std::max(128, std::min(cap, 8192));
 }
 
-float default_points_per_cell(int k) { return k <= 24 ? 3.1f : (k <= 40 ? 4.0f : 2.5f); }
+// Target density after whole-tile rounding (900K uniform sweeps on MI355X,
+// profiles/sweep_r1_tiles*.txt): K <= 40 is fastest at ~3.4 points/cell (64^3 for 900K: K=16
+// 0.503 ms vs 0.542 at 68^3 and 0.635 at 60^3; K=32 1.165 ms); K = 50 at ~2.9 (68^3, 2-ring
+// halo: 2.21 ms vs 2.37 at 72^3 with 3 rings). The reference uses 3.1 (knearests.cu:249).
+float default_points_per_cell(int k) { return k <= 40 ? 3.4f : 2.9f; }
 
 bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3]) {
     if (!(ppc > 0.f)) ppc = default_points_per_cell(k);
@@ -1415,32 +1419,36 @@ bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3
     const double cmax = std::min(4.0e8, std::max(16.0 * n, 1048576.0));  // cell_start <= 64 B/point
     if (c0 * f * f * f > cmax) f = std::cbrt(cmax / c0);
     if (f < 1.2) return false;
-    for (int a = 0; a < 3; ++a) out[a] = std::max(1, (int)std::ceil(dims[a] * f));
+    for (int a = 0; a < 3; ++a) out[a] = std::max(4, (int)std::ceil(dims[a] * f / 4.0) * 4);  // whole 4-cell tiles
     return true;
 }
 
 AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_hint,
                        const float* extent) {
     AutoParams p;
-    // reference density 3.1 points per cell (knearests.cu:249): measured best for K = 16 and 50
-    // on MI355X (scripts/sweep_tiles.py); larger K widen the halo instead of the cells
-    // grid density by K (900K uniform sweep, profiles/sweep_r1_tiles.txt): 3.1 (the reference's
-    // density, knearests.cu:249) is best up to K~24; K=32 prefers 4.0 (-12 %); K=50 prefers 2.5
-    // with the 3-ring halo it implies (-2 %, and no exact-path queries instead of 379)
     if (!(ppc > 0.f)) ppc = default_points_per_cell(k);
     const double cells = std::max(1.0, (double)n / ppc);
+    for (int a = 0; a < 3; ++a) p.tile[a] = (tile_hint && tile_hint[a] > 0) ? tile_hint[a] : 4;
+    double x[3];  // real-valued cells per axis
     if (extent && extent[0] > 0 && extent[1] > 0 && extent[2] > 0) {
         const double vol = (double)extent[0] * extent[1] * extent[2];
         const double h = std::cbrt(vol / cells);
-        for (int a = 0; a < 3; ++a) p.dims[a] = std::max(1, (int)std::lround(extent[a] / h));
+        for (int a = 0; a < 3; ++a) x[a] = extent[a] / h;
     } else {
-        const int sz = std::max(1, (int)std::lround(std::cbrt(cells)));
-        p.dims[0] = p.dims[1] = p.dims[2] = sz;
+        x[0] = x[1] = x[2] = std::cbrt(cells);
+    }
+    // Whole tiles: a partial edge tile costs a full halo staging for a fraction of the queries
+    // (66 cells = 16.5 tiles of 4 -> 17 % of the tiles partial), so axes of >= 4 tiles are
+    // rounded to a multiple of the tile edge (900K, K=16: 66^3 -> 64^3, solve 0.566 -> 0.505 ms).
+    for (int a = 0; a < 3; ++a) {
+        p.dims[a] = std::max(1, (int)std::lround(x[a]));
+        if (x[a] >= 4.0 * p.tile[a]) p.dims[a] = std::max(p.tile[a], (int)std::lround(x[a] / p.tile[a]) * p.tile[a]);
     }
     // guard against int overflow of the cell count
     while ((double)p.dims[0] * p.dims[1] * p.dims[2] > 4.0e8)
         for (int a = 0; a < 3; ++a) p.dims[a] = std::max(1, p.dims[a] * 4 / 5);
-    for (int a = 0; a < 3; ++a) p.tile[a] = (tile_hint && tile_hint[a] > 0) ? tile_hint[a] : 4;
+    if (n > 0)  // the halo (K-th radius in cells) and the LDS plan follow the ACTUAL density
+        ppc = (float)((double)n / ((double)p.dims[0] * p.dims[1] * p.dims[2]));
     if (halo_hint > 0) {
         p.halo = halo_hint;
     } else {

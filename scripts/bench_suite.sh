@@ -36,6 +36,8 @@ run 200 "cfg3 900K blue k16 gpu" --gen blue --n 900000 --k 16 --steps 50 --warmu
 run 200 "headline 900K uniform k16 gpu" --n 900000 --k 16 --steps 50 --warmup 10
 run 200 "900K uniform k50 gpu (reference K)" --n 900000 --k 50 --steps 20 --warmup 5
 run 300 "cfg4 10M uniform k32 gpu" --n 10000000 --k 32 --steps 10 --warmup 3
+run 200 "900K points on surfaces k16 gpu (occupancy-adaptive grid)" --gen surface --n 900000 --k 16 --steps 10 --warmup 2
+run 300 "900K clustered k16 gpu (occupancy-adaptive grid)" --gen clustered --n 900000 --k 16 --steps 5 --warmup 1
 run 300 "cfg5a 12.5M/rank k16 rccl world1 (100M/8 share)" --dist --n 12500000 --k 16 --steps 5 --warmup 2
 run 600 "cfg5b 100M k16 loopback 8 ranks on 1 gpu" --loopback 8 --n 12500000 --k 16 --steps 3 --warmup 1
 cat $OUT

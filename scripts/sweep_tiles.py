@@ -9,7 +9,10 @@ k = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 dev = torch.device("cuda", 0)
 pts = uniform_cloud(n, seed=0, device=dev)
 res = []
-for ppc, tile, halo in itertools.product([1.5, 2.0, 2.5, 3.1, 4.0, 5.0], [(4, 4, 4), (8, 4, 4), (4, 4, 2), (8, 8, 2), (6, 6, 6), (8, 4, 2)], [0]):
+PPC = [float(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1.5, 2.0, 2.5, 3.1, 4.0, 5.0]
+TILES = ([tuple(int(v) for v in t.split("x")) for t in sys.argv[4].split(",")] if len(sys.argv) > 4 else
+         [(4, 4, 4), (8, 4, 4), (4, 4, 2), (8, 8, 2), (6, 6, 6), (8, 4, 2)])
+for ppc, tile, halo in itertools.product(PPC, TILES, [0]):
     plan = ops.Plan.auto(n, k, ppc, tile, halo)
     if plan.lds_bytes > 160 * 1024:
         continue

@@ -97,8 +97,11 @@ def test_normalize_matches_reference_rule():
 
 def test_plan_auto_reference_density():
     p = kn.Plan.auto(900_000, 16)
-    # ~3.1 points per cell (reference knearests.cu:249): (900000/3.1)^(1/3) = 66.2
-    assert p.dims == [66, 66, 66]
+    # ~3.4 points per cell (reference knearests.cu:249 uses 3.1), rounded to whole 4-cell tiles:
+    # (900000/3.4)^(1/3) = 64.2 -> 64
+    assert p.dims == [64, 64, 64]
+    assert all(d % 4 == 0 for d in kn.Plan.auto(10_000_000, 32).dims)
+    assert kn.Plan.auto(1000, 8).dims == [7, 7, 7]  # small grids are not rounded
     assert p.halo >= 1 and p.lds_capacity >= 1024 and p.lds_bytes <= 160 * 1024
 
 
