@@ -14,9 +14,14 @@ from typing import Sequence
 import torch
 
 
-def factor3(world: int, extent: Sequence[float] = (1.0, 1.0, 1.0)) -> tuple:
-    """Balanced 3-factorisation of ``world`` (minimises the surface of the rank boxes)."""
-    best, best_cost = (world, 1, 1), math.inf
+def factor3(world: int, extent: Sequence[float] = (1.0, 1.0, 1.0), tol: float = 1e-2) -> tuple:
+    """Balanced 3-factorisation of ``world`` (minimises the surface of the rank boxes).
+
+    Factorisations within ``tol`` (relative) of the best surface count as ties and the first one
+    in a fixed order wins. A nearly cubic cloud (random data: extents 999.98 / 999.99 / 999.97)
+    therefore always gets the same grid as the exact cube. Otherwise the split axis would
+    follow noise, and data laid out by one grid would be re-routed by another."""
+    cands = []
     for a in range(1, world + 1):
         if world % a:
             continue
@@ -27,10 +32,9 @@ def factor3(world: int, extent: Sequence[float] = (1.0, 1.0, 1.0)) -> tuple:
             f = (a, b, c)
             # surface of one box for the given domain extent
             bx, by, bz = (extent[i] / f[i] for i in range(3))
-            cost = bx * by + by * bz + bx * bz
-            if cost < best_cost - 1e-12:
-                best, best_cost = f, cost
-    return best
+            cands.append((f, bx * by + by * bz + bx * bz))
+    best_cost = min(c for _, c in cands)
+    return next(f for f, c in cands if c <= best_cost * (1.0 + tol))
 
 
 @dataclass
