@@ -5,7 +5,11 @@
 //                    several K / N / distributions, permutation bijection, stored-space
 //                    semantics, set_k, save/load, N <= K edge cases)
 // Exit code = number of failed checks.
+// -DKN_UNIT_CPU_ONLY builds the host checks alone (no HIP / C API): the sanitizer build
+// (`python -m cuda_knearests_amd._build --asan` -> bin/knn_unit_asan).
+#ifndef KN_UNIT_CPU_ONLY
 #include <hip/hip_runtime.h>
+#endif
 
 #include <algorithm>
 #include <cmath>
@@ -15,7 +19,9 @@
 #include <string>
 #include <vector>
 
+#ifndef KN_UNIT_CPU_ONLY
 #include "knearests.h"
+#endif
 #include "../host/host.hpp"
 
 static int g_fail = 0, g_pass = 0;
@@ -85,6 +91,7 @@ static void cpu_tests() {
     }
 }
 
+#ifndef KN_UNIT_CPU_ONLY
 static bool run_case(const std::vector<float>& p, int k, int exact, const char* tag, float ppc = 0.f) {
     const int n = (int)p.size() / 3;
     kn_config cfg = kn_default_config();
@@ -168,10 +175,14 @@ static void gpu_tests() {
     }
 }
 
+#endif  // KN_UNIT_CPU_ONLY
+
 int main(int argc, char** argv) {
     const std::string what = argc > 1 ? argv[1] : "all";
     if (what == "cpu" || what == "all") cpu_tests();
+#ifndef KN_UNIT_CPU_ONLY
     if (what == "gpu" || what == "all") gpu_tests();
+#endif
     fprintf(stderr, "knn_unit: %d passed, %d failed\n", g_pass, g_fail);
     return g_fail;
 }

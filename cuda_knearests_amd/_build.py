@@ -170,12 +170,29 @@ def build_variant(name: str, hip_flags: list[str], jobs: int = 8) -> Path:
     return out
 
 
+def build_asan() -> Path:
+    """Host-only sanitizer build of the CPU unit tests (kd-tree, brute force, CPU grid solver,
+    .xyz I/O, checker): ``bin/knn_unit_asan`` with AddressSanitizer + UBSan (g++). GPU code is
+    not sanitized (GPU ASan / XNACK are unavailable on the MI355X pool)."""
+    san = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+    flags = [f for f in HOSTFLAGS if f != "-O3"] + san + ["-DKN_UNIT_CPU_ONLY=1"]
+    objs = [_compile(h, flags, "asan", False) for h in HOST]
+    objs.append(_compile("tools/knn_unit.cpp", flags, "asan", False))
+    exe = ROOT / "bin" / "knn_unit_asan"
+    exe.parent.mkdir(exist_ok=True)
+    _run([CXX, "-o", str(exe)] + [str(o) for o in objs] + san + ["-fopenmp"])
+    return exe
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="also build bin/knn_unit_asan (host ASan + UBSan)")
     a = ap.parse_args(argv)
     build(a.jobs, a.force)
+    if a.asan:
+        print(f"[build] asan: {build_asan()}")
     return 0
 
 

@@ -119,3 +119,15 @@ def test_cli_help():
     r = subprocess.run([str(REPO / "bin" / "knn_cli"), "--help"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0
     assert "usage" in r.stderr
+
+
+def test_cpp_unit_cpu_under_asan_ubsan():
+    """SURVEY §5 race/sanitizer item: the host library (kd-tree, brute force, CPU grid solver,
+    .xyz I/O, checker) runs clean under AddressSanitizer + UBSan (host-only build)."""
+    from cuda_knearests_amd import _build
+
+    exe = _build.build_asan()
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    r = subprocess.run([str(exe), "cpu"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
