@@ -176,7 +176,11 @@ def run_dist(args) -> dict:
     torch.cuda.set_device(dev)
     for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
         os.environ.setdefault(key, val)  # --dist without a launcher: a world of one
-    dist.init_process_group("nccl", device_id=dev)
+    import datetime
+
+    # failure detection: a rank that dies or hangs fails the collectives after 5 min instead of
+    # the 10-min default (RCCL async error handling is on by default in torch 2.x)
+    dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=300))
     rank, world = dist.get_rank(), dist.get_world_size()
     if args.layout == "partitioned":
         # spatial split: rank r holds a uniform sample of ITS box of the [0,1000]^3 cube (the
