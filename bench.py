@@ -172,6 +172,8 @@ def run_dist(args) -> dict:
     from cuda_knearests_amd.utils import uniform_cloud
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("KN_SAME_DEVICE"):  # rehearsal: every rank on cuda:0 (1-GPU box)
+        local = 0
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     for key, val in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
@@ -180,7 +182,11 @@ def run_dist(args) -> dict:
 
     # failure detection: a rank that dies or hangs fails the collectives after 5 min instead of
     # the 10-min default (RCCL async error handling is on by default in torch 2.x)
-    dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=300))
+    staged = os.environ.get("KN_DIST_BACKEND") == "gloo"  # 1-GPU multi-process rehearsal
+    if staged:
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
+    else:
+        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=300))
     rank, world = dist.get_rank(), dist.get_world_size()
     if args.layout == "partitioned":
         # spatial split: rank r holds a uniform sample of ITS box of the [0,1000]^3 cube (the
@@ -193,7 +199,10 @@ def run_dist(args) -> dict:
                + torch.tensor(blo, device=dev)).contiguous()
     else:
         pts = make_cloud(args, dev, 7919 * rank)
-    dk = DistributedKNearests(k=args.k, deterministic=args.deterministic)
+    from cuda_knearests_amd.parallel import HostStagedTransport
+
+    dk = DistributedKNearests(k=args.k, deterministic=args.deterministic,
+                              transport=HostStagedTransport() if staged else None)
     res = None
     for _ in range(args.warmup):
         res = dk.solve(pts, partitioned=args.layout == "partitioned")
@@ -206,19 +215,20 @@ def run_dist(args) -> dict:
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    cdev = torch.device("cpu") if staged else dev  # gloo collectives need host tensors
+    t = torch.tensor([dt], device=cdev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     chk = {}
     if not args.no_check and res is not None:
         # gather the global cloud ordered by id for a brute-force spot check on rank 0's queries
-        n_all = [torch.zeros(1, dtype=torch.long, device=dev) for _ in range(world)]
-        dist.all_gather(n_all, torch.tensor([pts.size(0)], device=dev))
-        allp = [torch.empty(int(c.item()), 3, device=dev) for c in n_all]
-        dist.all_gather(allp, pts)
-        cloud = torch.cat(allp)
+        n_all = [torch.zeros(1, dtype=torch.long, device=cdev) for _ in range(world)]
+        dist.all_gather(n_all, torch.tensor([pts.size(0)], device=cdev))
+        allp = [torch.empty(int(c.item()), 3, device=cdev) for c in n_all]
+        dist.all_gather(allp, pts.to(cdev))
+        cloud = torch.cat(allp).to(dev)
         qpts = cloud[res.ids.long()]
         chk = brute_check(cloud, res.neighbors, res.d2, args.k, nsample=1024, queries=qpts)
-        c = torch.tensor([chk["bad_rows"]], device=dev)
+        c = torch.tensor([chk["bad_rows"]], device=cdev)
         dist.all_reduce(c)
         chk["bad_rows_all_ranks"] = int(c.item())
     out = {"t": float(t.item()), "stats": res.stats if res else {}, "check": chk, "n_total": args.n * world,
@@ -296,7 +306,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=900_000, help="points per GPU")
+    ap.add_argument("--n", "--points", dest="n", type=int, default=900_000,
+                    help="points per GPU (use --points under torchrun: it claims --n* prefixes)")
     ap.add_argument("--k", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--layout", choices=["scattered", "partitioned"], default="partitioned")

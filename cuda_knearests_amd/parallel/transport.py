@@ -44,6 +44,28 @@ class TorchDistTransport:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
 
 
+class HostStagedTransport(TorchDistTransport):
+    """torch.distributed collectives on device tensors staged through host memory: lets a
+    CPU-only backend (gloo) drive the GPU algorithm. Used to rehearse multi-PROCESS runs of the
+    native path where RCCL cannot run them (several ranks on one GPU: "Duplicate GPU detected")."""
+
+    def all_gather(self, t: torch.Tensor) -> List[torch.Tensor]:
+        return [x.to(t.device) for x in super().all_gather(t.cpu())]
+
+    def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
+        return super().all_gather_cat(t.cpu()).to(t.device)
+
+    def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> None:
+        o = torch.empty(out.shape, dtype=out.dtype)
+        super().all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+        out.copy_(o)
+
+    def all_reduce_max(self, t: torch.Tensor) -> None:
+        c = t.cpu()
+        super().all_reduce_max(c)
+        t.copy_(c)
+
+
 class LoopbackHub:
     """Shared state of N virtual ranks (one per thread)."""
 

@@ -141,3 +141,63 @@ def test_device_plan_default_ids(cuda):
         same = (nb.long() == oi[ids_r].long()) | (d2.unsqueeze(-1) == od[ids_r].unsqueeze(-2)).any(-1)
         assert bool(same.all())
     assert bool(seen.all())
+
+
+def _staged_worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from cuda_knearests_amd.parallel import DistributedKNearests, HostStagedTransport
+    from cuda_knearests_amd.utils import uniform_cloud as uc
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    n = 40000
+    cloud = uc(n, seed=31)
+    owner = torch.arange(n) % world
+    m = owner == rank
+    ids = torch.nonzero(m).flatten().to(torch.int32)
+    dk = DistributedKNearests(k=16, transport=HostStagedTransport())
+    r = dk.solve(cloud[m].contiguous().to(dev), ids.to(dev))
+    q.put((rank, r.ids.cpu().numpy().copy(), r.neighbors.cpu().numpy().copy(), r.d2.cpu().numpy().copy(),
+           dict(r.stats)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_multiprocess_native_path_host_staged(cuda, world):
+    """Multi-PROCESS rehearsal of the native (device-planned) distributed path: separate
+    processes on one GPU, collectives through gloo (RCCL refuses several ranks per GPU)."""
+    import torch.multiprocessing as mp
+
+    import cuda_knearests_amd as kn
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_staged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    n = 40000
+    cloud = uniform_cloud(n, seed=31)
+    oi, od = kn.knn_cpu(cloud, 16, "kdtree")
+    seen = torch.zeros(n, dtype=torch.bool)
+    for rank, ids, nb, d2, stats in out:
+        ids, nb, d2 = torch.from_numpy(ids).long(), torch.from_numpy(nb), torch.from_numpy(d2)
+        assert not bool(seen[ids].any())
+        seen[ids] = True
+        assert torch.equal(d2, od[ids])
+        same = (nb.long() == oi[ids].long()) | (d2.unsqueeze(-1) == od[ids].unsqueeze(-2)).any(-1)
+        assert bool(same.all())
+    assert bool(seen.all())
