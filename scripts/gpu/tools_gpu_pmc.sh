@@ -17,3 +17,6 @@ for P in "$P1" "$P2"; do
   timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace -d $R/gpurun_out/pmc/p$i -o run -- python3 $R/scripts/prof_query.py 900000 16 2 > $R/gpurun_out/pmc/p$i.log 2>&1 || { echo PMC${i}_FAIL; tail -5 $R/gpurun_out/pmc/p$i.log; exit 1; }
   echo PMC${i}_OK
 done
+cd $R
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_native -o run -- python3 $R/bench.py --no-check --steps 30 --warmup 5 > $R/gpurun_out/prof_native.log 2>&1 || { echo PROF_FAIL; tail $R/gpurun_out/prof_native.log; exit 1; }
+echo PROF_OK
