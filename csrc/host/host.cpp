@@ -1,4 +1,8 @@
 // host.cpp -- CPU oracles, CPU grid kNN and .xyz I/O. See host.hpp.
+// Parity map (reference, read for behaviour only):
+//   kd-tree oracle      <- kd_tree.cpp:80-300 / kd_tree.h:64-207 (set_points, split, recursive query)
+//   .xyz loader + [0,1000]^3 normalisation <- test_knearests.cu:15-81 (get_bbox, load_file)
+//   result check vs oracle <- test_knearests.cu:117-236 (main's comparison loop)
 #include "host.hpp"
 
 #include <algorithm>

@@ -1,4 +1,7 @@
 // engine.cpp -- single-GPU host runtime. See engine.hpp.
+// Replaces the reference's kn_prepare / kn_firstbuild / kn_solve / kn_free (knearests.cu:152-438):
+// one arena instead of per-buffer gpuMalloc* (:205-335), deterministic scan instead of the
+// atomic `reserve` bump allocator, hipGraph replay of the whole build+solve step.
 #include "engine.hpp"
 
 #include <algorithm>
