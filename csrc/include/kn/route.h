@@ -31,9 +31,15 @@ constexpr int kPlanHdr = 16;
 
 // Receive-side table: source s's segment starts at seg[s], holds own[s] owned rows then its
 // halo rows; owned rows of all sources go first (own_pref), then halo rows (halo_pref).
+// Self-last layout (launch_route_scatter with self_last = rank): the rank's own segment is
+// not sent through the collective; recv then holds only the other sources' segments
+// (rows_cross rows, self's seg[] entry is a zero-length placeholder) and the self segment is
+// read from a separate buffer.
 struct UnpackTable {
     int world;
     int n_own;
+    int rows_cross;  // rows in recv; rows past it come from the self buffer
+    int self;        // source whose segment is the self buffer (-1: none)
     int seg[kRouteMaxWorld];
     int own[kRouteMaxWorld];
     int own_pref[kRouteMaxWorld];
@@ -47,12 +53,18 @@ int route_block_count(int n);
 // totals: 2*world ints = (owned, halo) rows per destination.
 hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int world, int* block_counts,
                               int* totals, hipStream_t s);
-// ids == nullptr: global id = p->id_offset + local index
+// ids == nullptr: global id = p->id_offset + local index.
+// self_last < 0: segments in destination order 0..world-1. self_last = rank: the other
+// destinations in order, then the rank's own segment at the end (kept out of the collective).
+// If the rows do not fit in send_rows the kernel writes nothing (the caller sees the totals
+// after its sync and re-launches with a larger buffer) -- so the scatter can be enqueued
+// before the host knows the sizes.
 hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams* p, int world,
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
-                                hipStream_t s);
-hipError_t launch_route_unpack(const float4* recv, int rows, const UnpackTable& t, float* pts, int* gids,
-                               hipStream_t s);
+                                int self_last, hipStream_t s);
+// rows = t.rows_cross + rows of the self buffer (self_rows may be null when t.self < 0)
+hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int rows, const UnpackTable& t,
+                               float* pts, int* gids, hipStream_t s);
 // metas: world x 8 doubles (every rank's launch_local_meta output, all-gathered on device).
 // Writes the RouteParams for decomposition `grid` (px*py*pz == world) and the plan header:
 // global domain, h = halo_factor x expected K-th neighbour radius of the whole cloud, the

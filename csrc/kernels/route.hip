@@ -117,22 +117,28 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
                                                             const RouteParams* __restrict__ pp,
                                                             const int* __restrict__ block_offsets, int nb,
                                                             const int* __restrict__ totals,
-                                                            float4* __restrict__ send, int send_rows) {
+                                                            float4* __restrict__ send, int send_rows,
+                                                            int self_last) {
     __shared__ int base[2 * kRouteMaxWorld];            // block's next row of every column
     __shared__ int wcnt[kRT / 64][2 * kRouteMaxWorld];  // per-wave counts of the current round
+    __shared__ int overflow;
     const RouteParams& p = *pp;
     const int cols = 2 * p.world;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) {
         int seg = 0;
-        for (int d = 0; d < p.world; ++d) {
+        for (int t = 0; t < p.world; ++t) {
+            // self_last >= 0: every other destination in order, then self
+            const int d = self_last < 0 ? t : (t == p.world - 1 ? self_last : (t < self_last ? t : t + 1));
             const int own = totals[2 * d], halo = totals[2 * d + 1];
             base[2 * d] = seg + block_offsets[(size_t)(2 * d) * nb + blockIdx.x];
             base[2 * d + 1] = seg + own + block_offsets[(size_t)(2 * d + 1) * nb + blockIdx.x];
             seg += own + halo;
         }
+        overflow = seg > send_rows;  // same decision in every block: nothing is written
     }
     __syncthreads();
+    if (overflow) return;
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int r = 0; r < kRounds; ++r) {
         const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
@@ -182,18 +188,29 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
     }
 }
 
-__global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restrict__ recv, int rows, UnpackTable t,
-                                                           float* __restrict__ pts, int* __restrict__ gids) {
+__global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restrict__ recv,
+                                                           const float4* __restrict__ self_rows, int rows,
+                                                           UnpackTable t, float* __restrict__ pts,
+                                                           int* __restrict__ gids) {
     const int j = blockIdx.x * kRT + threadIdx.x;
     if (j >= rows) return;
-    int lo = 0, hi = t.world - 1;  // last source whose segment starts at or before j
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (t.seg[mid] <= j) lo = mid; else hi = mid - 1;
+    int lo, o;
+    float4 v;
+    if (j >= t.rows_cross) {  // the self segment (kept out of the collective)
+        lo = t.self;
+        o = j - t.rows_cross;
+        v = self_rows[o];
+    } else {
+        lo = 0;
+        int hi = t.world - 1;  // last source whose segment starts at or before j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (t.seg[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        o = j - t.seg[lo];
+        v = recv[j];
     }
-    const int o = j - t.seg[lo];
     const int out = (o < t.own[lo]) ? t.own_pref[lo] + o : t.n_own + t.halo_pref[lo] + (o - t.own[lo]);
-    const float4 v = recv[j];
     const int oo = KN_IDX(out, rows, 402);
     pts[3 * oo] = v.x;
     pts[3 * oo + 1] = v.y;
@@ -256,6 +273,8 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
             p->box_hi[r][a] = (float)(c[a] == g[a] - 1 ? hi[a] : __dadd_rn(lo[a], __dmul_rn((double)(c[a] + 1), w)));
         }
     }
+    for (int r = world; r < kRouteMaxWorld; ++r)  // unused slots: defined bytes (plans compare equal)
+        for (int a = 0; a < 3; ++a) p->box_lo[r][a] = p->box_hi[r][a] = 0.f;
     for (int a = 0; a < 3; ++a) { hdr[a] = lo[a]; hdr[3 + a] = hi[a]; }
     hdr[6] = h;
     hdr[7] = hs;
@@ -333,11 +352,12 @@ hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int
 
 hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams* p, int world,
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
-                                hipStream_t s) {
-    if (world < 1 || world > kRouteMaxWorld) return hipErrorInvalidValue;
+                                int self_last, hipStream_t s) {
+    if (world < 1 || world > kRouteMaxWorld || self_last >= world) return hipErrorInvalidValue;
     const int nb = route_block_count(n);
     if (n > 0)
-        route_scatter_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, block_offsets, nb, totals, send, send_rows);
+        route_scatter_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, block_offsets, nb, totals, send, send_rows,
+                                                self_last);
     return hipGetLastError();
 }
 
@@ -349,10 +369,12 @@ hipError_t launch_route_plan(const double* metas, int world, int rank, const int
     return hipGetLastError();
 }
 
-hipError_t launch_route_unpack(const float4* recv, int rows, const UnpackTable& t, float* pts, int* gids,
-                               hipStream_t s) {
-    if (t.world < 1 || t.world > kRouteMaxWorld) return hipErrorInvalidValue;
-    if (rows > 0) route_unpack_kernel<<<cdiv(rows, kRT), kRT, 0, s>>>(recv, rows, t, pts, gids);
+hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int rows, const UnpackTable& t,
+                               float* pts, int* gids, hipStream_t s) {
+    if (t.world < 1 || t.world > kRouteMaxWorld || t.rows_cross > rows || t.self >= t.world ||
+        (rows > t.rows_cross && (t.self < 0 || self_rows == nullptr)))
+        return hipErrorInvalidValue;
+    if (rows > 0) route_unpack_kernel<<<cdiv(rows, kRT), kRT, 0, s>>>(recv, self_rows, rows, t, pts, gids);
     return hipGetLastError();
 }
 

@@ -234,7 +234,7 @@ std::vector<torch::Tensor> route_count_impl(const torch::Tensor& points, const k
 
 torch::Tensor route_scatter_impl(const torch::Tensor& points, const c10::optional<torch::Tensor>& ids,
                                  const kn::RouteParams* p, int world, const torch::Tensor& block_offsets,
-                                 const torch::Tensor& totals, int64_t rows) {
+                                 const torch::Tensor& totals, int64_t rows, int self_last = -1) {
     const int n = (int)points.size(0);
     const int* idp = nullptr;
     if (ids.has_value()) {
@@ -250,7 +250,7 @@ torch::Tensor route_scatter_impl(const torch::Tensor& points, const c10::optiona
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, p, world, block_offsets.data_ptr<int>(),
                                           totals.data_ptr<int>(), reinterpret_cast<float4*>(send.data_ptr<float>()),
-                                          (int)rows, s));
+                                          (int)rows, self_last, s));
     return send;
 }
 
@@ -302,11 +302,58 @@ std::vector<torch::Tensor> route_count_dev(torch::Tensor points, torch::Tensor p
 }
 
 torch::Tensor route_scatter_dev(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor plan,
-                                int64_t world, torch::Tensor block_offsets, torch::Tensor totals, int64_t rows) {
+                                int64_t world, torch::Tensor block_offsets, torch::Tensor totals, int64_t rows,
+                                int64_t self_last) {
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
     TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld, "world size must be in [1, 64]");
-    return route_scatter_impl(points, ids, params_ptr(plan), (int)world, block_offsets, totals, rows);
+    TORCH_CHECK(self_last >= -1 && self_last < world, "self_last must be -1 or a rank");
+    return route_scatter_impl(points, ids, params_ptr(plan), (int)world, block_offsets, totals, rows, (int)self_last);
+}
+
+// The whole pre-sync half of a distributed step in one call (no host round trip inside):
+// route plan from the gathered metas -> per-destination counts -> scatter into a send buffer
+// of `cap` rows in the self-last layout. If the rows do not fit, `send` is left unwritten and
+// the caller re-scatters after its sync (route_scatter_dev with self_last = rank).
+// `sync` (int32) packs everything the host reads at its one sync, so it is ONE copy:
+//   [0, 2*kPlanHdr)            plan header (kPlanHdr doubles)
+//   [2*kPlanHdr, +2*world)     totals: (owned, halo) rows this rank sends to each destination
+//   [2*kPlanHdr+2*world, end)  room for the counts all-to-all's output (rows to receive)
+// -> (plan, sync, scanned block counts, send (cap, 4))
+std::vector<torch::Tensor> route_begin(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor metas,
+                                       int64_t rank, std::vector<int64_t> grid, int64_t k, double halo_factor,
+                                       int64_t cap) {
+    check_points(points, true);
+    TORCH_CHECK(cap >= 0 && cap < INT32_MAX, "cap out of range");
+    TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
+                    metas.numel() % 8 == 0 && metas.numel() >= 8,
+                "metas must be a contiguous (world*8,) float64 GPU tensor");
+    TORCH_CHECK(grid.size() == 3, "grid must have 3 entries");
+    const int world = (int)(metas.numel() / 8);
+    TORCH_CHECK(world <= kn::kRouteMaxWorld, "world size must be <= 64");
+    const c10::DeviceGuard guard(points.device());
+    const int n = (int)points.size(0);
+    const int* idp = nullptr;
+    if (ids.has_value()) {
+        TORCH_CHECK(ids->is_cuda() && ids->scalar_type() == torch::kInt32 && ids->numel() == n && ids->is_contiguous(),
+                    "ids must be a contiguous int32 GPU tensor of N entries");
+        idp = ids->data_ptr<int>();
+    }
+    auto i32 = points.options().dtype(torch::kInt32);
+    auto plan = torch::empty({(int64_t)sizeof(kn::RouteParams)}, i32.dtype(torch::kUInt8));
+    auto sync = torch::empty({2 * (int64_t)kn::kPlanHdr + 4 * (int64_t)world}, i32);
+    auto bc = torch::empty({2 * (int64_t)world * kn::route_block_count(n)}, i32);
+    auto send = torch::empty({cap, 4}, points.options());
+    auto* pp = reinterpret_cast<kn::RouteParams*>(plan.data_ptr<uint8_t>());
+    int* totals = sync.data_ptr<int>() + 2 * kn::kPlanHdr;
+    const int g[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor, pp,
+                                       reinterpret_cast<double*>(sync.data_ptr<int>()), s));
+    KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, pp, world, bc.data_ptr<int>(), totals, s));
+    KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, world, bc.data_ptr<int>(), totals,
+                                          reinterpret_cast<float4*>(send.data_ptr<float>()), (int)cap, (int)rank, s));
+    return {plan, sync, bc, send};
 }
 
 // recv: rows received from every source, source s = [recv_own[s] owned | recv_halo[s] halo].
@@ -332,13 +379,101 @@ std::vector<torch::Tensor> route_unpack(torch::Tensor recv, std::vector<int64_t>
         halo += recv_halo[s];
     }
     t.n_own = (int)own;
+    t.rows_cross = (int)seg;
+    t.self = -1;
     TORCH_CHECK(seg == recv.size(0), "source table does not add up to the received rows");
     auto pts = torch::empty({seg, 3}, recv.options());
     auto gids = torch::empty({seg}, recv.options().dtype(torch::kInt32));
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-    KN_CHECK_HIP(kn::launch_route_unpack(reinterpret_cast<const float4*>(recv.data_ptr<float>()), (int)seg, t,
+    KN_CHECK_HIP(kn::launch_route_unpack(reinterpret_cast<const float4*>(recv.data_ptr<float>()), nullptr, (int)seg,
+                                         t, pts.data_ptr<float>(), gids.data_ptr<int>(), s));
+    return {pts, gids};
+}
+
+// Self-last variant: recv holds the other sources' segments only (in source order), the rank's
+// own segment (recv_own[rank] + recv_halo[rank] rows) is `self_rows`, taken straight from its
+// send buffer. Output order is the same as route_unpack's.
+std::vector<torch::Tensor> route_unpack_split(torch::Tensor recv, torch::Tensor self_rows, std::vector<int64_t> recv_own,
+                                              std::vector<int64_t> recv_halo, int64_t rank) {
+    auto ok = [](const torch::Tensor& x) {
+        return x.is_cuda() && x.dim() == 2 && x.size(1) == 4 && x.scalar_type() == torch::kFloat32 && x.is_contiguous();
+    };
+    TORCH_CHECK(ok(recv) && ok(self_rows), "recv / self_rows must be contiguous (R, 4) float32 GPU tensors");
+    const int world = (int)recv_own.size();
+    TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld && (int)recv_halo.size() == world && rank >= 0 && rank < world,
+                "bad source table");
+    const c10::DeviceGuard guard(recv.device());
+    kn::UnpackTable t{};
+    t.world = world;
+    int64_t seg = 0, own = 0, halo = 0;
+    for (int s = 0; s < world; ++s) {
+        TORCH_CHECK(recv_own[s] >= 0 && recv_halo[s] >= 0, "negative counts");
+        t.seg[s] = (int)seg;  // self: zero-length placeholder in recv
+        t.own[s] = (int)recv_own[s];
+        t.own_pref[s] = (int)own;
+        t.halo_pref[s] = (int)halo;
+        if (s != rank) seg += recv_own[s] + recv_halo[s];
+        own += recv_own[s];
+        halo += recv_halo[s];
+    }
+    t.n_own = (int)own;
+    t.rows_cross = (int)seg;
+    t.self = (int)rank;
+    const int64_t nself = recv_own[rank] + recv_halo[rank];
+    TORCH_CHECK(seg == recv.size(0) && nself == self_rows.size(0),
+                "source table does not add up to the received / self rows");
+    const int64_t rows = seg + nself;
+    TORCH_CHECK(rows < INT32_MAX, "too many rows");
+    auto pts = torch::empty({rows, 3}, recv.options());
+    auto gids = torch::empty({rows}, recv.options().dtype(torch::kInt32));
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_unpack(reinterpret_cast<const float4*>(recv.data_ptr<float>()),
+                                         reinterpret_cast<const float4*>(self_rows.data_ptr<float>()), (int)rows, t,
                                          pts.data_ptr<float>(), gids.data_ptr<int>(), s));
     return {pts, gids};
+}
+
+// The whole post-sync half of a distributed step in one call: unpack (self-last layout) ->
+// rank box / complete box / local grid box from the plan header -> tile plan -> grid build ->
+// queries of the owned points. Same arithmetic as the Python local path
+// (SpatialDecomposition.rank_box / complete_box, DistributedKNearests.local_solve), so both
+// give bit-identical results.
+// hdr: the plan header as doubles (kn::kPlanHdr). -> (pts, gids, idx, d2, counters)
+std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_rows, std::vector<int64_t> recv_own,
+                                      std::vector<int64_t> recv_halo, int64_t rank, std::vector<int64_t> grid,
+                                      std::vector<double> hdr, int64_t k, double ppc, bool deterministic) {
+    TORCH_CHECK(grid.size() == 3 && hdr.size() >= 12, "grid must have 3 entries, hdr >= 12");
+    const int64_t world = grid[0] * grid[1] * grid[2];
+    TORCH_CHECK(world == (int64_t)recv_own.size(), "grid does not match the source table");
+    auto pg = route_unpack_split(recv, self_rows, recv_own, recv_halo, rank);
+    int64_t n_owned = 0;
+    for (auto v : recv_own) n_owned += v;
+    const double h = hdr[6], hs = hdr[7];
+    const bool full = hdr[10] != 0.0;
+    const int64_t c[3] = {rank % grid[0], (rank / grid[0]) % grid[1], rank / (grid[0] * grid[1])};
+    std::vector<double> complete(6), box(6);
+    std::vector<double> ext(3);
+    for (int a = 0; a < 3; ++a) {
+        const double lo = hdr[a], hi = hdr[3 + a];
+        const double w = (hi - lo) / (double)grid[a];
+        const double blo = lo + (double)c[a] * w;
+        const double bhi = c[a] == grid[a] - 1 ? hi : lo + (double)(c[a] + 1) * w;
+        const double inf = std::numeric_limits<double>::infinity();
+        complete[a] = full ? -inf : (c[a] == 0 ? -inf : blo - h);
+        complete[3 + a] = full ? inf : (c[a] == grid[a] - 1 ? inf : bhi + h);
+        box[a] = std::max(lo, blo - hs);
+        box[3 + a] = std::min(hi, bhi + hs);
+        ext[a] = box[3 + a] - box[a];
+    }
+    const int64_t npts = pg[0].size(0);
+    float fext[3] = {(float)ext[0], (float)ext[1], (float)ext[2]};
+    const int th[3] = {0, 0, 0};
+    const kn::AutoParams ap = kn::auto_params((int)npts, (int)k, (float)ppc, th, 0, fext);
+    const std::vector<int64_t> dims = {ap.dims[0], ap.dims[1], ap.dims[2]};
+    auto g = build(pg[0], dims, deterministic, box);
+    auto q = query(g[0], g[1], g[3], dims, k, n_owned, pg[1], complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
+                   ap.halo, ap.lds_capacity, true, true, 0);
+    return {pg[0], pg[1], q[0], q[1], q[2]};
 }
 
 // occupancy-adaptive grid: sum over cells of count^2 (int64, on device, no sync)
@@ -536,7 +671,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("route_count_dev", &route_count_dev, "multi-GPU: route_count with the device plan");
     m.def("route_scatter_dev", &route_scatter_dev, "multi-GPU: route_scatter with the device plan (ids=None: offset + i)",
           py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("world"), py::arg("block_offsets"),
-          py::arg("totals"), py::arg("rows"));
+          py::arg("totals"), py::arg("rows"), py::arg("self_last") = -1);
+    m.def("route_begin", &route_begin,
+          "multi-GPU: plan + counts + scatter (self-last layout, cap rows) enqueued in one call",
+          py::arg("points"), py::arg("ids"), py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"),
+          py::arg("halo_factor"), py::arg("cap"));
+    m.def("dist_local", &dist_local,
+          "multi-GPU: unpack + local grid build + owned-point queries from the plan header, one call");
+    m.def("route_unpack_split", &route_unpack_split,
+          "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")

@@ -37,6 +37,7 @@ from .decomposition import SpatialDecomposition, factor3
 from .transport import TorchDistTransport
 
 INF = math.inf
+HDR = 16  # doubles in the device plan header (kn::kPlanHdr, csrc/include/kn/route.h)
 
 
 def _pack(points: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
@@ -99,6 +100,8 @@ class DistributedKNearests:
         self.world = self.comm.world
         self.device_plan = device_plan  # GPU: plan the routing on the device (1 host sync, not 2)
         self._grid = None
+        self._send_cap = 0  # send-buffer rows of the native path (grows to the largest step seen)
+        self.send_headroom = 0.25  # first-step send buffer: (1 + headroom) x local points
 
     # ------------------------------------------------------------------ helpers ------
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
@@ -186,29 +189,35 @@ class DistributedKNearests:
 
     # ------------------------------------------------------- native (GPU) fast path ------
     def _solve_native(self, points: torch.Tensor, ids: Optional[torch.Tensor]) -> DistResult:
-        """Device-planned solve: local meta -> all-gather -> route plan -> route counts ->
-        counts all-to-all are enqueued back to back and read with ONE host sync (the split
-        sizes the payload all-to-all needs); the certification flag is the second. The
-        decomposition grid is cached across calls and re-planned if the domain's shape asks
-        for another one."""
+        """Device-planned solve. Everything before the one routing sync is enqueued back to back:
+        local meta -> all-gather -> ``route_begin`` (route plan, per-destination counts, and the
+        scatter into a send buffer sized from earlier steps) -> counts all-to-all. The host then
+        reads the plan header and both count tables in ONE copy. The rank's own segment sits at
+        the end of the send buffer ("self-last") and never enters the collective: the payload
+        all-to-all carries only rows that change rank, and ``route_unpack_split`` reads the own
+        segment in place. The certification flag is the second sync. The decomposition grid is
+        cached across calls and re-planned if the domain's shape asks for another one."""
         C = ops.load()
         world, rank = self.world, self.rank
-        metas = self.comm.all_gather_cat(C.local_meta(points))  # (world*8,) f64, on device
+        metas = C.local_meta(points)
+        if world > 1:
+            metas = self.comm.all_gather_cat(metas)  # (world*8,) f64, on device
         grid = self._grid or factor3(world, (1.0, 1.0, 1.0))
         hf = self.halo_factor
+        nh = 2 * HDR
         src_pts, src_ids = points, (ids.to(torch.int32).contiguous() if ids is not None else None)
         rounds = 0
         own_pts = own_ids = None
         while True:
             rounds += 1
             while True:
-                plan, hdr = C.route_plan(metas, rank, list(grid), self.k, hf)
-                bc, totals = C.route_count_dev(src_pts, plan, world)
-                recv_tot = torch.empty_like(totals)
-                self.comm.all_to_all_single(recv_tot, totals)
+                cap = max(self._send_cap, int(src_pts.size(0) * (1.0 + self.send_headroom)) + 1024)
+                plan, sync, bc, send = C.route_begin(src_pts, src_ids, metas, rank, list(grid), self.k, hf, cap)
+                totals = sync[nh:nh + 2 * world]
+                if world > 1:  # rows to receive land in the tail of the same sync buffer
+                    self.comm.all_to_all_single(sync[nh + 2 * world:], totals)
                 # sync 1: plan header (f64 viewed as int32 pairs) + both count tables, one copy
-                host = torch.cat([hdr.view(torch.int32), totals.flatten(), recv_tot.flatten()]).cpu()
-                nh = 2 * hdr.numel()
+                host = sync.cpu()
                 hv = host[:nh].view(torch.float64).tolist() + host[nh:].tolist()
                 lo, hi = tuple(hv[0:3]), tuple(hv[3:6])
                 want = factor3(world, tuple(max(hi[a] - lo[a], 1e-30) for a in range(3)))
@@ -218,23 +227,32 @@ class DistributedKNearests:
             self._grid = tuple(grid)
             h, hs, full = hv[6], hv[7], hv[10] != 0.0
             tot = [int(x) for x in hv[16:16 + 2 * world]]
-            rtot = [int(x) for x in hv[16 + 2 * world:16 + 4 * world]]
+            rtot = [int(x) for x in hv[16 + 2 * world:16 + 4 * world]] if world > 1 else tot
             send_counts = [tot[2 * d] + tot[2 * d + 1] for d in range(world)]
             recv_own = [rtot[2 * d] for d in range(world)]
             recv_halo = [rtot[2 * d + 1] for d in range(world)]
-            send = C.route_scatter_dev(src_pts, src_ids, plan, world, bc, totals, sum(send_counts))
-            recv = self._a2a(send, send_counts, [a + b for a, b in zip(recv_own, recv_halo)])
-            pts, gids = C.route_unpack(recv, recv_own, recv_halo)
+            need = sum(send_counts)
+            self._send_cap = max(self._send_cap, need + need // 8 + 1024)
+            if need > send.size(0):  # did not fit: route_begin wrote nothing, scatter again
+                send = C.route_scatter_dev(src_pts, src_ids, plan, world, bc, totals, need, rank)
+            cross_send = [0 if d == rank else send_counts[d] for d in range(world)]
+            cross_recv = [0 if d == rank else recv_own[d] + recv_halo[d] for d in range(world)]
+            x = sum(cross_send)
+            if world > 1:
+                recv = self._a2a(send[:x], cross_send, cross_recv)
+            else:
+                recv = send[:0]
+            # unpack + local build + owned-point queries: one native call (same arithmetic as
+            # local_solve with SpatialDecomposition's boxes)
+            pts, gids, idx, d2, counters = C.dist_local(recv, send[x:x + send_counts[rank]], recv_own, recv_halo,
+                                                        rank, list(grid), hv[:HDR], self.k,
+                                                        self.points_per_cell, self.deterministic)
             n_owned = sum(recv_own)
             if rounds == 1:
                 own_pts, own_ids = pts[:n_owned], gids[:n_owned]
-            dec = SpatialDecomposition(world, lo, hi, tuple(grid))
-            blo, bhi = dec.rank_box(rank)
-            complete = dec.complete_box(rank, h) if not full else [-INF] * 3 + [INF] * 3
-            box = [max(lo[a], blo[a] - hs) for a in range(3)] + [min(hi[a], bhi[a] + hs) for a in range(3)]
-            idx, d2, n_unc = self.local_solve(pts, gids, n_owned, complete, box)
-            flag = n_unc.to(points.device)
-            self.comm.all_reduce_max(flag)
+            flag = counters[1:2]  # uncertified queries (int32)
+            if world > 1:
+                self.comm.all_reduce_max(flag)
             if int(flag.item()) == 0 or full or rounds >= self.max_rounds:  # sync 2
                 break
             hf *= 2.0

@@ -201,3 +201,64 @@ def test_multiprocess_native_path_host_staged(cuda, world):
         same = (nb.long() == oi[ids].long()) | (d2.unsqueeze(-1) == od[ids].unsqueeze(-2)).any(-1)
         assert bool(same.all())
     assert bool(seen.all())
+
+
+@pytest.mark.parametrize("world,rank", [(1, 0), (4, 0), (4, 2), (8, 7)])
+def test_route_begin_self_last(cuda, ext, world, rank):
+    """route_begin (plan + counts + scatter, one call) == the separate launches, with the rank's
+    own segment moved to the end; route_unpack_split == route_unpack of the full buffer."""
+    from cuda_knearests_amd.parallel import factor3
+
+    n = 30000
+    p = uniform_cloud(n, seed=5 + world, device=cuda)
+    ids = torch.arange(n, dtype=torch.int32, device=cuda) * 5 + 1
+    metas = ext.local_meta(p).repeat(world).contiguous()  # every rank "has" the same box
+    grid = list(factor3(world, (1.0, 1.0, 1.0)))
+    plan, sync, bc, send = ext.route_begin(p, ids, metas, rank, grid, 16, 2.5, world * n + 1024)
+    hdr, totals = sync[:32].view(torch.float64), sync[32:32 + 2 * world].view(world, 2)
+    plan2, hdr2 = ext.route_plan(metas, rank, grid, 16, 2.5)
+    assert torch.equal(plan, plan2) and torch.equal(hdr, hdr2)
+    bc2, totals2 = ext.route_count_dev(p, plan2, world)
+    assert torch.equal(totals, totals2) and torch.equal(bc, bc2)
+    c = totals.cpu().tolist()
+    need = sum(a + b for a, b in c)
+    assert need <= send.size(0)
+    if world > 1:
+        assert sum(b for _, b in c) > 0  # some halo rows
+    ref = ext.route_scatter_dev(p, ids, plan2, world, bc2, totals2, need)
+    segs, o = [], 0
+    for a, b in c:
+        segs.append(ref[o:o + a + b])
+        o += a + b
+    exp = torch.cat([segs[d] for d in range(world) if d != rank] + [segs[rank]])
+    assert torch.equal(send[:need].view(torch.int32), exp.view(torch.int32))
+    # unpack: the full buffer as if every source sent it vs the split form
+    own = [a for a, _ in c]
+    halo = [b for _, b in c]
+    full_pts, full_gids = ext.route_unpack(ref, own, halo)
+    x = need - (own[rank] + halo[rank])
+    sp, sg = ext.route_unpack_split(send[:x].contiguous(), send[x:need].contiguous(), own, halo, rank)
+    assert torch.equal(sp, full_pts) and torch.equal(sg, full_gids)
+
+
+def test_distributed_send_buffer_regrow(cuda):
+    """First step with a send buffer far too small (headroom -1): the re-scatter path gives the
+    same results as the default sizing."""
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+
+    world, n = 4, 30000
+    cloud = uniform_cloud(n, seed=11)
+    owner = torch.randint(0, world, (n,), generator=torch.Generator().manual_seed(2))
+
+    def fn(headroom):
+        def body(t):
+            m = owner == t.rank
+            dk = DistributedKNearests(k=16, transport=t)
+            dk.send_headroom = headroom
+            ids = torch.nonzero(m).flatten().to(torch.int32)
+            r = dk.solve(cloud[m].contiguous().to(cuda), ids.to(cuda))
+            return r.ids.cpu(), r.neighbors.cpu(), r.d2.cpu()
+        return run_loopback(world, body)
+
+    for (ia, na, da), (ib, nb, db) in zip(fn(0.25), fn(-1.0)):
+        assert torch.equal(ia, ib) and torch.equal(na, nb) and torch.equal(da, db)
