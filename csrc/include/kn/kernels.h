@@ -35,6 +35,16 @@ struct CompleteBox {
 
 constexpr int kScanItems = 4096;  // elements per scan block (256 threads x 16)
 
+// Bounding box: each of <= kBBoxBlocks blocks writes its 6 partial (lo, hi) encodings, the
+// single-block finaliser reduces them -- no same-address atomics, no memset.
+constexpr int kBBoxBlocks = 256;
+constexpr int kBBoxWords = 6 * kBBoxBlocks;
+int bbox_block_count(int n);
+// partials[a * kBBoxBlocks + b]: a < 3: max of ~ord(min_a), a >= 3: max of ord(max_a) over
+// block b's points (ord = order-preserving float -> uint). Blocks past bbox_block_count(n)
+// are not written.
+hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hipStream_t s);
+
 // Query counters (device, zeroed by every launch_query):
 //  [0] queries sent to the exact kernel   [1] uncertified (multi-GPU: K-th leaves complete box)
 //  [2] LDS-overflow (dense) tiles         [3] in-wave exact re-scans (truncation near-ties)
@@ -48,13 +58,14 @@ struct BuildBuffers {
     int n;
     int dims[3];
     // scratch / outputs (caller-allocated)
-    unsigned* bbox_words;     // 8 words, zeroed by the launcher (memset node)
+    unsigned* bbox_words;     // kBBoxWords words of per-block partials (no zeroing needed)
     GridGeom* geom;           // 1
     int* cell_count;          // C      (zeroed by the launcher)
     int* cell_scan;           // C      block-local exclusive scan
     int* block_sums;          // ceil(C / kScanItems) + 1
     int* cell_start;          // C + 1  final exclusive scan, cell_start[C] = N
-    int2* cell_rank;          // N      (cell, rank inside cell)
+    int2* cell_rank;          // N      (cell, rank inside cell) -- atomic binning only
+    float4* bin_tmp;          // N      bucketed binning scratch (may alias cell_rank)
     float4* sorted;           // N      {x, y, z, bits(original index)}
     unsigned* perm;           // N      perm[stored] = original index
     int deterministic;        // 1: sort each cell by original index
@@ -64,6 +75,18 @@ struct BuildBuffers {
 };
 
 size_t scan_block_count(int num_cells);
+
+// Bucketed binning (two-level counting sort, LDS atomics only): points are first split into
+// buckets of 2^shift consecutive cells by `nblocks` streaming blocks, then one workgroup per
+// bucket counts, scans and places its points. Used when the (bucket x block) count table fits
+// in the C+1-entry cell_count buffer; otherwise the build falls back to global-atomic binning.
+struct BinPlan {
+    int shift;     // log2(cells per bucket), 8..14
+    int nbuckets;  // ceil(C / 2^shift) <= 4096
+    int nblocks;   // streaming blocks
+    int per_block; // points per streaming block (multiple of 256)
+};
+bool bin_plan(int n, int num_cells, BinPlan* out);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t stream);
 
 struct QueryBuffers {

@@ -72,7 +72,8 @@ hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int 
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
                              double halo_factor, RouteParams* p, double* hdr, hipStream_t s);
 // Local meta of a rank's share: out = {lo[3], hi[3], n, 0} (doubles; +-inf box when n == 0).
-// words: 8 scratch words. One all_gather of `out` gives the global domain and the id offsets.
+// words: kBBoxWords scratch words (kn/kernels.h). One all_gather of `out` gives the global
+// domain and the id offsets.
 hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* out, hipStream_t s);
 hipError_t debug_words_route(unsigned out[4], bool reset);
 

@@ -75,6 +75,19 @@ __device__ __forceinline__ int kn_imax(int a, int b) { return a > b ? a : b; }
 
 KN_WAVE_REDUCE(wave_min_u32, unsigned, kn_umin)
 KN_WAVE_REDUCE(wave_max_u32, unsigned, kn_umax)
+
+// One wave reduces the per-block bbox partials of launch_bbox_partials (kn/kernels.h):
+// out[a] = max over blocks of partials[a * stride + b], a < 6. Result wave-uniform.
+__device__ __forceinline__ void bbox_reduce_partials(const unsigned* __restrict__ partials, int nblocks,
+                                                     int stride, unsigned out[6]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        unsigned v = 0u;
+        for (int b = lane; b < nblocks; b += 64) v = v > partials[a * stride + b] ? v : partials[a * stride + b];
+        out[a] = wave_max_u32(v);
+    }
+}
 KN_WAVE_REDUCE(wave_min_i32, int, kn_imin)
 KN_WAVE_REDUCE(wave_max_i32, int, kn_imax)
 

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "kn/kernels.h"
 #include "kn/wave.h"
@@ -30,30 +31,44 @@ __device__ __forceinline__ float unord_float(unsigned u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-// 6 reductions: words[0..2] = max(~ord(min)), words[3..5] = max(ord(max)); all start at 0.
-__global__ __launch_bounds__(256) void bbox_kernel(const float* __restrict__ pts, int n,
-                                                   unsigned* __restrict__ words) {
+// Per-block partial bbox (see launch_bbox_partials). VEC: 4 points = 3 aligned float4 loads
+// per iteration (x0 y0 z0 x1 | y1 z1 x2 y2 | z2 x3 y3 z3); needs a 16-B aligned base.
+template <bool VEC>
+__global__ __launch_bounds__(256) void bbox_partials_kernel(const float* __restrict__ pts, int n,
+                                                            unsigned* __restrict__ partials) {
     float mn[3] = {INFINITY, INFINITY, INFINITY};
     float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const float x = pts[3 * i + 0], y = pts[3 * i + 1], z = pts[3 * i + 2];
-        mn[0] = fminf(mn[0], x); mx[0] = fmaxf(mx[0], x);
-        mn[1] = fminf(mn[1], y); mx[1] = fmaxf(mx[1], y);
-        mn[2] = fminf(mn[2], z); mx[2] = fmaxf(mx[2], z);
+    auto acc = [&](int a, float v) { mn[a] = fminf(mn[a], v); mx[a] = fmaxf(mx[a], v); };
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    int i0 = tid;
+    if (VEC) {
+        const float4* p4 = reinterpret_cast<const float4*>(pts);
+        const int ng = n >> 2;
+        for (int g = tid; g < ng; g += nth) {
+            const float4 a = p4[3 * g], b = p4[3 * g + 1], c = p4[3 * g + 2];
+            acc(0, a.x); acc(1, a.y); acc(2, a.z);
+            acc(0, a.w); acc(1, b.x); acc(2, b.y);
+            acc(0, b.z); acc(1, b.w); acc(2, c.x);
+            acc(0, c.y); acc(1, c.z); acc(2, c.w);
+        }
+        i0 = 4 * ng + tid;
+    }
+    for (int i = i0; i < n; i += nth) {
+        acc(0, pts[3 * (size_t)i]); acc(1, pts[3 * (size_t)i + 1]); acc(2, pts[3 * (size_t)i + 2]);
     }
     __shared__ unsigned red[6][4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        unsigned lo = wave_max_u32(~ord_float(mn[a]));
-        unsigned hi = wave_max_u32(ord_float(mx[a]));
+        const unsigned lo = wave_max_u32(~ord_float(mn[a]));
+        const unsigned hi = wave_max_u32(ord_float(mx[a]));
         if (lane == 0) { red[a][wid] = lo; red[3 + a][wid] = hi; }
     }
     __syncthreads();
     if (threadIdx.x < 6) {
         unsigned v = red[threadIdx.x][0];
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) v = max(v, red[threadIdx.x][w]);
-        atomicMax(words + threadIdx.x, v);
+        partials[threadIdx.x * kBBoxBlocks + blockIdx.x] = v;
     }
 }
 
@@ -78,8 +93,10 @@ __device__ void write_geom(GridGeom* g, const float lo[3], const float hi[3], co
     g->pad = 0;
 }
 
-__global__ void geom_kernel(const unsigned* __restrict__ words, int d0, int d1, int d2,
+__global__ void geom_kernel(const unsigned* __restrict__ partials, int nblocks, int d0, int d1, int d2,
                             GridGeom* g) {
+    unsigned words[6];
+    bbox_reduce_partials(partials, nblocks, kBBoxBlocks, words);  // wave 0 (the only one)
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     float lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
@@ -253,6 +270,134 @@ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 size_t scan_block_count(int num_cells) { return cdiv((size_t)num_cells, kScanItems); }
 
+int bbox_block_count(int n) {
+    return std::max(1, std::min((int)cdiv((size_t)std::max(n, 0), 256 * 8), kBBoxBlocks));
+}
+
+hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int grid = bbox_block_count(n);
+    if ((reinterpret_cast<uintptr_t>(pts) & 15u) == 0)
+        bbox_partials_kernel<true><<<grid, 256, 0, s>>>(pts, n, partials);
+    else
+        bbox_partials_kernel<false><<<grid, 256, 0, s>>>(pts, n, partials);
+    return hipGetLastError();
+}
+
+// ---- bucketed binning ---------------------------------------------------------------
+// A1: per-(bucket, block) counts with LDS atomics, table column = bucket (bucket-major, so the
+// exclusive scan of the table gives every block its write offset inside every bucket).
+__global__ __launch_bounds__(256) void bucket_count_kernel(const float* __restrict__ pts, int n,
+                                                           const GridGeom* __restrict__ gp, int shift,
+                                                           int nbuckets, int nblocks, int per_block,
+                                                           int* __restrict__ table) {
+    extern __shared__ int hist[];
+    for (int j = threadIdx.x; j < nbuckets; j += 256) hist[j] = 0;
+    __syncthreads();
+    const GridGeom g = *gp;
+    const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
+    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+        const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
+        atomicAdd(&hist[cell_of(g, p) >> shift], 1);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < nbuckets; j += 256) table[(size_t)j * nblocks + blockIdx.x] = hist[j];
+}
+
+// A3: every point to its bucket's segment of bin_tmp as {x, y, z, bits(original index)}
+__global__ __launch_bounds__(256) void bucket_scatter_kernel(const float* __restrict__ pts, int n,
+                                                             const GridGeom* __restrict__ gp, int shift,
+                                                             int nbuckets, int nblocks, int per_block,
+                                                             const int* __restrict__ tscan,
+                                                             const int* __restrict__ tsums,
+                                                             float4* __restrict__ tmp) {
+    extern __shared__ int cur[];
+    for (int j = threadIdx.x; j < nbuckets; j += 256) {
+        const size_t t = (size_t)j * nblocks + blockIdx.x;
+        cur[j] = tscan[t] + tsums[t / kScanItems];
+    }
+    __syncthreads();
+    const GridGeom g = *gp;
+    const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
+    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+        const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
+        const int pos = atomicAdd(&cur[cell_of(g, p) >> shift], 1);
+        tmp[KN_IDX(pos, n, 104)] = make_float4(p[0], p[1], p[2], __uint_as_float((unsigned)i));
+    }
+}
+
+// B: one workgroup per bucket: LDS histogram of its 2^shift cells, LDS exclusive scan ->
+// cell_start, then every point to its final slot (LDS cursor atomics).
+__global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restrict__ tmp, int n,
+                                                          const GridGeom* __restrict__ gp, int shift,
+                                                          int nbuckets, int nblocks,
+                                                          const int* __restrict__ tscan,
+                                                          const int* __restrict__ tsums, int num_cells,
+                                                          int* __restrict__ cell_start,
+                                                          float4* __restrict__ sorted,
+                                                          unsigned* __restrict__ perm) {
+    extern __shared__ int cur[];  // 2^shift cells
+    __shared__ int wsum[4];
+    const int b = blockIdx.x;
+    const int cells = 1 << shift;
+    const int c0 = b << shift;
+    auto seg_start = [&](int bucket) {
+        const size_t t = (size_t)bucket * nblocks;
+        return tscan[t] + tsums[t / kScanItems];
+    };
+    const int bs = seg_start(b);
+    const int be = (b + 1 < nbuckets) ? seg_start(b + 1) : n;
+    for (int j = threadIdx.x; j < cells; j += 256) cur[j] = 0;
+    __syncthreads();
+    const GridGeom g = *gp;
+    for (int k = bs + threadIdx.x; k < be; k += 256) {
+        const float4 v = tmp[KN_IDX(k, n, 105)];
+        const float p[3] = {v.x, v.y, v.z};
+        atomicAdd(&cur[KN_IDX(cell_of(g, p) - c0, cells, 106)], 1);
+    }
+    __syncthreads();
+    // exclusive scan of cur[0, cells): thread t owns `per` consecutive cells
+    const int per = cells >> 8;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int s = 0;
+    for (int j = 0; j < per; ++j) s += cur[threadIdx.x * per + j];
+    const int incl = wave_inclusive_scan_add(s);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int run = incl - s;
+    for (int w = 0; w < wid; ++w) run += wsum[w];
+    for (int j = 0; j < per; ++j) {
+        const int c = threadIdx.x * per + j;
+        const int cnt = cur[c];
+        cur[c] = bs + run;
+        if (c0 + c < num_cells) cell_start[c0 + c] = bs + run;
+        run += cnt;
+    }
+    if (b == nbuckets - 1 && threadIdx.x == 0) cell_start[num_cells] = n;
+    __syncthreads();
+    for (int k = bs + threadIdx.x; k < be; k += 256) {
+        const float4 v = tmp[KN_IDX(k, n, 105)];
+        const float p[3] = {v.x, v.y, v.z};
+        const int pos = atomicAdd(&cur[cell_of(g, p) - c0], 1);
+        sorted[KN_IDX(pos, n, 107)] = v;
+        perm[pos] = __float_as_uint(v.w);
+    }
+}
+
+bool bin_plan(int n, int num_cells, BinPlan* out) {
+    if (n <= 0 || num_cells <= 0) return false;
+    const int nblocks = std::max(1, std::min((int)cdiv((size_t)n, 4096), 1024));
+    const int per_block = (int)(cdiv(cdiv((size_t)n, nblocks), 256) * 256);
+    for (int shift = 8; shift <= 14; ++shift) {
+        const long long nbuckets = ((long long)num_cells + (1ll << shift) - 1) >> shift;
+        if (nbuckets > 4096) continue;
+        if (nbuckets * nblocks > (long long)num_cells + 1) continue;
+        *out = BinPlan{shift, (int)nbuckets, (int)cdiv((size_t)n, per_block), per_block};
+        return true;
+    }
+    return false;
+}
+
 hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const int C = b.dims[0] * b.dims[1] * b.dims[2];
     const int n = b.n;
@@ -262,10 +407,31 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
                                          b.box_hi[1], b.box_hi[2], b.dims[0], b.dims[1],
                                          b.dims[2], b.geom);
     } else {
-        if ((e = hipMemsetAsync(b.bbox_words, 0, 8 * sizeof(unsigned), s)) != hipSuccess) return e;
-        const unsigned grid = std::max(1u, std::min(cdiv((size_t)n, 256 * 4), 1024u));
-        bbox_kernel<<<grid, 256, 0, s>>>(b.points, n, b.bbox_words);
-        geom_kernel<<<1, 64, 0, s>>>(b.bbox_words, b.dims[0], b.dims[1], b.dims[2], b.geom);
+        if ((e = launch_bbox_partials(b.points, n, b.bbox_words, s)) != hipSuccess) return e;
+        geom_kernel<<<1, 64, 0, s>>>(b.bbox_words, n > 0 ? bbox_block_count(n) : 0, b.dims[0], b.dims[1],
+                                     b.dims[2], b.geom);
+    }
+    BinPlan bp{};
+    static const bool force_atomic = [] {
+        const char* v = std::getenv("KN_BUILD_ALGO");
+        return v && std::atoi(v) == 1;
+    }();
+    if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp)) {
+        const size_t T = (size_t)bp.nbuckets * bp.nblocks;
+        bucket_count_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
+            b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count);
+        const unsigned nbt = (unsigned)scan_block_count((int)T);
+        scan_blocks_kernel<<<nbt, 256, 0, s>>>(b.cell_count, (int)T, b.cell_scan, b.block_sums);
+        scan_top_kernel<<<1, 1024, 0, s>>>(b.block_sums, (int)nbt);
+        bucket_scatter_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
+            b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_scan, b.block_sums,
+            b.bin_tmp);
+        bucket_sort_kernel<<<bp.nbuckets, 256, (1u << bp.shift) * sizeof(int), s>>>(
+            b.bin_tmp, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, b.cell_scan, b.block_sums, C, b.cell_start,
+            b.sorted, b.perm);
+        if (b.deterministic)
+            cell_sort_kernel<<<cdiv(C, 256), 256, 0, s>>>(b.cell_start, C, b.sorted, b.perm);
+        return hipGetLastError();
     }
     if ((e = hipMemsetAsync(b.cell_count, 0, (size_t)C * sizeof(int), s)) != hipSuccess) return e;
     if (n > 0) count_kernel<<<cdiv(n, 256), 256, 0, s>>>(b.points, n, b.geom, b.cell_count, b.cell_rank);

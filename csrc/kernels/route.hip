@@ -298,40 +298,19 @@ __device__ __forceinline__ float meta_unord(unsigned u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-__global__ __launch_bounds__(256) void meta_bbox_kernel(const float* __restrict__ pts, int n,
-                                                        unsigned* __restrict__ words) {
-    float mn[3] = {INFINITY, INFINITY, INFINITY};
-    float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float v = pts[3 * (size_t)i + a];
-            mn[a] = fminf(mn[a], v);
-            mx[a] = fmaxf(mx[a], v);
-        }
-    }
-    __shared__ unsigned red[6][4];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const unsigned lo = wave_max_u32(~meta_ord(mn[a]));
-        const unsigned hi = wave_max_u32(meta_ord(mx[a]));
-        if (lane == 0) { red[a][wid] = lo; red[3 + a][wid] = hi; }
-    }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        unsigned v = red[threadIdx.x][0];
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) v = max(v, red[threadIdx.x][w]);
-        atomicMax(words + threadIdx.x, v);
-    }
-}
-
-__global__ void meta_finalize_kernel(const unsigned* __restrict__ words, int n, double* __restrict__ out) {
+// words: the per-block partials of launch_bbox_partials (build.hip), same encoding
+__global__ void meta_finalize_kernel(const unsigned* __restrict__ partials, int nblocks, int n,
+                                     double* __restrict__ out) {
+    unsigned words[6];
+    bbox_reduce_partials(partials, nblocks, kBBoxBlocks, words);
     const int t = threadIdx.x;
     if (t >= 8) return;
     double v;
-    if (t < 3) v = n > 0 ? (double)meta_unord(~words[t]) : (double)INFINITY;
-    else if (t < 6) v = n > 0 ? (double)meta_unord(words[t]) : -(double)INFINITY;
+    unsigned wt = words[0];  // words[t] without dynamic register indexing
+#pragma unroll
+    for (int a = 1; a < 6; ++a) wt = (t == a) ? words[a] : wt;
+    if (t < 3) v = n > 0 ? (double)meta_unord(~wt) : (double)INFINITY;
+    else if (t < 6) v = n > 0 ? (double)meta_unord(wt) : -(double)INFINITY;
     else if (t == 6) v = (double)n;
     else v = 0.0;
     out[t] = v;
@@ -380,12 +359,8 @@ hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int 
 
 hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* out, hipStream_t s) {
     hipError_t e;
-    if ((e = hipMemsetAsync(words, 0, 8 * sizeof(unsigned), s)) != hipSuccess) return e;
-    if (n > 0) {
-        const unsigned grid = std::max(1u, std::min(cdiv((size_t)n, 256 * 4), 1024u));
-        meta_bbox_kernel<<<grid, 256, 0, s>>>(pts, n, words);
-    }
-    meta_finalize_kernel<<<1, 64, 0, s>>>(words, n, out);
+    if ((e = launch_bbox_partials(pts, n, words, s)) != hipSuccess) return e;
+    meta_finalize_kernel<<<1, 64, 0, s>>>(words, n > 0 ? bbox_block_count(n) : 0, n, out);
     return hipGetLastError();
 }
 

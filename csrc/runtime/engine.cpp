@@ -81,11 +81,11 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
     const size_t nb = scan_block_count(C) + 1;
     size_t bytes = 0;
     bytes += align_up((size_t)n * 3 * sizeof(float));
-    bytes += align_up(8 * sizeof(unsigned));
+    bytes += align_up(kBBoxWords * sizeof(unsigned));
     bytes += align_up(sizeof(GridGeom));
     bytes += 3 * align_up((size_t)(C + 1) * sizeof(int));
     bytes += align_up(nb * sizeof(int));
-    bytes += align_up((size_t)n * sizeof(int2));
+    bytes += align_up((size_t)n * sizeof(float4));  // bin_tmp (cell_rank aliases it)
     bytes += align_up((size_t)n * sizeof(float4));
     bytes += 2 * align_up((size_t)n * sizeof(unsigned));
     bytes += align_up(kNumCounters * sizeof(unsigned));
@@ -99,13 +99,14 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
     }
     char* p = arena_;
     points_ = carve<float>(p, (size_t)n * 3);
-    bbox_ = carve<unsigned>(p, 8);
+    bbox_ = carve<unsigned>(p, kBBoxWords);
     geom_ = carve<GridGeom>(p, 1);
     cell_count_ = carve<int>(p, C + 1);
     cell_scan_ = carve<int>(p, C + 1);
     cell_start_ = carve<int>(p, C + 1);
     block_sums_ = carve<int>(p, nb);
-    cell_rank_ = carve<int2>(p, n);
+    bin_tmp_ = carve<float4>(p, n);
+    cell_rank_ = reinterpret_cast<int2*>(bin_tmp_);
     sorted_ = carve<float4>(p, n);
     perm_ = carve<unsigned>(p, n);
     fallback_ = carve<unsigned>(p, n);
@@ -143,6 +144,7 @@ BuildBuffers Engine::build_buffers() const {
     b.block_sums = block_sums_;
     b.cell_start = cell_start_;
     b.cell_rank = cell_rank_;
+    b.bin_tmp = bin_tmp_;
     b.sorted = sorted_;
     b.perm = perm_;
     b.deterministic = cfg_.deterministic;

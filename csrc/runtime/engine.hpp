@@ -110,6 +110,7 @@ private:
     int* block_sums_ = nullptr;
     int* cell_start_ = nullptr;
     int2* cell_rank_ = nullptr;
+    float4* bin_tmp_ = nullptr;
     float4* sorted_ = nullptr;
     unsigned* perm_ = nullptr;
     unsigned* fallback_ = nullptr;

@@ -52,11 +52,11 @@ std::vector<torch::Tensor> build(torch::Tensor points, std::vector<int64_t> dims
     auto i32 = points.options().dtype(torch::kInt32);
     auto f32 = points.options().dtype(torch::kFloat32);
     const int64_t nb = (int64_t)kn::scan_block_count((int)C) + 1;
-    // workspace (int32 words): bbox 8 | geom-pad 16 | cell_count C+1 | cell_scan C+1 | block_sums nb
-    //                          | (8-byte aligned) cell_rank 2N
-    int64_t rank_off = 8 + 16 + 2 * (C + 1) + nb;
-    rank_off = (rank_off + 1) & ~(int64_t)1;
-    auto ws = torch::empty({rank_off + 2 * (int64_t)n}, i32);
+    // workspace (int32 words): bbox partials kBBoxWords | geom-pad 16 | cell_count C+1 | cell_scan C+1
+    //                          | block_sums nb | (16-byte aligned) bin_tmp 4N (cell_rank 2N aliases it)
+    int64_t rank_off = kn::kBBoxWords + 16 + 2 * (C + 1) + nb;
+    rank_off = (rank_off + 3) & ~(int64_t)3;
+    auto ws = torch::empty({rank_off + 4 * (int64_t)n}, i32);
     auto cell_start = torch::empty({C + 1}, i32);
     auto sorted = torch::empty({(int64_t)n, 4}, f32);
     auto perm = torch::empty({(int64_t)n}, i32);
@@ -68,10 +68,11 @@ std::vector<torch::Tensor> build(torch::Tensor points, std::vector<int64_t> dims
     for (int a = 0; a < 3; ++a) b.dims[a] = (int)dims[a];
     b.bbox_words = reinterpret_cast<unsigned*>(w);
     b.geom = reinterpret_cast<kn::GridGeom*>(geom.data_ptr<int>());
-    b.cell_count = w + 8 + 16;
+    b.cell_count = w + kn::kBBoxWords + 16;
     b.cell_scan = b.cell_count + (C + 1);
     b.block_sums = b.cell_scan + (C + 1);
     b.cell_rank = reinterpret_cast<int2*>(w + rank_off);
+    b.bin_tmp = reinterpret_cast<float4*>(w + rank_off);
     b.cell_start = cell_start.data_ptr<int>();
     b.sorted = reinterpret_cast<float4*>(sorted.data_ptr<float>());
     b.perm = reinterpret_cast<unsigned*>(perm.data_ptr<int>());
@@ -501,7 +502,7 @@ py::object refine_dims(std::vector<int64_t> dims, double w, int64_t k, double pp
 torch::Tensor local_meta(torch::Tensor points) {
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
-    auto words = torch::empty({8}, points.options().dtype(torch::kInt32));
+    auto words = torch::empty({kn::kBBoxWords}, points.options().dtype(torch::kInt32));
     auto out = torch::empty({8}, points.options().dtype(torch::kFloat64));
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_local_meta(points.data_ptr<float>(), (int)points.size(0),

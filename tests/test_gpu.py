@@ -3,7 +3,9 @@
 Every comparison is distance-aware: squared distances must equal the kd-tree oracle's bit for
 bit (same fp32 fma chain), ids may differ only inside runs of equal distance.
 """
+import os
 import subprocess
+import sys
 
 import pytest
 import torch
@@ -270,3 +272,33 @@ def test_in_cell_order_does_not_change_results(cuda):
         i0, d0 = kn.knn(p, k, deterministic=True)
         i1, d1 = kn.knn(p, k, deterministic=False)
         assert torch.equal(i0, i1) and torch.equal(d0, d1)
+
+
+def test_unaligned_points_slice(cuda):
+    """A row slice whose base is not 16-B aligned (bbox scalar-load path) == an aligned copy."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.utils import uniform_cloud
+
+    p = uniform_cloud(20_003, seed=41, device=cuda)[3:]
+    assert p.data_ptr() % 16 != 0
+    i0, d0 = kn.knn(p, 8)
+    i1, d1 = kn.knn(p.clone(), 8)
+    assert torch.equal(i0, i1) and torch.equal(d0, d1)
+
+
+def test_atomic_binning_fallback_matches(cuda):
+    """KN_BUILD_ALGO=1 forces the global-atomic binning path (used when the bucketed plan does not
+    fit); it must give the same results as the default bucketed binning."""
+    code = (
+        "import torch, cuda_knearests_amd as kn\n"
+        "from cuda_knearests_amd.utils import uniform_cloud\n"
+        "p = uniform_cloud(60_000, seed=8, device='cuda')\n"
+        "i, d = kn.knn(p, 12)\n"
+        "torch.save({'i': i.cpu(), 'd': d.cpu()}, '/tmp/kn_atomic_bin.pt')\n"
+    )
+    env = dict(os.environ, KN_BUILD_ALGO="1", PYTHONPATH=str(REPO))
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=240)
+    ref = torch.load("/tmp/kn_atomic_bin.pt", weights_only=True)
+    p = uniform_cloud(60_000, seed=8, device=cuda)
+    i, d = kn.knn(p, 12)
+    assert torch.equal(i.cpu(), ref["i"]) and torch.equal(d.cpu(), ref["d"])

@@ -78,9 +78,11 @@ def test_rccl_world1_end_to_end(cuda):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [0, 1, 777, 300_000])
-def test_local_meta_matches_torch(cuda, ext, n):
-    p = uniform_cloud(n, seed=n, device=cuda, lo=-250.0, hi=640.0)
+@pytest.mark.parametrize("n,offset", [(0, 0), (1, 0), (777, 0), (300_000, 0), (300_001, 1), (5, 3)])
+def test_local_meta_matches_torch(cuda, ext, n, offset):
+    """offset > 0: a row slice whose base is not 16-B aligned (scalar-load path)."""
+    p = uniform_cloud(n + offset, seed=n, device=cuda, lo=-250.0, hi=640.0)[offset:]
+    assert p.is_contiguous()
     v = ext.local_meta(p).cpu()
     assert v.dtype == torch.float64 and v.numel() == 8
     assert v[6].item() == n and v[7].item() == 0.0
