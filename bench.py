@@ -215,6 +215,21 @@ def run_dist(args) -> dict:
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
+    if os.environ.get("KN_HOST_MARKS"):  # host-side stage timing of the native step (stderr)
+        dk.host_marks = []
+        for _ in range(20):
+            dk.solve(pts, partitioned=args.layout == "partitioned")
+        torch.cuda.synchronize()
+        acc, prev, cnt = {}, None, {}
+        for stage, t in dk.host_marks:
+            if prev is not None:
+                key = "between_steps" if stage == "start" else stage
+                acc[key] = acc.get(key, 0.0) + (t - prev) * 1e6
+                cnt[key] = cnt.get(key, 0) + 1
+            prev = t
+        print("[bench] host stage us (since previous mark): "
+              + ", ".join(f"{k} {acc[k] / cnt[k]:.1f}" for k in acc), file=sys.stderr)
+        dk.host_marks = None
     cdev = torch.device("cpu") if staged else dev  # gloo collectives need host tensors
     t = torch.tensor([dt], device=cdev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -93,20 +93,38 @@ __device__ void write_geom(GridGeom* g, const float lo[3], const float hi[3], co
     g->pad = 0;
 }
 
-__global__ void geom_kernel(const unsigned* __restrict__ partials, int nblocks, int d0, int d1, int d2,
-                            GridGeom* g) {
+// Grid geometry from the bbox partials; called by one full wave (the reduction is wave-wide),
+// every lane gets the same result.
+__device__ void geom_from_partials(const unsigned* __restrict__ partials, int nblocks, const int dims[3],
+                                   GridGeom* g) {
     unsigned words[6];
-    bbox_reduce_partials(partials, nblocks, kBBoxBlocks, words);  // wave 0 (the only one)
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    bbox_reduce_partials(partials, nblocks, kBBoxBlocks, words);
     float lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
         lo[a] = unord_float(~words[a]);
         hi[a] = unord_float(words[3 + a]);
         if (!(hi[a] >= lo[a])) { lo[a] = 0.f; hi[a] = 1.f; }  // empty input
     }
-    const int dims[3] = {d0, d1, d2};
     write_geom(g, lo, hi, dims);
 }
+
+__global__ void geom_kernel(const unsigned* __restrict__ partials, int nblocks, int d0, int d1, int d2,
+                            GridGeom* g) {
+    const int dims[3] = {d0, d1, d2};
+    GridGeom t;
+    geom_from_partials(partials, nblocks, dims, &t);  // wave 0 (the only one)
+    if (threadIdx.x == 0 && blockIdx.x == 0) *g = t;
+}
+
+// Where the bucketed build's first kernel takes the grid geometry from (folded into it, so
+// no separate geometry launch): a fixed box, or the bbox partials.
+struct GeomSrc {
+    const unsigned* partials;
+    int nbb;
+    int use_box;
+    float lo[3], hi[3];
+    int dims[3];
+};
 
 __global__ void geom_box_kernel(float l0, float l1, float l2, float h0, float h1, float h2, int d0,
                                 int d1, int d2, GridGeom* g) {
@@ -287,14 +305,24 @@ hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hip
 // ---- bucketed binning ---------------------------------------------------------------
 // A1: per-(bucket, block) counts with LDS atomics, table column = bucket (bucket-major, so the
 // exclusive scan of the table gives every block its write offset inside every bucket).
-__global__ __launch_bounds__(256) void bucket_count_kernel(const float* __restrict__ pts, int n,
-                                                           const GridGeom* __restrict__ gp, int shift,
+__global__ __launch_bounds__(256) void bucket_count_kernel(const float* __restrict__ pts, int n, GeomSrc src,
+                                                           GridGeom* __restrict__ gout, int shift,
                                                            int nbuckets, int nblocks, int per_block,
                                                            int* __restrict__ table) {
     extern __shared__ int hist[];
+    __shared__ GridGeom gs;
     for (int j = threadIdx.x; j < nbuckets; j += 256) hist[j] = 0;
+    if (threadIdx.x < 64) {  // every block derives the geometry; block 0 publishes it
+        GridGeom t;
+        if (src.use_box) write_geom(&t, src.lo, src.hi, src.dims);
+        else geom_from_partials(src.partials, src.nbb, src.dims, &t);
+        if (threadIdx.x == 0) {
+            gs = t;
+            if (blockIdx.x == 0) *gout = t;
+        }
+    }
     __syncthreads();
-    const GridGeom g = *gp;
+    const GridGeom g = gs;
     const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
     for (int i = i0 + threadIdx.x; i < i1; i += 256) {
         const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
@@ -309,12 +337,22 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const float* __rest
                                                              const GridGeom* __restrict__ gp, int shift,
                                                              int nbuckets, int nblocks, int per_block,
                                                              const int* __restrict__ tscan,
-                                                             const int* __restrict__ tsums,
+                                                             const int* __restrict__ tsums, int nbt,
                                                              float4* __restrict__ tmp) {
     extern __shared__ int cur[];
+    __shared__ int pre[1024];  // exclusive prefix of the scan blocks' totals (nbt <= 1024)
+    if (threadIdx.x < 64) {
+        const int per = (nbt + 63) >> 6, j0 = threadIdx.x * per;
+        int s = 0;
+        for (int j = 0; j < per; ++j) s += (j0 + j < nbt) ? tsums[j0 + j] : 0;
+        int run = wave_inclusive_scan_add(s) - s;
+        for (int j = 0; j < per; ++j)
+            if (j0 + j < nbt) { pre[j0 + j] = run; run += tsums[j0 + j]; }
+    }
+    __syncthreads();
     for (int j = threadIdx.x; j < nbuckets; j += 256) {
         const size_t t = (size_t)j * nblocks + blockIdx.x;
-        cur[j] = tscan[t] + tsums[t / kScanItems];
+        cur[j] = tscan[t] + pre[t / kScanItems];
     }
     __syncthreads();
     const GridGeom g = *gp;
@@ -338,17 +376,30 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
                                                           unsigned* __restrict__ perm) {
     extern __shared__ int cur[];  // 2^shift cells
     __shared__ int wsum[4];
+    __shared__ int seg[2];
     const int b = blockIdx.x;
     const int cells = 1 << shift;
     const int c0 = b << shift;
-    auto seg_start = [&](int bucket) {
-        const size_t t = (size_t)bucket * nblocks;
-        return tscan[t] + tsums[t / kScanItems];
-    };
-    const int bs = seg_start(b);
-    const int be = (b + 1 < nbuckets) ? seg_start(b + 1) : n;
     for (int j = threadIdx.x; j < cells; j += 256) cur[j] = 0;
+    if (threadIdx.x < 64) {  // bucket segment [bs, be): scanned table + prefix of raw block totals
+        const size_t t0 = (size_t)b * nblocks, t1 = (size_t)(b + 1) * nblocks;
+        const int i0 = (int)(t0 / kScanItems);
+        const int i1 = (b + 1 < nbuckets) ? (int)(t1 / kScanItems) : 0;
+        int s0 = 0, s1 = 0;
+        for (int j = threadIdx.x; j < max(i0, i1); j += 64) {
+            const int v = tsums[j];
+            s0 += j < i0 ? v : 0;
+            s1 += j < i1 ? v : 0;
+        }
+        s0 = __shfl(wave_inclusive_scan_add(s0), 63, 64);
+        s1 = __shfl(wave_inclusive_scan_add(s1), 63, 64);
+        if (threadIdx.x == 0) {
+            seg[0] = tscan[t0] + s0;
+            seg[1] = (b + 1 < nbuckets) ? tscan[t1] + s1 : n;
+        }
+    }
     __syncthreads();
+    const int bs = seg[0], be = seg[1];
     const GridGeom g = *gp;
     for (int k = bs + threadIdx.x; k < be; k += 256) {
         const float4 v = tmp[KN_IDX(k, n, 105)];
@@ -402,6 +453,37 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
     const int C = b.dims[0] * b.dims[1] * b.dims[2];
     const int n = b.n;
     hipError_t e;
+    BinPlan bp{};
+    static const bool force_atomic = [] {
+        const char* v = std::getenv("KN_BUILD_ALGO");
+        return v && std::atoi(v) == 1;
+    }();
+    if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp)) {
+        // geometry folded into bucket_count; scan top level folded into its consumers
+        GeomSrc src{};
+        src.use_box = b.use_box;
+        for (int a = 0; a < 3; ++a) { src.lo[a] = b.box_lo[a]; src.hi[a] = b.box_hi[a]; src.dims[a] = b.dims[a]; }
+        if (!b.use_box) {
+            if ((e = launch_bbox_partials(b.points, n, b.bbox_words, s)) != hipSuccess) return e;
+            src.partials = b.bbox_words;
+            src.nbb = bbox_block_count(n);
+        }
+        const size_t T = (size_t)bp.nbuckets * bp.nblocks;
+        bucket_count_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
+            b.points, n, src, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count);
+        const unsigned nbt = (unsigned)scan_block_count((int)T);
+        scan_blocks_kernel<<<nbt, 256, 0, s>>>(b.cell_count, (int)T, b.cell_scan, b.block_sums);
+        bucket_scatter_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
+            b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_scan, b.block_sums,
+            (int)nbt, b.bin_tmp);
+        bucket_sort_kernel<<<bp.nbuckets, 256, (1u << bp.shift) * sizeof(int), s>>>(
+            b.bin_tmp, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, b.cell_scan, b.block_sums, C, b.cell_start,
+            b.sorted, b.perm);
+        if (b.deterministic)
+            cell_sort_kernel<<<cdiv(C, 256), 256, 0, s>>>(b.cell_start, C, b.sorted, b.perm);
+        return hipGetLastError();
+    }
+    // global-atomic binning (fallback)
     if (b.use_box) {
         geom_box_kernel<<<1, 64, 0, s>>>(b.box_lo[0], b.box_lo[1], b.box_lo[2], b.box_hi[0],
                                          b.box_hi[1], b.box_hi[2], b.dims[0], b.dims[1],
@@ -410,28 +492,6 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         if ((e = launch_bbox_partials(b.points, n, b.bbox_words, s)) != hipSuccess) return e;
         geom_kernel<<<1, 64, 0, s>>>(b.bbox_words, n > 0 ? bbox_block_count(n) : 0, b.dims[0], b.dims[1],
                                      b.dims[2], b.geom);
-    }
-    BinPlan bp{};
-    static const bool force_atomic = [] {
-        const char* v = std::getenv("KN_BUILD_ALGO");
-        return v && std::atoi(v) == 1;
-    }();
-    if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp)) {
-        const size_t T = (size_t)bp.nbuckets * bp.nblocks;
-        bucket_count_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
-            b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count);
-        const unsigned nbt = (unsigned)scan_block_count((int)T);
-        scan_blocks_kernel<<<nbt, 256, 0, s>>>(b.cell_count, (int)T, b.cell_scan, b.block_sums);
-        scan_top_kernel<<<1, 1024, 0, s>>>(b.block_sums, (int)nbt);
-        bucket_scatter_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
-            b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_scan, b.block_sums,
-            b.bin_tmp);
-        bucket_sort_kernel<<<bp.nbuckets, 256, (1u << bp.shift) * sizeof(int), s>>>(
-            b.bin_tmp, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, b.cell_scan, b.block_sums, C, b.cell_start,
-            b.sorted, b.perm);
-        if (b.deterministic)
-            cell_sort_kernel<<<cdiv(C, 256), 256, 0, s>>>(b.cell_start, C, b.sorted, b.perm);
-        return hipGetLastError();
     }
     if ((e = hipMemsetAsync(b.cell_count, 0, (size_t)C * sizeof(int), s)) != hipSuccess) return e;
     if (n > 0) count_kernel<<<cdiv(n, 256), 256, 0, s>>>(b.points, n, b.geom, b.cell_count, b.cell_rank);

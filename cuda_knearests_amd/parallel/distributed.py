@@ -27,6 +27,7 @@ counts, certification flag) and one bulk collective.
 from __future__ import annotations
 
 import math
+import time
 from dataclasses import dataclass
 from typing import Optional
 
@@ -102,6 +103,7 @@ class DistributedKNearests:
         self._grid = None
         self._send_cap = 0  # send-buffer rows of the native path (grows to the largest step seen)
         self.send_headroom = 0.25  # first-step send buffer: (1 + headroom) x local points
+        self.host_marks = None  # list -> (stage, perf_counter) marks of the native step (profiling)
 
     # ------------------------------------------------------------------ helpers ------
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
@@ -199,6 +201,9 @@ class DistributedKNearests:
         cached across calls and re-planned if the domain's shape asks for another one."""
         C = ops.load()
         world, rank = self.world, self.rank
+        marks = self.host_marks
+        mark = marks.append if marks is not None else (lambda _: None)
+        mark(("start", time.perf_counter()))
         metas = C.local_meta(points)
         if world > 1:
             metas = self.comm.all_gather_cat(metas)  # (world*8,) f64, on device
@@ -217,7 +222,9 @@ class DistributedKNearests:
                 if world > 1:  # rows to receive land in the tail of the same sync buffer
                     self.comm.all_to_all_single(sync[nh + 2 * world:], totals)
                 # sync 1: plan header (f64 viewed as int32 pairs) + both count tables, one copy
+                mark(("enqueued", time.perf_counter()))
                 host = sync.cpu()
+                mark(("synced", time.perf_counter()))
                 hv = host[:nh].view(torch.float64).tolist() + host[nh:].tolist()
                 lo, hi = tuple(hv[0:3]), tuple(hv[3:6])
                 want = factor3(world, tuple(max(hi[a] - lo[a], 1e-30) for a in range(3)))
@@ -247,13 +254,16 @@ class DistributedKNearests:
             pts, gids, idx, d2, counters = C.dist_local(recv, send[x:x + send_counts[rank]], recv_own, recv_halo,
                                                         rank, list(grid), hv[:HDR], self.k,
                                                         self.points_per_cell, self.deterministic)
+            mark(("local_enqueued", time.perf_counter()))
             n_owned = sum(recv_own)
             if rounds == 1:
                 own_pts, own_ids = pts[:n_owned], gids[:n_owned]
             flag = counters[1:2]  # uncertified queries (int32)
             if world > 1:
                 self.comm.all_reduce_max(flag)
-            if int(flag.item()) == 0 or full or rounds >= self.max_rounds:  # sync 2
+            done = int(flag.item()) == 0 or full or rounds >= self.max_rounds  # sync 2
+            mark(("flag_synced", time.perf_counter()))
+            if done:
                 break
             hf *= 2.0
             src_pts, src_ids = own_pts, own_ids
