@@ -104,6 +104,12 @@ class DistributedKNearests:
         self._send_cap = 0  # send-buffer rows of the native path (grows to the largest step seen)
         self.send_headroom = 0.25  # first-step send buffer: (1 + headroom) x local points
         self.host_marks = None  # list -> (stage, perf_counter) marks of the native step (profiling)
+        # Speculative routing (world > 1): plan with the previous step's gathered metas and
+        # exchange {this step's meta, counts} in ONE all-gather instead of an all-gather of the
+        # metas followed by an all-to-all of the counts. Checked exactly on the host: if any
+        # rank's meta changed, the step re-plans with the new metas (one extra round trip).
+        self.speculative = True
+        self._spec = None  # (metas on device, metas on host (world, 8) f64, grid)
 
     # ------------------------------------------------------------------ helpers ------
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
@@ -204,10 +210,13 @@ class DistributedKNearests:
         marks = self.host_marks
         mark = marks.append if marks is not None else (lambda _: None)
         mark(("start", time.perf_counter()))
-        metas = C.local_meta(points)
-        if world > 1:
-            metas = self.comm.all_gather_cat(metas)  # (world*8,) f64, on device
-        grid = self._grid or factor3(world, (1.0, 1.0, 1.0))
+        local = C.local_meta(points)
+        spec = self._spec if (world > 1 and self.speculative) else None
+        if spec is not None:
+            metas, grid = spec[0], spec[2]
+        else:
+            metas = self.comm.all_gather_cat(local) if world > 1 else local  # (world*8,) f64, on device
+            grid = self._grid or factor3(world, (1.0, 1.0, 1.0))
         hf = self.halo_factor
         nh = 2 * HDR
         src_pts, src_ids = points, (ids.to(torch.int32).contiguous() if ids is not None else None)
@@ -219,19 +228,45 @@ class DistributedKNearests:
                 cap = max(self._send_cap, int(src_pts.size(0) * (1.0 + self.send_headroom)) + 1024)
                 plan, sync, bc, send = C.route_begin(src_pts, src_ids, metas, rank, list(grid), self.k, hf, cap)
                 totals = sync[nh:nh + 2 * world]
-                if world > 1:  # rows to receive land in the tail of the same sync buffer
-                    self.comm.all_to_all_single(sync[nh + 2 * world:], totals)
-                # sync 1: plan header (f64 viewed as int32 pairs) + both count tables, one copy
-                mark(("enqueued", time.perf_counter()))
-                host = sync.cpu()
-                mark(("synced", time.perf_counter()))
-                hv = host[:nh].view(torch.float64).tolist() + host[nh:].tolist()
+                if spec is not None:
+                    # one all-gather of {meta, counts}; the rows this rank receives are column
+                    # `rank` of every source's counts
+                    row = nh // 2 + 2 * world  # int32 per rank: 8 f64 meta + 2*world counts
+                    gathered = self.comm.all_gather_cat(torch.cat([local.view(torch.int32), totals]))
+                    mark(("enqueued", time.perf_counter()))
+                    host = torch.cat([sync[:nh], gathered]).cpu()
+                    mark(("synced", time.perf_counter()))
+                    g = host[nh:].view(world, row)
+                    new_metas = g[:, :16].contiguous().view(torch.float64)
+                    if not torch.equal(new_metas, spec[1]):
+                        # a rank's cloud changed: re-plan with this step's metas (on device)
+                        metas = gathered.view(world, row)[:, :16].contiguous().view(torch.float64).flatten()
+                        spec = self._spec = None
+                        continue
+                    gl = g.tolist()
+                    rt = [v for d in range(world) for v in gl[d][16 + 2 * rank:18 + 2 * rank]]
+                    hv = host[:nh].view(torch.float64).tolist() + gl[rank][16:] + rt
+                    meta_host = spec[1]
+                else:
+                    if world > 1:  # rows to receive land in the tail of the same sync buffer
+                        self.comm.all_to_all_single(sync[nh + 2 * world:], totals)
+                    # sync 1: plan header (f64 viewed as int32 pairs) + both count tables (+ the
+                    # gathered metas, kept for the next step's speculative routing), one copy
+                    mark(("enqueued", time.perf_counter()))
+                    host = torch.cat([sync, metas.view(torch.int32)]).cpu() if world > 1 else sync.cpu()
+                    mark(("synced", time.perf_counter()))
+                    meta_host = host[sync.numel():].view(torch.float64).view(world, 8) if world > 1 else None
+                    host = host[:sync.numel()]
+                    hv = host[:nh].view(torch.float64).tolist() + host[nh:].tolist()
                 lo, hi = tuple(hv[0:3]), tuple(hv[3:6])
                 want = factor3(world, tuple(max(hi[a] - lo[a], 1e-30) for a in range(3)))
                 if want == tuple(grid):
                     break
                 grid = want  # domain shape changed: re-plan with the matching decomposition
             self._grid = tuple(grid)
+            if world > 1 and rounds == 1:
+                self._spec = (metas, meta_host, tuple(grid))
+            spec = None  # growth rounds re-route with the normal exchange
             h, hs, full = hv[6], hv[7], hv[10] != 0.0
             tot = [int(x) for x in hv[16:16 + 2 * world]]
             rtot = [int(x) for x in hv[16 + 2 * world:16 + 4 * world]] if world > 1 else tot

@@ -264,3 +264,40 @@ def test_distributed_send_buffer_regrow(cuda):
 
     for (ia, na, da), (ib, nb, db) in zip(fn(0.25), fn(-1.0)):
         assert torch.equal(ia, ib) and torch.equal(na, nb) and torch.equal(da, db)
+
+
+def test_speculative_routing_repeat_and_change(cuda):
+    """Repeated solves take the speculative exchange (plan from the previous step's metas, one
+    all-gather of {meta, counts}); a changed cloud falls back to re-planning. Every result must
+    equal a non-speculative solve of the same data."""
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+
+    world, n, k = 4, 24000, 12
+    cloud = uniform_cloud(n, seed=31)
+    owner = torch.randint(0, world, (n,), generator=torch.Generator().manual_seed(4))
+
+    def body(t):
+        m = owner == t.rank
+        ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
+        pts = cloud[m].contiguous().to(cuda)
+        spec = DistributedKNearests(k=k, transport=t)
+        ref = DistributedKNearests(k=k, transport=t)
+        ref.speculative = False
+        outs = []
+        # step 1 (normal), step 2 (speculative hit), step 3: rank 0 drops half its points (miss),
+        # step 4: hit again on the changed cloud
+        for step in range(4):
+            if step >= 2 and t.rank == 0:
+                keep = torch.arange(pts.size(0), device=cuda) % 2 == 0
+                p, i = pts[keep].contiguous(), ids[keep].contiguous()
+            else:
+                p, i = pts, ids
+            a = spec.solve(p, i)
+            b = ref.solve(p, i)
+            outs.append((torch.equal(a.ids, b.ids) and torch.equal(a.neighbors, b.neighbors)
+                         and torch.equal(a.d2, b.d2), spec._spec is not None))
+        return outs
+
+    for outs in run_loopback(world, body):
+        assert all(eq for eq, _ in outs)
+        assert all(cached for _, cached in outs)
