@@ -99,6 +99,9 @@ struct QueryBuffers {
     int k;
     int n_queries;            // points with original index < n_queries are queries
     const unsigned* id_map;   // optional: output id = id_map[original index]
+    const unsigned* row_of;   // optional: global-id mode -- each stored point's w is its global id
+                              // (| 0x80000000 on non-query halo points) and a query's output row
+                              // is row_of[stored index]; id_map is then unused
     CompleteBox complete;
     unsigned* out_idx;        // n_queries x k   (row = original index), UINT_MAX = empty
     float* out_dist;          // optional n_queries x k squared distances

@@ -63,6 +63,10 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
                                 int self_last, hipStream_t s);
 // rows = t.rows_cross + rows of the self buffer (self_rows may be null when t.self < 0)
+// sorted[i].w = gid[perm[i]] | (perm[i] >= n_owned ? 0x80000000 : 0): prepares a rank's grid
+// for the query kernels' global-id mode (QueryBuffers::row_of = perm).
+hipError_t launch_global_w(float4* sorted, const unsigned* perm, const int* gids, int n, int n_owned,
+                           hipStream_t stream);
 hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int rows, const UnpackTable& t,
                                float* pts, int* gids, hipStream_t s);
 // metas: world x 8 doubles (every rank's launch_local_meta output, all-gathered on device).

@@ -57,6 +57,7 @@ struct TileArgs {
     int k;
     int n_queries;
     const unsigned* id_map;
+    const unsigned* row_of;  // non-null: global-id mode (see w_live / w_id / w_row)
     CompleteBox complete;
     unsigned* out_idx;
     float* out_dist;
@@ -77,12 +78,16 @@ struct TileArgs {
 #ifndef KN_YPRUNE
 #define KN_YPRUNE 1
 #endif
+#ifndef KN_LANE_UNROLL
+#define KN_LANE_UNROLL 2
+#endif
 #ifndef KN_LDS_PIPE
 #define KN_LDS_PIPE 1
 #endif
 constexpr int kQueryForceRescan = 1;
 constexpr int kQueryAlgoStream = 2;
 constexpr int kQueryAlgoTile = 4;
+constexpr int kQueryAlgoLane = 8;
 #if defined(KN_CHECKED) && KN_CHECKED
 constexpr bool kStats = true;
 #else
@@ -95,6 +100,28 @@ __device__ __forceinline__ float complete_margin(const CompleteBox& cb, float q,
 
 __device__ __forceinline__ bool pair_less(float da, unsigned ia, float db, unsigned ib) {
     return da < db || (da == db && ia < ib);
+}
+
+// The w field of a stored point. Default mode: its original (local) index -- queries are the
+// indices < n_queries, the output row is that index, and the output id is id_map[index].
+// Global-id mode (row_of != nullptr, multi-GPU ranks): w already holds the point's GLOBAL id,
+// with kHaloBit set on halo (non-query) points, and row_of[stored index] gives a query's output
+// row. The output ids then need no gather through id_map: at 12.5M points per rank that
+// random gather (K per query from a 50 MB table) cost more than the whole lane-walk search.
+constexpr unsigned kHaloBit = 0x80000000u;
+template <class A>
+__device__ __forceinline__ bool w_live(const A& a, unsigned w) {
+    return a.row_of ? !(w & kHaloBit) : (int)w < a.n_queries;
+}
+template <class A>
+__device__ __forceinline__ unsigned w_id(const A& a, unsigned w) { return a.row_of ? (w & ~kHaloBit) : w; }
+template <class A>
+__device__ __forceinline__ unsigned w_row(const A& a, unsigned w, unsigned sidx) {
+    return a.row_of ? a.row_of[KN_IDX(sidx, (unsigned)a.n, 231)] : w;
+}
+template <class A>
+__device__ __forceinline__ unsigned out_id(const A& a, unsigned id) {
+    return (a.row_of || !a.id_map) ? id : a.id_map[KN_IDX(id, (unsigned)a.n, 232)];
 }
 
 // Bijective XCD-aware remap: consecutive tiles (which share halo cells) land on one XCD's L2.
@@ -116,6 +143,16 @@ __device__ __forceinline__ unsigned cand_key(const float4& p, float qx, float qy
     return key;
 }
 
+// cand_key with a per-lane (VGPR) slot: the lane-walk variant's candidates differ per lane.
+__device__ __forceinline__ unsigned cand_key_v(const float4& p, float qx, float qy, float qz, unsigned himask,
+                                               int s) {
+    const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    unsigned key;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(key) : "v"(himask), "v"(__float_as_uint(d2)), "v"((unsigned)s));
+    return key;
+}
+
 // Sorted-array insertion of `key` into keys[0..KM) (ascending), dropping the largest:
 // new[j] = med3(old[j-1], key, old[j]) -- one v_med3_u32 per slot, all independent. Skipped
 // (uniform branch) when no lane of the wave improves; a non-improving key is a no-op anyway.
@@ -133,7 +170,12 @@ __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key
     return 0u;
 }
 
-template <int KT, int M>
+// LANE = false: wave-uniform candidate stream over the union of the chunk's needs (LDS
+// broadcast reads). LANE = true ("lane walk"): each lane walks ITS OWN rows of the staged
+// block -- centre-out over the (2H+1)^2 row offsets around its cell, x-range cut by its own
+// bound -- as a divergent loop with per-lane LDS gathers. ~90 candidates per query instead of
+// the ~535 the union stream feeds every lane, at the price of divergent trip counts.
+template <int KT, int M, bool LANE>
 __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     // K + M margin slots + 1: the query itself is not filtered in the hot loop (that cost 3
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
@@ -205,7 +247,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             const int r = (ty0 - sy0 + lo % ntry) + nys * (tz0 - sz0 + lo / ntry);
             const unsigned sidx = (unsigned)(cb[r * cbs + hx] + (t - qpref[lo]));
             const unsigned orig = __float_as_uint(a.sorted[KN_IDX(sidx, (unsigned)a.n, 204)].w);
-            if ((int)orig < a.n_queries) {
+            if (w_live(a, orig)) {
                 const unsigned pos = atomicAdd(a.counters + 0, 1u);
                 a.fallback_list[KN_IDX(pos, (unsigned)a.n, 205)] = sidx;
             }
@@ -266,27 +308,73 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         const unsigned qsidx = (unsigned)(cb[qrow * cbs] + qoff);
         const float4 qp = pts[KN_IDX(qslot, S, 206)];
         const unsigned qorig = __float_as_uint(qp.w);
-        const bool live = (int)qorig < a.n_queries;  // halo points of a multi-GPU rank are not queries
+        const bool live = w_live(a, qorig);  // halo points of a multi-GPU rank are not queries
         const float qx = qp.x, qy = qp.y, qz = qp.z;
         const int cx = cell_coord(g, 0, qx) - sx0;
         const int cy = cell_coord(g, 1, qy) - sy0;
         const int cz = cell_coord(g, 2, qz) - sz0;
-        // wave bounding box of the live queries' cells: 3 packed (-min, max) reductions
-        const int2 bx = wave_minmax_i32(live ? cx : INT_MAX, live ? cx : INT_MIN);
-        if (bx.x > bx.y) continue;  // no live query in this chunk (uniform)
-        const int2 by = wave_minmax_i32(live ? cy : INT_MAX, live ? cy : INT_MIN);
-        const int2 bz = wave_minmax_i32(live ? cz : INT_MAX, live ? cz : INT_MIN);
-        const int rx0 = max(0, bx.x - a.H), rx1 = min(nxs - 1, bx.y + a.H);
-        const int ry0 = max(0, by.x - a.H), ry1 = min(nys - 1, by.y + a.H);
-        const int rz0 = max(0, bz.x - a.H), rz1 = min(nzs - 1, bz.y + a.H);
+        // scanned region: the wave's bounding box of the live queries' cells + H (union
+        // stream), or each lane's own cell + H (lane walk)
+        int rx0, rx1, ry0, ry1, rz0, rz1, zc = 0, yc = 0, nzt = 0, nyt = 0;
+        if constexpr (LANE) {
+            if (!__builtin_amdgcn_ballot_w64(live)) continue;  // no live query in this chunk
+            rx0 = max(0, cx - a.H); rx1 = min(nxs - 1, cx + a.H);
+            ry0 = max(0, cy - a.H); ry1 = min(nys - 1, cy + a.H);
+            rz0 = max(0, cz - a.H); rz1 = min(nzs - 1, cz + a.H);
+        } else {
+            // 3 packed (-min, max) reductions
+            const int2 bx = wave_minmax_i32(live ? cx : INT_MAX, live ? cx : INT_MIN);
+            if (bx.x > bx.y) continue;  // no live query in this chunk (uniform)
+            const int2 by = wave_minmax_i32(live ? cy : INT_MAX, live ? cy : INT_MIN);
+            const int2 bz = wave_minmax_i32(live ? cz : INT_MAX, live ? cz : INT_MIN);
+            rx0 = max(0, bx.x - a.H); rx1 = min(nxs - 1, bx.y + a.H);
+            ry0 = max(0, by.x - a.H); ry1 = min(nys - 1, by.y + a.H);
+            rz0 = max(0, bz.x - a.H); rz1 = min(nzs - 1, bz.y + a.H);
+            zc = (bz.x + bz.y) >> 1; yc = (by.x + by.y) >> 1;
+            nzt = 2 * max(zc - rz0, rz1 - zc) + 1;
+            nyt = 2 * max(yc - ry0, ry1 - yc) + 1;
+        }
 
         // Visit the region's rows centre-out; for each row every live lane derives the x-range of
-        // cells its current bound `tau` still needs (|x - qx|^2 <= tau - dyz^2), the wave takes
-        // the union, and `body(s0, s1)` streams the uniform LDS slot range [s0, s1).
-        const int zc = (bz.x + bz.y) >> 1, yc = (by.x + by.y) >> 1;
-        const int nzt = 2 * max(zc - rz0, rz1 - zc) + 1;
-        const int nyt = 2 * max(yc - ry0, ry1 - yc) + 1;
+        // cells its current bound `tau` still needs (|x - qx|^2 <= tau - dyz^2). Union stream: the
+        // wave takes the union, and `body(s0, s1)` streams the uniform LDS slot range [s0, s1).
+        // Lane walk: the row offset is uniform, the row itself and [s0, s1) are per lane.
         auto scan_region = [&](auto&& lane_tau, auto&& body) {
+          if constexpr (LANE) {
+            const int side = 2 * a.H + 1;
+            for (int tz_ = 0; tz_ < side; ++tz_) {
+                const int z = cz + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
+                const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
+                const float dz2 = dzb * dzb;
+                const bool zin = live && z >= rz0 && z <= rz1;
+                if (!__builtin_amdgcn_ballot_w64(zin && dz2 <= lane_tau())) continue;
+                for (int ty_ = 0; ty_ < side; ++ty_) {
+                    const int y = cy + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
+                    const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
+                    const float dyz2 = fmaf(dyb, dyb, dz2);
+                    const float tau = lane_tau();
+                    int lx0 = 0, lx1 = -1;
+                    if (zin && y >= ry0 && y <= ry1 && dyz2 <= tau) {
+                        if (tau == INFINITY) {
+                            lx0 = rx0; lx1 = rx1;
+                        } else {
+                            const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                            lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
+                            lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
+                        }
+                    }
+                    if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
+                    int s0 = 0, s1 = 0;
+                    if (lx0 <= lx1) {
+                        const int r = y + nys * z;
+                        const int rb = rowbase[r] - cb[r * cbs];
+                        s0 = rb + cb[r * cbs + lx0];
+                        s1 = KN_IDX(rb + cb[r * cbs + lx1 + 1], S + 1, 212);
+                    }
+                    body(s0, s1);
+                }
+            }
+          } else {
             for (int tz_ = 0; tz_ < nzt; ++tz_) {
                 const int z = zc + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
                 if (z < rz0 || z > rz1) continue;
@@ -338,6 +426,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     body(s0, s1);
                 }
             }
+          }
         };
 
         unsigned keys[KM];
@@ -353,6 +442,31 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             },
             [&](int s0, int s1) {
                 int s = s0;
+                if constexpr (LANE) {
+                    // divergent per-lane walk: KN_LANE_UNROLL gathers in flight per lane
+                    if constexpr (kStats) {
+                        st_rows += (s1 > s0) ? 1u : 0u;
+                        st_cand += (unsigned)max(0, s1 - s0);
+                    }
+                    for (; s + KN_LANE_UNROLL <= s1; s += KN_LANE_UNROLL) {
+                        float4 p[KN_LANE_UNROLL];
+                        unsigned kk[KN_LANE_UNROLL];
+#pragma unroll
+                        for (int u = 0; u < KN_LANE_UNROLL; ++u) p[u] = pts[s + u];
+#pragma unroll
+                        for (int u = 0; u < KN_LANE_UNROLL; ++u) kk[u] = cand_key_v(p[u], qx, qy, qz, HIMASK, s + u);
+#pragma unroll
+                        for (int u = 0; u < KN_LANE_UNROLL; ++u) {
+                            const unsigned i0 = topk_push<KM>(keys, kk[u]);
+                            if constexpr (kStats) st_ins += i0;
+                        }
+                    }
+                    for (; s < s1; ++s) {
+                        const unsigned i0 = topk_push<KM>(keys, cand_key_v(pts[s], qx, qy, qz, HIMASK, s));
+                        if constexpr (kStats) st_ins += i0;
+                    }
+                    return;
+                } else {
                 if constexpr (kStats) {
                     st_rows += 1u;
                     st_cand += (unsigned)(s1 - s0);
@@ -408,8 +522,18 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const unsigned i0 = topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
                     if constexpr (kStats) st_ins += i0;
                 }
+                }
             });
-        if (kStats && lane == 0) {  // wave-uniform work statistics (4 atomics per chunk)
+        if (kStats && LANE) {  // lane walk: per-lane rows / candidates, summed over live lanes
+            if (live && in_range) {
+                atomicAdd(a.counters + 4, st_rows);
+                atomicAdd(a.counters + 5, st_cand);
+            }
+            if (lane == 0) {
+                atomicAdd(a.counters + 6, st_ins);
+                atomicAdd(a.counters + 7, 1u);
+            }
+        } else if (kStats && lane == 0) {  // wave-uniform work statistics (4 atomics per chunk)
             atomicAdd(a.counters + 4, st_rows);
             atomicAdd(a.counters + 5, st_cand);
             atomicAdd(a.counters + 6, st_ins);
@@ -426,7 +550,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
             const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
             dd[j] = valid ? d : INFINITY;
-            ii[j] = valid ? __float_as_uint(p.w) : SENT;
+            ii[j] = valid ? w_id(a, __float_as_uint(p.w)) : SENT;
         }
         // keys are sorted by truncated distance; the exact order differs only inside equal
         // truncation buckets (near-ties: clouds can hold several candidates within 2^-12 of
@@ -479,7 +603,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                                 const float4 p = pts[s];
                                 const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
                                 const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                                const unsigned id = __float_as_uint(p.w);
+                                const unsigned id = w_id(a, __float_as_uint(p.w));
                                 const bool take = s != qslot && d2 <= thr && pair_less(d2, id, dd[KM - 1], ii[KM - 1]);
                                 if (__builtin_amdgcn_ballot_w64(take)) {
                                     if (take) {
@@ -523,12 +647,12 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         }
         const bool geo_ok = (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
         if (geo_ok) {
-            const size_t row = (size_t)qorig * (size_t)k;
+            const size_t row = (size_t)w_row(a, qorig, qsidx) * (size_t)k;
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
                 if (j < k) {
                     const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 209);
-                    a.out_idx[o] = a.id_map ? a.id_map[KN_IDX(ii[j], (unsigned)a.n, 211)] : ii[j];
+                    a.out_idx[o] = out_id(a, ii[j]);
                     if (a.out_dist) a.out_dist[o] = dd[j];
                 }
             }
@@ -633,7 +757,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
         const unsigned qsidx = (unsigned)(cb[qrow * cbs + hx] + (qi - qpref[lo]));
         const float4 qp = a.sorted[KN_IDX(qsidx, (unsigned)a.n, 222)];
         const unsigned qorig = __float_as_uint(qp.w);
-        const bool live = (int)qorig < a.n_queries;
+        const bool live = w_live(a, qorig);
         const float qx = qp.x, qy = qp.y, qz = qp.z;
         const int cx = cell_coord(g, 0, qx) - sx0;
         const int cy = cell_coord(g, 1, qy) - sy0;
@@ -791,7 +915,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
             const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
             const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
             dd[j] = valid ? d : INFINITY;
-            ii[j] = valid ? __float_as_uint(p.w) : SENT;
+            ii[j] = valid ? w_id(a, __float_as_uint(p.w)) : SENT;
             // at most 4 gathers in flight: 19 float4 loads hoisted together cost 76 VGPRs
             if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
         }
@@ -838,7 +962,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
                     const float4 p = a.sorted[KN_IDX(s, a.n, 227)];
                     const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
                     const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                    const unsigned id = __float_as_uint(p.w);
+                    const unsigned id = w_id(a, __float_as_uint(p.w));
                     const bool take = (unsigned)s != qsidx && d2 <= thr && pair_less(d2, id, dd[KM - 1], ii[KM - 1]);
                     if (__builtin_amdgcn_ballot_w64(take)) {
                         if (take) {
@@ -879,12 +1003,12 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
         }
         const bool geo_ok = (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
         if (geo_ok) {
-            const size_t row = (size_t)qorig * (size_t)k;
+            const size_t row = (size_t)w_row(a, qorig, qsidx) * (size_t)k;
 #pragma unroll
             for (int j = 0; j < KM; ++j) {
                 if (j < k) {
                     const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 228);
-                    a.out_idx[o] = a.id_map ? a.id_map[KN_IDX(ii[j], (unsigned)a.n, 229)] : ii[j];
+                    a.out_idx[o] = out_id(a, ii[j]);
                     if (a.out_dist) a.out_dist[o] = dd[j];
                 }
             }
@@ -904,6 +1028,7 @@ struct ExactArgs {
     int k;
     int n_queries;
     const unsigned* id_map;
+    const unsigned* row_of;
     CompleteBox complete;
     unsigned* out_idx;
     float* out_dist;
@@ -987,8 +1112,9 @@ struct LdsTopK {
 template <class Top>
 __device__ __forceinline__ void exact_query(const ExactArgs& a, const GridGeom& g, unsigned sidx, Top& top) {
     const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 302)];
-    const unsigned qorig = __float_as_uint(qp.w);
-    if ((int)qorig >= a.n_queries) return;
+    const unsigned qw = __float_as_uint(qp.w);
+    if (!w_live(a, qw)) return;
+    const unsigned qorig = w_row(a, qw, sidx);
     const float qx = qp.x, qy = qp.y, qz = qp.z;
     const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
     const int k = a.k;
@@ -1015,7 +1141,7 @@ __device__ __forceinline__ void exact_query(const ExactArgs& a, const GridGeom& 
                         const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
                         const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
                         const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                        const unsigned id = __float_as_uint(c.w);
+                        const unsigned id = w_id(a, __float_as_uint(c.w));
                         if (top.improves(d2, id)) top.insert(d2, id);
                     }
                 }
@@ -1045,7 +1171,7 @@ __device__ __forceinline__ void exact_query(const ExactArgs& a, const GridGeom& 
     const size_t row = (size_t)qorig * (size_t)k;
     top.emit(k, [&](int j, float d, unsigned i) {
         const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 305);
-        a.out_idx[o] = (i == SENT) ? SENT : (a.id_map ? a.id_map[KN_IDX(i, (unsigned)a.n, 307)] : i);
+        a.out_idx[o] = (i == SENT) ? SENT : out_id(a, i);
         if (a.out_dist) a.out_dist[o] = d;
     });
 }
@@ -1106,8 +1232,9 @@ __global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
         const unsigned sidx = (unsigned)__builtin_amdgcn_readfirstlane(
             (int)(a.list ? a.list[KN_IDX(t, a.n, 301)] : (unsigned)t));
         const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 302)];
-        const unsigned qorig = __float_as_uint(qp.w);
-        if ((int)qorig >= a.n_queries) continue;
+        const unsigned qw = __float_as_uint(qp.w);
+        if (!w_live(a, qw)) continue;
+        const unsigned qorig = w_row(a, qw, sidx);
         const float qx = qp.x, qy = qp.y, qz = qp.z;
         const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
         RegTopK<KT> top;
@@ -1141,7 +1268,7 @@ __global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
                 const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
                 const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
                 const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                const unsigned id = __float_as_uint(c.w);
+                const unsigned id = w_id(a, __float_as_uint(c.w));
                 if (top.improves(d2, id)) top.insert(d2, id);
             };
             if (dense) {
@@ -1241,7 +1368,7 @@ __global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
             const size_t o = KN_IDX((size_t)qorig * (size_t)k + lane, (size_t)a.n_queries * k, 305);
             const unsigned id = (unsigned)v;
             const bool empty = (v == ~0ull);
-            a.out_idx[o] = empty ? SENT : (a.id_map ? a.id_map[KN_IDX(id, (unsigned)a.n, 307)] : id);
+            a.out_idx[o] = empty ? SENT : out_id(a, id);
             if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
         }
     }
@@ -1267,20 +1394,27 @@ __global__ void to_stored_kernel(const unsigned* __restrict__ out_orig, const un
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
-// Query algorithm: flags bit 1 -> stream kernel, bit 2 -> LDS-staged tile kernel; neither ->
-// the process default (env KN_QUERY_ALGO = "tile" | "stream", else kDefaultAlgo).
-constexpr int kAlgoTile = 1, kAlgoStream = 2;
-constexpr int kDefaultAlgo = kAlgoTile;
-inline int query_algo(int flags) {
+// Query algorithm: flags bit 1 -> stream kernel, bit 2 -> LDS-staged tile kernel (union
+// stream), bit 3 -> tile kernel (lane walk); none -> the process default (env KN_QUERY_ALGO =
+// "tile" | "stream" | "lane", else the measured default for K: the lane walk, except the
+// 2.9-points/cell band 40 < K <= 50, where the lane's own +-H region certifies fewer queries
+// than the wave's union region (900K uniform, MI355X: K=16 0.513 -> 0.331 ms, K=32 1.21 -> 0.95,
+// K=64 4.01 -> 3.26, but K=50 2.28 -> 2.40 with 3x the exact-path queries;
+// profiles/ab_r1_lane_walk.jsonl).
+constexpr int kAlgoTile = 1, kAlgoStream = 2, kAlgoLane = 3;
+inline int default_algo(int k) { return (k > 40 && k <= 50) ? kAlgoTile : kAlgoLane; }
+inline int query_algo(int flags, int k) {
     if (flags & kQueryAlgoStream) return kAlgoStream;
     if (flags & kQueryAlgoTile) return kAlgoTile;
+    if (flags & kQueryAlgoLane) return kAlgoLane;
     static const int def = [] {
         const char* e = std::getenv("KN_QUERY_ALGO");
         if (e && std::strcmp(e, "stream") == 0) return kAlgoStream;
         if (e && std::strcmp(e, "tile") == 0) return kAlgoTile;
-        return kDefaultAlgo;
+        if (e && std::strcmp(e, "lane") == 0) return kAlgoLane;
+        return 0;
     }();
-    return def;
+    return def ? def : default_algo(k);
 }
 
 template <int KT>
@@ -1298,6 +1432,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         TileArgs a;
         a.sorted = q.sorted; a.cell_start = q.cell_start; a.geom = q.geom; a.n = q.n;
         a.X = X; a.Y = Y; a.Z = Z; a.k = q.k; a.n_queries = q.n_queries; a.id_map = q.id_map;
+        a.row_of = q.row_of;
         a.complete = q.complete; a.out_idx = q.out_idx; a.out_dist = q.out_dist;
         a.fallback_list = q.fallback_list; a.counters = q.counters;
         a.TX = q.tile[0]; a.TY = q.tile[1]; a.TZ = q.tile[2]; a.H = q.halo;
@@ -1310,7 +1445,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.cb_stride = std::min(X, a.TX + 2 * a.H) + 1;
         a.max_rows = std::min(Y, a.TY + 2 * a.H) * std::min(Z, a.TZ + 2 * a.H);
         const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
-        if (query_algo(q.flags) == kAlgoStream) {
+        if (query_algo(q.flags, q.k) == kAlgoStream) {
             a.flags = q.flags & kQueryForceRescan;
             const size_t dyn = ((size_t)a.max_rows * a.cb_stride + (size_t)a.TY * a.TZ + 1) * sizeof(int);
             if constexpr (KT <= 64) knn_stream_kernel<KT, M><<<nt, kWG, dyn, s>>>(a);
@@ -1318,18 +1453,25 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         const size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity);
         static bool attr_set = false;
         if (!attr_set) {
-            if constexpr (KT <= 64)
-                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M>,
+            if constexpr (KT <= 64) {
+                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M, false>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M, true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            }
             attr_set = true;
         }
-        if constexpr (KT <= 64) knn_tile_kernel<KT, M><<<nt, kWG, lds, s>>>(a);
+        if constexpr (KT <= 64) {
+            if (query_algo(q.flags, q.k) == kAlgoLane) knn_tile_kernel<KT, M, true><<<nt, kWG, lds, s>>>(a);
+            else knn_tile_kernel<KT, M, false><<<nt, kWG, lds, s>>>(a);
+        }
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     ExactArgs b;
     b.sorted = q.sorted; b.cell_start = q.cell_start; b.geom = q.geom; b.n = q.n;
     b.X = X; b.Y = Y; b.Z = Z; b.k = q.k; b.n_queries = q.n_queries; b.id_map = q.id_map;
+    b.row_of = q.row_of;
     b.complete = q.complete; b.out_idx = q.out_idx; b.out_dist = q.out_dist;
     b.list = tiles ? q.fallback_list : nullptr;
     b.list_count = q.counters + 0;

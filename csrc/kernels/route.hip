@@ -316,6 +316,19 @@ __global__ void meta_finalize_kernel(const unsigned* __restrict__ partials, int 
     out[t] = v;
 }
 
+// Global-id mode of the query kernels (query.hip, w_live / w_id / w_row): the stored point at
+// sorted slot i gets w = gid[perm[i]], with the halo bit on non-owned points (perm[i] >=
+// n_owned). One coalesced pass over the N stored points replaces K random id_map gathers per
+// query in the query epilogue.
+__global__ void global_w_kernel(float4* __restrict__ sorted, const unsigned* __restrict__ perm,
+                                const int* __restrict__ gids, int n, int n_owned) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned local = perm[KN_IDX(i, n, 420)];
+    const unsigned gid = (unsigned)gids[KN_IDX(local, (unsigned)n, 421)];
+    sorted[i].w = __uint_as_float((gid & 0x7FFFFFFFu) | ((int)local >= n_owned ? 0x80000000u : 0u));
+}
+
 }  // namespace
 
 int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
@@ -361,6 +374,11 @@ hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* o
     hipError_t e;
     if ((e = launch_bbox_partials(pts, n, words, s)) != hipSuccess) return e;
     meta_finalize_kernel<<<1, 64, 0, s>>>(words, n > 0 ? bbox_block_count(n) : 0, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_global_w(float4* sorted, const unsigned* perm, const int* gids, int n, int n_owned, hipStream_t s) {
+    if (n > 0) global_w_kernel<<<cdiv(n, kRT), kRT, 0, s>>>(sorted, perm, gids, n, n_owned);
     return hipGetLastError();
 }
 

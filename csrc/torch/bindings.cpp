@@ -92,7 +92,8 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                                  std::vector<int64_t> dims, int64_t k, int64_t n_queries,
                                  c10::optional<torch::Tensor> id_map, std::vector<double> complete,
                                  std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
-                                 bool use_tiles, bool with_dist, int64_t flags) {
+                                 bool use_tiles, bool with_dist, int64_t flags,
+                                 c10::optional<torch::Tensor> row_of) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
@@ -123,6 +124,11 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
         TORCH_CHECK(id_map->is_cuda() && id_map->scalar_type() == torch::kInt32 && id_map->numel() >= n,
                     "id_map must be an int32 GPU tensor with >= N entries");
         q.id_map = reinterpret_cast<const unsigned*>(id_map->data_ptr<int>());
+    }
+    if (row_of.has_value()) {
+        TORCH_CHECK(row_of->is_cuda() && row_of->scalar_type() == torch::kInt32 && row_of->numel() >= n,
+                    "row_of must be an int32 GPU tensor with >= N entries");
+        q.row_of = reinterpret_cast<const unsigned*>(row_of->data_ptr<int>());
     }
     for (int a = 0; a < 3; ++a) { q.complete.lo[a] = (float)complete[a]; q.complete.hi[a] = (float)complete[3 + a]; }
     q.out_idx = reinterpret_cast<unsigned*>(out_idx.data_ptr<int>());
@@ -472,8 +478,15 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     const kn::AutoParams ap = kn::auto_params((int)npts, (int)k, (float)ppc, th, 0, fext);
     const std::vector<int64_t> dims = {ap.dims[0], ap.dims[1], ap.dims[2]};
     auto g = build(pg[0], dims, deterministic, box);
-    auto q = query(g[0], g[1], g[3], dims, k, n_owned, pg[1], complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
-                   ap.halo, ap.lds_capacity, true, true, 0);
+    // global-id mode: the stored points carry their global ids (halo bit on non-owned points), so
+    // the query epilogue writes ids without a random gather through the id table
+    const int64_t nst = g[0].size(0);
+    KN_CHECK_HIP(kn::launch_global_w(reinterpret_cast<float4*>(g[0].data_ptr<float>()),
+                                     reinterpret_cast<const unsigned*>(g[2].data_ptr<int>()), pg[1].data_ptr<int>(),
+                                     (int)nst, (int)n_owned,
+                                     c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+    auto q = query(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
+                   ap.halo, ap.lds_capacity, true, true, 0, g[2]);
     return {pg[0], pg[1], q[0], q[1], q[2]};
 }
 
@@ -661,7 +674,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("query", &query, "k-nearest-neighbour queries on a built grid (GPU)", py::arg("sorted"),
           py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("k"), py::arg("n_queries"),
           py::arg("id_map"), py::arg("complete"), py::arg("tile"), py::arg("halo"), py::arg("lds_capacity"),
-          py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0);
+          py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0, py::arg("row_of") = py::none());
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");

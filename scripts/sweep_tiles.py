@@ -1,4 +1,6 @@
-"""Sweep grid density / tile shape / halo for the tile kernel (solve time, device events)."""
+"""Sweep grid density / tile shape / halo for the tile kernel (solve time, device events).
+KN_QUERY_ALGO=lane|tile selects the kernel variant.
+usage: python scripts/sweep_tiles.py [n] [k] [ppc,..] [TXxTYxTZ,..] [halo,..]"""
 import itertools, json, sys
 import torch
 from cuda_knearests_amd.ops import knn_ops as ops
@@ -12,7 +14,8 @@ res = []
 PPC = [float(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1.5, 2.0, 2.5, 3.1, 4.0, 5.0]
 TILES = ([tuple(int(v) for v in t.split("x")) for t in sys.argv[4].split(",")] if len(sys.argv) > 4 else
          [(4, 4, 4), (8, 4, 4), (4, 4, 2), (8, 8, 2), (6, 6, 6), (8, 4, 2)])
-for ppc, tile, halo in itertools.product(PPC, TILES, [0]):
+HALOS = [int(h) for h in sys.argv[5].split(",")] if len(sys.argv) > 5 else [0]  # 0 = plan default
+for ppc, tile, halo in itertools.product(PPC, TILES, HALOS):
     plan = ops.Plan.auto(n, k, ppc, tile, halo)
     if plan.lds_bytes > 160 * 1024:
         continue

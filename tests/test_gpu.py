@@ -64,6 +64,31 @@ def test_stream_kernel_vs_oracle(cuda, k, gen):
     assert torch.equal(idx, i2) and torch.equal(d2, e2)
 
 
+@pytest.mark.parametrize("k,gen", [(1, "uniform"), (8, "blue"), (16, "uniform"), (32, "uniform"), (50, "uniform"),
+                                   (64, "uniform"), (16, "clustered")])
+def test_lane_walk_vs_union_stream(cuda, k, gen):
+    # per-lane walk (flags bit 3, the default) vs the wave-uniform union stream (bit 2) of the
+    # same LDS-staged tile kernel: oracle-exact and bit-identical to each other
+    mk = {"uniform": uniform_cloud, "clustered": clustered_cloud, "blue": blue_cloud}[gen]
+    p = mk(30000, seed=500 + k).to(cuda)
+    g = kn.build_grid(p, k)
+    idx, d2 = kn.query(g, k, flags=8)
+    _assert_matches_oracle(p, idx, d2, k)
+    i2, e2 = kn.query(g, k, flags=4)
+    assert torch.equal(idx, i2) and torch.equal(d2, e2)
+    i3, e3 = kn.query(g, k)  # default algorithm
+    assert torch.equal(idx, i3) and torch.equal(d2, e3)
+
+
+@pytest.mark.parametrize("algo", [4, 8])
+def test_tile_variants_forced_rescan(cuda, algo):
+    p = uniform_cloud(20000, seed=402, device=cuda)
+    g = kn.build_grid(p, 16)
+    idx, d2, info = kn.query(g, 16, return_info=True, flags=1 | algo)
+    assert int(info["counters"][3]) == p.size(0)
+    _assert_matches_oracle(p, idx, d2, 16)
+
+
 def test_stream_kernel_forced_rescan(cuda):
     p = uniform_cloud(20000, seed=401, device=cuda)
     g = kn.build_grid(p, 16)
