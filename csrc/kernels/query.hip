@@ -84,6 +84,14 @@ struct TileArgs {
 #ifndef KN_LDS_PIPE
 #define KN_LDS_PIPE 1
 #endif
+// Lane walk region: the lane's own cell +- H, then (full mode) the rest of the staged block
+// (tile + H) for the lanes whose bound still reaches past their own box. KN_LANE_FULL: 0 never,
+// 1 for K buckets > 40 (measured: 900K K=50 2.41 -> 2.22 ms with 2728 -> 638 exact-path
+// queries, K=64 3.31 -> 3.29; but K=16 0.349 -> 0.366, K=32 0.947 -> 0.966 from the extra
+// code; profiles/ab_r1_lane_full.jsonl), 2 always.
+#ifndef KN_LANE_FULL
+#define KN_LANE_FULL 1
+#endif
 constexpr int kQueryForceRescan = 1;
 constexpr int kQueryAlgoStream = 2;
 constexpr int kQueryAlgoTile = 4;
@@ -180,6 +188,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     // K + M margin slots + 1: the query itself is not filtered in the hot loop (that cost 3
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
     constexpr int KM = KT + M + 1;
+    constexpr bool kFull = LANE && (KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4* pts = reinterpret_cast<float4*>(smem);
     int* cb = reinterpret_cast<int*>(smem + (size_t)a.cap * sizeof(float4));
@@ -316,11 +325,20 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         // scanned region: the wave's bounding box of the live queries' cells + H (union
         // stream), or each lane's own cell + H (lane walk)
         int rx0, rx1, ry0, ry1, rz0, rz1, zc = 0, yc = 0, nzt = 0, nyt = 0;
+        // lane walk: the lane's own cell +- H (phase 1 of the walk)
+        int hx0 = 0, hx1 = -1, hy0 = 0, hy1 = -1, hz0 = 0, hz1 = -1;
         if constexpr (LANE) {
             if (!__builtin_amdgcn_ballot_w64(live)) continue;  // no live query in this chunk
-            rx0 = max(0, cx - a.H); rx1 = min(nxs - 1, cx + a.H);
-            ry0 = max(0, cy - a.H); ry1 = min(nys - 1, cy + a.H);
-            rz0 = max(0, cz - a.H); rz1 = min(nzs - 1, cz + a.H);
+            hx0 = max(0, cx - a.H); hx1 = min(nxs - 1, cx + a.H);
+            hy0 = max(0, cy - a.H); hy1 = min(nys - 1, cy + a.H);
+            hz0 = max(0, cz - a.H); hz1 = min(nzs - 1, cz + a.H);
+            if constexpr (kFull) {
+                rx0 = 0; rx1 = nxs - 1;
+                ry0 = 0; ry1 = nys - 1;
+                rz0 = 0; rz1 = nzs - 1;
+            } else {
+                rx0 = hx0; rx1 = hx1; ry0 = hy0; ry1 = hy1; rz0 = hz0; rz1 = hz1;
+            }
         } else {
             // 3 packed (-min, max) reductions
             const int2 bx = wave_minmax_i32(live ? cx : INT_MAX, live ? cx : INT_MIN);
@@ -339,14 +357,26 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         // cells its current bound `tau` still needs (|x - qx|^2 <= tau - dyz^2). Union stream: the
         // wave takes the union, and `body(s0, s1)` streams the uniform LDS slot range [s0, s1).
         // Lane walk: the row offset is uniform, the row itself and [s0, s1) are per lane.
-        auto scan_region = [&](auto&& lane_tau, auto&& body) {
+        auto scan_region = [&](auto&& lane_tau, auto&& body2) {
           if constexpr (LANE) {
             const int side = 2 * a.H + 1;
+            // LDS slot range [s0, s1) of cells [x0, x1] of staged row (y, z); empty if x0 > x1
+            auto lane_span = [&](int y, int z, int x0, int x1) {
+                int2 sp = make_int2(0, 0);
+                if (x0 <= x1) {
+                    const int r = y + nys * z;
+                    const int rb = rowbase[r] - cb[r * cbs];
+                    sp.x = rb + cb[r * cbs + x0];
+                    sp.y = KN_IDX(rb + cb[r * cbs + x1 + 1], S + 1, 212);
+                }
+                return sp;
+            };
+            auto body = [&](int2 sp) { body2(sp.x, sp.y); };
             for (int tz_ = 0; tz_ < side; ++tz_) {
                 const int z = cz + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
                 const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
                 const float dz2 = dzb * dzb;
-                const bool zin = live && z >= rz0 && z <= rz1;
+                const bool zin = live && z >= hz0 && z <= hz1;
                 if (!__builtin_amdgcn_ballot_w64(zin && dz2 <= lane_tau())) continue;
                 for (int ty_ = 0; ty_ < side; ++ty_) {
                     const int y = cy + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
@@ -354,25 +384,91 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const float dyz2 = fmaf(dyb, dyb, dz2);
                     const float tau = lane_tau();
                     int lx0 = 0, lx1 = -1;
-                    if (zin && y >= ry0 && y <= ry1 && dyz2 <= tau) {
+                    if (zin && y >= hy0 && y <= hy1 && dyz2 <= tau) {
                         if (tau == INFINITY) {
-                            lx0 = rx0; lx1 = rx1;
+                            lx0 = hx0; lx1 = hx1;
                         } else {
                             const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
-                            lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
-                            lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
+                            lx0 = max(hx0, cell_coord(g, 0, qx - rr) - sx0);
+                            lx1 = min(hx1, cell_coord(g, 0, qx + rr) - sx0);
                         }
                     }
                     if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
-                    int s0 = 0, s1 = 0;
-                    if (lx0 <= lx1) {
-                        const int r = y + nys * z;
-                        const int rb = rowbase[r] - cb[r * cbs];
-                        s0 = rb + cb[r * cbs + lx0];
-                        s1 = KN_IDX(rb + cb[r * cbs + lx1 + 1], S + 1, 212);
-                    }
-                    body(s0, s1);
+                    body(lane_span(y, z, lx0, lx1));
                 }
+            }
+            if constexpr (kFull) {
+            // Phase 2: the rest of the staged block, only for lanes whose bound still reaches
+            // a cell outside their own +-H box (the slabs just outside it are the nearest such
+            // cells on each axis). Centre-out per axis; a magnitude no lane reaches on either
+            // side ends the axis loop (slab distance grows with it, the bound only shrinks).
+            // Rows of the phase-1 band skip the x-interval phase 1 already scanned.
+            bool more = false;
+            {
+                const float t = lane_tau();
+                auto out = [&](int axis, float q, int c, int s0c) {
+                    const float d = slab_dist(g, axis, q, s0c + c, s0c + c);
+                    return d * d <= t;
+                };
+                more = (hx0 > rx0 && out(0, qx, hx0 - 1, sx0)) || (hx1 < rx1 && out(0, qx, hx1 + 1, sx0)) ||
+                       (hy0 > ry0 && out(1, qy, hy0 - 1, sy0)) || (hy1 < ry1 && out(1, qy, hy1 + 1, sy0)) ||
+                       (hz0 > rz0 && out(2, qz, hz0 - 1, sz0)) || (hz1 < rz1 && out(2, qz, hz1 + 1, sz0));
+                more = more && live;
+            }
+            if (__builtin_amdgcn_ballot_w64(more)) {
+                for (int tz_ = 0; tz_ < 2 * nzs; ++tz_) {
+                    const int mz = (tz_ + 1) >> 1;
+                    const int z = cz + ((tz_ & 1) ? mz : -mz);
+                    if (tz_ & 1) {
+                        const float t = lane_tau();
+                        bool reach = false;
+                        if (more) {
+                            if (cz + mz <= rz1) { const float d = slab_dist(g, 2, qz, sz0 + cz + mz, sz0 + cz + mz); reach |= d * d <= t; }
+                            if (cz - mz >= rz0) { const float d = slab_dist(g, 2, qz, sz0 + cz - mz, sz0 + cz - mz); reach |= d * d <= t; }
+                        }
+                        if (!__builtin_amdgcn_ballot_w64(reach)) break;
+                    }
+                    const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
+                    const float dz2 = dzb * dzb;
+                    const bool zin = more && z >= rz0 && z <= rz1;
+                    if (!__builtin_amdgcn_ballot_w64(zin && dz2 <= lane_tau())) continue;
+                    const bool zband = z >= hz0 && z <= hz1;
+                    for (int ty_ = 0; ty_ < 2 * nys; ++ty_) {
+                        const int my = (ty_ + 1) >> 1;
+                        const int y = cy + ((ty_ & 1) ? my : -my);
+                        if (ty_ & 1) {
+                            const float t = lane_tau();
+                            bool reach = false;
+                            if (zin) {
+                                if (cy + my <= ry1) { const float d = slab_dist(g, 1, qy, sy0 + cy + my, sy0 + cy + my); reach |= fmaf(d, d, dz2) <= t; }
+                                if (cy - my >= ry0) { const float d = slab_dist(g, 1, qy, sy0 + cy - my, sy0 + cy - my); reach |= fmaf(d, d, dz2) <= t; }
+                            }
+                            if (!__builtin_amdgcn_ballot_w64(reach)) break;
+                        }
+                        const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
+                        const float dyz2 = fmaf(dyb, dyb, dz2);
+                        const float tau = lane_tau();
+                        int lx0 = 0, lx1 = -1;
+                        if (zin && y >= ry0 && y <= ry1 && dyz2 <= tau) {
+                            if (tau == INFINITY) {
+                                lx0 = rx0; lx1 = rx1;
+                            } else {
+                                const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                                lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
+                                lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
+                            }
+                        }
+                        if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
+                        int bx0 = 0, bx1 = -1;  // right part of a phase-1 band row
+                        if (zband && y >= hy0 && y <= hy1) {
+                            bx0 = max(lx0, hx1 + 1); bx1 = lx1;
+                            lx1 = min(lx1, hx0 - 1);
+                        }
+                        body(lane_span(y, z, lx0, lx1));
+                        if (__builtin_amdgcn_ballot_w64(bx0 <= bx1)) body(lane_span(y, z, bx0, bx1));
+                    }
+                }
+            }
             }
           } else {
             for (int tz_ = 0; tz_ < nzt; ++tz_) {
@@ -423,7 +519,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     // uniform bounds -> scalar loop control
                     const int s0 = __builtin_amdgcn_readfirstlane(rb + cb[r * cbs + X.x]);
                     const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + cb[r * cbs + X.y + 1], S + 1, 207));
-                    body(s0, s1);
+                    body2(s0, s1);
                 }
             }
           }
@@ -1396,13 +1492,12 @@ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 // Query algorithm: flags bit 1 -> stream kernel, bit 2 -> LDS-staged tile kernel (union
 // stream), bit 3 -> tile kernel (lane walk); none -> the process default (env KN_QUERY_ALGO =
-// "tile" | "stream" | "lane", else the measured default for K: the lane walk, except the
-// 2.9-points/cell band 40 < K <= 50, where the lane's own +-H region certifies fewer queries
-// than the wave's union region (900K uniform, MI355X: K=16 0.513 -> 0.331 ms, K=32 1.21 -> 0.95,
-// K=64 4.01 -> 3.26, but K=50 2.28 -> 2.40 with 3x the exact-path queries;
-// profiles/ab_r1_lane_walk.jsonl).
+// "tile" | "stream" | "lane", else the measured default: the lane walk for every K (900K
+// uniform, MI355X: K=16 0.513 -> 0.331 ms, K=32 1.21 -> 0.95, K=64 4.01 -> 3.26,
+// profiles/ab_r1_lane_walk.jsonl; K=50 2.27 -> 2.22 once the lane walk covers the whole staged
+// block above K=40, profiles/ab_r1_lane_full.jsonl).
 constexpr int kAlgoTile = 1, kAlgoStream = 2, kAlgoLane = 3;
-inline int default_algo(int k) { return (k > 40 && k <= 50) ? kAlgoTile : kAlgoLane; }
+inline int default_algo(int) { return kAlgoLane; }
 inline int query_algo(int flags, int k) {
     if (flags & kQueryAlgoStream) return kAlgoStream;
     if (flags & kQueryAlgoTile) return kAlgoTile;

@@ -65,7 +65,7 @@ def test_stream_kernel_vs_oracle(cuda, k, gen):
 
 
 @pytest.mark.parametrize("k,gen", [(1, "uniform"), (8, "blue"), (16, "uniform"), (32, "uniform"), (50, "uniform"),
-                                   (64, "uniform"), (16, "clustered")])
+                                   (64, "uniform"), (16, "clustered"), (50, "clustered"), (48, "blue")])
 def test_lane_walk_vs_union_stream(cuda, k, gen):
     # per-lane walk (flags bit 3, the default) vs the wave-uniform union stream (bit 2) of the
     # same LDS-staged tile kernel: oracle-exact and bit-identical to each other
@@ -80,13 +80,14 @@ def test_lane_walk_vs_union_stream(cuda, k, gen):
     assert torch.equal(idx, i3) and torch.equal(d2, e3)
 
 
-@pytest.mark.parametrize("algo", [4, 8])
-def test_tile_variants_forced_rescan(cuda, algo):
+@pytest.mark.parametrize("algo,k", [(4, 16), (8, 16), (8, 50)])
+def test_tile_variants_forced_rescan(cuda, algo, k):
+    # k=50: the lane walk's second phase (rest of the staged block, K buckets > 40) in the re-scan
     p = uniform_cloud(20000, seed=402, device=cuda)
-    g = kn.build_grid(p, 16)
-    idx, d2, info = kn.query(g, 16, return_info=True, flags=1 | algo)
+    g = kn.build_grid(p, k)
+    idx, d2, info = kn.query(g, k, return_info=True, flags=1 | algo)
     assert int(info["counters"][3]) == p.size(0)
-    _assert_matches_oracle(p, idx, d2, 16)
+    _assert_matches_oracle(p, idx, d2, k)
 
 
 def test_stream_kernel_forced_rescan(cuda):
