@@ -100,7 +100,9 @@ def test_plan_auto_reference_density():
     # ~3.4 points per cell (reference knearests.cu:249 uses 3.1), rounded to whole 4-cell tiles:
     # (900000/3.4)^(1/3) = 64.2 -> 64
     assert p.dims == [64, 64, 64]
-    assert all(d % 4 == 0 for d in kn.Plan.auto(10_000_000, 32).dims)
+    q = kn.Plan.auto(10_000_000, 32)
+    assert q.tile == [4, 4, 4] and all(d % t == 0 for d, t in zip(q.dims, q.tile))
+    assert kn.Plan.auto(900_000, 50).halo == 3
     assert kn.Plan.auto(1000, 8).dims == [7, 7, 7]  # small grids are not rounded
     assert p.halo >= 1 and p.lds_capacity >= 1024 and p.lds_bytes <= 160 * 1024
 
