@@ -1641,16 +1641,16 @@ int lds_capacity_for(double staged) {
     return std::max(128, std::min(cap, 8192));
 }
 
-// Target density after whole-tile rounding (900K uniform sweeps on MI355X,
-// profiles/sweep_r1_tiles*.txt): K <= 40 is fastest at ~3.4 points/cell (64^3 for 900K: K=16
-// 0.503 ms vs 0.542 at 68^3 and 0.635 at 60^3; K=32 1.165 ms); K = 50 at ~2.9 (68^3, 2-ring
-// halo: 2.21 ms vs 2.37 at 72^3 with 3 rings). The reference uses 3.1 (knearests.cu:249).
+// Target density after whole-tile rounding. The reference uses 3.1 (knearests.cu:249). With the
+// union-stream kernel (profiles/sweep_r1_tiles*.txt) K <= 40 was fastest at ~3.4 points/cell
+// (64^3 for 900K: K=16 0.503 ms vs 0.542 at 68^3 and 0.635 at 60^3) and K=50 at ~2.9.
 // Lane-walk density targets from sweeps on MI355X (profiles/sweep_r1_lane.txt,
-// profiles/sweep_r1_lane_k32_k50.txt): 3.4 pts/cell with 4x4x4 tiles up to K=50 (K=50 with a
-// 3-ring halo: 2.20 -> 1.96 ms at 900K, no exact-path queries), 2.9 above. K=32 at 5.0 pts/cell
+// profiles/sweep_r1_lane_k32_k50.txt, profiles/sweep_r1_lane_k64.txt): 3.4 pts/cell with 4x4x4
+// tiles for every tile-path K (<= 64); above K=40 with a 3-ring halo (K=50 at 900K 2.20 ->
+// 1.96 ms; K=64 vs 2.9 pts/cell: 900K 3.26 -> 2.81 ms, 3M 9.43 -> 8.70). K=32 at 5.0 pts/cell
 // with 4x4x2 tiles won at 900K (0.94 -> 0.79 ms) but lost at 3M (2.31 -> 2.66) and 10M
-// (6.94 -> 8.01), so it is not the default.
-float default_points_per_cell(int k) { return k <= 50 ? 3.4f : 2.9f; }
+// (6.94 -> 8.01), so it is not the default. K > 64 (exact kernel only): 2.9.
+float default_points_per_cell(int k) { return k <= 64 ? 3.4f : 2.9f; }
 
 bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3]) {
     if (!(ppc > 0.f)) ppc = default_points_per_cell(k);
@@ -1697,7 +1697,7 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
         // K-th neighbour radius in cells for a uniform cloud: (3(K+1)/(4 pi ppc))^(1/3)
         const double rk = std::cbrt(3.0 * (k + 1) / (4.0 * M_PI * ppc));
         p.halo = std::max(1, (int)std::ceil(rk + 0.35));
-        if (k > 40 && k <= 50) p.halo = std::max(p.halo, 3);  // measured: 3 rings beat 2 + exact path
+        if (k > 40 && k <= 64) p.halo = std::max(p.halo, 3);  // measured: 3 rings beat 2 + exact path
     }
     const double staged = (double)(p.tile[0] + 2 * p.halo) * (p.tile[1] + 2 * p.halo) *
                           (p.tile[2] + 2 * p.halo) * ppc;
