@@ -1679,6 +1679,12 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
     } else {
         x[0] = x[1] = x[2] = std::cbrt(cells);
     }
+    // Small clouds: fewer 4^3 tiles than CUs leave most of the chip idle; 2^3 tiles give 8x the
+    // workgroups (20K points, K=8: 0.049 -> 0.046 ms; at 300K 4^3 stays faster, 0.185 vs 0.197
+    // for 4x4x2; profiles/sweep_r1_small.txt)
+    if (!(tile_hint && (tile_hint[0] > 0 || tile_hint[1] > 0 || tile_hint[2] > 0)) &&
+        std::ceil(x[0] / 4) * std::ceil(x[1] / 4) * std::ceil(x[2] / 4) < 256.0)
+        for (int a = 0; a < 3; ++a) p.tile[a] = 2;
     // Whole tiles: a partial edge tile costs a full halo staging for a fraction of the queries
     // (66 cells = 16.5 tiles of 4 -> 17 % of the tiles partial), so axes of >= 4 tiles are
     // rounded to a multiple of the tile edge (900K, K=16: 66^3 -> 64^3, solve 0.566 -> 0.505 ms).
