@@ -34,33 +34,37 @@ METRIC = "queries/sec (whole node) + ms/build for 900K pts, k=16, at 1/2/4/8 MI3
 CPU_ORACLE_QPS = 1.35e6  # reference kd_tree.cpp, 900K uniform, K=16, 8-vCPU host
 
 
-def brute_check(points: torch.Tensor, idx: torch.Tensor, d2: torch.Tensor, k: int, nsample: int = 2048,
-                ids: torch.Tensor | None = None, queries: torch.Tensor | None = None) -> dict:
-    """Compare a random subset of rows with an exact brute force (fp32, same fma order)."""
+def brute_check(cloud: torch.Tensor, qids: torch.Tensor, idx: torch.Tensor, d2: torch.Tensor, k: int,
+                nsample: int = 2048) -> dict:
+    """Spot check of a random subset of rows against an exact brute force on the GPU.
+    ``cloud`` (N, 3) every point, indexed by the ids the rows hold; ``qids`` (M,) each row's query
+    id. Distances: vs the brute force's top-k (it rounds without fma: 1e-5 relative). Ids
+    (utils/check.py): distinct, not the query, and each reproduces its reported distance from the
+    points -- reported separately as ``bad_id_rows``."""
+    from cuda_knearests_amd.utils.check import knn_row_errors
+
     g = torch.Generator(device="cpu")
     g.manual_seed(1234)
     nq = idx.size(0)
-    sel = torch.randperm(nq, generator=g)[: min(nsample, nq)].to(points.device)
-    q = (queries if queries is not None else points)[sel]
+    sel = torch.randperm(nq, generator=g)[: min(nsample, nq)].to(cloud.device)
+    qsel = qids.to(cloud.device).long()[sel]
+    q = cloud[qsel]
     bad = 0
     # bound the (rows x N) temporaries to ~2e8 elements (multi-GPU clouds reach 10^8 points)
-    step = max(1, min(256, int(2e8) // max(1, points.size(0))))
+    step = max(1, min(256, int(2e8) // max(1, cloud.size(0))))
     for c0 in range(0, sel.numel(), step):
         qs = q[c0:c0 + step]
-        dx = points[None, :, 0] - qs[:, None, 0]
-        dy = points[None, :, 1] - qs[:, None, 1]
-        dz = points[None, :, 2] - qs[:, None, 2]
+        dx = cloud[None, :, 0] - qs[:, None, 0]
+        dy = cloud[None, :, 1] - qs[:, None, 1]
+        dz = cloud[None, :, 2] - qs[:, None, 2]
         dd = torch.addcmul(torch.addcmul(dx * dx, dy, dy), dz, dz)
-        self_idx = sel[c0:c0 + step] if queries is None else None
-        if self_idx is not None:
-            dd[torch.arange(qs.size(0), device=dd.device), self_idx] = float("inf")
-        else:
-            dd[dd == 0] = float("inf")  # distributed: exclude self by zero distance (ids differ)
+        dd[torch.arange(qs.size(0), device=dd.device), qsel[c0:c0 + step]] = float("inf")  # self, by id
         ref = torch.topk(dd, k, dim=1, largest=False).values
         got = d2[sel[c0:c0 + step]]
-        # brute force rounds without fma: allow 1e-5 relative
         bad += int(((got - ref).abs() > 1e-5 * ref.abs().clamp(min=1e-6)).any(1).sum())
-    return {"checked": int(sel.numel()), "bad_rows": bad}
+    e = knn_row_errors(cloud, qsel, idx[sel], d2[sel])
+    bad_id = sum(v for key, v in e.items() if key not in ("rows", "dist"))
+    return {"checked": int(sel.numel()), "bad_rows": bad, "bad_id_rows": bad_id}
 
 
 def make_cloud(args, dev, seed_offset: int = 0) -> torch.Tensor:
@@ -113,7 +117,7 @@ def run_native(args) -> dict:
     dt = time.perf_counter() - t0
     log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
     idx, d2 = e.results(dev)
-    chk = brute_check(pts, idx, d2, args.k) if not args.no_check else {}
+    chk = brute_check(pts, torch.arange(pts.size(0), device=dev), idx, d2, args.k) if not args.no_check else {}
     log(f"check {chk}")
     bts, sts = [], []
     for _ in range(5):
@@ -151,7 +155,8 @@ def run_single(args) -> dict:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
-    chk = brute_check(pts, kn.neighbors, kn.distances, args.k) if not args.no_check else {}
+    chk = brute_check(pts, torch.arange(pts.size(0), device=dev), kn.neighbors, kn.distances, args.k) \
+        if not args.no_check else {}
     log(f"check {chk}")
     # per-phase device times, median of a few eager runs
     bts, sts = [], []
@@ -241,9 +246,8 @@ def run_dist(args) -> dict:
         allp = [torch.empty(int(c.item()), 3, device=cdev) for c in n_all]
         dist.all_gather(allp, pts.to(cdev))
         cloud = torch.cat(allp).to(dev)
-        qpts = cloud[res.ids.long()]
-        chk = brute_check(cloud, res.neighbors, res.d2, args.k, nsample=1024, queries=qpts)
-        c = torch.tensor([chk["bad_rows"]], device=cdev)
+        chk = brute_check(cloud, res.ids, res.neighbors, res.d2, args.k, nsample=1024)
+        c = torch.tensor([chk["bad_rows"] + chk["bad_id_rows"]], device=cdev)
         dist.all_reduce(c)
         chk["bad_rows_all_ranks"] = int(c.item())
     out = {"t": float(t.item()), "stats": res.stats if res else {}, "check": chk, "n_total": args.n * world,
@@ -291,8 +295,8 @@ def run_loopback_bench(args) -> dict:
         cloud = torch.cat(shares)
         bad = checked = 0
         for res in out[:2]:
-            c = brute_check(cloud, res.neighbors, res.d2, args.k, nsample=128, queries=cloud[res.ids.long()])
-            bad += c["bad_rows"]
+            c = brute_check(cloud, res.ids, res.neighbors, res.d2, args.k, nsample=128)
+            bad += c["bad_rows"] + c["bad_id_rows"]
             checked += c["checked"]
         chk = {"checked": checked, "bad_rows": bad}
     st = out[0].stats

@@ -160,7 +160,7 @@ void grid_knn_cpu(const float* pts, int n, int n_queries, int k, float ppc, cons
     float lo[3], hi[3];
     for (int a = 0; a < 3; ++a) { lo[a] = std::numeric_limits<float>::infinity(); hi[a] = -lo[a]; }
     for (int i = 0; i < n; ++i)
-        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], pts[3 * i + a]); hi[a] = std::max(hi[a], pts[3 * i + a]); }
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], pts[3 * (size_t)i + a]); hi[a] = std::max(hi[a], pts[3 * (size_t)i + a]); }
     if (n == 0) { for (int a = 0; a < 3; ++a) { lo[a] = 0; hi[a] = 1; } }
     const int sz = std::max(1, (int)std::lround(std::cbrt(std::max(1.0, (double)n / ppc))));
     const int D[3] = {sz, sz, sz};
@@ -185,7 +185,7 @@ void grid_knn_cpu(const float* pts, int n, int n_queries, int k, float ppc, cons
     const long C = (long)D[0] * D[1] * D[2];
     std::vector<int> start(C + 1, 0), cellof(n);
     for (int i = 0; i < n; ++i) {
-        const int c = coord(0, pts[3 * i]) + D[0] * (coord(1, pts[3 * i + 1]) + D[1] * coord(2, pts[3 * i + 2]));
+        const int c = coord(0, pts[3 * (size_t)i]) + D[0] * (coord(1, pts[3 * (size_t)i + 1]) + D[1] * coord(2, pts[3 * (size_t)i + 2]));
         cellof[i] = c;
         start[c + 1]++;
     }
@@ -287,7 +287,7 @@ static void bbox_inflated(const std::vector<float>& xyz, float lo[3], float hi[3
     const size_t n = xyz.size() / 3;
     for (int a = 0; a < 3; ++a) { lo[a] = hi[a] = n ? xyz[a] : 0.f; }
     for (size_t i = 1; i < n; ++i)
-        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], xyz[3 * i + a]); hi[a] = std::max(hi[a], xyz[3 * i + a]); }
+        for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], xyz[3 * (size_t)i + a]); hi[a] = std::max(hi[a], xyz[3 * (size_t)i + a]); }
     const float d = 0.001f * std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]});
     for (int a = 0; a < 3; ++a) { lo[a] -= d; hi[a] += d; }
 }
@@ -301,7 +301,7 @@ void normalize_1000(std::vector<float>& xyz) {
     const size_t n = xyz.size() / 3;
 #pragma omp parallel for
     for (long i = 0; i < (long)n; ++i)
-        for (int a = 0; a < 3; ++a) xyz[3 * i + a] = (float)(1000.0 * (xyz[3 * i + a] - lo[a]) / side);
+        for (int a = 0; a < 3; ++a) xyz[3 * (size_t)i + a] = (float)(1000.0 * (xyz[3 * (size_t)i + a] - lo[a]) / side);
 }
 
 bool read_xyz(const std::string& path, std::vector<float>& xyz, bool normalize, std::string* err) {
@@ -339,7 +339,7 @@ bool write_xyz(const std::string& path, const float* xyz, int n, std::string* er
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) { if (err) *err = "cannot write " + path; return false; }
     std::fprintf(f, "%d\n", n);
-    for (int i = 0; i < n; ++i) std::fprintf(f, "%.9g %.9g %.9g\n", xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+    for (int i = 0; i < n; ++i) std::fprintf(f, "%.9g %.9g %.9g\n", xyz[3 * (size_t)i], xyz[3 * (size_t)i + 1], xyz[3 * (size_t)i + 2]);
     const bool ok = std::fclose(f) == 0;
     if (!ok && err) *err = "write failed: " + path;
     return ok;

@@ -124,6 +124,8 @@ hipError_t launch_to_stored_space(const unsigned* out_orig, const unsigned* perm
                                   unsigned* out_sorted, const float* dist_orig,
                                   float* dist_sorted, hipStream_t stream);
 hipError_t launch_invert_perm(const unsigned* perm, int n, unsigned* inv, hipStream_t stream);
+// xyz[3i..3i+2] = sorted[i].xyz : the reference's float3 stored-point view (kn_problem field).
+hipError_t launch_sorted_xyz(const float4* sorted, int n, float* xyz, hipStream_t stream);
 
 // Grid-occupancy statistics (reference kn_print_stats, knearests.cu:440-466):
 // out[0]=min, out[1]=max, out[2]=empty cells, out[3..3+hist_len) = histogram of counts.

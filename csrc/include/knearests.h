@@ -79,16 +79,34 @@ typedef struct {
     float ms_solve;           /* tiled query + fallback (device time)               */
 } kn_stats;
 
+/* The problem handle. Field names follow the reference struct (reference knearests.h:3-16);
+ * divergences, all documented here:
+ *   - d_cell_offsets / d_cell_offset_dists / d_cell_max / d_globcounter are NULL: the ring walk
+ *     is analytic (no offset table), there is no racy max-ring buffer (reference defect D2)
+ *     and no atomic bump allocator (cells are laid out by a deterministic scan, defect D5);
+ *   - d_ptrs has C+1 entries (exclusive scan, d_ptrs[C] = N); d_counters is NULL: the count
+ *     of cell c is d_ptrs[c+1] - d_ptrs[c];
+ *   - d_stored_points is a float3 array in stored order, as in the reference; the engine's own
+ *     float4 rows {x, y, z, bits(original index)} are d_stored_points4;
+ *   - d_knearests holds the N x K stored-space result after kn_solve, as in the reference
+ *     (knearests.cu:329-364), with UINT_MAX in slots that cannot be filled;
+ *   - k and impl are additions (runtime K, engine state). */
 typedef struct {
-    int allocated_points;        /* number of input points (reference field)               */
-    int dimx, dimy, dimz;        /* grid resolution (reference field)                      */
-    int num_cell_offsets;        /* kept for source compatibility; ring walk is analytic   */
-    int k;                       /* neighbours per point                                   */
-    unsigned int *d_permutation; /* device: perm[stored] = original index                  */
-    int *d_cell_start;           /* device: first stored index of each cell, C+1 entries   */
-    float *d_stored_points;      /* device: float4 {x,y,z,bits(original index)} per point  */
-    unsigned int *d_knearests;   /* device: N x K neighbours in stored space               */
-    void *impl;                  /* engine state (opaque)                                  */
+    int allocated_points;          /* number of input points                                */
+    int dimx, dimy, dimz;          /* grid resolution                                       */
+    int num_cell_offsets;          /* 0: no offset table (analytic ring walk)               */
+    int *d_cell_offsets;           /* NULL (see above)                                      */
+    float *d_cell_offset_dists;    /* NULL                                                  */
+    float *d_cell_max;             /* NULL                                                  */
+    unsigned int *d_permutation;   /* device: perm[stored] = original index                 */
+    int *d_counters;               /* NULL: counts are d_ptrs[c+1] - d_ptrs[c]              */
+    int *d_ptrs;                   /* device: first stored index of each cell, C+1 entries  */
+    int *d_globcounter;            /* NULL                                                  */
+    kn_float3 *d_stored_points;    /* device: N points in stored order (float3)             */
+    unsigned int *d_knearests;     /* device: N x K neighbours in stored space (after solve) */
+    int k;                         /* neighbours per point                                  */
+    float *d_stored_points4;       /* device: N float4 {x,y,z,bits(original index)}         */
+    void *impl;                    /* engine state (opaque)                                 */
 } kn_problem;
 
 /* ---- reference-compatible API ---------------------------------------------------- */
@@ -120,6 +138,10 @@ kn_problem *kn_load(const char *path, const kn_config *cfg);
  * a malloc()'d array of *n points, or NULL (see kn_last_error()). */
 kn_float3 *kn_read_xyz(const char *path, int *n, int normalize);
 kn_status kn_write_xyz(const char *path, const kn_float3 *pts, int n);
+
+/* ABI self-check for bindings (ctypes, other languages): sizeof of the public structs as
+ * compiled into the library. which: 0 kn_config, 1 kn_problem, 2 kn_stats. */
+size_t kn_struct_size(int which);
 
 #ifdef __cplusplus
 }

@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void bbox_partials_kernel(const float* __restr
         const float4* p4 = reinterpret_cast<const float4*>(pts);
         const int ng = n >> 2;
         for (int g = tid; g < ng; g += nth) {
-            const float4 a = p4[3 * g], b = p4[3 * g + 1], c = p4[3 * g + 2];
+            const size_t g3 = 3 * (size_t)g;
+            const float4 a = p4[g3], b = p4[g3 + 1], c = p4[g3 + 2];
             acc(0, a.x); acc(1, a.y); acc(2, a.z);
             acc(0, a.w); acc(1, b.x); acc(2, b.y);
             acc(0, b.z); acc(1, b.w); acc(2, c.x);
@@ -140,7 +141,8 @@ __global__ __launch_bounds__(256) void count_kernel(const float* __restrict__ pt
                                                     int2* __restrict__ cell_rank) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float p[3] = {pts[3 * i + 0], pts[3 * i + 1], pts[3 * i + 2]};
+    const size_t i3 = 3 * (size_t)i;  // 64-bit: 3*i overflows int above 715M points
+    const float p[3] = {pts[i3 + 0], pts[i3 + 1], pts[i3 + 2]};
     const int c = cell_of(*g, p);
     const int r = atomicAdd(cell_count + c, 1);
     cell_rank[i] = make_int2(c, r);
@@ -222,7 +224,8 @@ __global__ __launch_bounds__(256) void scatter_kernel(
     if (i < n) {
         const int2 cr = cell_rank[i];
         const int pos = KN_IDX(cell_scan[KN_IDX(cr.x, num_cells, 103)] + block_sums[cr.x / kScanItems] + cr.y, n, 102);
-        sorted[pos] = make_float4(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], __uint_as_float((unsigned)i));
+        const size_t i3 = 3 * (size_t)i;
+        sorted[pos] = make_float4(pts[i3], pts[i3 + 1], pts[i3 + 2], __uint_as_float((unsigned)i));
         perm[pos] = (unsigned)i;
     }
     // finalise cell_start (grid-stride; the scatter grid has >= num_cells+1 threads only if

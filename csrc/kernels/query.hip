@@ -1475,6 +1475,16 @@ __global__ void invert_perm_kernel(const unsigned* __restrict__ perm, int n, uns
     if (i < n) inv[perm[i]] = (unsigned)i;
 }
 
+__global__ void sorted_xyz_kernel(const float4* __restrict__ sorted, int n, float* __restrict__ xyz) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 v = sorted[i];
+    const size_t o = 3 * (size_t)i;
+    xyz[o] = v.x;
+    xyz[o + 1] = v.y;
+    xyz[o + 2] = v.z;
+}
+
 __global__ void to_stored_kernel(const unsigned* __restrict__ out_orig, const unsigned* __restrict__ perm,
                                  const unsigned* __restrict__ inv, int n, int k,
                                  unsigned* __restrict__ out_sorted, const float* __restrict__ dist_orig,
@@ -1617,6 +1627,11 @@ hipError_t launch_query(const QueryBuffers& q, hipStream_t s) {
 
 hipError_t launch_invert_perm(const unsigned* perm, int n, unsigned* inv, hipStream_t s) {
     if (n > 0) invert_perm_kernel<<<cdiv(n, 256), 256, 0, s>>>(perm, n, inv);
+    return hipGetLastError();
+}
+
+hipError_t launch_sorted_xyz(const float4* sorted, int n, float* xyz, hipStream_t s) {
+    if (n > 0) sorted_xyz_kernel<<<cdiv(n, 256), 256, 0, s>>>(sorted, n, xyz);
     return hipGetLastError();
 }
 

@@ -71,7 +71,8 @@ __global__ __launch_bounds__(kRT) void route_count_kernel(const float* __restric
     for (int r = 0; r < kRounds; ++r) {
         const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
         if (i < n) {
-            const float x = pts[3 * i], y = pts[3 * i + 1], z = pts[3 * i + 2];
+            const size_t i3 = 3 * (size_t)i;  // 64-bit: 3*i overflows int above 715M points
+            const float x = pts[i3], y = pts[i3 + 1], z = pts[i3 + 2];
             const int o = route_owner(p, x, y, z);
             atomicAdd(&cnt[2 * o], 1);
             unsigned long long m = route_halo(p, x, y, z, o);
@@ -147,7 +148,8 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
         int o = -1;
         unsigned long long m = 0;
         if (valid) {
-            x = pts[3 * i]; y = pts[3 * i + 1]; z = pts[3 * i + 2];
+            const size_t i3 = 3 * (size_t)i;
+            x = pts[i3]; y = pts[i3 + 1]; z = pts[i3 + 2];
             o = route_owner(p, x, y, z);
             m = route_halo(p, x, y, z, o);
         }
@@ -212,9 +214,10 @@ __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restr
     }
     const int out = (o < t.own[lo]) ? t.own_pref[lo] + o : t.n_own + t.halo_pref[lo] + (o - t.own[lo]);
     const int oo = KN_IDX(out, rows, 402);
-    pts[3 * oo] = v.x;
-    pts[3 * oo + 1] = v.y;
-    pts[3 * oo + 2] = v.z;
+    const size_t o3 = 3 * (size_t)oo;
+    pts[o3] = v.x;
+    pts[o3 + 1] = v.y;
+    pts[o3 + 2] = v.z;
     gids[oo] = __float_as_int(v.w);
 }
 

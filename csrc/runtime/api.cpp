@@ -22,11 +22,17 @@ void sync_fields(kn_problem* kn) {
     kn->dimy = e->dims()[1];
     kn->dimz = e->dims()[2];
     kn->num_cell_offsets = 0;
+    kn->d_cell_offsets = nullptr;
+    kn->d_cell_offset_dists = nullptr;
+    kn->d_cell_max = nullptr;
+    kn->d_counters = nullptr;
+    kn->d_globcounter = nullptr;
     kn->k = e->k();
     kn->d_permutation = e->d_perm();
-    kn->d_cell_start = e->d_cell_start();
-    kn->d_stored_points = reinterpret_cast<float*>(e->d_sorted());
-    kn->d_knearests = nullptr;
+    kn->d_ptrs = e->d_cell_start();
+    kn->d_stored_points4 = reinterpret_cast<float*>(e->d_sorted());
+    kn->d_stored_points = reinterpret_cast<kn_float3*>(e->d_points3());
+    kn->d_knearests = e->d_knn_stored_if_valid();
 }
 
 kn::EngineConfig to_engine(const kn_config* c) {
@@ -83,7 +89,11 @@ kn_status kn_solve_ex(kn_problem* kn) {
     kn::Engine* e = eng(kn);
     if (!e) { g_err = "null problem"; return KN_ERR_INVALID_ARGUMENT; }
     kn_status s = e->solve();
+    // reference semantics: d_knearests holds the stored-space result after kn_solve
+    // (knearests.cu:329-364); the engine solves in original space, one remap kernel converts
+    if (s == KN_OK && !e->d_knn_stored()) s = KN_ERR_DEVICE;
     if (s != KN_OK) g_err = e->error();
+    sync_fields(kn);
     return s;
 }
 
@@ -94,7 +104,7 @@ kn_status kn_set_k(kn_problem* kn, int k) {
     if (!e) { g_err = "null problem"; return KN_ERR_INVALID_ARGUMENT; }
     kn_status s = e->set_k(k);
     if (s != KN_OK) g_err = e->error();
-    kn->k = e->k();
+    sync_fields(kn);  // d_knearests is stale until the next kn_solve
     return s;
 }
 
@@ -126,7 +136,7 @@ unsigned int* kn_get_knearests(kn_problem* kn) {
     if (!e) return nullptr;
     unsigned* p = e->get_knearests_stored();
     if (!p) g_err = e->error();
-    kn->d_knearests = e->d_knn_stored();
+    kn->d_knearests = e->d_knn_stored_if_valid();
     return p;
 }
 
@@ -189,6 +199,15 @@ kn_problem* kn_load(const char* path, const kn_config* cfg) {
     kn->impl = e;
     sync_fields(kn);
     return kn;
+}
+
+size_t kn_struct_size(int which) {
+    switch (which) {
+        case 0: return sizeof(kn_config);
+        case 1: return sizeof(kn_problem);
+        case 2: return sizeof(kn_stats);
+        default: return 0;
+    }
 }
 
 kn_float3* kn_read_xyz(const char* path, int* n, int normalize) {

@@ -38,6 +38,7 @@ void Engine::release() {
     if (inv_perm_) { (void)hipFree(inv_perm_); inv_perm_ = nullptr; }
     if (knn_stored_) { (void)hipFree(knn_stored_); knn_stored_ = nullptr; }
     if (dist_stored_) { (void)hipFree(dist_stored_); dist_stored_ = nullptr; }
+    if (points3_) { (void)hipFree(points3_); points3_ = nullptr; }
     for (auto& e : ev_) if (e) { (void)hipEventDestroy(e); e = nullptr; }  // reference leaks these (D6)
     if (stream_) { (void)hipStreamDestroy(stream_); stream_ = nullptr; }
 }
@@ -114,7 +115,7 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
     occ_ = carve<unsigned long long>(p, 1);
     // outputs
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
-                     (void**)&dist_stored_})
+                     (void**)&dist_stored_, (void**)&points3_})
         if (*q) { (void)hipFree(*q); *q = nullptr; }
     const size_t nk = std::max<size_t>(1, (size_t)n * cfg_.k);
     if ((st = check(hipMalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
@@ -123,7 +124,7 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
         return st;
     n_ = n;
     C_ = C;
-    built_ = solved_ = stored_valid_ = false;
+    built_ = solved_ = stored_valid_ = points3_valid_ = false;
     if (cfg_.verbose)
         fprintf(stderr, "[knearests] N=%d K=%d grid %dx%dx%d tile %dx%dx%d halo %d lds %zu B, GPU memory %.1f MB\n",
                 n, cfg_.k, ap_.dims[0], ap_.dims[1], ap_.dims[2], ap_.tile[0], ap_.tile[1],
@@ -199,6 +200,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
         if (n > 0 && (st = check(hipMemcpyAsync(points_, src, (size_t)n * 12, kind, stream_), "copy points")) != KN_OK)
             return st;
         (void)hipEventRecord(ev_[0], stream_);
+        points3_valid_ = false;
         if ((st = build_async()) != KN_OK) return st;
         (void)hipEventRecord(ev_[1], stream_);
         if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
@@ -230,6 +232,7 @@ kn_status Engine::upload_device(const float* d_pts, int n) {
                              "D2D points")) != KN_OK)
         return st;
     built_ = true;  // the next launch_graph() (or solve after a build) owns the grid
+    points3_valid_ = stored_valid_ = false;
     return KN_OK;
 }
 
@@ -309,7 +312,7 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     (void)hipEventElapsedTime(&ms, ev_[0], ev_[1]);
     if (ms_per_iter) *ms_per_iter = iters > 0 ? ms / iters : 0.f;
     solved_ = true;
-    stored_valid_ = false;
+    stored_valid_ = points3_valid_ = false;  // the graph rebuilt the grid
     return KN_OK;
 }
 
@@ -332,7 +335,7 @@ kn_status Engine::launch_graph(int iters) {
     for (int i = 0; i < iters; ++i)
         if ((st = check(hipGraphLaunch(graph_, stream_), "graph launch")) != KN_OK) return st;
     solved_ = true;
-    stored_valid_ = false;
+    stored_valid_ = points3_valid_ = false;  // the graph rebuilds the grid
     return KN_OK;
 }
 
@@ -376,6 +379,18 @@ unsigned* Engine::d_knn_stored() {
     return knn_stored_;
 }
 
+float* Engine::d_points3() {
+    if (!built_) return nullptr;
+    if (points3_valid_) return points3_;
+    if (!points3_ && check(hipMalloc(&points3_, std::max<size_t>(1, (size_t)n_ * 3) * sizeof(float)),
+                           "hipMalloc(points3)") != KN_OK)
+        return nullptr;
+    if (check(launch_sorted_xyz(sorted_, n_, points3_, stream_), "sorted xyz") != KN_OK) return nullptr;
+    if (check(hipStreamSynchronize(stream_), "sync") != KN_OK) return nullptr;
+    points3_valid_ = true;
+    return points3_;
+}
+
 template <class T>
 static T* d2h(const T* d, size_t count, hipStream_t s) {
     T* h = (T*)malloc(std::max<size_t>(1, count) * sizeof(T));
@@ -393,7 +408,7 @@ float* Engine::get_points_sorted() {
     float4* tmp = d2h(sorted_, (size_t)n_, stream_);
     if (!tmp) return nullptr;
     float* out = (float*)malloc(std::max<size_t>(1, (size_t)n_ * 3) * sizeof(float));
-    for (int i = 0; i < n_; ++i) { out[3 * i] = tmp[i].x; out[3 * i + 1] = tmp[i].y; out[3 * i + 2] = tmp[i].z; }
+    for (size_t i = 0; i < (size_t)n_; ++i) { out[3 * i] = tmp[i].x; out[3 * i + 1] = tmp[i].y; out[3 * i + 2] = tmp[i].z; }
     free(tmp);
     return out;
 }
@@ -449,8 +464,9 @@ kn_status Engine::stats(kn_stats* out, std::vector<int>* hist) {
 }
 
 namespace {
-constexpr unsigned kMagic = 0x4b4e4731;  // "KNG1"
-}
+constexpr unsigned kMagicV1 = 0x4b4e4731;  // "KNG1": {magic, n, dims[3], k}
+constexpr unsigned kMagic = 0x4b4e4732;    // "KNG2": + {tile[3], halo, lds_capacity, refined}
+}  // namespace
 
 kn_status Engine::save(const char* path) {
     if (!built_) return fail(KN_ERR_STATE, "not prepared");
@@ -461,9 +477,12 @@ kn_status Engine::save(const char* path) {
     if ((st = check(hipMemcpy(&g, geom_, sizeof(g), hipMemcpyDeviceToHost), "D2H geom")) != KN_OK) return st;
     std::vector<float4> s(n_);
     std::vector<int> cs(C_ + 1);
-    if (n_ && (st = check(hipMemcpy(s.data(), sorted_, n_ * sizeof(float4), hipMemcpyDeviceToHost), "D2H")) != KN_OK) return st;
-    if ((st = check(hipMemcpy(cs.data(), cell_start_, (C_ + 1) * sizeof(int), hipMemcpyDeviceToHost), "D2H")) != KN_OK) return st;
-    const int hdr[6] = {(int)kMagic, n_, ap_.dims[0], ap_.dims[1], ap_.dims[2], cfg_.k};
+    if (n_ && (st = check(hipMemcpy(s.data(), sorted_, (size_t)n_ * sizeof(float4), hipMemcpyDeviceToHost), "D2H")) != KN_OK) return st;
+    if ((st = check(hipMemcpy(cs.data(), cell_start_, ((size_t)C_ + 1) * sizeof(int), hipMemcpyDeviceToHost), "D2H")) != KN_OK) return st;
+    // the tile / halo / LDS plan travels with the grid: a refined (occupancy-adaptive) grid keeps
+    // the plan of the target density, which allocate() cannot re-derive from n / C
+    const int hdr[12] = {(int)kMagic, n_, ap_.dims[0], ap_.dims[1], ap_.dims[2], cfg_.k,
+                         ap_.tile[0], ap_.tile[1], ap_.tile[2], ap_.halo, ap_.lds_capacity, 1};
     f.write((const char*)hdr, sizeof(hdr));
     f.write((const char*)&g, sizeof(g));
     f.write((const char*)s.data(), s.size() * sizeof(float4));
@@ -474,33 +493,51 @@ kn_status Engine::save(const char* path) {
 Engine* Engine::load(const char* path, const EngineConfig& cfg, std::string* err) {
     std::ifstream f(path, std::ios::binary);
     if (!f) { if (err) *err = std::string("cannot open ") + path; return nullptr; }
-    int hdr[6];
-    f.read((char*)hdr, sizeof(hdr));
-    if (!f || hdr[0] != (int)kMagic || hdr[1] < 0) { if (err) *err = "bad file header"; return nullptr; }
+    int hdr[12] = {0};
+    f.read((char*)hdr, 6 * sizeof(int));
+    const bool v2 = f && hdr[0] == (int)kMagic;
+    if (!f || (!v2 && hdr[0] != (int)kMagicV1) || hdr[1] < 0) { if (err) *err = "bad file header"; return nullptr; }
+    if (v2) f.read((char*)(hdr + 6), 6 * sizeof(int));
     GridGeom g;
     f.read((char*)&g, sizeof(g));
     const int n = hdr[1];
-    std::vector<float4> s(n);
     const long C = (long)hdr[2] * hdr[3] * hdr[4];
-    if (C <= 0 || C > 400000000L) { if (err) *err = "bad grid"; return nullptr; }
+    if (hdr[2] <= 0 || hdr[3] <= 0 || hdr[4] <= 0 || C > 400000000L) { if (err) *err = "bad grid"; return nullptr; }
+    std::vector<float4> s(n);
     std::vector<int> cs(C + 1);
     f.read((char*)s.data(), s.size() * sizeof(float4));
     f.read((char*)cs.data(), cs.size() * sizeof(int));
     if (!f) { if (err) *err = "truncated file"; return nullptr; }
+    // validate before anything reaches the device: the query kernels index with these values
+    if (cs[0] != 0 || cs[C] != n) { if (err) *err = "corrupt file: cell_start bounds"; return nullptr; }
+    for (long c = 0; c < C; ++c)
+        if (cs[c + 1] < cs[c]) { if (err) *err = "corrupt file: cell_start not monotone"; return nullptr; }
+    std::vector<unsigned> perm(n);
+    std::vector<unsigned char> seen(n, 0);
+    for (int i = 0; i < n; ++i) {
+        unsigned u;
+        std::memcpy(&u, &s[i].w, 4);
+        if (u >= (unsigned)n || seen[u]) { if (err) *err = "corrupt file: ids are not a permutation"; return nullptr; }
+        seen[u] = 1;
+        perm[i] = u;
+    }
+    for (int a = 0; a < 3; ++a)
+        if (g.dims[a] != hdr[2 + a]) { if (err) *err = "corrupt file: geometry / dims mismatch"; return nullptr; }
     EngineConfig c = cfg;
     if (c.k <= 0) c.k = hdr[5];
     Engine* e = new Engine(c);
     const int dims[3] = {hdr[2], hdr[3], hdr[4]};
     if (e->allocate(n, dims) != KN_OK) { if (err) *err = e->error(); delete e; return nullptr; }
-    std::vector<unsigned> perm(n);
-    for (int i = 0; i < n; ++i) {
-        unsigned u;
-        std::memcpy(&u, &s[i].w, 4);
-        perm[i] = u;
+    if (v2 && hdr[11] && c.k == hdr[5]) {
+        // same K: restore the saved plan (refined grids keep the target density's LDS plan)
+        for (int a = 0; a < 3; ++a) e->ap_.tile[a] = std::max(1, hdr[6 + a]);
+        e->ap_.halo = std::max(1, hdr[9]);
+        e->ap_.lds_capacity = std::max(128, std::min(hdr[10], 8192));
+        e->ap_.lds_bytes = query_lds_bytes(e->ap_.tile, e->ap_.halo, e->ap_.lds_capacity);
     }
     bool ok = hipMemcpy(e->geom_, &g, sizeof(g), hipMemcpyHostToDevice) == hipSuccess &&
-              (n == 0 || hipMemcpy(e->sorted_, s.data(), n * sizeof(float4), hipMemcpyHostToDevice) == hipSuccess) &&
-              (n == 0 || hipMemcpy(e->perm_, perm.data(), n * sizeof(unsigned), hipMemcpyHostToDevice) == hipSuccess) &&
+              (n == 0 || hipMemcpy(e->sorted_, s.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice) == hipSuccess) &&
+              (n == 0 || hipMemcpy(e->perm_, perm.data(), (size_t)n * sizeof(unsigned), hipMemcpyHostToDevice) == hipSuccess) &&
               hipMemcpy(e->cell_start_, cs.data(), (C + 1) * sizeof(int), hipMemcpyHostToDevice) == hipSuccess;
     if (!ok) { if (err) *err = "upload failed"; delete e; return nullptr; }
     e->built_ = true;

@@ -79,7 +79,9 @@ public:
     float4* d_sorted() const { return sorted_; }
     int* d_cell_start() const { return cell_start_; }
     unsigned* d_perm() const { return perm_; }
-    unsigned* d_knn_stored();
+    unsigned* d_knn_stored();                    // converts on first use after a solve
+    unsigned* d_knn_stored_if_valid() const { return stored_valid_ ? knn_stored_ : nullptr; }
+    float* d_points3();                          // stored-order float3 view (reference field)
 
 private:
     kn_status fail(kn_status s, const std::string& msg);
@@ -122,6 +124,8 @@ private:
     unsigned* inv_perm_ = nullptr;
     unsigned* knn_stored_ = nullptr;
     float* dist_stored_ = nullptr;
+    float* points3_ = nullptr;  // stored-order float3 copy of sorted_ (reference d_stored_points)
+    bool points3_valid_ = false;
     bool built_ = false, solved_ = false, stored_valid_ = false;
     float ms_build_ = 0.f, ms_solve_ = 0.f;
 };

@@ -10,14 +10,25 @@ from cuda_knearests_amd.utils import dataset
 
 class KnConfig(C.Structure):
     _fields_ = [("k", C.c_int), ("points_per_cell", C.c_float), ("tile", C.c_int * 3), ("halo", C.c_int),
-                ("deterministic", C.c_int), ("device", C.c_int), ("verbose", C.c_int), ("exact_only", C.c_int)]
+                ("deterministic", C.c_int), ("device", C.c_int), ("verbose", C.c_int), ("exact_only", C.c_int),
+                ("fixed_grid", C.c_int)]
 
 
 class KnProblem(C.Structure):
+    # reference field names (reference knearests.h:3-16) + k, d_stored_points4, impl
     _fields_ = [("allocated_points", C.c_int), ("dimx", C.c_int), ("dimy", C.c_int), ("dimz", C.c_int),
-                ("num_cell_offsets", C.c_int), ("k", C.c_int), ("d_permutation", C.c_void_p),
-                ("d_cell_start", C.c_void_p), ("d_stored_points", C.c_void_p), ("d_knearests", C.c_void_p),
+                ("num_cell_offsets", C.c_int), ("d_cell_offsets", C.c_void_p), ("d_cell_offset_dists", C.c_void_p),
+                ("d_cell_max", C.c_void_p), ("d_permutation", C.c_void_p), ("d_counters", C.c_void_p),
+                ("d_ptrs", C.c_void_p), ("d_globcounter", C.c_void_p), ("d_stored_points", C.c_void_p),
+                ("d_knearests", C.c_void_p), ("k", C.c_int), ("d_stored_points4", C.c_void_p),
                 ("impl", C.c_void_p)]
+
+
+class KnStats(C.Structure):
+    _fields_ = [("num_points", C.c_int), ("k", C.c_int), ("dims", C.c_int * 3), ("num_cells", C.c_int),
+                ("min_cell", C.c_int), ("max_cell", C.c_int), ("avg_cell", C.c_float), ("empty_cells", C.c_int),
+                ("fallback_queries", C.c_int), ("uncertified_queries", C.c_int), ("ms_build", C.c_float),
+                ("ms_solve", C.c_float)]
 
 
 def _lib():
@@ -36,12 +47,23 @@ def _lib():
     lib.kn_get_distances.argtypes = [C.POINTER(KnProblem)]
     lib.kn_solve.argtypes = [C.POINTER(KnProblem)]
     lib.kn_solve_ex.argtypes = [C.POINTER(KnProblem)]
+    lib.kn_get_stats.argtypes = [C.POINTER(KnProblem), C.POINTER(KnStats)]
     lib.kn_free.argtypes = [C.POINTER(C.POINTER(KnProblem))]
     lib.kn_read_xyz.restype = C.POINTER(C.c_float)
     lib.kn_read_xyz.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.c_int]
     lib.kn_last_error.restype = C.c_char_p
     lib.kn_print_stats.argtypes = [C.POINTER(KnProblem)]
+    lib.kn_struct_size.restype = C.c_size_t
+    lib.kn_struct_size.argtypes = [C.c_int]
     return lib
+
+
+def test_struct_layout_matches_library():
+    """ctypes mirrors == the structs compiled into libknearests.so (drift fails loudly: a short
+    KnConfig once let kn_default_config write past the ctypes buffer)."""
+    lib = _lib()
+    for which, cls in enumerate((KnConfig, KnProblem, KnStats)):
+        assert lib.kn_struct_size(which) == C.sizeof(cls), cls.__name__
 
 
 def test_read_xyz_cpu():
@@ -60,6 +82,7 @@ def test_read_xyz_cpu():
 def test_default_config_matches_reference_params():
     c = _lib().kn_default_config()
     assert c.k == 50 and c.deterministic == 1  # reference params.h:4 DEFAULT_NB_PLANES
+    assert c.fixed_grid == 0 and c.exact_only == 0
 
 
 @pytest.mark.gpu
@@ -78,9 +101,27 @@ def test_capi_reference_flow():
     assert prob, lib.kn_last_error()
     assert prob.contents.allocated_points == 30000 and prob.contents.dimx > 0
     lib.kn_solve(prob)
-    knn = np.ctypeslib.as_array(lib.kn_get_knearests(prob), shape=(30000 * 16,)).reshape(30000, 16).copy()
-    perm = np.ctypeslib.as_array(lib.kn_get_permutation(prob), shape=(30000,)).copy()
-    stored = np.ctypeslib.as_array(lib.kn_get_points(prob), shape=(30000 * 3,)).reshape(30000, 3).copy()
+    pr = prob.contents
+    # reference field semantics: after kn_solve the device fields hold the stored-space result
+    # and the float3 stored points (reference knearests.cu:329-364, knearests.h:14-15)
+    assert pr.d_knearests and pr.d_stored_points and pr.d_ptrs and pr.d_permutation
+    assert not pr.d_cell_offsets and not pr.d_counters and pr.k == 16
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    dev_knn = np.empty((30000, 16), dtype=np.uint32)
+    dev_pts = np.empty((30000, 3), dtype=np.float32)
+    assert hip.hipMemcpy(dev_knn.ctypes.data, pr.d_knearests, dev_knn.nbytes, 2) == 0  # D2H
+    assert hip.hipMemcpy(dev_pts.ctypes.data, pr.d_stored_points, dev_pts.nbytes, 2) == 0
+    gk, gp, gs = lib.kn_get_knearests(prob), lib.kn_get_permutation(prob), lib.kn_get_points(prob)
+    knn = np.ctypeslib.as_array(gk, shape=(30000 * 16,)).reshape(30000, 16).copy()
+    perm = np.ctypeslib.as_array(gp, shape=(30000,)).copy()
+    stored = np.ctypeslib.as_array(gs, shape=(30000 * 3,)).reshape(30000, 3).copy()
+    for ptr in (gk, gp, gs):
+        libc.free(ptr)  # getters return malloc'd buffers (reference knearests.cu:411,421,431)
+    assert np.array_equal(dev_knn, knn)
+    assert np.array_equal(dev_pts, stored)
+    st = KnStats()
+    assert lib.kn_get_stats(prob, C.byref(st)) == 0 and st.num_points == 30000 and st.k == 16
     lib.kn_print_stats(prob)
     pp = C.pointer(prob)
     lib.kn_free(pp)

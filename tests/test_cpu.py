@@ -9,12 +9,14 @@ import torch
 
 import cuda_knearests_amd as kn
 from cuda_knearests_amd.utils import REPO, blue_cloud, clustered_cloud, dataset, uniform_cloud
+from cuda_knearests_amd.utils.check import assert_knn_exact, knn_row_errors
 
 
-def _same_up_to_ties(i1, d1, i2, d2):
+def _same_up_to_ties(p, i1, d1, i2, d2):
+    """(i1, d1) vs the reference (i2, d2): equal distances, valid ids (utils/check.py)."""
     assert torch.equal(d1, d2)
-    same = (i1 == i2) | (d1.unsqueeze(-1) == d2.unsqueeze(-2)).any(-1)
-    assert bool(same.all())
+    assert_knn_exact(p, torch.arange(p.size(0)), i1, d1, d2)
+    assert_knn_exact(p, torch.arange(p.size(0)), i2, d2, d2)
 
 
 @pytest.mark.parametrize("k", [1, 8, 16, 50])
@@ -33,8 +35,8 @@ def test_oracles_agree(k, gen):
     ki, kd = kn.knn_cpu(p, k, "kdtree")
     gi, gd, unc = kn.knn_cpu(p, k, "grid")
     assert unc.numel() == 0
-    _same_up_to_ties(ki, kd, bi, bd)
-    _same_up_to_ties(gi, gd, bi, bd)
+    _same_up_to_ties(p, ki, kd, bi, bd)
+    _same_up_to_ties(p, gi, gd, bi, bd)
     # ascending, no self
     assert bool((bd[:, 1:] >= bd[:, :-1]).all())
     assert not bool((bi == torch.arange(p.size(0)).unsqueeze(1)).any())
@@ -65,7 +67,7 @@ def test_pts20k_reference_dataset_k8():
     assert 0.0 < float(p.min()) and float(p.max()) < 1000.0
     ki, kd = kn.knn_cpu(p, 8, "kdtree")
     gi, gd, unc = kn.knn_cpu(p, 8, "grid")
-    _same_up_to_ties(gi, gd, ki, kd)
+    _same_up_to_ties(p, gi, gd, ki, kd)
     # blue noise: min NN spacing ~25 after x1000
     nn = kd[:, 0].sqrt()
     assert 20.0 < float(nn.min()) < 30.0

@@ -12,6 +12,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
+from cuda_knearests_amd.utils.check import assert_knn_exact
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -83,8 +85,7 @@ def test_distributed_matches_single(world, k, gen, partitioned):
         assert not bool(seen[ids].any()), "a point is owned by two ranks"
         seen[ids] = True
         assert torch.equal(d2, od[ids]), f"rank {rank}: distances differ"
-        same = (nb.long() == oi[ids].long()) | (d2.unsqueeze(-1) == od[ids].unsqueeze(-2)).any(-1)
-        assert bool(same.all())
+        assert_knn_exact(cloud.cpu(), ids, nb.cpu(), d2.cpu(), od[ids])
     assert bool(seen.all()), "some points were lost in redistribution"
 
 
@@ -137,8 +138,7 @@ def _loopback_check(world, k, gen, device, native, n=6000, halo_factor=1.6, scat
         assert not bool(seen[ids_r].any()), "a point is owned by two ranks"
         seen[ids_r] = True
         assert torch.equal(d2, od[ids_r]), "distances differ from the oracle"
-        same = (nb.long() == oi[ids_r].long()) | (d2.unsqueeze(-1) == od[ids_r].unsqueeze(-2)).any(-1)
-        assert bool(same.all())
+        assert_knn_exact(cloud.cpu(), ids_r, nb.cpu(), d2.cpu(), od[ids_r])
     assert bool(seen.all()), "some points were lost in routing"
     return out
 

@@ -1,7 +1,9 @@
 """GPU tests (MI355X): HIP kernels vs the CPU oracles.
 
 Every comparison is distance-aware: squared distances must equal the kd-tree oracle's bit for
-bit (same fp32 fma chain), ids may differ only inside runs of equal distance.
+bit (same fp32 fma chain); every returned id must be distinct, not the query, and reproduce its
+distance from the points (cuda_knearests_amd/utils/check.py), so ids can differ from the
+oracle's only inside runs of equal distance.
 """
 import os
 import subprocess
@@ -12,6 +14,7 @@ import torch
 
 import cuda_knearests_amd as kn
 from cuda_knearests_amd.utils import REPO, blue_cloud, clustered_cloud, dataset, uniform_cloud
+from cuda_knearests_amd.utils.check import assert_knn_exact
 
 pytestmark = pytest.mark.gpu
 
@@ -22,8 +25,8 @@ def _assert_matches_oracle(p, idx, d2, k):
     assert idx.shape == oi.shape
     mism = (d2 != od).any(1)
     assert int(mism.sum()) == 0, f"{int(mism.sum())} rows differ; first {int(mism.nonzero()[0, 0])}"
-    same = (idx == oi) | (d2.unsqueeze(-1) == od.unsqueeze(-2)).any(-1)
-    assert bool(same.all())
+    # ids: distinct, not self, and each reproduces its distance (utils/check.py)
+    assert_knn_exact(p.cpu(), torch.arange(p.size(0)), idx, d2, od)
 
 
 def test_native_extension_loaded(cuda, ext):
@@ -328,3 +331,33 @@ def test_atomic_binning_fallback_matches(cuda):
     p = uniform_cloud(60_000, seed=8, device=cuda)
     i, d = kn.knn(p, 12)
     assert torch.equal(i.cpu(), ref["i"]) and torch.equal(d.cpu(), ref["d"])
+
+
+def test_beyond_int32_point_offsets(cuda):
+    """N > 715,827,882: 3*i and 16*i point offsets exceed 2^31 (round-1 finding: int32 `3*i`
+    in the routing / fallback binning kernels). 725M uniform points, K=1 through the default
+    build (bucketed binning or its global-atomic fallback) and query; the rows of queries whose
+    stored AND original offsets lie beyond 2^31/3 are brute-forced on the GPU."""
+    n = 725_000_000
+    p = uniform_cloud(n, seed=21, device=cuda)
+    g = kn.build_grid(p, 1)
+    idx, d2, info = kn.query(g, 1, return_info=True)
+    assert int(info["counters"][1]) == 0
+    assert bool((idx >= 0).all())
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    hi = torch.randint(716_000_000, n, (24,), generator=gen)
+    lo = torch.randint(0, n, (8,), generator=gen)
+    sel = torch.cat([hi, lo, torch.tensor([n - 1])]).to(cuda)
+    # stored slots past 2^31/3 too: the last stored points of the cell order
+    sel = torch.cat([sel, g.perm[-8:].long()])
+    for q in sel.tolist():
+        dd = p - p[q]
+        dd = (dd * dd).sum(1)
+        dd[q] = float("inf")
+        j = int(torch.argmin(dd))
+        assert float(dd[j]) == pytest.approx(float(d2[q, 0]), rel=1e-6), q
+        # the returned id reproduces the reported distance (ties may pick another point)
+        e = p[int(idx[q, 0])] - p[q]
+        assert float((e * e).sum()) == pytest.approx(float(d2[q, 0]), rel=1e-6), q
+    del p, g, idx, d2
+    torch.cuda.empty_cache()

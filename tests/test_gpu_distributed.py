@@ -12,6 +12,7 @@ import torch
 
 from cuda_knearests_amd.parallel import SpatialDecomposition, halo_send_width, route_rows_torch
 from cuda_knearests_amd.utils import uniform_cloud
+from cuda_knearests_amd.utils.check import assert_knn_exact
 
 from test_distributed import _loopback_check
 
@@ -140,8 +141,7 @@ def test_device_plan_default_ids(cuda):
         ids_r = ids_r.long()
         seen[ids_r] = True
         assert torch.equal(d2, od[ids_r])
-        same = (nb.long() == oi[ids_r].long()) | (d2.unsqueeze(-1) == od[ids_r].unsqueeze(-2)).any(-1)
-        assert bool(same.all())
+        assert_knn_exact(cat, ids_r, nb.cpu(), d2.cpu(), od[ids_r])
     assert bool(seen.all())
 
 
@@ -200,8 +200,7 @@ def test_multiprocess_native_path_host_staged(cuda, world):
         assert not bool(seen[ids].any())
         seen[ids] = True
         assert torch.equal(d2, od[ids])
-        same = (nb.long() == oi[ids].long()) | (d2.unsqueeze(-1) == od[ids].unsqueeze(-2)).any(-1)
-        assert bool(same.all())
+        assert_knn_exact(cloud.cpu(), ids, nb.cpu(), d2.cpu(), od[ids])
     assert bool(seen.all())
 
 
