@@ -47,7 +47,7 @@ hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hip
 
 // Query counters (device, zeroed by every launch_query):
 //  [0] queries sent to the exact kernel   [1] uncertified (multi-GPU: K-th leaves complete box)
-//  [2] LDS-overflow (dense) tiles         [3] in-wave exact re-scans (truncation near-ties)
+//  [2] LDS-overflow (dense) tiles         [3] in-wave cooperative re-ranks / exact re-scans
 //  [4] rows streamed (per wave)           [5] candidates streamed (per wave)
 //  [6] insertion networks executed        [7] query chunks (waves x chunk iterations)
 constexpr int kNumCounters = 8;

@@ -36,6 +36,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "kn/kernels.h"
 #include "kn/wave.h"
@@ -92,6 +93,14 @@ struct TileArgs {
 #ifndef KN_LANE_FULL
 #define KN_LANE_FULL 1
 #endif
+// Re-rank of the kept keys: 1 = streaming window (O(kWin) live registers), 0 = odd-even
+// transposition over (d2, id) arrays of KM entries each plus the in-wave exact re-scan of
+// truncation near-ties (round 1).
+#ifndef KN_WINDOW_RERANK
+#define KN_WINDOW_RERANK 1
+#endif
+constexpr int kWin = 3;
+constexpr int kCoopCap = 128;  // per-wave LDS buffer of the cooperative re-scan (u64 keys)
 constexpr int kQueryForceRescan = 1;
 constexpr int kQueryAlgoStream = 2;
 constexpr int kQueryAlgoTile = 4;
@@ -137,6 +146,47 @@ __device__ __forceinline__ int xcd_remap(int b, int nblocks) {
     const int xcd = b & 7, idx = b >> 3;
     const int q = nblocks >> 3, r = nblocks & 7;
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ unsigned long long pack_key64(float d, unsigned id) {
+    return ((unsigned long long)__float_as_uint(d) << 32) | id;
+}
+
+// Ascending bitonic sort of E*64 64-bit keys held E per lane (element index e*64 + lane):
+// cross-lane stages exchange through ds_bpermute (__shfl_xor), the stride-64 stage of E = 2
+// compares a lane's two elements.
+template <int E>
+__device__ __forceinline__ void wave_bitonic_sort_u64(unsigned long long (&v)[E], int lane) {
+    constexpr int N = 64 * E;
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int f = e ^ (stride >> 6);
+                    if (e < f) {
+                        const bool up = (((e << 6) | lane) & size) == 0;
+                        const unsigned long long mn = v[e] < v[f] ? v[e] : v[f], mx = v[e] < v[f] ? v[f] : v[e];
+                        v[e] = up ? mn : mx;
+                        v[f] = up ? mx : mn;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v[e], stride, 64);
+                    const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(v[e] >> 32), stride, 64);
+                    const unsigned long long o = ((unsigned long long)hi << 32) | lo;
+                    const bool up = (((e << 6) | lane) & size) == 0;
+                    const bool lower = (lane & stride) == 0;
+                    const unsigned long long mn = v[e] < o ? v[e] : o, mx = v[e] < o ? o : v[e];
+                    v[e] = (up == lower) ? mn : mx;
+                }
+            }
+        }
+    }
 }
 
 // Packed 32-bit key of one candidate: squared-distance float bits with the low SB mantissa
@@ -195,6 +245,9 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     int* rowbase = cb + a.max_rows * a.cb_stride;
     int* qpref = rowbase + a.max_rows + 1;  // TY*TZ + 1 entries
     int* misc = qpref + a.TY * a.TZ + 1;
+    // per-wave buffers of the cooperative re-scan, 16-B aligned after misc (query_lds_bytes)
+    unsigned long long* cbuf = reinterpret_cast<unsigned long long*>(
+        (reinterpret_cast<uintptr_t>(misc + 4) + 15) & ~(uintptr_t)15);
 
     const GridGeom g = *a.geom;
     const int ntiles = a.ntx * a.nty * a.ntz;
@@ -636,6 +689,200 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             atomicAdd(a.counters + 7, 1u);
         }
 
+        const int k = a.k;
+        const bool act = in_range && live;
+#if KN_WINDOW_RERANK
+        // ---- exact re-rank: streaming window ---------------------------------------------
+        // keys are sorted by (truncated d2, slot); the exact (d2, id) order can differ only
+        // inside a run of equal truncation buckets. A kept candidate's output position is its
+        // number of valid predecessors in key order plus the signed count of same-bucket
+        // neighbours within +-kWin that cross it in exact order. Computed on the fly, so only a
+        // window of 2*kWin+1 exact (d2, id) pairs is live instead of two KM-arrays (the odd-even
+        // transposition re-rank held both: K=50 176 VGPRs = 2 waves/SIMD). Rows are written
+        // before certification; a row that fails it is rewritten by the exact kernel, which
+        // runs later on the same stream. Runs longer than kWin + 1 (lattices, heavy
+        // duplication) take the wave-cooperative sort below.
+        const unsigned qs = (unsigned)qslot;
+        auto kvalid = [&](unsigned key) { return key != SENT && (key & MASK) != qs; };
+        bool ovf = (a.flags & kQueryForceRescan) != 0;
+        int nfound = 0;
+#pragma unroll
+        for (int j = 0; j + kWin + 1 < KM; ++j)
+            ovf |= keys[j + kWin + 1] != SENT && ((keys[j] ^ keys[j + kWin + 1]) & HIMASK) == 0u;
+        const unsigned orow = act ? w_row(a, qorig, qsidx) : 0u;
+        const size_t row = (size_t)orow * (size_t)k;
+        float dK2 = INFINITY;
+        // precision reference taken before the window pass consumes the keys
+        const unsigned last = keys[KM - 1];
+        if (!ovf) {
+            // Rolled loop over the kept keys with constant register indices only: the key array
+            // shifts down one slot per step (KM moves) and the window rotates, so no unrolled
+            // straight-line code gives the scheduler room to pull every entry's LDS read and
+            // compare forward (fully unrolled, K=50 needed 214 VGPRs; rolled it stays near the
+            // scan loop's own pressure).
+            constexpr int NW = 2 * kWin + 1;
+            float wd[NW];
+            unsigned wi[NW], wk[NW];
+            auto ld = [&](unsigned key, int t) {
+                const bool v = kvalid(key);
+                const float4 p = pts[KN_IDX(v ? (key & MASK) : 0u, (unsigned)S, 208)];
+                const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
+                wk[t] = v ? key : SENT;
+                wd[t] = v ? fmaf(dz, dz, fmaf(dy, dy, dx * dx)) : INFINITY;
+                wi[t] = v ? w_id(a, __float_as_uint(p.w)) : SENT;
+            };
+#pragma unroll
+            for (int t = 0; t < NW; ++t) ld((t >= kWin && t - kWin < KM) ? keys[t - kWin] : SENT, t);
+            int base = 0;
+#pragma unroll 1
+            for (int j = 0; j < KM; ++j) {
+                const bool vj = wk[kWin] != SENT;
+                int pos = base;
+#pragma unroll
+                for (int t = 0; t < NW; ++t) {
+                    if (t == kWin) continue;
+                    // branch-free: bitwise &/| (short-circuit forms compile to exec-mask branches)
+                    const int same = (int)(wk[t] != SENT) & (int)(((wk[t] ^ wk[kWin]) & HIMASK) == 0u);
+                    const float da = t > kWin ? wd[t] : wd[kWin], db = t > kWin ? wd[kWin] : wd[t];
+                    const unsigned ia = t > kWin ? wi[t] : wi[kWin], ib = t > kWin ? wi[kWin] : wi[t];
+                    const int lt = (int)(da < db) | ((int)(da == db) & (int)(ia < ib));
+                    pos += (t > kWin ? 1 : -1) * (same & lt);
+                }
+                if (vj && act && pos < k) {
+                    const size_t o = KN_IDX(row + pos, (size_t)a.n_queries * k, 209);
+                    a.out_idx[o] = out_id(a, wi[kWin]);
+                    if (a.out_dist) a.out_dist[o] = wd[kWin];
+                }
+                dK2 = (vj && pos == k - 1) ? wd[kWin] : dK2;
+                base += vj ? 1 : 0;
+#pragma unroll
+                for (int t = 0; t + 1 < NW; ++t) { wk[t] = wk[t + 1]; wd[t] = wd[t + 1]; wi[t] = wi[t + 1]; }
+                // entry j + kWin + 1 sits at keys[kWin + 1] after j + 1 shifts
+                ld(KM > kWin + 1 ? keys[kWin + 1 < KM ? kWin + 1 : KM - 1] : SENT, NW - 1);
+#pragma unroll
+                for (int t = 0; t + 1 < KM; ++t) keys[t] = keys[t + 1];
+                keys[KM - 1] = SENT;
+            }
+            nfound = base;
+        }
+        // Wave-cooperative finish of ONE lane's query at a time (rare paths): the wave holds
+        // 64-bit (d2 bits, id) keys, E per lane, bitonic-sorts them across lanes and writes the
+        // lane's row; the lane gets its exact K-th distance and found count back.
+        const size_t rowq = row;
+        auto coop_finish = [&](int L, auto& v) {
+            constexpr int E = (int)std::extent<std::remove_reference_t<decltype(v)>>::value;
+            wave_bitonic_sort_u64<E>(v, lane);
+            const size_t rowL = (size_t)__builtin_amdgcn_readlane((int)(rowq / (size_t)k), L) * (size_t)k;
+            int nf = 0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) nf += __builtin_popcountll(__builtin_amdgcn_ballot_w64(v[e] != ~0ull));
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int r = 64 * e + lane;
+                if (r < k && v[e] != ~0ull) {
+                    const size_t o = KN_IDX(rowL + r, (size_t)a.n_queries * k, 214);
+                    a.out_idx[o] = out_id(a, (unsigned)v[e]);
+                    if (a.out_dist) a.out_dist[o] = __uint_as_float((unsigned)(v[e] >> 32));
+                }
+            }
+            float dk = INFINITY;
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+                if ((k - 1) / 64 == e)
+                    dk = __uint_as_float((unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v[e] >> 32), (k - 1) & 63));
+            if (nf < k) dk = INFINITY;
+            if (lane == L) { dK2 = dk; nfound = nf; }
+        };
+        // (1) window overflow (or every lane under kQueryForceRescan): sort the lane's KM kept keys
+        for (unsigned long long om = __builtin_amdgcn_ballot_w64(ovf && act); om; om &= om - 1) {
+            const int L = __builtin_ctzll(om);
+            constexpr int E = (KM + 63) / 64;
+            const unsigned qsL = (unsigned)__builtin_amdgcn_readlane((int)qs, L);
+            const float qxL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qx), L));
+            const float qyL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qy), L));
+            const float qzL = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qz), L));
+            unsigned long long v[E];
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                unsigned key = SENT;
+#pragma unroll
+                for (int j = 64 * e; j < KM && j < 64 * (e + 1); ++j) {
+                    const unsigned kj = (unsigned)__builtin_amdgcn_readlane((int)keys[j], L);
+                    key = (lane == j - 64 * e) ? kj : key;
+                }
+                const bool valid = key != SENT && (key & MASK) != qsL;
+                const float4 p = pts[KN_IDX(valid ? (key & MASK) : 0u, (unsigned)S, 213)];
+                const float dx = p.x - qxL, dy = p.y - qyL, dz = p.z - qzL;
+                const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                v[e] = valid ? pack_key64(d, w_id(a, __float_as_uint(p.w))) : ~0ull;
+            }
+            coop_finish(L, v);
+            if (lane == 0) atomicAdd(a.counters + 3, 1u);  // cooperative re-ranks (diagnostic)
+        }
+        // (2) precision: everything truncated away has exact d2 >= the floor of the last key's
+        // bucket. If the exact K-th distance reaches into it (K-th and last kept candidates
+        // within one truncation ulp), the wave re-scans the lane's region exactly: every point
+        // with d2 <= that K-th distance (an upper bound of the true one) is compacted into a
+        // per-wave LDS buffer, then sorted and written as above. More than kCoopCap such
+        // points (heavy duplication) leave the query to the exact kernel.
+        bool prec_fail = last != SENT && !(dK2 <= __uint_as_float(last & HIMASK));
+        for (unsigned long long om = __builtin_amdgcn_ballot_w64(prec_fail && act); om; om &= om - 1) {
+            const int L = __builtin_ctzll(om);
+            auto rl = [&](int v) { return __builtin_amdgcn_readlane(v, L); };
+            auto rlf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L)); };
+            const int qsL = rl(qslot);
+            const float qxL = rlf(qx), qyL = rlf(qy), qzL = rlf(qz), thr = rlf(dK2);
+            const int x0 = rl(rx0), x1 = rl(rx1), y0 = rl(ry0), y1 = rl(ry1), z0 = rl(rz0), z1 = rl(rz1);
+            unsigned long long* buf = cbuf + wid * kCoopCap;
+            const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+            int cnt = 0;
+            for (int z = z0; z <= z1; ++z) {
+                const float dzb = slab_dist(g, 2, qzL, sz0 + z, sz0 + z);
+                const float dz2 = dzb * dzb;
+                if (!(dz2 <= thr)) continue;
+                for (int y = y0; y <= y1; ++y) {
+                    const float dyb = slab_dist(g, 1, qyL, sy0 + y, sy0 + y);
+                    const float dyz2 = fmaf(dyb, dyb, dz2);
+                    if (!(dyz2 <= thr)) continue;
+                    const float rr = sqrtf(thr - dyz2) * 1.000001f + g.eps;
+                    const int lx0 = max(x0, cell_coord(g, 0, qxL - rr) - sx0);
+                    const int lx1 = min(x1, cell_coord(g, 0, qxL + rr) - sx0);
+                    if (lx0 > lx1) continue;
+                    const int r = y + nys * z;
+                    const int rb = rowbase[r] - cb[r * cbs];
+                    const int s0 = __builtin_amdgcn_readfirstlane(rb + cb[r * cbs + lx0]);
+                    const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + cb[r * cbs + lx1 + 1], S + 1, 215));
+                    for (int sb = s0; sb < s1; sb += 64) {
+                        const int sl = sb + lane;
+                        bool pass = false;
+                        unsigned long long key = 0;
+                        if (sl < s1 && sl != qsL) {
+                            const float4 p = pts[sl];
+                            const float dx = p.x - qxL, dy = p.y - qyL, dz = p.z - qzL;
+                            const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                            pass = d <= thr;
+                            key = pack_key64(d, w_id(a, __float_as_uint(p.w)));
+                        }
+                        const unsigned long long bal = __builtin_amdgcn_ballot_w64(pass);
+                        const int at = cnt + __builtin_popcountll(bal & lt);
+                        if (pass && at < kCoopCap) buf[at] = key;
+                        cnt += __builtin_popcountll(bal);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (cnt <= kCoopCap) {
+                unsigned long long v[kCoopCap / 64];
+#pragma unroll
+                for (int e = 0; e < kCoopCap / 64; ++e) v[e] = (64 * e + lane < cnt) ? buf[64 * e + lane] : ~0ull;
+                __builtin_amdgcn_wave_barrier();
+                coop_finish(L, v);
+                if (lane == L) prec_fail = false;
+            }
+            if (lane == 0) atomicAdd(a.counters + 3, 1u);  // cooperative re-ranks (diagnostic)
+        }
+        if (!act) continue;
+#else
         // ---- exact re-rank of the K+M kept candidates (branch-free) ----------------------
         float dd[KM];
         unsigned ii[KM];
@@ -668,7 +915,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             if (!__builtin_amdgcn_ballot_w64(swapped)) break;
         }
 
-        const int k = a.k;
         auto kth = [&]() {
             float v = INFINITY;
 #pragma unroll
@@ -722,7 +968,9 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         int nfound = 0;
 #pragma unroll
         for (int j = 0; j < KM; ++j) nfound += (ii[j] != SENT) ? 1 : 0;
-        if (!(in_range && live)) continue;
+        if (!act) continue;
+        const bool prec_fail = false;  // the in-wave re-scan resolved it
+#endif
 
         // distance to the boundary of the scanned region (grid faces do not count: no points
         // exist beyond the grid) and to the complete box (multi-GPU halo limit)
@@ -741,7 +989,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             m = fminf(m, complete_margin(a.complete, qz, 2));
             m -= g.eps;
         }
-        const bool geo_ok = (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
+        const bool geo_ok = !prec_fail && (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
+#if !KN_WINDOW_RERANK
         if (geo_ok) {
             const size_t row = (size_t)w_row(a, qorig, qsidx) * (size_t)k;
 #pragma unroll
@@ -752,7 +1001,9 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     if (a.out_dist) a.out_dist[o] = dd[j];
                 }
             }
-        } else {
+        }
+#endif
+        if (!geo_ok) {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
             a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx;
         }
@@ -1313,9 +1564,6 @@ __device__ __forceinline__ unsigned wave_sum_u32(unsigned x) {
            (unsigned)__builtin_amdgcn_readlane((int)x, 32) + (unsigned)__builtin_amdgcn_readlane((int)x, 48);
 }
 
-__device__ __forceinline__ unsigned long long pack_key64(float d, unsigned id) {
-    return ((unsigned long long)__float_as_uint(d) << 32) | id;
-}
 
 template <int KT>
 __global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
@@ -1604,7 +1852,9 @@ size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity) {
     b += (size_t)(rows + 1) * 4;
     b += (size_t)(tile[1] * tile[2] + 1) * 4;
     b += 16;
-    return (b + 15) & ~(size_t)15;
+    b = (b + 15) & ~(size_t)15;
+    b += (size_t)kWaves * kCoopCap * 8;  // cooperative re-scan buffers
+    return b;
 }
 
 KN_DEFINE_DEBUG_READER(debug_words_query)

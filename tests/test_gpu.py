@@ -44,12 +44,14 @@ def test_uniform_tile_vs_oracle(cuda, k):
 
 @pytest.mark.parametrize("k", [1, 16, 50])
 def test_forced_exact_rescan(cuda, k):
-    # the in-wave exact re-scan normally runs only for truncation near-ties; force it for every
-    # query so the branch is covered (rare data-dependent branches need their test)
+    # the wave-cooperative exact re-rank normally runs only for window overflows (long runs of
+    # equal truncated distances) and truncation near-ties; force it for every query so the
+    # branch is covered (rare data-dependent branches need their test). counters[3]
+    # counts cooperative finishes: >= 1 per query (a near-tie adds its re-scan)
     p = uniform_cloud(20000, seed=200 + k, device=cuda)
     g = kn.build_grid(p, k)
     idx, d2, info = kn.query(g, k, return_info=True, flags=1)
-    assert int(info["counters"][3]) == p.size(0)
+    assert int(info["counters"][3]) >= p.size(0)
     _assert_matches_oracle(p, idx, d2, k)
 
 
@@ -89,7 +91,7 @@ def test_tile_variants_forced_rescan(cuda, algo, k):
     p = uniform_cloud(20000, seed=402, device=cuda)
     g = kn.build_grid(p, k)
     idx, d2, info = kn.query(g, k, return_info=True, flags=1 | algo)
-    assert int(info["counters"][3]) == p.size(0)
+    assert int(info["counters"][3]) >= p.size(0)
     _assert_matches_oracle(p, idx, d2, k)
 
 
