@@ -114,6 +114,9 @@ struct QueryBuffers {
     int use_tiles;            // 0: exact ring walk for every query (debug / reference path)
     int flags;                // 1: force the exact re-scan for every query (tests); 2: stream kernel;
                               // 4: LDS-staged tile kernel (neither: env KN_QUERY_ALGO / default)
+    int exact_grid;           // workgroups of the fallback launch; 0 = default (sized for long
+                              // lists). The engine passes a small grid when the previous solve's
+                              // list was short (the launch then costs ~3 us less).
 };
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);

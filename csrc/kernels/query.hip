@@ -18,17 +18,21 @@
 //      v_med3_u32 per slot (new[j] = med3(old[j-1], key, old[j])), branch-free; the whole
 //      network is skipped by a uniform ballot when no lane improves.
 //   4. Exact re-rank: the K+M kept slots are re-evaluated in full fp32 and ordered by
-//      (distance, original id). A query is CERTIFIED when (a) its exact K-th distance does
-//      not exceed the truncation floor of the (K+M)-th key, so nothing truncated away can
-//      be closer, and (b) the K-th distance is within the distance to the boundary of the
-//      region it scanned (and of the rank's complete box in multi-GPU runs).
-//      Uncertified queries (rare) are appended to a list for the exact kernel below.
-//      (Reference defect D1: its "no guarantee" flag never fires, knearests.cu:136-139.)
+//      (distance, original id) with a streaming window (a slot's position = its valid
+//      predecessors +- the same-bucket neighbours that cross it), rare long runs of equal
+//      buckets and truncation near-ties by a wave-cooperative bitonic sort / exact re-scan.
+//      A query is CERTIFIED when (a) its exact K-th distance does not exceed the truncation
+//      floor of the (K+M)-th key, so nothing truncated away can be closer, and (b) the K-th
+//      distance is within the distance to the boundary of the region it scanned (and of the
+//      rank's complete box in multi-GPU runs). Uncertified queries (rare) are appended to a
+//      list for the exact kernel below. (Reference defect D1: its "no guarantee" flag never
+//      fires, knearests.cu:136-139.)
 //
-// knn_exact_kernel -- one lane per query, exact (distance, id) insertion network, analytic
-//   Chebyshev ring walk from the query's cell over contiguous x-row ranges with a true
-//   per-query stopping rule (distance to the scanned block). Serves the fallback list, and
-//   every query when tiles are disabled.
+// knn_exact_coop_kernel -- one WAVE per query: analytic Chebyshev shell walk from the query's
+//   cell, candidates tested 64 at a time, those within the current K-th distance compacted
+//   into a per-wave LDS buffer that is bitonic-sorted and truncated to K whenever it fills;
+//   a true per-query stopping rule (distance to the scanned block). Serves the fallback list,
+//   and every query when tiles are disabled.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -158,9 +162,9 @@ __device__ __forceinline__ unsigned long long pack_key64(float d, unsigned id) {
 template <int E>
 __device__ __forceinline__ void wave_bitonic_sort_u64(unsigned long long (&v)[E], int lane) {
     constexpr int N = 64 * E;
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int size = 2; size <= N; size <<= 1) {
-#pragma unroll
+#pragma clang loop unroll(full)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
             if (stride >= 64) {
 #pragma unroll
@@ -1385,176 +1389,7 @@ struct ExactArgs {
     unsigned* uncert_list;     // optional: original indices of uncertified queries
 };
 
-// Top-K storage policies for the exact kernel: registers (K <= 64: static-index insertion
-// network, no scratch) or a per-lane column in LDS (K > 64: keeps the register file free;
-// layout [slot][lane] so a wave's accesses to one slot hit 64 consecutive dwords).
-template <int KT>
-struct RegTopK {
-    float dd[KT];
-    unsigned ii[KT];
-    __device__ __forceinline__ void init(unsigned char*) {
-#pragma unroll
-        for (int j = 0; j < KT; ++j) { dd[j] = INFINITY; ii[j] = SENT; }
-    }
-    __device__ __forceinline__ bool improves(float d2, unsigned id) const { return pair_less(d2, id, dd[KT - 1], ii[KT - 1]); }
-    __device__ __forceinline__ void insert(float d2, unsigned id) {
-#pragma unroll
-        for (int j = KT - 1; j > 0; --j) {
-            const bool before_prev = pair_less(d2, id, dd[j - 1], ii[j - 1]);
-            const bool before_cur = pair_less(d2, id, dd[j], ii[j]);
-            const float nd = before_prev ? dd[j - 1] : (before_cur ? d2 : dd[j]);
-            const unsigned ni = before_prev ? ii[j - 1] : (before_cur ? id : ii[j]);
-            dd[j] = nd; ii[j] = ni;
-        }
-        if (pair_less(d2, id, dd[0], ii[0])) { dd[0] = d2; ii[0] = id; }
-    }
-    __device__ __forceinline__ float dist(int k) const {
-        float r = INFINITY;
-#pragma unroll
-        for (int j = 0; j < KT; ++j) if (j == k) r = dd[j];
-        return r;
-    }
-    template <class F>
-    __device__ __forceinline__ void emit(int k, F&& f) const {
-#pragma unroll
-        for (int j = 0; j < KT; ++j) if (j < k) f(j, dd[j], ii[j]);
-    }
-};
-
-template <int KT>
-struct LdsTopK {
-    float* dd;
-    unsigned* ii;
-    float worst_d;
-    unsigned worst_i;
-    __device__ __forceinline__ void init(unsigned char* smem) {
-        const int lane = threadIdx.x;
-        dd = reinterpret_cast<float*>(smem) + lane;
-        ii = reinterpret_cast<unsigned*>(smem + (size_t)KT * 64 * sizeof(float)) + lane;
-        for (int j = 0; j < KT; ++j) { dd[j * 64] = INFINITY; ii[j * 64] = SENT; }
-        worst_d = INFINITY;
-        worst_i = SENT;
-    }
-    __device__ __forceinline__ bool improves(float d2, unsigned id) const { return pair_less(d2, id, worst_d, worst_i); }
-    __device__ __forceinline__ void insert(float d2, unsigned id) {
-        int j = KT - 1;
-        while (j > 0) {
-            const float pd = dd[(j - 1) * 64];
-            const unsigned pi = ii[(j - 1) * 64];
-            if (!pair_less(d2, id, pd, pi)) break;
-            dd[j * 64] = pd; ii[j * 64] = pi;
-            --j;
-        }
-        dd[j * 64] = d2; ii[j * 64] = id;
-        worst_d = dd[(KT - 1) * 64];
-        worst_i = ii[(KT - 1) * 64];
-    }
-    __device__ __forceinline__ float dist(int k) const { return (k >= 0 && k < KT) ? dd[k * 64] : INFINITY; }
-    template <class F>
-    __device__ __forceinline__ void emit(int k, F&& f) const {
-        for (int j = 0; j < k && j < KT; ++j) f(j, dd[j * 64], ii[j * 64]);
-    }
-};
-
-template <class Top>
-__device__ __forceinline__ void exact_query(const ExactArgs& a, const GridGeom& g, unsigned sidx, Top& top) {
-    const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 302)];
-    const unsigned qw = __float_as_uint(qp.w);
-    if (!w_live(a, qw)) return;
-    const unsigned qorig = w_row(a, qw, sidx);
-    const float qx = qp.x, qy = qp.y, qz = qp.z;
-    const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
-    const int k = a.k;
-    const int rmax = max(max(max(cx, a.X - 1 - cx), max(cy, a.Y - 1 - cy)), max(cz, a.Z - 1 - cz));
-    bool certified = false;
-    for (int r = 0; r <= rmax; ++r) {
-        const int z0 = max(0, cz - r), z1 = min(a.Z - 1, cz + r);
-        const int y0 = max(0, cy - r), y1 = min(a.Y - 1, cy + r);
-        for (int z = z0; z <= z1; ++z) {
-            for (int y = y0; y <= y1; ++y) {
-                const bool shell = (z == cz - r) || (z == cz + r) || (y == cy - r) || (y == cy + r);
-                const int rowc = (z * a.Y + y) * a.X;
-                // the shell row is one contiguous x range; interior rows contribute 2 cells
-                for (int part = 0; part < (shell ? 1 : 2); ++part) {
-                    int xa, xb;
-                    if (shell) { xa = max(0, cx - r); xb = min(a.X - 1, cx + r); }
-                    else if (part == 0) { xa = cx - r; xb = cx - r; }
-                    else { xa = cx + r; xb = cx + r; }
-                    if (xa < 0 || xb > a.X - 1 || xa > xb) continue;
-                    const int p0 = a.cell_start[KN_IDX(rowc + xa, a.X * a.Y * a.Z + 1, 303)];
-                    const int p1 = a.cell_start[KN_IDX(rowc + xb + 1, a.X * a.Y * a.Z + 1, 303)];
-                    for (int p = p0; p < p1; ++p) {
-                        if ((unsigned)p == sidx) continue;
-                        const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
-                        const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
-                        const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                        const unsigned id = w_id(a, __float_as_uint(c.w));
-                        if (top.improves(d2, id)) top.insert(d2, id);
-                    }
-                }
-            }
-        }
-        // stopping rule: distance from q to the outside of the scanned block
-        float m = INFINITY;
-        if (cx - r > 0) m = fminf(m, qx - (g.origin[0] + (cx - r) * g.cell[0]));
-        if (cx + r < a.X - 1) m = fminf(m, g.origin[0] + (cx + r + 1) * g.cell[0] - qx);
-        if (cy - r > 0) m = fminf(m, qy - (g.origin[1] + (cy - r) * g.cell[1]));
-        if (cy + r < a.Y - 1) m = fminf(m, g.origin[1] + (cy + r + 1) * g.cell[1] - qy);
-        if (cz - r > 0) m = fminf(m, qz - (g.origin[2] + (cz - r) * g.cell[2]));
-        if (cz + r < a.Z - 1) m = fminf(m, g.origin[2] + (cz + r + 1) * g.cell[2] - qz);
-        m -= g.eps;
-        const float dK2 = top.dist(k - 1);
-        if (m == INFINITY || (m > 0.f && dK2 <= m * m)) { certified = true; break; }
-    }
-    // the complete box (multi-GPU): the K-th distance must stay inside it
-    const float dK2 = top.dist(k - 1);
-    const float m = fminf(fminf(complete_margin(a.complete, qx, 0), complete_margin(a.complete, qy, 1)),
-                          complete_margin(a.complete, qz, 2)) - g.eps;
-    if (!(m == INFINITY || (m > 0.f && dK2 <= m * m))) certified = false;
-    if (!certified) {
-        const unsigned pos = atomicAdd(a.counters + 1, 1u);
-        if (a.uncert_list) a.uncert_list[KN_IDX(pos, (unsigned)a.n_queries, 306)] = qorig;
-    }
-    const size_t row = (size_t)qorig * (size_t)k;
-    top.emit(k, [&](int j, float d, unsigned i) {
-        const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 305);
-        a.out_idx[o] = (i == SENT) ? SENT : out_id(a, i);
-        if (a.out_dist) a.out_dist[o] = d;
-    });
-}
-
-template <int KT>
-__global__ __launch_bounds__(256) void knn_exact_kernel(ExactArgs a) {
-    const GridGeom g = *a.geom;
-    const int total = a.list ? (int)*a.list_count : a.n;
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        RegTopK<KT> top;
-        top.init(nullptr);
-        exact_query(a, g, a.list ? a.list[KN_IDX(t, a.n, 301)] : (unsigned)t, top);
-    }
-}
-
-// K > 64: 64-thread workgroups, top-K columns in LDS (KT * 64 * 8 bytes).
-template <int KT>
-__global__ __launch_bounds__(64) void knn_exact_lds_kernel(ExactArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const GridGeom g = *a.geom;
-    const int total = a.list ? (int)*a.list_count : a.n;
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        LdsTopK<KT> top;
-        top.init(smem);
-        exact_query(a, g, a.list ? a.list[KN_IDX(t, a.n, 301)] : (unsigned)t, top);
-    }
-}
-
-// ---- wave-per-query exact kernel (fallback list, K <= 64) ---------------------------------
-// A single lane walking rings issues its global loads one dependent row at a time, so even a
-// handful of fallback queries cost ~200 us of latency (measured). Here one WAVE serves one
-// query: the rows of each Chebyshev shell are dealt to the 64 lanes, every lane keeps a
-// private sorted (d2, id) list of its own candidates, and the wave decides certification by
-// COUNTING (sum over lanes of entries within the scanned-block margin >= K, i.e. the K-th
-// distance is inside). The final K are selected by a wave-wide binary search on the 64-bit
-// (d2 bits, id) key, compacted through LDS and ordered by a 64-lane bitonic sort.
+// Wave-wide sum (DPP within rows of 16, then the 4 row totals).
 __device__ __forceinline__ unsigned wave_sum_u32(unsigned x) {
     x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false);
     x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false);
@@ -1564,81 +1399,143 @@ __device__ __forceinline__ unsigned wave_sum_u32(unsigned x) {
            (unsigned)__builtin_amdgcn_readlane((int)x, 32) + (unsigned)__builtin_amdgcn_readlane((int)x, 48);
 }
 
-
-template <int KT>
-__global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
-    __shared__ unsigned long long s_sel[4][64];
+// ---- wave-per-query exact kernel: threshold compaction + wave bitonic sort (any K <= 128) ----
+// One wave serves one query of the fallback list (or every query without tiles). It walks the
+// query's Chebyshev shells of cells; candidates are tested 64 at a time (dense shells: a row's
+// points dealt to the lanes; sparse shells: one row per lane) and every candidate with
+// d2 <= thr is appended to a per-wave LDS buffer by ballot compaction. When the buffer could
+// overflow, and after each shell once K candidates are held, the wave bitonic-sorts the buffer
+// by (d2 bits, id), keeps the first K and lowers thr to the K-th distance, so the buffer stays
+// small however dense the cells are (clustered clouds). A shell ends the walk once the K-th
+// distance lies inside the scanned block. Registers hold 4 keys per lane for any K, instead of
+// a per-lane K-entry (d2, id) list (K=50: 256 VGPRs plus scratch in the round-1 kernel).
+constexpr int kXCap = 256;
+// Workgroups of the fallback launch (4 query waves each). The list length is only known on the
+// device, so the grid is fixed: enough waves to hide the walk's load latency when the list is
+// long (clustered clouds) at a small fixed cost when it is empty.
+#ifndef KN_EXACT_GRID
+#define KN_EXACT_GRID 1024
+#endif  // per-wave candidate buffer (u64 keys); >= K + 64 for K <= 128
+__global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
+    __shared__ unsigned long long s_buf[4][kXCap];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long* buf = s_buf[wid];
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const GridGeom g = *a.geom;
     const int total = a.list ? (int)*a.list_count : a.n;
     const int k = a.k;
     for (int t = blockIdx.x * 4 + wid; t < total; t += gridDim.x * 4) {
         const unsigned sidx = (unsigned)__builtin_amdgcn_readfirstlane(
-            (int)(a.list ? a.list[KN_IDX(t, a.n, 301)] : (unsigned)t));
-        const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 302)];
+            (int)(a.list ? a.list[KN_IDX(t, a.n, 311)] : (unsigned)t));
+        const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 312)];
         const unsigned qw = __float_as_uint(qp.w);
         if (!w_live(a, qw)) continue;
         const unsigned qorig = w_row(a, qw, sidx);
         const float qx = qp.x, qy = qp.y, qz = qp.z;
         const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
-        RegTopK<KT> top;
-        top.init(nullptr);
+        int cnt = 0;            // keys in buf (uniform)
+        float thr = INFINITY;   // current K-th distance bound (uniform)
+        // sort buf[0, cnt), keep the first min(cnt, k), thr = K-th distance once K are held
+        auto compact = [&]() __attribute__((always_inline)) {
+            __builtin_amdgcn_wave_barrier();
+            unsigned long long v[kXCap / 64];
+#pragma unroll
+            for (int e = 0; e < kXCap / 64; ++e) v[e] = (64 * e + lane < cnt) ? buf[64 * e + lane] : ~0ull;
+            __builtin_amdgcn_wave_barrier();
+            wave_bitonic_sort_u64<kXCap / 64>(v, lane);
+#pragma unroll
+            for (int e = 0; e < kXCap / 64; ++e)
+                if (64 * e + lane < k) buf[64 * e + lane] = v[e];
+            cnt = min(cnt, k);
+            if (cnt >= k) {
+                unsigned hb = 0;
+#pragma unroll
+                for (int e = 0; e < kXCap / 64; ++e)
+                    if ((k - 1) / 64 == e) hb = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v[e] >> 32), (k - 1) & 63);
+                thr = __uint_as_float(hb);
+            }
+            __builtin_amdgcn_wave_barrier();
+        };
+        // test one candidate per lane (p < 0: none) and append the passing ones
+        auto offer = [&](int p) __attribute__((always_inline)) {
+            if (cnt + 64 > kXCap) compact();
+            bool pass = false;
+            unsigned long long key = 0;
+            if (p >= 0 && (unsigned)p != sidx) {
+                const float4 c = a.sorted[KN_IDX(p, a.n, 313)];
+                const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
+                const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                pass = d2 <= thr;
+                key = pack_key64(d2, w_id(a, __float_as_uint(c.w)));
+            }
+            const unsigned long long bal = __builtin_amdgcn_ballot_w64(pass);
+            if (pass) buf[cnt + __builtin_popcountll(bal & lt)] = key;
+            cnt += __builtin_popcountll(bal);
+        };
         const int rmax = max(max(max(cx, a.X - 1 - cx), max(cy, a.Y - 1 - cy)), max(cz, a.Z - 1 - cz));
-        bool certified = false;
+        bool certified = false, sorted_now = false;
         bool dense = true;  // ring 0 is one row: candidate-parallel
         for (int r = 0; r <= rmax; ++r) {
             const int z0 = max(0, cz - r), z1 = min(a.Z - 1, cz + r);
             const int y0 = max(0, cy - r), y1 = min(a.Y - 1, cy + r);
             const int ny = y1 - y0 + 1, nrows = (z1 - z0 + 1) * ny;
-            // stored range of part `part` of shell row `tr` (rows on the shell's y/z faces are
-            // whole x-runs, interior rows contribute their two x-end cells)
+            // stored range of part `part` of shell row `tr`: rows on the shell's y/z faces are
+            // whole x-runs, interior rows contribute their two x-end cells
             auto seg = [&](int tr, int part, int& p0, int& p1) -> bool {
                 const int z = z0 + tr / ny, y = y0 + tr % ny;
                 const bool shell = (z == cz - r) || (z == cz + r) || (y == cy - r) || (y == cy + r);
-                if (!shell && part == 1 && r == 0) return false;
-                if (shell && part == 1) return false;
+                if (shell ? part == 1 : (r == 0 && part == 1)) return false;
                 int xa, xb;
                 if (shell) { xa = max(0, cx - r); xb = min(a.X - 1, cx + r); }
                 else if (part == 0) { xa = cx - r; xb = cx - r; }
                 else { xa = cx + r; xb = cx + r; }
                 if (xa < 0 || xb > a.X - 1 || xa > xb) return false;
+                if (thr != INFINITY) {
+                    // only the cells of the row that reach into the current K-th ball (dense
+                    // clusters: the ball is far smaller than a shell, most rows are skipped)
+                    const float dyb = slab_dist(g, 1, qy, y, y), dzb = slab_dist(g, 2, qz, z, z);
+                    const float dyz2 = fmaf(dyb, dyb, dzb * dzb);
+                    if (!(dyz2 <= thr)) return false;
+                    const float rr = sqrtf(thr - dyz2) * 1.000001f + g.eps;
+                    xa = max(xa, cell_coord(g, 0, qx - rr));
+                    xb = min(xb, cell_coord(g, 0, qx + rr));
+                    if (xa > xb) return false;
+                }
                 const int rowc = (z * a.Y + y) * a.X;
-                p0 = a.cell_start[KN_IDX(rowc + xa, a.X * a.Y * a.Z + 1, 303)];
-                p1 = a.cell_start[KN_IDX(rowc + xb + 1, a.X * a.Y * a.Z + 1, 303)];
+                p0 = a.cell_start[KN_IDX(rowc + xa, a.X * a.Y * a.Z + 1, 314)];
+                p1 = a.cell_start[KN_IDX(rowc + xb + 1, a.X * a.Y * a.Z + 1, 314)];
                 return p0 < p1;
             };
-            auto test = [&](int p) {
-                if ((unsigned)p == sidx) return;
-                const float4 c = a.sorted[KN_IDX(p, a.n, 304)];
-                const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
-                const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                const unsigned id = w_id(a, __float_as_uint(c.w));
-                if (top.improves(d2, id)) top.insert(d2, id);
-            };
+            unsigned shell_pts = 0;
             if (dense) {
-                // dense shells (clusters; always ring 0, a single row): candidate-parallel --
-                // each row's points are dealt to the 64 lanes (coalesced) instead of one lane
-                // walking a long row while the others idle
-                unsigned pts = 0;
                 for (int tr = 0; tr < nrows; ++tr)
                     for (int part = 0; part < 2; ++part) {
                         int p0, p1;
                         if (!seg(tr, part, p0, p1)) continue;
-                        pts += (unsigned)(p1 - p0);
-                        for (int p = p0 + lane; p < p1; p += 64) test(p);
+                        shell_pts += (unsigned)(p1 - p0);
+                        for (int pb = p0; pb < p1; pb += 64) offer(pb + lane < p1 ? pb + lane : -1);
                     }
-                dense = pts > 32u * (unsigned)nrows;  // the next shell is probably alike
             } else {
-                unsigned pts = 0;  // rows of the shell dealt to the lanes
-                for (int tr = lane; tr < nrows; tr += 64)
-                    for (int part = 0; part < 2; ++part) {
-                        int p0, p1;
-                        if (!seg(tr, part, p0, p1)) continue;
-                        pts += (unsigned)(p1 - p0);
-                        for (int p = p0; p < p1; ++p) test(p);
+                for (int tb = 0; tb < nrows; tb += 64) {
+                    // one row per lane: walk its (up to two) segments, 64 candidates per step
+                    int c0 = 0, c1 = 0, d0 = 0, d1 = 0;
+                    if (tb + lane < nrows) {
+                        if (!seg(tb + lane, 0, c0, c1)) c0 = c1 = 0;
+                        if (!seg(tb + lane, 1, d0, d1)) d0 = d1 = 0;
                     }
-                dense = wave_sum_u32(pts) > 32u * (unsigned)nrows;
+                    shell_pts += (unsigned)((c1 - c0) + (d1 - d0));
+                    while (__builtin_amdgcn_ballot_w64(c0 < c1 || d0 < d1)) {
+                        int p = -1;
+                        if (c0 < c1) p = c0++;
+                        else if (d0 < d1) p = d0++;
+                        offer(p);
+                    }
+                }
+                shell_pts = wave_sum_u32(shell_pts);
             }
+            if (dense) shell_pts = (unsigned)__builtin_amdgcn_readfirstlane((int)shell_pts);
+            dense = shell_pts > 32u * (unsigned)nrows;  // the next shell is probably alike
+            // stopping rule: distance from q to the outside of the scanned block
             float m = INFINITY;
             if (cx - r > 0) m = fminf(m, qx - (g.origin[0] + (cx - r) * g.cell[0]));
             if (cx + r < a.X - 1) m = fminf(m, g.origin[0] + (cx + r + 1) * g.cell[0] - qx);
@@ -1647,74 +1544,34 @@ __global__ __launch_bounds__(256) void knn_exact_wave_kernel(ExactArgs a) {
             if (cz - r > 0) m = fminf(m, qz - (g.origin[2] + (cz - r) * g.cell[2]));
             if (cz + r < a.Z - 1) m = fminf(m, g.origin[2] + (cz + r + 1) * g.cell[2] - qz);
             m -= g.eps;
-            if (m == INFINITY) { certified = true; break; }  // the block covers the whole grid
-            if (m > 0.f) {
-                const float m2 = m * m;
-                unsigned c = 0;
-#pragma unroll
-                for (int j = 0; j < KT; ++j) c += (top.dd[j] <= m2) ? 1u : 0u;
-                if ((int)wave_sum_u32(c) >= k) { certified = true; break; }
+            if (m == INFINITY) { compact(); sorted_now = true; certified = true; break; }
+            if (cnt >= k) {
+                compact();
+                sorted_now = true;
+                if (m > 0.f && thr <= m * m) { certified = true; break; }
+            } else {
+                sorted_now = false;
             }
         }
-        // wave-wide k-th smallest 64-bit key: binary search on the key value
-        unsigned long long lo = 0, hi = ~0ull;
-        unsigned have = 0;
-#pragma unroll
-        for (int j = 0; j < KT; ++j) have += (top.ii[j] != SENT) ? 1u : 0u;
-        const unsigned avail = wave_sum_u32(have);
-        {
-            const unsigned want = min((unsigned)k, avail);
-            if (want == 0) hi = 0;
-            while (lo < hi) {
-                const unsigned long long mid = lo + ((hi - lo) >> 1);
-                unsigned c = 0;
-#pragma unroll
-                for (int j = 0; j < KT; ++j) c += (pack_key64(top.dd[j], top.ii[j]) <= mid) ? 1u : 0u;
-                if (wave_sum_u32(c) >= want) hi = mid; else lo = mid + 1;
-            }
-        }
-        const unsigned long long kth = lo;
-        // compaction: every lane's entries <= kth go to LDS (<= k <= 64 of them in total)
-        unsigned mine = 0;
-#pragma unroll
-        for (int j = 0; j < KT; ++j) mine += (top.ii[j] != SENT && pack_key64(top.dd[j], top.ii[j]) <= kth) ? 1u : 0u;
-        const unsigned incl = (unsigned)wave_inclusive_scan_add((int)mine);
-        const unsigned base = incl - mine;
-        s_sel[wid][lane] = ~0ull;
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int j = 0; j < KT; ++j)
-            if ((unsigned)j < mine) s_sel[wid][KN_IDX(base + j, 64u, 308)] = pack_key64(top.dd[j], top.ii[j]);
-        __builtin_amdgcn_wave_barrier();
-        unsigned long long v = s_sel[wid][lane];
-        // 64-lane bitonic sort (ascending)
-        for (int size = 2; size <= 64; size <<= 1) {
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                const unsigned lo32 = (unsigned)__shfl_xor((int)(unsigned)v, stride, 64);
-                const unsigned hi32 = (unsigned)__shfl_xor((int)(unsigned)(v >> 32), stride, 64);
-                const unsigned long long o = ((unsigned long long)hi32 << 32) | lo32;
-                const bool up = (lane & size) == 0;
-                const bool lower = (lane & stride) == 0;
-                const unsigned long long mn = v < o ? v : o, mx = v < o ? o : v;
-                v = (up == lower) ? mn : mx;
-            }
-        }
-        // certification against the rank's complete box (multi-GPU); needs the k-th distance
-        const float dk = ((int)avail < k) ? INFINITY : __uint_as_float((unsigned)(kth >> 32));
+        if (!sorted_now) compact();
+        // certification against the rank's complete box (multi-GPU); needs the K-th distance
+        const float dk = (cnt < k) ? INFINITY : thr;
         const float mc = fminf(fminf(complete_margin(a.complete, qx, 0), complete_margin(a.complete, qy, 1)),
                                complete_margin(a.complete, qz, 2)) - g.eps;
         const bool cert = certified && (mc == INFINITY || (mc > 0.f && dk <= mc * mc));
         if (!cert && lane == 0) {
             const unsigned pos = atomicAdd(a.counters + 1, 1u);
-            if (a.uncert_list) a.uncert_list[KN_IDX(pos, (unsigned)a.n_queries, 306)] = qorig;
+            if (a.uncert_list) a.uncert_list[KN_IDX(pos, (unsigned)a.n_queries, 316)] = qorig;
         }
-        if (lane < k) {
-            const size_t o = KN_IDX((size_t)qorig * (size_t)k + lane, (size_t)a.n_queries * k, 305);
-            const unsigned id = (unsigned)v;
+        __builtin_amdgcn_wave_barrier();
+        for (int j = lane; j < k; j += 64) {
+            const size_t o = KN_IDX((size_t)qorig * (size_t)k + j, (size_t)a.n_queries * k, 315);
+            const unsigned long long v = (j < cnt) ? buf[j] : ~0ull;
             const bool empty = (v == ~0ull);
-            a.out_idx[o] = empty ? SENT : out_id(a, id);
+            a.out_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
             if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1830,15 +1687,10 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     b.list_count = q.counters + 0;
     b.counters = q.counters;
     b.uncert_list = q.uncert_list;
-    if constexpr (KT <= 64) {
-        // one wave per query; the fallback list is short, so 256 workgroups (1024 waves) suffice
-        const unsigned grid = tiles ? 256u : std::max(1u, std::min(cdiv(q.n, 4), 16384u));
-        knn_exact_wave_kernel<KT><<<grid, 256, 0, s>>>(b);
-    } else {
-        const unsigned grid = tiles ? 2048u : std::max(1u, std::min(cdiv(q.n, 64), 65535u));
-        const size_t lds = (size_t)KT * 64 * 8;
-        knn_exact_lds_kernel<KT><<<grid, 64, lds, s>>>(b);
-    }
+    // one wave per query (threshold compaction, any K): 1024 waves for the fallback list
+    const unsigned grid = tiles ? (unsigned)(q.exact_grid > 0 ? q.exact_grid : KN_EXACT_GRID)
+                                : std::max(1u, std::min(cdiv(q.n, 4), 16384u));
+    knn_exact_coop_kernel<<<grid, 256, 0, s>>>(b);
     return hipGetLastError();
 }
 
@@ -1968,7 +1820,11 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
         // K-th neighbour radius in cells for a uniform cloud: (3(K+1)/(4 pi ppc))^(1/3)
         const double rk = std::cbrt(3.0 * (k + 1) / (4.0 * M_PI * ppc));
         p.halo = std::max(1, (int)std::ceil(rk + 0.35));
-        if (k > 40 && k <= 64) p.halo = std::max(p.halo, 3);  // measured: 3 rings beat 2 + exact path
+        // 40 < K <= 64: the lane walk scans the whole staged block (KN_LANE_FULL), so 2 rings
+        // certify all but the domain-boundary queries, which the exact kernel finishes; 2 rings
+        // keep the workgroup at ~40 KB of LDS (4 per CU) where 3 rings took 70 KB (2 per CU).
+        // 900K uniform: K=50 1.31 -> 0.95 ms, K=64 1.68 -> 1.33 ms (profiles/ab_r2_exact.log)
+        if (k > 40 && k <= 64) p.halo = std::min(p.halo, 2);
     }
     const double staged = (double)(p.tile[0] + 2 * p.halo) * (p.tile[1] + 2 * p.halo) *
                           (p.tile[2] + 2 * p.halo) * ppc;

@@ -173,6 +173,8 @@ QueryBuffers Engine::query_buffers() const {
     q.halo = ap_.halo;
     q.lds_capacity = ap_.lds_capacity;
     q.use_tiles = cfg_.use_tiles;
+    // fallback grid from the last observed fallback count: 256 workgroups when it was short
+    q.exact_grid = last_fallback_ < 4096u ? 256 : 0;
     return q;
 }
 
@@ -244,6 +246,9 @@ kn_status Engine::solve() {
     (void)hipEventRecord(ev_[3], stream_);
     if ((st = check(hipEventSynchronize(ev_[3]), "solve sync")) != KN_OK) return st;
     (void)hipEventElapsedTime(&ms_solve_, ev_[2], ev_[3]);
+    // the stream is idle: one word tells the next launches how long the fallback list runs
+    if (hipMemcpy(&last_fallback_, counters_, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
+        last_fallback_ = ~0u;
     if (cfg_.verbose) {
         unsigned c[kNumCounters] = {0};
         (void)hipMemcpy(c, counters_, sizeof(c), hipMemcpyDeviceToHost);

@@ -127,6 +127,7 @@ private:
     float* points3_ = nullptr;  // stored-order float3 copy of sorted_ (reference d_stored_points)
     bool points3_valid_ = false;
     bool built_ = false, solved_ = false, stored_valid_ = false;
+    unsigned last_fallback_ = ~0u;  // fallback-list length of the last eager solve (~0: unknown)
     float ms_build_ = 0.f, ms_solve_ = 0.f;
 };
 

@@ -104,7 +104,7 @@ def test_plan_auto_reference_density():
     assert p.dims == [64, 64, 64]
     q = kn.Plan.auto(10_000_000, 32)
     assert q.tile == [4, 4, 4] and all(d % t == 0 for d, t in zip(q.dims, q.tile))
-    assert kn.Plan.auto(900_000, 50).halo == 3
+    assert kn.Plan.auto(900_000, 50).halo == 2
     assert kn.Plan.auto(1000, 8).dims == [7, 7, 7]  # small grids are not rounded
     assert p.halo >= 1 and p.lds_capacity >= 1024 and p.lds_bytes <= 160 * 1024
 
