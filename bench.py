@@ -193,33 +193,56 @@ def run_dist(args) -> dict:
     else:
         dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=300))
     rank, world = dist.get_rank(), dist.get_world_size()
+    # weak scaling: args.n points per rank; strong scaling: args.n points in total
+    n_rank = args.n if args.scaling == "weak" else args.n // world + (1 if rank < args.n % world else 0)
     if args.layout == "partitioned":
         # spatial split: rank r holds a uniform sample of ITS box of the [0,1000]^3 cube (the
         # decomposition the engine itself derives), i.e. a globally uniform cloud of N x 900K
         from cuda_knearests_amd.parallel import SpatialDecomposition
 
         blo, bhi = SpatialDecomposition(world, (0.0,) * 3, (1000.0,) * 3).rank_box(rank)
-        u = uniform_cloud(args.n, seed=args.seed + 7919 * rank, device=dev, lo=0.0, hi=1.0)
+        u = uniform_cloud(n_rank, seed=args.seed + 7919 * rank, device=dev, lo=0.0, hi=1.0)
         pts = (u * torch.tensor([bhi[a] - blo[a] for a in range(3)], device=dev)
                + torch.tensor(blo, device=dev)).contiguous()
     else:
-        pts = make_cloud(args, dev, 7919 * rank)
+        a2 = argparse.Namespace(**vars(args))
+        a2.n = n_rank
+        pts = make_cloud(a2, dev, 7919 * rank)
     from cuda_knearests_amd.parallel import HostStagedTransport
 
-    dk = DistributedKNearests(k=args.k, deterministic=args.deterministic,
+    # failure detection: a dead or hung peer fails this rank's collective after 120 s
+    # (CollectiveError -> non-zero exit) instead of blocking the job
+    dk = DistributedKNearests(k=args.k, deterministic=args.deterministic, timeout_s=120.0,
                               transport=HostStagedTransport() if staged else None)
     res = None
+    part = args.layout == "partitioned"
     for _ in range(args.warmup):
-        res = dk.solve(pts, partitioned=args.layout == "partitioned")
+        res = dk.solve(pts, partitioned=part)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
+    # timed steps run asynchronously (no host synchronisation inside a step once the routing is
+    # steady); every step's device flag is checked after the timed region
+    steps = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = dk.solve(pts, partitioned=args.layout == "partitioned")
+        steps.append(dk.solve(pts, partitioned=part, async_=not args.sync_steps))
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
+    invalid = sum(0 if r.valid() else 1 for r in steps)
+    res = steps[-1] if steps else res
+    if invalid:
+        # some step's routing assumption failed: time the synchronous (validated) form instead
+        log(f"{invalid} asynchronous steps were invalid; re-timing synchronously")
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = dk.solve(pts, partitioned=part)
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = time.perf_counter() - t0
     if os.environ.get("KN_HOST_MARKS"):  # host-side stage timing of the native step (stderr)
         dk.host_marks = []
         for _ in range(20):
@@ -250,8 +273,10 @@ def run_dist(args) -> dict:
         c = torch.tensor([chk["bad_rows"] + chk["bad_id_rows"]], device=cdev)
         dist.all_reduce(c)
         chk["bad_rows_all_ranks"] = int(c.item())
-    out = {"t": float(t.item()), "stats": res.stats if res else {}, "check": chk, "n_total": args.n * world,
-           "rank": rank, "world": world}
+    nt = torch.tensor([pts.size(0)], device=cdev, dtype=torch.int64)
+    dist.all_reduce(nt)
+    out = {"t": float(t.item()), "stats": res.stats if res else {}, "check": chk, "n_total": int(nt.item()),
+           "rank": rank, "world": world, "invalid_async_steps": invalid}
     dist.barrier()
     dist.destroy_process_group()
     return out
@@ -278,13 +303,16 @@ def run_loopback_bench(args) -> dict:
 
     def body(t):
         dk = DistributedKNearests(k=args.k, transport=t)
-        res = None
+        res, steps = None, []
         for i in range(args.warmup + args.steps):
             if i == args.warmup and t.rank == 0:
                 torch.cuda.synchronize()
                 times.append(time.perf_counter())
-            res = dk.solve(shares[t.rank])
+            res = dk.solve(shares[t.rank], async_=i >= args.warmup and not args.sync_steps)
+            steps.append(res)
         torch.cuda.synchronize()
+        if not all(r.valid() for r in steps):
+            raise RuntimeError("an asynchronous loopback step was invalid")
         return res
 
     out = run_loopback(W, body, timeout=1800)
@@ -348,6 +376,10 @@ def main() -> int:
     ap.add_argument("--loopback", type=int, default=0,
                     help="W virtual ranks on one GPU (multi-rank algorithm at W x n points)")
     ap.add_argument("--cpu-oracle", action="store_true", help="time the CPU kd-tree path (BASELINE config 1)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="N GPUs: weak = --n points per GPU; strong = --n points in total, split over the ranks")
+    ap.add_argument("--sync-steps", action="store_true",
+                    help="N GPUs: validate every step before the next (no asynchronous steady-state steps)")
     args = ap.parse_args()
     if os.environ.get("KN_BENCH_WATCHDOG"):
         import faulthandler
@@ -380,7 +412,9 @@ def main() -> int:
             return 0
         n_gpus = r["world"]
         extra = {"halo_width": r["stats"].get("halo_width"), "n_halo_rank0": r["stats"].get("n_halo"),
-                 "rounds": r["stats"].get("rounds"), "rank_grid": r["stats"].get("grid"), "layout": args.layout}
+                 "rounds": r["stats"].get("rounds"), "rank_grid": r["stats"].get("grid"), "layout": args.layout,
+                 "steady_async": bool(r["stats"].get("steady")) and not args.sync_steps,
+                 "invalid_async_steps": r["invalid_async_steps"], "path": "distributed"}
     else:
         r = run_native(args) if args.path == "native" else run_single(args)
         n_gpus = 1
@@ -391,11 +425,13 @@ def main() -> int:
     qps = r["n_total"] * args.steps / r["t"]
     line = {
         "metric": METRIC, "value": qps, "unit": "queries/s", "n_gpus": n_gpus, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": args.scaling,
         "vs_baseline": None, "dtype": "fp32",
         "data": args.xyz or (f"synthetic {args.gen} random [0,1000]^3 (seeded per rank" +
                              (f", {args.layout} layout)" if n_gpus > 1 or args.dist else ")")),
-        "config": {"model": f"uniform-grid kNN, {args.n} pts/GPU, k={args.k}", "global_batch": r["n_total"],
+        "config": {"model": (f"uniform-grid kNN, {args.n} pts/GPU, k={args.k}" if args.scaling == "weak"
+                             else f"uniform-grid kNN, {args.n} pts total, k={args.k}"),
+                   "global_batch": r["n_total"],
                    "seq_len": args.k, "parallelism": f"spatial{n_gpus}" if n_gpus > 1 else "single"},
         "vs_cpu_oracle": qps / CPU_ORACLE_QPS, "check": r.get("check", {}), "in_cell_sort": args.deterministic,
         **extra,

@@ -120,6 +120,10 @@ struct QueryBuffers {
 };
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);
+// Exact K nearest of EXTERNAL points {x, y, z, bits(global id)} among the grid's points (multi-GPU
+// query forwarding): row t of q.out_idx / q.out_dist; a point with the query's global id is
+// skipped (self). Uses q.sorted / cell_start / geom / dims / k / row_of / counters.
+hipError_t launch_query_external(const QueryBuffers& q, const float4* ext, int n_ext, hipStream_t stream);
 
 // out_sorted[i*k + j] = inv(out_orig[perm[i]*k + j]) : reference (stored-space) view.
 hipError_t launch_to_stored_space(const unsigned* out_orig, const unsigned* perm,

@@ -79,6 +79,11 @@ hipError_t launch_route_plan(const double* metas, int world, int rank, const int
 // words: kBBoxWords scratch words (kn/kernels.h). One all_gather of `out` gives the global
 // domain and the id offsets.
 hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* out, hipStream_t s);
+// Steady-state check of a sync-free distributed step, one wave: flag[0] = (this rank's meta or
+// send counts differ from the planned ones) + (any uncertified query). No host involvement.
+hipError_t launch_steady_flag(const double* local, const double* planned_meta, const int* totals,
+                              const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
+                              hipStream_t s);
 hipError_t debug_words_route(unsigned out[4], bool reset);
 
 }  // namespace kn

@@ -1387,6 +1387,8 @@ struct ExactArgs {
     const unsigned* list_count;
     unsigned* counters;        // [1] uncertified count
     unsigned* uncert_list;     // optional: original indices of uncertified queries
+    const float4* ext;         // external queries {x, y, z, bits(global id)} (nullptr: stored points)
+    int n_ext;
 };
 
 // Wave-wide sum (DPP within rows of 16, then the 4 row totals).
@@ -1422,15 +1424,17 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
     unsigned long long* buf = s_buf[wid];
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const GridGeom g = *a.geom;
-    const int total = a.list ? (int)*a.list_count : a.n;
+    const int total = a.ext ? a.n_ext : (a.list ? (int)*a.list_count : a.n);
     const int k = a.k;
     for (int t = blockIdx.x * 4 + wid; t < total; t += gridDim.x * 4) {
-        const unsigned sidx = (unsigned)__builtin_amdgcn_readfirstlane(
+        // external queries (multi-GPU forwarding): a point of another rank, self = same global id
+        const unsigned sidx = a.ext ? ~0u : (unsigned)__builtin_amdgcn_readfirstlane(
             (int)(a.list ? a.list[KN_IDX(t, a.n, 311)] : (unsigned)t));
-        const float4 qp = a.sorted[KN_IDX(sidx, (unsigned)a.n, 312)];
+        const float4 qp = a.ext ? a.ext[t] : a.sorted[KN_IDX(sidx, (unsigned)a.n, 312)];
         const unsigned qw = __float_as_uint(qp.w);
-        if (!w_live(a, qw)) continue;
-        const unsigned qorig = w_row(a, qw, sidx);
+        if (!a.ext && !w_live(a, qw)) continue;
+        const unsigned qorig = a.ext ? (unsigned)t : w_row(a, qw, sidx);
+        const unsigned qid = a.ext ? w_id(a, qw) : ~0u;
         const float qx = qp.x, qy = qp.y, qz = qp.z;
         const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
         int cnt = 0;            // keys in buf (uniform)
@@ -1465,8 +1469,9 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
                 const float4 c = a.sorted[KN_IDX(p, a.n, 313)];
                 const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
                 const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                pass = d2 <= thr;
-                key = pack_key64(d2, w_id(a, __float_as_uint(c.w)));
+                const unsigned cid = w_id(a, __float_as_uint(c.w));
+                pass = d2 <= thr && cid != qid;
+                key = pack_key64(d2, cid);
             }
             const unsigned long long bal = __builtin_amdgcn_ballot_w64(pass);
             if (pass) buf[cnt + __builtin_popcountll(bal & lt)] = key;
@@ -1687,6 +1692,8 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     b.list_count = q.counters + 0;
     b.counters = q.counters;
     b.uncert_list = q.uncert_list;
+    b.ext = nullptr;
+    b.n_ext = 0;
     // one wave per query (threshold compaction, any K): 1024 waves for the fallback list
     const unsigned grid = tiles ? (unsigned)(q.exact_grid > 0 ? q.exact_grid : KN_EXACT_GRID)
                                 : std::max(1u, std::min(cdiv(q.n, 4), 16384u));
@@ -1710,6 +1717,24 @@ size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity) {
 }
 
 KN_DEFINE_DEBUG_READER(debug_words_query)
+
+hipError_t launch_query_external(const QueryBuffers& q, const float4* ext, int n_ext, hipStream_t s) {
+    if (q.k <= 0 || q.k > 128 || n_ext < 0) return hipErrorInvalidValue;
+    if (n_ext == 0) return hipSuccess;
+    ExactArgs b{};
+    b.sorted = q.sorted; b.cell_start = q.cell_start; b.geom = q.geom; b.n = q.n;
+    b.X = q.dims[0]; b.Y = q.dims[1]; b.Z = q.dims[2]; b.k = q.k; b.n_queries = n_ext;
+    b.id_map = q.id_map; b.row_of = q.row_of;
+    for (int a = 0; a < 3; ++a) { b.complete.lo[a] = -INFINITY; b.complete.hi[a] = INFINITY; }
+    b.out_idx = q.out_idx; b.out_dist = q.out_dist;
+    b.list = nullptr; b.list_count = nullptr;
+    b.counters = q.counters;
+    b.uncert_list = nullptr;
+    b.ext = ext;
+    b.n_ext = n_ext;
+    knn_exact_coop_kernel<<<std::max(1u, std::min(cdiv((size_t)n_ext, 4), 16384u)), 256, 0, s>>>(b);
+    return hipGetLastError();
+}
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t s) {
     const int k = q.k;

@@ -332,6 +332,17 @@ __global__ void global_w_kernel(float4* __restrict__ sorted, const unsigned* __r
     sorted[i].w = __uint_as_float((gid & 0x7FFFFFFFu) | ((int)local >= n_owned ? 0x80000000u : 0u));
 }
 
+__global__ void steady_flag_kernel(const double* __restrict__ local, const double* __restrict__ planned,
+                                   const int* __restrict__ totals, const int* __restrict__ ptotals, int nt,
+                                   const unsigned* __restrict__ counters, int* __restrict__ flag) {
+    const int lane = threadIdx.x;
+    bool diff = false;
+    if (lane < 8) diff = local[lane] != planned[lane];  // {lo, hi, n}: a NaN never matches either
+    for (int i = lane; i < nt; i += 64) diff |= totals[i] != ptotals[i];
+    const bool any = __builtin_amdgcn_ballot_w64(diff) != 0ull;
+    if (lane == 0) flag[0] = (any ? 1 : 0) + (counters[1] != 0u ? 1 : 0);
+}
+
 }  // namespace
 
 int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
@@ -377,6 +388,13 @@ hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* o
     hipError_t e;
     if ((e = launch_bbox_partials(pts, n, words, s)) != hipSuccess) return e;
     meta_finalize_kernel<<<1, 64, 0, s>>>(words, n > 0 ? bbox_block_count(n) : 0, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_steady_flag(const double* local, const double* planned_meta, const int* totals,
+                              const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
+                              hipStream_t s) {
+    steady_flag_kernel<<<1, 64, 0, s>>>(local, planned_meta, totals, planned_totals, n_totals, counters, flag);
     return hipGetLastError();
 }
 

@@ -93,7 +93,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                                  c10::optional<torch::Tensor> id_map, std::vector<double> complete,
                                  std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
                                  bool use_tiles, bool with_dist, int64_t flags,
-                                 c10::optional<torch::Tensor> row_of) {
+                                 c10::optional<torch::Tensor> row_of, int64_t exact_grid = 0) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
@@ -141,6 +141,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     q.lds_capacity = (int)lds_capacity;
     q.use_tiles = use_tiles ? 1 : 0;
     q.flags = (int)flags;
+    q.exact_grid = (int)exact_grid;
     TORCH_CHECK(lds_capacity >= 64 && lds_capacity % 64 == 0 && lds_capacity <= 8192,
                 "lds_capacity must be a multiple of 64 in [64, 8192]");
     TORCH_CHECK(kn::query_lds_bytes(q.tile, q.halo, q.lds_capacity) <= 160 * 1024, "tile plan exceeds 160 KiB LDS");
@@ -448,7 +449,8 @@ std::vector<torch::Tensor> route_unpack_split(torch::Tensor recv, torch::Tensor 
 // hdr: the plan header as doubles (kn::kPlanHdr). -> (pts, gids, idx, d2, counters)
 std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_rows, std::vector<int64_t> recv_own,
                                       std::vector<int64_t> recv_halo, int64_t rank, std::vector<int64_t> grid,
-                                      std::vector<double> hdr, int64_t k, double ppc, bool deterministic) {
+                                      std::vector<double> hdr, int64_t k, double ppc, bool deterministic,
+                                      int64_t exact_grid = 0) {
     TORCH_CHECK(grid.size() == 3 && hdr.size() >= 12, "grid must have 3 entries, hdr >= 12");
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world == (int64_t)recv_own.size(), "grid does not match the source table");
@@ -486,8 +488,64 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
                                      (int)nst, (int)n_owned,
                                      c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
     auto q = query(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
-                   ap.halo, ap.lds_capacity, true, true, 0, g[2]);
-    return {pg[0], pg[1], q[0], q[1], q[2]};
+                   ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid);
+    // + the local grid (global-id mode) and the uncertified list, for query forwarding
+    auto dims_t = torch::tensor({ap.dims[0], ap.dims[1], ap.dims[2]}, torch::kInt64);
+    return {pg[0], pg[1], q[0], q[1], q[2], g[0], g[1], g[3], g[2], q[3], dims_t};
+}
+
+// Exact K nearest of external points (multi-GPU query forwarding) among a global-id-mode local
+// grid: ext (M, 4) float32 {x, y, z, bits(global id)} -> (idx (M, k) global ids, d2 (M, k))
+std::vector<torch::Tensor> query_external(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom,
+                                          std::vector<int64_t> dims, int64_t k, torch::Tensor ext,
+                                          torch::Tensor row_of) {
+    TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4, "sorted must be (N,4) GPU");
+    TORCH_CHECK(ext.is_cuda() && ext.dim() == 2 && ext.size(1) == 4 && ext.scalar_type() == torch::kFloat32 &&
+                    ext.is_contiguous(), "ext must be a contiguous (M,4) float32 GPU tensor");
+    TORCH_CHECK(dims.size() == 3 && cell_start.numel() == dims[0] * dims[1] * dims[2] + 1, "bad dims");
+    TORCH_CHECK(k >= 1 && k <= 128, "k must be in [1, 128]");
+    TORCH_CHECK(row_of.is_cuda() && row_of.scalar_type() == torch::kInt32 && row_of.numel() >= sorted.size(0),
+                "row_of must be the grid's int32 perm");
+    const c10::DeviceGuard guard(sorted.device());
+    const int64_t m = ext.size(0);
+    auto idx = torch::empty({m, k}, sorted.options().dtype(torch::kInt32));
+    auto d2 = torch::empty({m, k}, sorted.options());
+    auto counters = torch::zeros({kn::kNumCounters}, sorted.options().dtype(torch::kInt32));
+    kn::QueryBuffers q{};
+    q.sorted = reinterpret_cast<const float4*>(sorted.data_ptr<float>());
+    q.cell_start = cell_start.data_ptr<int>();
+    q.geom = reinterpret_cast<const kn::GridGeom*>(geom.data_ptr<int>());
+    q.n = (int)sorted.size(0);
+    for (int a = 0; a < 3; ++a) q.dims[a] = (int)dims[a];
+    q.k = (int)k;
+    q.row_of = reinterpret_cast<const unsigned*>(row_of.data_ptr<int>());
+    q.out_idx = reinterpret_cast<unsigned*>(idx.data_ptr<int>());
+    q.out_dist = d2.data_ptr<float>();
+    q.counters = reinterpret_cast<unsigned*>(counters.data_ptr<int>());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_query_external(q, reinterpret_cast<const float4*>(ext.data_ptr<float>()), (int)m, s));
+    return {idx, d2};
+}
+
+// Sync-free distributed step check (one wave, on device): (1,) int32 = mismatch of this rank's
+// meta / send counts against the planned ones + (uncertified queries > 0)
+torch::Tensor steady_flag(torch::Tensor local, torch::Tensor metas, int64_t rank, torch::Tensor totals,
+                          torch::Tensor planned_totals, torch::Tensor counters) {
+    TORCH_CHECK(local.is_cuda() && local.scalar_type() == torch::kFloat64 && local.numel() == 8, "local: (8,) f64 GPU");
+    TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.numel() >= 8 * (rank + 1) &&
+                    metas.is_contiguous(), "metas: (world*8,) f64 GPU");
+    TORCH_CHECK(totals.is_cuda() && planned_totals.is_cuda() && totals.scalar_type() == torch::kInt32 &&
+                    planned_totals.scalar_type() == torch::kInt32 && totals.numel() == planned_totals.numel() &&
+                    totals.is_contiguous() && planned_totals.is_contiguous(), "totals: matching int32 GPU tensors");
+    TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == torch::kInt32 && counters.numel() >= 2, "counters");
+    const c10::DeviceGuard guard(local.device());
+    auto flag = torch::empty({1}, counters.options());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_steady_flag(local.data_ptr<double>(), metas.data_ptr<double>() + 8 * rank,
+                                        totals.data_ptr<int>(), planned_totals.data_ptr<int>(), (int)totals.numel(),
+                                        reinterpret_cast<const unsigned*>(counters.data_ptr<int>()),
+                                        flag.data_ptr<int>(), s));
+    return flag;
 }
 
 // occupancy-adaptive grid: sum over cells of count^2 (int64, on device, no sync)
@@ -674,7 +732,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("query", &query, "k-nearest-neighbour queries on a built grid (GPU)", py::arg("sorted"),
           py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("k"), py::arg("n_queries"),
           py::arg("id_map"), py::arg("complete"), py::arg("tile"), py::arg("halo"), py::arg("lds_capacity"),
-          py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0, py::arg("row_of") = py::none());
+          py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0, py::arg("row_of") = py::none(),
+          py::arg("exact_grid") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");
@@ -690,8 +749,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "multi-GPU: plan + counts + scatter (self-last layout, cap rows) enqueued in one call",
           py::arg("points"), py::arg("ids"), py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"),
           py::arg("halo_factor"), py::arg("cap"));
+    m.def("query_external", &query_external,
+          "multi-GPU query forwarding: exact K nearest of external points among a local grid");
+    m.def("steady_flag", &steady_flag, "multi-GPU: on-device check of a sync-free steady-state step");
     m.def("dist_local", &dist_local,
-          "multi-GPU: unpack + local grid build + owned-point queries from the plan header, one call");
+          "multi-GPU: unpack + local grid build + owned-point queries from the plan header, one call",
+          py::arg("recv"), py::arg("self_rows"), py::arg("recv_own"), py::arg("recv_halo"), py::arg("rank"),
+          py::arg("grid"), py::arg("hdr"), py::arg("k"), py::arg("ppc"), py::arg("deterministic"),
+          py::arg("exact_grid") = 0);
     m.def("route_unpack_split", &route_unpack_split,
           "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");

@@ -35,7 +35,7 @@ import torch
 
 from ..ops import knn_ops as ops
 from .decomposition import SpatialDecomposition, factor3
-from .transport import TorchDistTransport
+from .transport import HostStagedTransport, TorchDistTransport
 
 INF = math.inf
 HDR = 16  # doubles in the device plan header (kn::kPlanHdr, csrc/include/kn/route.h)
@@ -79,6 +79,19 @@ class DistResult:
     neighbors: torch.Tensor  # (n_owned, k) global ids (-1 = empty)
     d2: torch.Tensor         # (n_owned, k) squared distances
     stats: dict
+    # steady-state (sync-free) steps: a device flag, copied to pinned host memory at the end of
+    # the step. Non-zero: the step's routing assumption (previous step's metas and counts) did not
+    # hold on some rank, or some query was not certified -- the rows must not be used.
+    flag: Optional[torch.Tensor] = None
+    event: Optional[object] = None
+
+    def valid(self) -> bool:
+        """True when the rows are final (waits for the step's flag; no-op for synchronous steps)."""
+        if self.flag is None:
+            return True
+        if self.event is not None:
+            self.event.synchronize()
+        return int(self.flag.item()) == 0
 
 
 class DistributedKNearests:
@@ -88,7 +101,7 @@ class DistributedKNearests:
     # tail ~1e-13 per query for +4 % halo points per rank.
     def __init__(self, k: int = 16, group=None, halo_factor: float = 2.5, points_per_cell: float = 0.0,
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
-                 transport=None, device_plan: bool = True):
+                 transport=None, device_plan: bool = True, timeout_s: Optional[float] = None):
         self.k = int(k)
         self.group = group
         self.halo_factor = float(halo_factor)
@@ -96,7 +109,9 @@ class DistributedKNearests:
         self.deterministic = deterministic
         self.max_rounds = max_rounds
         self.native_route = native_route  # None: native router on GPU tensors, torch router on CPU
-        self.comm = transport if transport is not None else TorchDistTransport(group)
+        # timeout_s: failure detection -- a collective that fails or does not complete in time
+        # raises CollectiveError on this rank instead of hanging (transport.py)
+        self.comm = transport if transport is not None else TorchDistTransport(group, timeout_s=timeout_s)
         self.rank = self.comm.rank
         self.world = self.comm.world
         self.device_plan = device_plan  # GPU: plan the routing on the device (1 host sync, not 2)
@@ -110,6 +125,23 @@ class DistributedKNearests:
         # rank's meta changed, the step re-plans with the new metas (one extra round trip).
         self.speculative = True
         self._spec = None  # (metas on device, metas on host (world, 8) f64, grid)
+        # Steady state (no host synchronisation at all): once a full step has been validated, the
+        # next steps assume the same metas and counts, enqueue everything with the known split
+        # sizes, and verify the assumption ON THE DEVICE (own meta and send counts unchanged, no
+        # uncertified query); the per-step flag is all-reduced and copied back asynchronously
+        # (DistResult.valid). A failed assumption costs one re-run of that step the full way.
+        self.steady = True
+        self._steady = None
+        # uncertified queries: forward just those queries to the ranks within their K-th distance
+        # (one targeted round) instead of re-routing everything with a doubled halo
+        self.forward = True
+        # hipGraph replay of the steady step (torch.cuda.CUDAGraph), opt-in: KN_DIST_GRAPH=1 or
+        # graph_steady = True. Replayed rows live in the graph's static buffers until the next
+        # solve. Off by default: back-to-back replays of the captured step at 900K points faulted
+        # once on MI355X (illegal address) while separately synchronised replays and the eager
+        # steady step did not; not yet root-caused.
+        self.graph_steady = None
+        self._graph = None
 
     # ------------------------------------------------------------------ helpers ------
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
@@ -286,35 +318,226 @@ class DistributedKNearests:
                 recv = send[:0]
             # unpack + local build + owned-point queries: one native call (same arithmetic as
             # local_solve with SpatialDecomposition's boxes)
-            pts, gids, idx, d2, counters = C.dist_local(recv, send[x:x + send_counts[rank]], recv_own, recv_halo,
-                                                        rank, list(grid), hv[:HDR], self.k,
-                                                        self.points_per_cell, self.deterministic)
+            pts, gids, idx, d2, counters, *local_grid = C.dist_local(
+                recv, send[x:x + send_counts[rank]], recv_own, recv_halo, rank, list(grid), hv[:HDR], self.k,
+                self.points_per_cell, self.deterministic)
             mark(("local_enqueued", time.perf_counter()))
             n_owned = sum(recv_own)
             if rounds == 1:
                 own_pts, own_ids = pts[:n_owned], gids[:n_owned]
-            flag = counters[1:2]  # uncertified queries (int32)
+            flag = counters[1:2].clone()  # uncertified queries (int32)
             if world > 1:
                 self.comm.all_reduce_max(flag)
             done = int(flag.item()) == 0 or full or rounds >= self.max_rounds  # sync 2
             mark(("flag_synced", time.perf_counter()))
+            n_fwd = 0
+            if not done and self.forward:
+                # targeted second round: only the uncertified queries travel (query forwarding)
+                n_fwd = self._forward_round(hv, grid, pts, gids, idx, d2, counters, local_grid)
+                rounds += 1
+                done = True
             if done:
                 break
             hf *= 2.0
             src_pts, src_ids = own_pts, own_ids
         stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
-                 "grid": tuple(grid)}
+                 "grid": tuple(grid), "forwarded": n_fwd}
+        if rounds == 1 and not full and self.steady:
+            # validated single-round step: the steady-state assumption for the next ones
+            self._steady = {
+                "metas": metas, "grid": tuple(grid), "hdr": hv[:HDR], "cap": int(send.size(0)),
+                "tot": torch.tensor(tot, dtype=torch.int32, device=points.device),
+                "send_counts": send_counts, "recv_own": recv_own, "recv_halo": recv_halo,
+                "cross_send": cross_send, "cross_recv": cross_recv, "x": x,
+                "n": int(points.size(0)), "ids": ids is not None, "stats": dict(stats),
+                # fallback launch sized from the validated step's list (short list: 256 WGs)
+                "exact_grid": 256 if int(counters[0].item()) < 4096 else 0,
+            }
+        else:
+            self._steady = None
         return DistResult(own_ids, idx, d2, stats)
+
+    def _forward_round(self, hv, grid, pts, gids, idx, d2, counters, local_grid) -> int:
+        """Query forwarding for the uncertified queries of a round (targeted second round,
+        replaces re-routing every owned point with a doubled halo). Each uncertified query q
+        with local K-th distance r (an upper bound of the true one: the local set is a subset)
+        goes to every other rank whose box lies within r; that rank answers with the exact K
+        nearest among ITS local points (owned + halo, global-id grid); the origin merges its own
+        K with the answers (deduplicated by global id). Every true neighbour lies within r, so it
+        is owned by a consulted rank and ranks in that rank's own local top K: the merge is
+        exact in one round. Returns the number of forwarded queries (all ranks)."""
+        C = ops.load()
+        world, rank, k = self.world, self.rank, self.k
+        dev = pts.device
+        sorted_, cell_start, geom, perm, uncert, dims_t = local_grid[:6]
+        n_unc = int(counters[1].item())
+        U = uncert[:n_unc].long()
+        q = pts[U]
+        qg = gids[U]
+        r2 = d2[U, k - 1] if n_unc else d2.new_empty(0)
+        lo, hi = tuple(hv[0:3]), tuple(hv[3:6])
+        dec = SpatialDecomposition(world, lo, hi, tuple(grid))
+        # conservative box test: the float32 box arithmetic may not miss a rank
+        r2c = torch.where(torch.isfinite(r2), r2 * (1.0 + 1e-5) + 1e-6, torch.full_like(r2, INF))
+        masks = []
+        for d in range(world):
+            if d == rank:
+                masks.append(torch.zeros(n_unc, dtype=torch.bool, device=dev))
+            else:
+                masks.append(dec.box_dist2(q, d) <= r2c)
+        rows = torch.cat([q, qg.to(torch.int32).view(torch.float32).unsqueeze(1)], 1)
+        send = torch.cat([rows[m] for m in masks]) if n_unc else rows[:0]
+        scount = torch.tensor([int(m.sum()) for m in masks], dtype=torch.int64)
+        rcount = torch.empty_like(scount)
+        cdev = torch.device("cpu") if isinstance(self.comm, HostStagedTransport) or not pts.is_cuda else dev
+        sc_d = scount.to(cdev)
+        rc_d = torch.empty_like(sc_d)
+        self.comm.all_to_all_single(rc_d, sc_d, [1] * world, [1] * world)
+        rcount = rc_d.cpu()
+        recv = self._a2a(send.contiguous(), scount.tolist(), rcount.tolist())
+        # answer the received queries from the local grid
+        if recv.size(0):
+            ridx, rd2 = C.query_external(sorted_, cell_start, geom, dims_t.tolist(), k, recv.contiguous(), perm)
+        else:
+            ridx, rd2 = idx.new_empty((0, k)), d2.new_empty((0, k))
+        back = torch.cat([ridx.view(torch.float32), rd2], 1).contiguous()  # (M, 2k)
+        ans = self._a2a(back, rcount.tolist(), scount.tolist())
+        if n_unc:
+            M = k * world
+            cand_d = torch.full((n_unc, M), INF, device=dev)
+            cand_i = torch.full((n_unc, M), -1, dtype=torch.int32, device=dev)
+            cand_d[:, :k] = d2[U]
+            cand_i[:, :k] = idx[U]
+            off = 0
+            for d in range(world):
+                m = masks[d]
+                c = int(scount[d])
+                if c:
+                    blk = ans[off:off + c]
+                    sel = torch.nonzero(m).flatten()
+                    cand_i[sel, (d + 1 if d < rank else d) * k:(d + 1 if d < rank else d) * k + k] = \
+                        blk[:, :k].contiguous().view(torch.int32)
+                    cand_d[sel, (d + 1 if d < rank else d) * k:(d + 1 if d < rank else d) * k + k] = blk[:, k:]
+                off += c
+            # (d2, id) order; duplicates (a halo copy answered by two ranks) are adjacent
+            key = (cand_d.view(torch.int32).to(torch.int64) << 32) | (cand_i.to(torch.int64) & 0xFFFFFFFF)
+            key = torch.where(cand_i >= 0, key, torch.full_like(key, torch.iinfo(torch.int64).max))
+            key = torch.sort(key, dim=1).values
+            dup = torch.zeros_like(key, dtype=torch.bool)
+            dup[:, 1:] = key[:, 1:] == key[:, :-1]
+            key = torch.where(dup, torch.full_like(key, torch.iinfo(torch.int64).max), key)
+            key = torch.sort(key, dim=1).values[:, :k]
+            empty = key == torch.iinfo(torch.int64).max
+            new_i = torch.where(empty, torch.full_like(key, -1), key & 0xFFFFFFFF).to(torch.int32)
+            new_d = torch.where(empty, torch.full_like(key, 0x7F800000), key >> 32).to(torch.int32).view(torch.float32)
+            idx[U] = new_i
+            d2[U] = new_d
+        tot = torch.tensor([n_unc], dtype=torch.int64, device=cdev)
+        if world > 1:
+            # the sum is only a statistic: max-reduce the per-rank counts' sum through a MAX of one
+            parts = self.comm.all_gather(tot)
+            return int(sum(int(x.item()) for x in parts))
+        return n_unc
+
+    def _steady_body(self, points: torch.Tensor, ids: Optional[torch.Tensor]):
+        """Device work of one steady step (no host synchronisation): -> (owned gids, idx, d2,
+        flag); the flag is already all-reduced."""
+        st = self._steady
+        C = ops.load()
+        world, rank = self.world, self.rank
+        nh = 2 * HDR
+        src_ids = ids.to(torch.int32).contiguous() if ids is not None else None
+        local = C.local_meta(points)
+        plan, sync, bc, send = C.route_begin(points, src_ids, st["metas"], rank, list(st["grid"]), self.k,
+                                             self.halo_factor, st["cap"])
+        totals = sync[nh:nh + 2 * world]
+        x = st["x"]
+        if world > 1:
+            recv = self._a2a(send[:x], st["cross_send"], st["cross_recv"])
+        else:
+            recv = send[:0]
+        sc = st["send_counts"][rank]
+        pts, gids, idx, d2, counters, *_ = C.dist_local(recv, send[x:x + sc], st["recv_own"], st["recv_halo"],
+                                                        rank, list(st["grid"]), st["hdr"], self.k,
+                                                        self.points_per_cell, self.deterministic, st["exact_grid"])
+        flag = C.steady_flag(local, st["metas"], rank, totals, st["tot"], counters)
+        if world > 1:
+            self.comm.all_reduce_max(flag)
+        return gids[:sum(st["recv_own"])], idx, d2, flag
+
+    def _use_graph(self, points: torch.Tensor) -> bool:
+        if not points.is_cuda:
+            return False
+        if self.graph_steady is not None:
+            return bool(self.graph_steady)
+        import os
+
+        return os.environ.get("KN_DIST_GRAPH") == "1" and isinstance(self.comm, TorchDistTransport)
+
+    def _solve_steady(self, points: torch.Tensor, ids: Optional[torch.Tensor]) -> DistResult:
+        """One step with no host synchronisation (see ``self.steady``), replayed from a hipGraph
+        when ``_use_graph``."""
+        st = self._steady
+        if self._use_graph(points):
+            g = self._graph
+            if g is None or g["st"] is not st or g["n"] != points.size(0) or g["ids"] != (ids is not None):
+                sp = points.clone()
+                si = ids.to(torch.int32).contiguous().clone() if ids is not None else None
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    for _ in range(2):  # warm-up: allocator pools, kernel attributes
+                        self._steady_body(sp, si)
+                torch.cuda.current_stream().wait_stream(side)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    out = self._steady_body(sp, si)
+                g = self._graph = {"graph": graph, "pts": sp, "ids": si is not None, "idsb": si, "out": out,
+                                   "st": st, "n": points.size(0)}
+            g["pts"].copy_(points)
+            if ids is not None:
+                g["idsb"].copy_(ids.to(torch.int32))
+            g["graph"].replay()
+            gid, idx, d2, flag = g["out"]
+        else:
+            gid, idx, d2, flag = self._steady_body(points, ids)
+        host = torch.empty(1, dtype=torch.int32, pin_memory=points.is_cuda)
+        host.copy_(flag, non_blocking=True)
+        ev = torch.cuda.Event() if points.is_cuda else None
+        if ev is not None:
+            ev.record()
+        stats = dict(st["stats"])
+        stats["steady"] = True
+        stats["graph"] = self._graph is not None and self._use_graph(points)
+        return DistResult(gid, idx, d2, stats, flag=host, event=ev)
 
     # -------------------------------------------------------------------- solve ------
     def solve(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None,
-              partitioned: bool = False, domain=None) -> DistResult:
+              partitioned: bool = False, domain=None, async_: bool = False) -> DistResult:
         """kNN of the distributed cloud. ``points``: this rank's (N_r, 3) float32 share (any
         distribution; ``partitioned`` is accepted for API compatibility -- points already in
         this rank's box simply route to itself). ``ids``: their global ids (int32); default =
-        rank offset + arange."""
+        rank offset + arange.
+
+        ``async_``: in the steady state (same share sizes and layout as the last validated
+        step) return without any host synchronisation; the caller checks ``result.valid()``
+        before using the rows and re-solves synchronously if it is False. Synchronous calls
+        (the default) do that check themselves."""
         points = points.contiguous().float()
         if domain is None and self._use_native(points) and self.device_plan:
+            # every rank takes the same path: _steady is set and cleared only on collective
+            # outcomes (the all-reduced flags), so it is never decided from local data alone -- a
+            # rank whose share changed still runs the steady step and its on-device check fails
+            if self.steady and self._steady is not None:
+                res = self._solve_steady(points, ids)
+                if async_:
+                    return res
+                if res.valid():
+                    if res.stats.get("graph"):  # graph buffers are reused by the next replay
+                        res = DistResult(res.ids.clone(), res.neighbors.clone(), res.d2.clone(), res.stats)
+                    return res
+                self._steady = None  # assumption failed or a query is uncertified: the full way
+                self._graph = None
             return self._solve_native(points, ids)
         dev = points.device
         lo, hi, counts = self.meta(points)

@@ -20,28 +20,57 @@ import torch
 import torch.distributed as dist
 
 
+class CollectiveError(RuntimeError):
+    """A collective of the distributed engine failed or did not complete within the timeout
+    (a peer rank died or hangs). The process should exit non-zero: the group is unusable."""
+
+
 class TorchDistTransport:
-    def __init__(self, group=None):
+    """``timeout_s``: every collective is issued asynchronously and waited for at most that long
+    (failure detection inside the library, independent of the process group's own timeout).
+    GPU collectives complete on the device stream, so a device-side hang is caught by the
+    group's watchdog (``TORCH_NCCL_ASYNC_ERROR_HANDLING``, on by default) instead; this timeout
+    covers the host side of every collective and all of a CPU (gloo) one."""
+
+    def __init__(self, group=None, timeout_s: Optional[float] = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.timeout_s = timeout_s
+
+    def _run(self, name: str, fn):
+        if self.timeout_s is None:
+            fn(False)
+            return
+        import datetime
+
+        try:
+            work = fn(True)
+            if work is not None and not work.wait(datetime.timedelta(seconds=self.timeout_s)):
+                raise CollectiveError(f"rank {self.rank}: {name} did not complete within {self.timeout_s} s")
+        except CollectiveError:
+            raise
+        except Exception as e:  # noqa: BLE001 - report which collective and rank
+            raise CollectiveError(f"rank {self.rank}: {name} failed: {e}") from e
 
     def all_gather(self, t: torch.Tensor) -> List[torch.Tensor]:
         parts = [torch.empty_like(t) for _ in range(self.world)]
-        dist.all_gather(parts, t, group=self.group)
+        self._run("all_gather", lambda a: dist.all_gather(parts, t, group=self.group, async_op=a))
         return parts
 
     def all_gather_cat(self, t: torch.Tensor) -> torch.Tensor:
         """All ranks' ``t`` concatenated (rank order), left on the device (no host sync)."""
         out = t.new_empty((self.world * t.numel(),))
-        dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=self.group)
+        self._run("all_gather_into_tensor",
+                  lambda a: dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=self.group, async_op=a))
         return out
 
     def all_to_all_single(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None) -> None:
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        self._run("all_to_all_single",
+                  lambda a: dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group, async_op=a))
 
     def all_reduce_max(self, t: torch.Tensor) -> None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        self._run("all_reduce", lambda a: dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group, async_op=a))
 
 
 class HostStagedTransport(TorchDistTransport):

@@ -193,3 +193,52 @@ def test_torch_transport_collectives():
         exp = torch.cat([torch.full((rank + 1, 4), float(10 * s + rank)) for s in range(world)])
         assert torch.equal(torch.from_numpy(recv), exp)
         assert m == max(float(r * 3 % 5) for r in range(world))
+
+
+def _failing_worker(rank, world, port, mode):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import time
+
+    import torch.distributed as dist
+
+    from cuda_knearests_amd.parallel import CollectiveError, DistributedKNearests
+    from cuda_knearests_amd.utils import uniform_cloud
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if rank == 1:
+        if mode == "raise":
+            raise RuntimeError("simulated rank failure before the exchange")
+        time.sleep(120)  # "hang": never joins the collective
+        os._exit(0)
+    dk = DistributedKNearests(k=8, timeout_s=8.0)
+    try:
+        dk.solve(uniform_cloud(2000, 5 + rank))
+    except CollectiveError as e:
+        print(f"rank {rank}: {e}", flush=True)
+        os._exit(3)  # the group is unusable: exit non-zero, no teardown collectives
+    os._exit(0)
+
+
+@pytest.mark.parametrize("mode", ["raise", "hang"])
+def test_dead_peer_fails_fast(mode):
+    """SURVEY §5 failure detection: when a peer rank raises (its process exits) or hangs, the
+    surviving rank's collective fails with CollectiveError within the library timeout and the
+    process exits non-zero instead of blocking forever."""
+    import time
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, mode)) for r in range(world)]
+    t0 = time.time()
+    for p in procs:
+        p.start()
+    procs[0].join(timeout=90)
+    elapsed = time.time() - t0
+    for p in procs[1:]:
+        if p.is_alive():
+            p.kill()
+        p.join(timeout=30)
+    assert procs[0].exitcode == 3, f"rank 0 exit code {procs[0].exitcode}"
+    assert elapsed < 80, f"rank 0 took {elapsed:.0f} s to fail"

@@ -70,11 +70,24 @@ def test_rccl_world1_end_to_end(cuda):
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=cuda)
     try:
         p = uniform_cloud(40000, seed=77, device=cuda)
-        r = DistributedKNearests(k=16).solve(p)
+        dk = DistributedKNearests(k=16)
+        r = dk.solve(p)
         i, d = kn.knn(p, 16)
         assert torch.equal(r.ids.long().cpu(), torch.arange(p.size(0)))
         assert torch.equal(r.d2, d)
         assert torch.equal(r.neighbors, i)
+        # steady state: sync-free steps, same rows bit for bit; new points of the same size run
+        # through the same step and fail its on-device check
+        for _ in range(3):
+            r2 = dk.solve(p, async_=True)
+        assert r2.valid() and r2.stats["steady"]
+        assert torch.equal(r2.d2, d) and torch.equal(r2.neighbors, i)
+        q = uniform_cloud(40000, seed=78, device=cuda) * 0.5
+        r3 = dk.solve(q, async_=True)
+        assert not r3.valid()
+        r4 = dk.solve(q)  # synchronous: re-plans
+        i4, d4 = kn.knn(q, 16)
+        assert torch.equal(r4.d2, d4) and torch.equal(r4.neighbors, i4)
     finally:
         dist.destroy_process_group()
 
@@ -300,3 +313,41 @@ def test_speculative_routing_repeat_and_change(cuda):
     for outs in run_loopback(world, body):
         assert all(eq for eq, _ in outs)
         assert all(cached for _, cached in outs)
+
+
+@pytest.mark.parametrize("world", [1, 4])
+def test_steady_state_async_steps(cuda, world):
+    """After one validated step the solve runs with no host synchronisation (steady state): the
+    rows equal the validated step's bit for bit and the device flag says valid. A step whose
+    points changed (same sizes) fails the on-device check: valid() is False, and a synchronous
+    solve of the same points re-plans and is exact."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+
+    n, k = 24000, 12
+    cloud = uniform_cloud(n, seed=77)
+    moved = cloud.clone()
+    moved[:, 0] = (moved[:, 0] * 0.9 + 37.0)  # same sizes, different geometry (metas change)
+    owner = torch.arange(n) % world
+
+    def body(t):
+        m = owner == t.rank
+        ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
+        dk = DistributedKNearests(k=k, transport=t)
+        r0 = dk.solve(cloud[m].contiguous().to(cuda), ids)
+        r1 = dk.solve(cloud[m].contiguous().to(cuda), ids, async_=True)
+        ok1 = r1.valid()
+        r2 = dk.solve(moved[m].contiguous().to(cuda), ids, async_=True)
+        ok2 = r2.valid()
+        r3 = dk.solve(moved[m].contiguous().to(cuda), ids)
+        return (r0.ids.cpu(), r0.neighbors.cpu(), r0.d2.cpu(), r1.ids.cpu(), r1.neighbors.cpu(), r1.d2.cpu(),
+                bool(r1.stats.get("steady")), ok1, ok2, r3.ids.cpu(), r3.neighbors.cpu(), r3.d2.cpu())
+
+    out = run_loopback(world, body)
+    _, od = kn.knn_cpu(moved, k, "kdtree")
+    for (i0, n0, d0, i1, n1, d1, steady, ok1, ok2, i3, n3, d3) in out:
+        assert steady and ok1 and not ok2
+        assert torch.equal(i0, i1) and torch.equal(n0, n1) and torch.equal(d0, d1)
+        ids = i3.long()
+        assert torch.equal(d3, od[ids])
+        assert_knn_exact(moved, ids, n3, d3, od[ids])
