@@ -139,6 +139,22 @@ kn_problem *kn_load(const char *path, const kn_config *cfg);
 kn_float3 *kn_read_xyz(const char *path, int *n, int normalize);
 kn_status kn_write_xyz(const char *path, const kn_float3 *pts, int n);
 
+/* ---- multi-GPU in one process (extension; the reference is single-GPU) --------------- */
+/* The cloud is split over `ndevices` ranks (devices[i] = HIP device of rank i; NULL: 0..n-1;
+ * repeated devices = virtual ranks on one GPU). A solve routes every point to the owner of
+ * its box of a px*py*pz spatial split plus halo copies to the neighbouring boxes, in one
+ * exchange (RCCL ncclSend/ncclRecv over one communicator per device when the devices are
+ * distinct, device copies otherwise), then every rank solves its owned points with the
+ * single-GPU kernels and certifies them against its halo (uncertified -> wider halo). */
+typedef struct kn_multi kn_multi;
+kn_multi *kn_prepare_multi(const kn_float3 *points, int numpoints, const int *devices, int ndevices,
+                           const kn_config *cfg);
+kn_status kn_solve_multi(kn_multi *m);
+unsigned int *kn_get_neighbors_multi(kn_multi *m);  /* N x K original ids, row = original index */
+float *kn_get_distances_multi(kn_multi *m);         /* N x K squared distances */
+kn_status kn_get_multi_info(kn_multi *m, int *ranks, int *rounds, int *halo_points, int *uses_rccl);
+void kn_free_multi(kn_multi **m);
+
 /* ABI self-check for bindings (ctypes, other languages): sizeof of the public structs as
  * compiled into the library. which: 0 kn_config, 1 kn_problem, 2 kn_stats. */
 size_t kn_struct_size(int which);

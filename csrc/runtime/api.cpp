@@ -53,6 +53,8 @@ kn::EngineConfig to_engine(const kn_config* c) {
 
 extern "C" {
 
+void kn_set_last_error_internal(const char* msg) { g_err = msg ? msg : ""; }
+
 kn_config kn_default_config(void) {
     kn_config c;
     std::memset(&c, 0, sizeof(c));

@@ -31,6 +31,8 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 KERNELS = ["kernels/build.hip", "kernels/query.hip", "kernels/route.hip"]
 HOST = ["host/host.cpp"]
 RUNTIME = ["runtime/engine.cpp", "runtime/api.cpp"]
+MULTI = "runtime/multi.cpp"  # C-API multi-GPU runtime: libknearests.so only (links RCCL)
+RCCL_OK = os.path.exists(os.path.join(ROCM, "include", "rccl", "rccl.h"))
 
 CXX = os.environ.get("CXX", "g++")
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-D__HIP_PLATFORM_AMD__=1"]
@@ -112,10 +114,12 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
         futs[ex.submit(_compile, "torch/bindings.cpp", HOSTFLAGS + chk_tflags +
                        ["-Wno-unused-function", "-DTORCH_EXTENSION_NAME=_C_checked", "-DKN_CHECKED=1"],
                        "torchchk", force)] = ("torchchk", "bindings")
+        futs[ex.submit(_compile, MULTI, HOSTFLAGS + (["-DKN_HAVE_RCCL=1"] if RCCL_OK else []), "rt", force)] = \
+            ("multi", MULTI)
         futs[ex.submit(_compile, "tools/knn_cli.cpp", HOSTFLAGS, "tool", force)] = ("tool", "cli")
         futs[ex.submit(_compile, "tools/knn_unit.cpp", HOSTFLAGS, "tool", force)] = ("tool", "unit")
         objs: dict[str, list[Path]] = {"kern": [], "kernchk": [], "host": [], "rt": [], "torch": [],
-                                       "torchchk": [], "tool": []}
+                                       "torchchk": [], "tool": [], "multi": []}
         tools: dict[str, Path] = {}
         for f in cf.as_completed(futs):
             kind, name = futs[f]
@@ -130,7 +134,8 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
     libdir.mkdir(exist_ok=True)
     lib = libdir / "libknearests.so"
     hiplink = [f"--offload-arch={ARCH}", "-fopenmp", f"-L{ROCM}/lib", "-lamdhip64"]
-    _run([HIPCC, "-shared", "-o", str(lib)] + [str(o) for o in kern + host + rt] + hiplink)
+    _run([HIPCC, "-shared", "-o", str(lib)] + [str(o) for o in kern + host + rt + objs["multi"]] + hiplink +
+         (["-lrccl", f"-Wl,-rpath,{ROCM}/lib"] if RCCL_OK else []))
     cext = PKG / f"_C{ext}"
     _run([HIPCC, "-shared", "-o", str(cext)] + [str(o) for o in kern + host + rt + objs["torch"]] + hiplink + tld)
     cchk = PKG / f"_C_checked{ext}"

@@ -134,3 +134,58 @@ def test_capi_reference_flow():
     q = torch.from_numpy(pts)
     d = ((q[torch.from_numpy(nb.astype(np.int64))] - q[:, None, :]) ** 2).sum(-1)
     assert torch.allclose(d, od, rtol=1e-5, atol=1e-3)
+
+
+def _multi_lib():
+    lib = _lib()
+    lib.kn_prepare_multi.restype = C.c_void_p
+    lib.kn_prepare_multi.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.c_int, C.POINTER(KnConfig)]
+    lib.kn_solve_multi.argtypes = [C.c_void_p]
+    lib.kn_get_neighbors_multi.restype = C.POINTER(C.c_uint)
+    lib.kn_get_neighbors_multi.argtypes = [C.c_void_p]
+    lib.kn_get_distances_multi.restype = C.POINTER(C.c_float)
+    lib.kn_get_distances_multi.argtypes = [C.c_void_p]
+    lib.kn_get_multi_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 4
+    lib.kn_free_multi.argtypes = [C.POINTER(C.c_void_p)]
+    return lib
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0], [0] * 8])
+def test_capi_multi_device(devices):
+    """kn_prepare_multi / kn_solve_multi: one process, one rank per entry of `devices` (RCCL
+    ncclSend/ncclRecv for distinct devices, device copies for virtual ranks on one GPU);
+    original-order rows equal the kd-tree oracle."""
+    import torch
+
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.utils.check import assert_knn_exact
+
+    lib = _multi_lib()
+    libc = C.CDLL(None)
+    n, k = 40000, 12
+    rng = np.random.default_rng(len(devices))
+    pts = (rng.random((n, 3), dtype=np.float32) * 1000).astype(np.float32)
+    cfg = lib.kn_default_config()
+    cfg.k = k
+    devs = (C.c_int * len(devices))(*devices)
+    m = lib.kn_prepare_multi(pts.ctypes.data, n, devs, len(devices), C.byref(cfg))
+    assert m, lib.kn_last_error()
+    assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
+    info = [C.c_int(0) for _ in range(4)]
+    lib.kn_get_multi_info(m, *[C.byref(x) for x in info])
+    ranks, rounds, halo, rccl = (x.value for x in info)
+    assert ranks == len(devices) and rounds >= 1
+    assert rccl == (1 if len(set(devices)) == len(devices) else 0)
+    gi, gd = lib.kn_get_neighbors_multi(m), lib.kn_get_distances_multi(m)
+    idx = np.ctypeslib.as_array(gi, shape=(n * k,)).reshape(n, k).astype(np.int64).copy()
+    d2 = np.ctypeslib.as_array(gd, shape=(n * k,)).reshape(n, k).copy()
+    libc.free(gi)
+    libc.free(gd)
+    h = C.c_void_p(m)
+    lib.kn_free_multi(C.byref(h))
+    assert not h.value
+    cloud = torch.from_numpy(pts)
+    _, od = kn.knn_cpu(cloud, k, "kdtree")
+    assert torch.equal(torch.from_numpy(d2), od)
+    assert_knn_exact(cloud, torch.arange(n), torch.from_numpy(idx), torch.from_numpy(d2), od)
