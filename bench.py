@@ -101,7 +101,8 @@ def run_native(args) -> dict:
     dev = torch.device("cuda", 0)
     pts = make_cloud(args, dev)
     args.n = pts.size(0)
-    e = C.Engine(args.k, deterministic=args.deterministic, adaptive=not args.fixed_grid)
+    e = C.Engine(args.k, deterministic=args.deterministic, adaptive=not args.fixed_grid,
+                 algo={"auto": 0, "grid": 1, "tree": 2}[args.algo])
     log("native eager prepare+solve")
     e.prepare(pts)
     e.solve()
@@ -128,7 +129,7 @@ def run_native(args) -> dict:
         sts.append(i["ms_solve"])
     bts.sort(), sts.sort()
     return {"t": dt, "ms_build": bts[2], "ms_solve": sts[2], "info": {"exact_path": cnt[0], "uncertified": cnt[1]},
-            "check": chk, "n_total": args.n, "dims": info0.get("dims")}
+            "check": chk, "n_total": args.n, "dims": info0.get("dims"), "algo": info0.get("algo")}
 
 
 def run_single(args) -> dict:
@@ -373,6 +374,9 @@ def main() -> int:
     ap.add_argument("--xyz", default="", help="read points from a reference-format .xyz file instead")
     ap.add_argument("--fixed-grid", action="store_true",
                     help="1 GPU: no occupancy refinement of the grid (the reference's fixed 3.1 pts/cell)")
+    ap.add_argument("--algo", choices=["auto", "grid", "tree"], default="auto",
+                    help="1 GPU native: query structure (auto: the Morton-leaf tree when the adaptive grid "
+                         "had to be refined, i.e. clustered / surface clouds)")
     ap.add_argument("--loopback", type=int, default=0,
                     help="W virtual ranks on one GPU (multi-rank algorithm at W x n points)")
     ap.add_argument("--cpu-oracle", action="store_true", help="time the CPU kd-tree path (BASELINE config 1)")
@@ -419,7 +423,7 @@ def main() -> int:
         r = run_native(args) if args.path == "native" else run_single(args)
         n_gpus = 1
         extra = {"ms_build": round(r["ms_build"], 4), "ms_solve": round(r["ms_solve"], 4),
-                 "grid": r.get("dims"),
+                 "grid": r.get("dims"), "query_algo": r.get("algo", "grid"),
                  "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph, "path": args.path}
     ms = r["t"] / args.steps * 1e3
     qps = r["n_total"] * args.steps / r["t"]

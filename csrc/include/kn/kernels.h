@@ -88,6 +88,12 @@ struct BinPlan {
 };
 bool bin_plan(int n, int num_cells, BinPlan* out);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t stream);
+// The deterministic in-cell order (by original index) of launch_build, alone (rank of each point
+// in its cell, O(N x mean cell occupancy) parallel work; tmp: N float4 scratch). The occupancy-
+// adaptive build bins its probe grids without it (a clustered cloud's first grid has cells of
+// thousands of points) and orders the final grid once.
+hipError_t launch_cell_sort(const int* cell_start, const GridGeom* geom, int n, float4* sorted, unsigned* perm,
+                            float4* tmp, hipStream_t stream);
 
 struct QueryBuffers {
     const float4* sorted;

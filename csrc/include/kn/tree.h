@@ -1,0 +1,83 @@
+// kn/tree.h -- Morton-leaf tree kNN path (csrc/kernels/tree.hip).
+//
+// The uniform grid (kn/kernels.h) is the fastest structure for near-uniform clouds, but one cell
+// size cannot serve a cloud whose density varies by 10^4 (Gaussian clusters over a sparse
+// background, scans): dense cells hold hundreds of points, sparse queries need many rings, tiles
+// overflow the LDS budget. The tree path adapts to any density:
+//
+//   build:  30-bit Morton code of every point (cubic quantisation of the grid's domain) ->
+//           radix sort (hipCUB) -> points gathered into Morton order -> leaves of <= 64
+//           consecutive points (one wave), cut at the curve's large jumps -> leaf boxes (wave DPP
+//           reductions) -> implicit complete binary tree of boxes over the leaves (heap index,
+//           root 1, leaf l = node P + l), reduced bottom-up 6 levels per launch in LDS.
+//   query:  one wave per leaf, lanes = the leaf's 64 points. Wave-uniform near-first traversal
+//           (a node is entered when ANY lane's box distance is within its own K-th bound);
+//           every visited leaf is staged once in the wave's LDS slice and streamed to all
+//           lanes (broadcast reads) into the same packed-key / v_med3_u32 register top-K as the
+//           grid kernels, key slot = (visit index, point in leaf). Exact re-rank of the kept
+//           slots by (d2, id) and certification against the truncation floor; uncertified
+//           queries (near-ties, > 64 visited leaves) go to a list finished by a wave-per-query
+//           exact traversal with threshold compaction (same semantics as the grid's exact
+//           kernel, so results are identical to the oracle's).
+//
+// Output format is that of launch_query: row = the point's original index (w field), ids are
+// original indices (or id_map[...]).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stddef.h>
+
+#include "kn/kernels.h"
+
+namespace kn {
+
+constexpr int kTreeLeaf = 64;
+
+// A tree: one workspace (carved by tree_view) plus a node buffer sized from the leaf count.
+struct TreeView {
+    float4* pts;          // n points in Morton order {x, y, z, w} (w copied from the input)
+    unsigned* leaf_start; // L + 1 leaf boundaries (<= 64 points per leaf)
+    unsigned* seg_start;  // scratch: segment boundaries between forced cuts
+    unsigned* list;       // n: tree positions of queries for the exact finish
+    float* thr;           // n: their distance bound
+    unsigned* flag;       // n scratch
+    unsigned* incl;       // n scratch
+    unsigned* codes;      // 2n Morton codes (sort double buffer)
+    unsigned* vals;       // 2n source indices
+    unsigned* info;       // [0] = L after launch_tree_leaves (device)
+    void* sort_temp;      // hipCUB temp storage (sort / scan)
+    size_t sort_temp_bytes;
+    float4* nlo;          // 2P node boxes (lower corner; heap index, root 1, leaf l = node P + l)
+    float4* nhi;          // 2P upper corners; empty padded leaves: lo = +inf, hi = -inf
+    float4* slo;          // 4L sub-boxes: points [16 r, 16 r + 16) of leaf l at 4 l + r
+    float4* shi;
+    int n, L, P;          // points, leaves, P = next power of two >= L
+};
+
+size_t tree_workspace_bytes(int n);
+TreeView tree_view(void* ws, int n);
+// Phase 1 (stream-ordered): Morton codes of `in` (n points {x, y, z, w}, typically the grid's
+// sorted array) over the grid's domain, sort, gather, leaf boundaries; the leaf count lands in
+// t.info[0]. The caller reads it (one host sync) to size the node buffer.
+hipError_t launch_tree_leaves(const float4* in, const GridGeom* geom, const TreeView& t, hipStream_t s);
+size_t tree_node_bytes(int L);
+void tree_attach_nodes(TreeView& t, void* nodes, int L);
+// Phase 2: leaf boxes and the implicit tree's node boxes.
+hipError_t launch_tree_nodes(const TreeView& t, hipStream_t s);
+
+struct TreeQuery {
+    int k;
+    int n_queries;            // points whose w < n_queries are queries
+    const unsigned* id_map;   // optional output id map (as QueryBuffers::id_map)
+    unsigned* out_idx;        // n_queries x k, row = original index
+    float* out_dist;          // optional
+    unsigned* counters;       // kNumCounters words: [0] exact-finish queries, [2] waves over the
+                              // visit cap, [3] queries whose re-rank stayed unsorted, [4] queries
+                              // whose K-th is not below the truncation floor, [5] leaves
+                              // visited, [6] insertion networks (checked builds), [7] waves
+    int flags;                // 1: every query takes the exact finish (tests)
+};
+hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t s);
+hipError_t debug_words_tree(unsigned out[4], bool reset);
+
+}  // namespace kn

@@ -62,6 +62,8 @@ typedef struct {
     int verbose;             /* 0 silent, 1 timings (reference IF_VERBOSE), 2 debug        */
     int exact_only;          /* 1 -> skip the LDS tile kernel (exact ring walk for all)      */
     int fixed_grid;          /* 1 -> no occupancy refinement of the grid (clusters/surfaces) */
+    int algo;                /* query structure: 0 auto (the Morton-leaf tree when the
+                                occupancy-adaptive grid had to be refined), 1 grid, 2 tree    */
 } kn_config;
 
 /* Per-solve statistics (reference kn_print_stats + cell_max, knearests.cu:378-466). */

@@ -257,6 +257,35 @@ __global__ __launch_bounds__(256) void cell_sort_kernel(const int* __restrict__ 
     }
 }
 
+// Deterministic in-cell order without a per-cell serial sort: every point counts the points of
+// its cell with a smaller original index (its rank) and moves to cell start + rank in `tmp`; a
+// copy pass writes the result back. O(sum over cells of count^2) = O(N x mean occupancy of a
+// point's cell) work, all of it parallel (the one-thread-per-cell insertion sort is serial in the
+// largest cell: 0.58 ms on a clustered cloud's 216-point cells).
+__global__ __launch_bounds__(256) void cell_rank_kernel(const float4* __restrict__ sorted, const int* __restrict__ cell_start,
+                                                        const GridGeom* __restrict__ gp, int n, float4* __restrict__ tmp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GridGeom g = *gp;
+    const float4 v = sorted[i];
+    const float p[3] = {v.x, v.y, v.z};
+    const int c = cell_of(g, p);
+    const int a = cell_start[c], b = cell_start[c + 1];
+    const unsigned key = __float_as_uint(v.w);
+    int r = 0;
+    for (int j = a; j < b; ++j) r += __float_as_uint(sorted[j].w) < key ? 1 : 0;
+    tmp[KN_IDX(a + r, n, 108)] = v;
+}
+
+__global__ void cell_copy_kernel(const float4* __restrict__ tmp, int n, float4* __restrict__ sorted,
+                                 unsigned* __restrict__ perm) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 v = tmp[i];
+    sorted[i] = v;
+    perm[i] = __float_as_uint(v.w);
+}
+
 __global__ __launch_bounds__(256) void cell_occupancy_kernel(const int* __restrict__ cell_start, int num_cells,
                                                              unsigned long long* __restrict__ out) {
     unsigned long long acc = 0;
@@ -438,6 +467,14 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
     }
 }
 
+hipError_t launch_cell_sort(const int* cell_start, const GridGeom* geom, int n, float4* sorted, unsigned* perm,
+                            float4* tmp, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    cell_rank_kernel<<<cdiv(n, 256), 256, 0, s>>>(sorted, cell_start, geom, n, tmp);
+    cell_copy_kernel<<<cdiv(n, 256), 256, 0, s>>>(tmp, n, sorted, perm);
+    return hipGetLastError();
+}
+
 bool bin_plan(int n, int num_cells, BinPlan* out) {
     if (n <= 0 || num_cells <= 0) return false;
     const int nblocks = std::max(1, std::min((int)cdiv((size_t)n, 4096), 1024));
@@ -482,8 +519,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         bucket_sort_kernel<<<bp.nbuckets, 256, (1u << bp.shift) * sizeof(int), s>>>(
             b.bin_tmp, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, b.cell_scan, b.block_sums, C, b.cell_start,
             b.sorted, b.perm);
-        if (b.deterministic)
-            cell_sort_kernel<<<cdiv(C, 256), 256, 0, s>>>(b.cell_start, C, b.sorted, b.perm);
+        if (b.deterministic) return launch_cell_sort(b.cell_start, b.geom, n, b.sorted, b.perm, b.bin_tmp, s);
         return hipGetLastError();
     }
     // global-atomic binning (fallback)

@@ -43,6 +43,7 @@
 #include <type_traits>
 
 #include "kn/kernels.h"
+#include "kn/knn_device.h"
 #include "kn/wave.h"
 
 namespace kn {
@@ -109,128 +110,8 @@ constexpr int kQueryForceRescan = 1;
 constexpr int kQueryAlgoStream = 2;
 constexpr int kQueryAlgoTile = 4;
 constexpr int kQueryAlgoLane = 8;
-#if defined(KN_CHECKED) && KN_CHECKED
-constexpr bool kStats = true;
-#else
-constexpr bool kStats = false;
-#endif
 
-__device__ __forceinline__ float complete_margin(const CompleteBox& cb, float q, int a) {
-    return fminf(q - cb.lo[a], cb.hi[a] - q);
-}
-
-__device__ __forceinline__ bool pair_less(float da, unsigned ia, float db, unsigned ib) {
-    return da < db || (da == db && ia < ib);
-}
-
-// The w field of a stored point. Default mode: its original (local) index -- queries are the
-// indices < n_queries, the output row is that index, and the output id is id_map[index].
-// Global-id mode (row_of != nullptr, multi-GPU ranks): w already holds the point's GLOBAL id,
-// with kHaloBit set on halo (non-query) points, and row_of[stored index] gives a query's output
-// row. The output ids then need no gather through id_map: at 12.5M points per rank that
-// random gather (K per query from a 50 MB table) cost more than the whole lane-walk search.
-constexpr unsigned kHaloBit = 0x80000000u;
-template <class A>
-__device__ __forceinline__ bool w_live(const A& a, unsigned w) {
-    return a.row_of ? !(w & kHaloBit) : (int)w < a.n_queries;
-}
-template <class A>
-__device__ __forceinline__ unsigned w_id(const A& a, unsigned w) { return a.row_of ? (w & ~kHaloBit) : w; }
-template <class A>
-__device__ __forceinline__ unsigned w_row(const A& a, unsigned w, unsigned sidx) {
-    return a.row_of ? a.row_of[KN_IDX(sidx, (unsigned)a.n, 231)] : w;
-}
-template <class A>
-__device__ __forceinline__ unsigned out_id(const A& a, unsigned id) {
-    return (a.row_of || !a.id_map) ? id : a.id_map[KN_IDX(id, (unsigned)a.n, 232)];
-}
-
-// Bijective XCD-aware remap: consecutive tiles (which share halo cells) land on one XCD's L2.
-__device__ __forceinline__ int xcd_remap(int b, int nblocks) {
-    const int xcd = b & 7, idx = b >> 3;
-    const int q = nblocks >> 3, r = nblocks & 7;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-}
-
-__device__ __forceinline__ unsigned long long pack_key64(float d, unsigned id) {
-    return ((unsigned long long)__float_as_uint(d) << 32) | id;
-}
-
-// Ascending bitonic sort of E*64 64-bit keys held E per lane (element index e*64 + lane):
-// cross-lane stages exchange through ds_bpermute (__shfl_xor), the stride-64 stage of E = 2
-// compares a lane's two elements.
-template <int E>
-__device__ __forceinline__ void wave_bitonic_sort_u64(unsigned long long (&v)[E], int lane) {
-    constexpr int N = 64 * E;
-#pragma clang loop unroll(full)
-    for (int size = 2; size <= N; size <<= 1) {
-#pragma clang loop unroll(full)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            if (stride >= 64) {
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int f = e ^ (stride >> 6);
-                    if (e < f) {
-                        const bool up = (((e << 6) | lane) & size) == 0;
-                        const unsigned long long mn = v[e] < v[f] ? v[e] : v[f], mx = v[e] < v[f] ? v[f] : v[e];
-                        v[e] = up ? mn : mx;
-                        v[f] = up ? mx : mn;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const unsigned lo = (unsigned)__shfl_xor((int)(unsigned)v[e], stride, 64);
-                    const unsigned hi = (unsigned)__shfl_xor((int)(unsigned)(v[e] >> 32), stride, 64);
-                    const unsigned long long o = ((unsigned long long)hi << 32) | lo;
-                    const bool up = (((e << 6) | lane) & size) == 0;
-                    const bool lower = (lane & stride) == 0;
-                    const unsigned long long mn = v[e] < o ? v[e] : o, mx = v[e] < o ? o : v[e];
-                    v[e] = (up == lower) ? mn : mx;
-                }
-            }
-        }
-    }
-}
-
-// Packed 32-bit key of one candidate: squared-distance float bits with the low SB mantissa
-// bits replaced by the candidate's LDS slot (one v_bfi_b32).
-__device__ __forceinline__ unsigned cand_key(const float4& p, float qx, float qy, float qz, unsigned himask,
-                                             int s, int /*qslot*/) {
-    const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
-    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-    unsigned key;
-    // VOP3 reads at most one SGPR on gfx9: keep the (loop-invariant) mask in a VGPR
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(key) : "v"(himask), "v"(__float_as_uint(d2)), "s"((unsigned)s));
-    return key;
-}
-
-// cand_key with a per-lane (VGPR) slot: the lane-walk variant's candidates differ per lane.
-__device__ __forceinline__ unsigned cand_key_v(const float4& p, float qx, float qy, float qz, unsigned himask,
-                                               int s) {
-    const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
-    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-    unsigned key;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(key) : "v"(himask), "v"(__float_as_uint(d2)), "v"((unsigned)s));
-    return key;
-}
-
-// Sorted-array insertion of `key` into keys[0..KM) (ascending), dropping the largest:
-// new[j] = med3(old[j-1], key, old[j]) -- one v_med3_u32 per slot, all independent. Skipped
-// (uniform branch) when no lane of the wave improves; a non-improving key is a no-op anyway.
-#ifndef KN_BRANCHFREE_INSERT
-#define KN_BRANCHFREE_INSERT 0
-#endif
-template <int KM>
-__device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key) {
-    if (KN_BRANCHFREE_INSERT || __builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
-#pragma unroll
-        for (int j = KM - 1; j > 0; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
-        keys[0] = min(keys[0], key);
-        return 1u;
-    }
-    return 0u;
-}
+// Shared device helpers (key packing, med3 top-K insertion, id modes, wave sort): kn/knn_device.h
 
 // LANE = false: wave-uniform candidate stream over the union of the chunk's needs (LDS
 // broadcast reads). LANE = true ("lane walk"): each lane walks ITS OWN rows of the staged
@@ -1390,16 +1271,6 @@ struct ExactArgs {
     const float4* ext;         // external queries {x, y, z, bits(global id)} (nullptr: stored points)
     int n_ext;
 };
-
-// Wave-wide sum (DPP within rows of 16, then the 4 row totals).
-__device__ __forceinline__ unsigned wave_sum_u32(unsigned x) {
-    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false);
-    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false);
-    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false);
-    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, KN_DPP_ROW_MIRROR, 0xF, 0xF, false);
-    return (unsigned)__builtin_amdgcn_readlane((int)x, 0) + (unsigned)__builtin_amdgcn_readlane((int)x, 16) +
-           (unsigned)__builtin_amdgcn_readlane((int)x, 32) + (unsigned)__builtin_amdgcn_readlane((int)x, 48);
-}
 
 // ---- wave-per-query exact kernel: threshold compaction + wave bitonic sort (any K <= 128) ----
 // One wave serves one query of the fallback list (or every query without tiles). It walks the

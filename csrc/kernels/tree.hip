@@ -1,0 +1,633 @@
+// tree.hip -- Morton-leaf tree kNN for strongly non-uniform clouds (design: kn/tree.h).
+//
+// Reference: knearests.cu:93-148 walks a uniform grid whose cell size is fixed by the point count
+// (knearests.cu:249); its README scopes it to uniformly distributed points. The grid path of this
+// framework (query.hip) keeps that structure for uniform clouds; this file is the density-
+// adaptive path: an implicit box tree over 64-point Morton leaves, traversed one wave per leaf.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <hipcub/hipcub.hpp>
+
+#include "kn/knn_device.h"
+#include "kn/tree.h"
+#include "kn/wave.h"
+
+namespace kn {
+
+namespace {
+
+constexpr unsigned SENT = 0xFFFFFFFFu;
+constexpr int kVisitBits = 7;                 // key slot = visit index (7 bits) | point in leaf (6 bits)
+constexpr int kMaxVisit = 1 << kVisitBits;    // leaves a wave may visit before its queries go exact
+constexpr unsigned kMask = (1u << (kVisitBits + 6)) - 1u;
+constexpr int kStack = 64;                    // traversal stack (depth <= log2(P) + 1)
+constexpr int kTCap = 256;                    // exact-finish candidate buffer per wave (u64 keys)
+constexpr int kSortPasses = 3;                // odd-even passes of the exact re-rank (then checked)
+// A point inside a box can compute a squared distance a few ulps below the box's: nodes are
+// pruned only when the box distance exceeds the bound by more than that.
+constexpr float kShrink = 0.99999f;
+constexpr int kExactGrid = 512;
+
+struct TArgs {
+    const float4* pts;
+    const unsigned* leaf_start;  // L + 1
+    const float4* nlo;
+    const float4* nhi;
+    const float4* slo;  // 4 sub-boxes per leaf (points [16 r, 16 r + 16) of the leaf)
+    const float4* shi;
+    unsigned* list;
+    float* thr;
+    int n, L, P;
+    int k;
+    int n_queries;
+    const unsigned* id_map;
+    const unsigned* row_of;  // always null: local mode of w_live / w_id / w_row / out_id
+    unsigned* out_idx;
+    float* out_dist;
+    unsigned* counters;
+    int flags;
+};
+
+__device__ __forceinline__ unsigned ordf(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unordf(unsigned u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+// 10 bits -> every third bit of 30
+__device__ __forceinline__ unsigned spread10(unsigned v) {
+    v &= 0x3FFu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__device__ __forceinline__ float box_d2(float qx, float qy, float qz, const float4& lo, const float4& hi) {
+    const float dx = fmaxf(fmaxf(lo.x - qx, qx - hi.x), 0.f);
+    const float dy = fmaxf(fmaxf(lo.y - qy, qy - hi.y), 0.f);
+    const float dz = fmaxf(fmaxf(lo.z - qz, qz - hi.z), 0.f);
+    return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+}
+
+// Cubic quantisation of the grid's domain to 1024 steps per axis (cells of a finer level stay
+// cubes, so the implicit octree's boxes are balanced).
+__global__ void morton_kernel(const float4* __restrict__ in, int n, const GridGeom* __restrict__ geom,
+                              unsigned* __restrict__ codes, unsigned* __restrict__ vals) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GridGeom g = *geom;
+    const float ext = fmaxf(fmaxf(g.cell[0] * g.dims[0], g.cell[1] * g.dims[1]), g.cell[2] * g.dims[2]);
+    const float s = ext > 0.f ? 1024.f / ext : 0.f;
+    const float4 p = in[i];
+    const int qx = clampi((int)((p.x - g.origin[0]) * s), 0, 1023);
+    const int qy = clampi((int)((p.y - g.origin[1]) * s), 0, 1023);
+    const int qz = clampi((int)((p.z - g.origin[2]) * s), 0, 1023);
+    codes[i] = spread10(qx) | (spread10(qy) << 1) | (spread10(qz) << 2);
+    vals[i] = (unsigned)i;
+}
+
+__global__ void gather_kernel(const float4* __restrict__ in, const unsigned* __restrict__ src, int n,
+                              float4* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[src[i]];
+}
+
+// Leaf boundaries. Fixed 64-point runs of the Morton order straddle the curve's jumps: a run that
+// crosses the boundary of a large octree node holds points from two far-apart corners and gets a
+// huge box (every wave nearby then visits it, and its own queries need two regions). A cut is
+// forced at b when the jump between b-1 and b (highest differing code bit) is 2+ octree levels
+// coarser than the local spacing on both sides (the jumps across 8 points before and after);
+// segments between cuts are split into ceil(len / 64) near-equal leaves.
+__device__ __forceinline__ int hibit(unsigned x) { return x ? 31 - __builtin_clz(x) : -1; }
+
+__global__ void cut_kernel(const unsigned* __restrict__ c, int n, unsigned* __restrict__ flag) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    unsigned f = 1u;
+    if (b > 0) {
+        const int jump = hibit(c[b - 1] ^ c[b]);
+        const int ja = b >= 8 ? hibit(c[b - 8] ^ c[b - 1]) : -1;
+        const int jb = b + 8 <= n ? hibit(c[b] ^ c[b + 7]) : -1;
+        f = (jump >= 0 && jump >= max(ja, jb) + 6) ? 1u : 0u;
+    }
+    flag[b] = f;
+}
+
+// incl = inclusive scan of flag: segment (or leaf) id of b = incl[b] - 1; starts[id] = b at flagged
+// positions, starts[count] = n, count -> *total
+__global__ void starts_kernel(const unsigned* __restrict__ flag, const unsigned* __restrict__ incl, int n,
+                              unsigned* __restrict__ starts, unsigned* __restrict__ total) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    if (flag[b]) starts[incl[b] - 1] = (unsigned)b;
+    if (b == n - 1) {
+        starts[incl[b]] = (unsigned)n;
+        if (total) *total = incl[b];
+    }
+}
+
+// flag[b] = b starts a leaf: segment [s, e) splits at s + floor(j len / c), c = ceil(len / 64)
+__global__ void leaf_flag_kernel(const unsigned* __restrict__ incl, const unsigned* __restrict__ seg_start, int n,
+                                 unsigned* __restrict__ flag) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    const unsigned sg = incl[b] - 1;
+    const unsigned long long s0 = seg_start[sg], len = seg_start[sg + 1] - s0;
+    const unsigned long long c = (len + kTreeLeaf - 1) / kTreeLeaf, o = (unsigned long long)b - s0;
+    const unsigned long long j = (o * c + len - 1) / len;
+    flag[b] = (j * len / c == o) ? 1u : 0u;
+}
+
+// 16-lane row reduction (every lane of the row gets the row's result)
+__device__ __forceinline__ unsigned row_min_u32(unsigned x) {
+    x = kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false));
+    x = kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false));
+    x = kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false));
+    return kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_MIRROR, 0xF, 0xF, false));
+}
+__device__ __forceinline__ unsigned row_max_u32(unsigned x) {
+    x = kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false));
+    x = kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false));
+    x = kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false));
+    return kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_MIRROR, 0xF, 0xF, false));
+}
+
+// One wave per leaf (P leaves: the padded ones get empty boxes): the leaf box (node P + leaf) and
+// its 4 sub-boxes of 16 points (empty sub-groups: empty boxes).
+__global__ __launch_bounds__(256) void leaf_box_kernel(const float4* __restrict__ pts, const unsigned* __restrict__ leaf_start,
+                                                       int L, int P, float4* __restrict__ nlo, float4* __restrict__ nhi,
+                                                       float4* __restrict__ slo, float4* __restrict__ shi) {
+    const int leaf = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (leaf >= P) return;
+    if (leaf >= L) {
+        if (lane == 0) {
+            nlo[P + leaf] = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+            nhi[P + leaf] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        }
+        return;
+    }
+    const unsigned i = leaf_start[leaf] + lane;
+    const bool v = i < leaf_start[leaf + 1];
+    const float4 p = v ? pts[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const unsigned ox = v ? ordf(p.x) : SENT, oy = v ? ordf(p.y) : SENT, oz = v ? ordf(p.z) : SENT;
+    const unsigned px = v ? ordf(p.x) : 0u, py = v ? ordf(p.y) : 0u, pz = v ? ordf(p.z) : 0u;
+    const unsigned lx = row_min_u32(ox), ly = row_min_u32(oy), lz = row_min_u32(oz);
+    const unsigned hx = row_max_u32(px), hy = row_max_u32(py), hz = row_max_u32(pz);
+    if ((lane & 15) == 0) {
+        const bool any = lx != SENT;  // the row holds at least one point
+        const size_t o = 4 * (size_t)leaf + (lane >> 4);
+        slo[o] = any ? make_float4(unordf(lx), unordf(ly), unordf(lz), 0.f) : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+        shi[o] = any ? make_float4(unordf(hx), unordf(hy), unordf(hz), 0.f)
+                     : make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+    }
+    const unsigned wlx = wave_min_u32(lx), wly = wave_min_u32(ly), wlz = wave_min_u32(lz);
+    const unsigned whx = wave_max_u32(hx), why = wave_max_u32(hy), whz = wave_max_u32(hz);
+    if (lane == 0) {
+        nlo[P + leaf] = make_float4(unordf(wlx), unordf(wly), unordf(wlz), 0.f);
+        nhi[P + leaf] = make_float4(unordf(whx), unordf(why), unordf(whz), 0.f);
+    }
+}
+
+// Nodes [m, 2m) -> their ancestors up to log2(min(m, 64)) levels, one 64-thread workgroup per
+// group of min(m, 64) siblings, in LDS.
+__global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, float4* __restrict__ nhi, int m) {
+    __shared__ float4 slo[64], shi[64];
+    const int t = threadIdx.x;
+    const int cnt = min(m, 64);
+    int nb = m + blockIdx.x * cnt;
+    if (t < cnt) { slo[t] = nlo[nb + t]; shi[t] = nhi[nb + t]; }
+    __syncthreads();
+    for (int c = cnt; c > 1; c >>= 1) {
+        const int h = c >> 1;
+        float4 l = make_float4(0.f, 0.f, 0.f, 0.f), u = l;
+        if (t < h) {
+            const float4 a0 = slo[2 * t], a1 = slo[2 * t + 1], b0 = shi[2 * t], b1 = shi[2 * t + 1];
+            l = make_float4(fminf(a0.x, a1.x), fminf(a0.y, a1.y), fminf(a0.z, a1.z), 0.f);
+            u = make_float4(fmaxf(b0.x, b1.x), fmaxf(b0.y, b1.y), fmaxf(b0.z, b1.z), 0.f);
+        }
+        __syncthreads();
+        nb >>= 1;
+        if (t < h) { slo[t] = l; shi[t] = u; nlo[nb + t] = l; nhi[nb + t] = u; }
+        __syncthreads();
+    }
+}
+
+// ---- query: one wave per leaf, lanes = the leaf's points ---------------------------------------
+template <int KT, int M>
+__global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
+    constexpr int KM = KT + M + 1;  // + 1: the query itself enters its own list at d2 = 0
+    __shared__ float4 s_pts[4][kTreeLeaf];
+    __shared__ int s_visit[4][kMaxVisit];  // first point of each visited leaf
+    __shared__ int s_stack[4][kStack];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int leaf = xcd_remap(blockIdx.x, gridDim.x) * 4 + wid;
+    if (leaf >= a.L) return;
+    float4* buf = s_pts[wid];
+    int* vis = s_visit[wid];
+    int* stk = s_stack[wid];
+    const int base = (int)a.leaf_start[leaf];
+    const int qcnt = (int)a.leaf_start[leaf + 1] - base;
+    // lanes past the leaf's last point duplicate it (same candidate stream, never written back)
+    const unsigned qpos = (unsigned)(base + min(lane, qcnt - 1));
+    const float4 qp = a.pts[KN_IDX(qpos, (unsigned)a.n, 401)];
+    const unsigned qw = __float_as_uint(qp.w);
+    const bool live = lane < qcnt && w_live(a, qw);
+    if (!__builtin_amdgcn_ballot_w64(live)) return;
+    const float qx = qp.x, qy = qp.y, qz = qp.z;
+
+    unsigned keys[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) keys[j] = SENT;
+    unsigned nnet = 0;
+    int nv = 0;
+    bool over = false;
+
+    // stage leaf lf in the wave's LDS slice and stream its points to every lane
+    auto visit = [&](int lf) __attribute__((always_inline)) {
+        const int b = (int)a.leaf_start[lf];
+        const int cnt = (int)a.leaf_start[lf + 1] - b;
+        if (lane < cnt) buf[lane] = a.pts[KN_IDX(b + lane, a.n, 402)];
+        if (lane == 0) vis[nv] = b;
+        __builtin_amdgcn_wave_barrier();
+        const int sb = nv << 6;
+        // 16-point sub-groups no lane's bound reaches are skipped
+        for (int r = 0; r * 16 < cnt; ++r) {
+            const unsigned last = keys[KM - 1];
+            const float ub = last == SENT ? INFINITY : __uint_as_float(last | kMask);
+            const float bd = box_d2(qx, qy, qz, a.slo[4 * lf + r], a.shi[4 * lf + r]);
+            if (!__builtin_amdgcn_ballot_w64(live && bd * kShrink <= ub)) continue;
+            const int j1 = min(cnt, 16 * r + 16);
+#pragma unroll 4
+            for (int j = 16 * r; j < j1; ++j) {
+                const float4 c = buf[j];
+                nnet += topk_push(keys, cand_key(c, qx, qy, qz, ~kMask, sb + j, 0));
+            }
+        }
+        ++nv;
+        __builtin_amdgcn_wave_barrier();
+    };
+    visit(leaf);
+
+    // wave-uniform near-first traversal from the root (P == 1: the root is this leaf)
+    int sp = 0;
+    if (a.P > 1) {
+        if (lane == 0) stk[0] = 1;
+        sp = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    while (sp > 0) {
+        --sp;
+        const int node = __builtin_amdgcn_readfirstlane(stk[sp]);
+        const unsigned last = keys[KM - 1];
+        const float ub = last == SENT ? INFINITY : __uint_as_float(last | kMask);
+        const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
+        if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
+        if (node >= a.P) {
+            if (node - a.P == leaf) continue;
+            if (nv == kMaxVisit) { over = true; break; }
+            visit(node - a.P);
+            continue;
+        }
+        const int c0 = 2 * node;
+        const float b0 = box_d2(qx, qy, qz, a.nlo[c0], a.nhi[c0]);
+        const float b1 = box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]);
+        const bool need0 = __builtin_amdgcn_ballot_w64(live && b0 < INFINITY && b0 * kShrink <= ub) != 0;
+        const bool need1 = __builtin_amdgcn_ballot_w64(live && b1 < INFINITY && b1 * kShrink <= ub) != 0;
+        // nearer child (for most live lanes) on top of the stack
+        const int votes = __builtin_popcountll(__builtin_amdgcn_ballot_w64(live && b0 <= b1));
+        const bool first0 = 2 * votes >= __builtin_popcountll(__builtin_amdgcn_ballot_w64(live));
+        const int nearc = first0 ? c0 : c0 + 1, farc = first0 ? c0 + 1 : c0;
+        const bool nn = first0 ? need0 : need1, nf = first0 ? need1 : need0;
+        if (lane == 0) {
+            if (nf) stk[sp] = farc;
+            if (nn) stk[sp + (nf ? 1 : 0)] = nearc;
+        }
+        sp += (nf ? 1 : 0) + (nn ? 1 : 0);
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // exact re-rank of the kept slots by (d2, id). The query itself gets the smallest key (it sits
+    // in the run of d2 = 0 keys, so it moves to the front within the passes below) and is dropped
+    // from the front; were it pushed out by more than K+M exact duplicates, nothing is dropped.
+    unsigned long long e[KM];
+    bool has_self = false;
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+        const unsigned key = keys[j];
+        unsigned long long v = ~0ull;
+        if (key != SENT) {
+            const unsigned slot = key & kMask;
+            const unsigned pidx = (unsigned)vis[slot >> 6] + (slot & 63u);
+            if (pidx != qpos) {
+                const float4 c = a.pts[KN_IDX(pidx, (unsigned)a.n, 403)];
+                const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
+                v = pack_key64(fmaf(dz, dz, fmaf(dy, dy, dx * dx)), w_id(a, __float_as_uint(c.w)));
+            } else {
+                v = 0ull;
+                has_self = true;
+            }
+        }
+        e[j] = v;
+    }
+    // keys order the slots by truncated distance: only slots of equal truncation buckets can be
+    // out of exact order, so a few odd-even passes sort them; checked below (else: exact finish)
+#pragma unroll
+    for (int r = 0; r < kSortPasses; ++r) {
+#pragma unroll
+        for (int j = r & 1; j + 1 < KM; j += 2) {
+            const unsigned long long x = e[j], y = e[j + 1];
+            const bool s = y < x;
+            e[j] = s ? y : x;
+            e[j + 1] = s ? x : y;
+        }
+    }
+    bool sorted = true;
+#pragma unroll
+    for (int j = 0; j + 1 < KM; ++j) sorted = sorted && !(e[j + 1] < e[j]);
+    const int k = a.k;
+    const int off = has_self ? 1 : 0;
+    unsigned long long ek = ~0ull;
+    unsigned kb = SENT;
+#pragma unroll
+    for (int j = 0; j < KT + 2; ++j) {
+        if (j == k - 1 + off) ek = e[j];
+        if (j == k) kb = keys[j];
+    }
+    const unsigned last = keys[KM - 1];
+    const bool full = last != SENT;
+    // nothing truncated away (exact d2 >= its key's floor >= the last key's floor) can precede the
+    // K-th exact neighbour when that lies strictly below the floor
+    bool cert = !over && sorted &&
+                (!full || (ek != ~0ull && __uint_as_float((unsigned)(ek >> 32)) < __uint_as_float(last & ~kMask)));
+    if (a.flags & 1) cert = false;
+    const unsigned long long unc = __builtin_amdgcn_ballot_w64(live && !cert);
+    if (unc) {
+        unsigned pos0 = 0;
+        if (lane == 0) pos0 = atomicAdd(a.counters + 0, (unsigned)__builtin_popcountll(unc));
+        pos0 = (unsigned)__builtin_amdgcn_readfirstlane((int)pos0);
+        if (live && !cert) {
+            const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+            const unsigned pos = pos0 + (unsigned)__builtin_popcountll(unc & lt);
+            a.list[KN_IDX(pos, (unsigned)a.n, 404)] = qpos;
+            // the K+1 smallest keys hold at most one self: a bound on the K-th distance
+            a.thr[KN_IDX(pos, (unsigned)a.n, 405)] = kb == SENT ? INFINITY : __uint_as_float(kb | kMask);
+        }
+    }
+    if (lane == 0) {
+        if (over) atomicAdd(a.counters + 2, 1u);
+        atomicAdd(a.counters + 5, (unsigned)nv);  // leaves visited
+        atomicAdd(a.counters + 7, 1u);            // waves
+    }
+    if (unc) {  // causes (diagnostics): [3] re-rank left unsorted, [4] K-th not below the floor
+        const unsigned nu = (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live && !over && !sorted));
+        const unsigned nf = (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live && !over && sorted && !cert));
+        if (lane == 0 && nu) atomicAdd(a.counters + 3, nu);
+        if (lane == 0 && nf) atomicAdd(a.counters + 4, nf);
+    }
+    if (kStats) {
+        const unsigned nets = (unsigned)__builtin_amdgcn_readfirstlane((int)nnet);
+        if (lane == 0) atomicAdd(a.counters + 6, nets);
+    }
+    if (live && cert) {
+        const unsigned row = w_row(a, qw, qpos);
+#pragma unroll
+        for (int j = 0; j < KT; ++j) {
+            if (j < k) {
+                const size_t o = KN_IDX((size_t)row * (size_t)k + j, (size_t)a.n_queries * k, 406);
+                const unsigned long long v = has_self ? e[j + 1] : e[j];
+                const bool empty = v == ~0ull;
+                a.out_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
+                if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
+            }
+        }
+    }
+}
+
+// ---- exact finish: one wave per listed query (or every point: list == nullptr) ------------------
+// Near-first traversal with the query's distance bound; every candidate with d2 <= thr is
+// ballot-compacted into the wave's LDS buffer, which is bitonic-sorted by (d2, id) and cut to K
+// (thr = K-th distance) when it could overflow -- the semantics of query.hip's exact kernel.
+__global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
+    __shared__ unsigned long long s_buf[4][kTCap];
+    __shared__ int s_stack[4][kStack];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    unsigned long long* buf = s_buf[wid];
+    int* stk = s_stack[wid];
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int total = all ? a.n : (int)a.counters[0];
+    const int k = a.k;
+    for (int t = blockIdx.x * 4 + wid; t < total; t += gridDim.x * 4) {
+        const unsigned qpos = all ? (unsigned)t : (unsigned)__builtin_amdgcn_readfirstlane((int)a.list[KN_IDX(t, a.n, 411)]);
+        const float4 qp = a.pts[KN_IDX(qpos, (unsigned)a.n, 412)];
+        const unsigned qw = __float_as_uint(qp.w);
+        if (!w_live(a, qw)) continue;
+        const float qx = qp.x, qy = qp.y, qz = qp.z;
+        float thr = all ? INFINITY : a.thr[KN_IDX(t, a.n, 413)];
+        int cnt = 0;
+        auto compact = [&]() __attribute__((always_inline)) {
+            __builtin_amdgcn_wave_barrier();
+            unsigned long long v[kTCap / 64];
+#pragma unroll
+            for (int e = 0; e < kTCap / 64; ++e) v[e] = (64 * e + lane < cnt) ? buf[64 * e + lane] : ~0ull;
+            __builtin_amdgcn_wave_barrier();
+            wave_bitonic_sort_u64<kTCap / 64>(v, lane);
+#pragma unroll
+            for (int e = 0; e < kTCap / 64; ++e)
+                if (64 * e + lane < k) buf[64 * e + lane] = v[e];
+            cnt = min(cnt, k);
+            if (cnt >= k) {
+                unsigned hb = 0;
+#pragma unroll
+                for (int e = 0; e < kTCap / 64; ++e)
+                    if ((k - 1) / 64 == e) hb = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v[e] >> 32), (k - 1) & 63);
+                thr = __uint_as_float(hb);
+            }
+            __builtin_amdgcn_wave_barrier();
+        };
+        int sp = 1;
+        if (lane == 0) stk[0] = 1;
+        __builtin_amdgcn_wave_barrier();
+        while (sp > 0) {
+            --sp;
+            const int node = __builtin_amdgcn_readfirstlane(stk[sp]);
+            const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
+            if (!(bd < INFINITY && bd * kShrink <= thr)) continue;
+            if (node >= a.P) {
+                if (cnt + 64 > kTCap) compact();
+                const int lf = node - a.P;
+                const int p = (int)a.leaf_start[lf] + lane;
+                bool pass = false;
+                unsigned long long key = 0;
+                if (p < (int)a.leaf_start[lf + 1] && (unsigned)p != qpos) {
+                    const float4 c = a.pts[KN_IDX(p, a.n, 414)];
+                    const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
+                    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                    pass = d2 <= thr;
+                    key = pack_key64(d2, w_id(a, __float_as_uint(c.w)));
+                }
+                const unsigned long long bal = __builtin_amdgcn_ballot_w64(pass);
+                if (pass) buf[cnt + __builtin_popcountll(bal & lt)] = key;
+                cnt += __builtin_popcountll(bal);
+                continue;
+            }
+            const int c0 = 2 * node;
+            const float b0 = box_d2(qx, qy, qz, a.nlo[c0], a.nhi[c0]);
+            const float b1 = box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]);
+            const bool need0 = b0 < INFINITY && b0 * kShrink <= thr;
+            const bool need1 = b1 < INFINITY && b1 * kShrink <= thr;
+            const bool first0 = b0 <= b1;
+            const int nearc = first0 ? c0 : c0 + 1, farc = first0 ? c0 + 1 : c0;
+            const bool nn = first0 ? need0 : need1, nf = first0 ? need1 : need0;
+            if (lane == 0) {
+                if (nf) stk[sp] = farc;
+                if (nn) stk[sp + (nf ? 1 : 0)] = nearc;
+            }
+            sp += (nf ? 1 : 0) + (nn ? 1 : 0);
+            __builtin_amdgcn_wave_barrier();
+        }
+        compact();
+        const unsigned row = w_row(a, qw, qpos);
+        for (int j = lane; j < k; j += 64) {
+            const size_t o = KN_IDX((size_t)row * (size_t)k + j, (size_t)a.n_queries * k, 415);
+            const unsigned long long v = (j < cnt) ? buf[j] : ~0ull;
+            const bool empty = (v == ~0ull);
+            a.out_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
+            if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+size_t sort_temp_bytes(int n) {
+    size_t bytes = 0, b2 = 0;
+    hipcub::DoubleBuffer<unsigned> kb(nullptr, nullptr), vb(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, n, 0, 30);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, b2, (const unsigned*)nullptr, (unsigned*)nullptr, n);
+    return std::max(bytes, b2);
+}
+
+}  // namespace
+
+static int tree_pow2(int L) {
+    int P = 1;
+    while (P < L) P <<= 1;
+    return P;
+}
+
+size_t tree_workspace_bytes(int n) {
+    if (n <= 0) return 256;
+    size_t b = align256((size_t)n * 16);         // pts
+    b += 2 * align256(((size_t)n + 1) * 4);      // leaf_start, seg_start
+    b += 4 * align256((size_t)n * 4);            // list, thr, flag, incl
+    b += 2 * align256((size_t)n * 8);            // codes, vals (double buffers)
+    b += align256(16);                           // info
+    b += align256(sort_temp_bytes(n));
+    return b;
+}
+
+TreeView tree_view(void* ws, int n) {
+    TreeView t{};
+    t.n = std::max(n, 0);
+    if (n <= 0) return t;
+    char* p = static_cast<char*>(ws);
+    auto take = [&](size_t bytes) { char* r = p; p += align256(bytes); return r; };
+    t.pts = reinterpret_cast<float4*>(take((size_t)n * 16));
+    t.leaf_start = reinterpret_cast<unsigned*>(take(((size_t)n + 1) * 4));
+    t.seg_start = reinterpret_cast<unsigned*>(take(((size_t)n + 1) * 4));
+    t.list = reinterpret_cast<unsigned*>(take((size_t)n * 4));
+    t.thr = reinterpret_cast<float*>(take((size_t)n * 4));
+    t.flag = reinterpret_cast<unsigned*>(take((size_t)n * 4));
+    t.incl = reinterpret_cast<unsigned*>(take((size_t)n * 4));
+    t.codes = reinterpret_cast<unsigned*>(take((size_t)n * 8));
+    t.vals = reinterpret_cast<unsigned*>(take((size_t)n * 8));
+    t.info = reinterpret_cast<unsigned*>(take(16));
+    t.sort_temp_bytes = sort_temp_bytes(n);
+    t.sort_temp = take(t.sort_temp_bytes);
+    return t;
+}
+
+size_t tree_node_bytes(int L) {
+    return (2 * (size_t)tree_pow2(std::max(L, 1)) * 2 + 4 * (size_t)std::max(L, 1) * 2) * sizeof(float4);
+}
+
+void tree_attach_nodes(TreeView& t, void* nodes, int L) {
+    t.L = L;
+    t.P = tree_pow2(std::max(L, 1));
+    t.nlo = static_cast<float4*>(nodes);
+    t.nhi = t.nlo + 2 * (size_t)t.P;
+    t.slo = t.nhi + 2 * (size_t)t.P;
+    t.shi = t.slo + 4 * (size_t)std::max(L, 1);
+}
+
+hipError_t launch_tree_leaves(const float4* in, const GridGeom* geom, const TreeView& t, hipStream_t s) {
+    const int n = t.n;
+    if (n <= 0) return hipSuccess;
+    morton_kernel<<<cdiv(n, 256), 256, 0, s>>>(in, n, geom, t.codes, t.vals);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipcub::DoubleBuffer<unsigned> kb(t.codes, t.codes + n), vb(t.vals, t.vals + n);
+    size_t bytes = t.sort_temp_bytes;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(t.sort_temp, bytes, kb, vb, n, 0, 30, s)) != hipSuccess) return e;
+    gather_kernel<<<cdiv(n, 256), 256, 0, s>>>(in, vb.Current(), n, t.pts);
+    cut_kernel<<<cdiv(n, 256), 256, 0, s>>>(kb.Current(), n, t.flag);
+    bytes = t.sort_temp_bytes;
+    if ((e = hipcub::DeviceScan::InclusiveSum(t.sort_temp, bytes, t.flag, t.incl, n, s)) != hipSuccess) return e;
+    starts_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.flag, t.incl, n, t.seg_start, nullptr);
+    leaf_flag_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.incl, t.seg_start, n, t.flag);
+    bytes = t.sort_temp_bytes;
+    if ((e = hipcub::DeviceScan::InclusiveSum(t.sort_temp, bytes, t.flag, t.incl, n, s)) != hipSuccess) return e;
+    starts_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.flag, t.incl, n, t.leaf_start, t.info);
+    return hipGetLastError();
+}
+
+hipError_t launch_tree_nodes(const TreeView& t, hipStream_t s) {
+    if (t.n <= 0) return hipSuccess;
+    if (!t.nlo || t.L < 1) return hipErrorInvalidValue;
+    leaf_box_kernel<<<cdiv(t.P, 4), 256, 0, s>>>(t.pts, t.leaf_start, t.L, t.P, t.nlo, t.nhi, t.slo, t.shi);
+    for (int m = t.P; m > 1; m /= std::min(m, 64))
+        node_box_kernel<<<m / std::min(m, 64), 64, 0, s>>>(t.nlo, t.nhi, m);
+    return hipGetLastError();
+}
+
+hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t s) {
+    if (q.k <= 0 || q.k > 128) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s);
+    if (e != hipSuccess || t.n == 0 || q.n_queries == 0) return e;
+    if (!t.nlo || t.L < 1) return hipErrorInvalidValue;
+    TArgs a{};
+    a.pts = t.pts; a.leaf_start = t.leaf_start; a.nlo = t.nlo; a.nhi = t.nhi; a.slo = t.slo; a.shi = t.shi; a.list = t.list; a.thr = t.thr;
+    a.n = t.n; a.L = t.L; a.P = t.P; a.k = q.k; a.n_queries = q.n_queries; a.id_map = q.id_map;
+    a.row_of = nullptr; a.out_idx = q.out_idx; a.out_dist = q.out_dist; a.counters = q.counters;
+    a.flags = q.flags;
+    constexpr int M = 2;
+    const unsigned grid = cdiv(t.L, 4);
+    const int k = q.k;
+    bool all = false;
+    if (k <= 4) knn_tree_kernel<4, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 8) knn_tree_kernel<8, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 12) knn_tree_kernel<12, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 16) knn_tree_kernel<16, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 24) knn_tree_kernel<24, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 32) knn_tree_kernel<32, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 40) knn_tree_kernel<40, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 50) knn_tree_kernel<50, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 64) knn_tree_kernel<64, M><<<grid, 256, 0, s>>>(a);
+    else all = true;  // K > 64: the exact traversal serves every query
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const unsigned eg = all ? std::max(1u, std::min(cdiv(t.n, 4), 16384u)) : (unsigned)kExactGrid;
+    knn_tree_exact_kernel<<<eg, 256, 0, s>>>(a, all ? 1 : 0);
+    return hipGetLastError();
+}
+
+KN_DEFINE_DEBUG_READER(debug_words_tree)
+
+}  // namespace kn

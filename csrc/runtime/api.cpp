@@ -47,6 +47,7 @@ kn::EngineConfig to_engine(const kn_config* c) {
     e.verbose = c->verbose;
     e.use_tiles = c->exact_only ? 0 : 1;
     e.adaptive = c->fixed_grid ? 0 : 1;
+    e.algo = c->algo;
     return e;
 }
 }  // namespace

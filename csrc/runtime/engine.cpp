@@ -39,6 +39,8 @@ void Engine::release() {
     if (knn_stored_) { (void)hipFree(knn_stored_); knn_stored_ = nullptr; }
     if (dist_stored_) { (void)hipFree(dist_stored_); dist_stored_ = nullptr; }
     if (points3_) { (void)hipFree(points3_); points3_ = nullptr; }
+    if (tree_ws_) { (void)hipFree(tree_ws_); tree_ws_ = nullptr; }
+    if (tree_nodes_) { (void)hipFree(tree_nodes_); tree_nodes_ = nullptr; }
     for (auto& e : ev_) if (e) { (void)hipEventDestroy(e); e = nullptr; }  // reference leaks these (D6)
     if (stream_) { (void)hipStreamDestroy(stream_); stream_ = nullptr; }
 }
@@ -179,7 +181,48 @@ QueryBuffers Engine::query_buffers() const {
 }
 
 kn_status Engine::build_async() { return check(launch_build(build_buffers(), stream_), "build"); }
-kn_status Engine::query_async() { return check(launch_query(query_buffers(), stream_), "query"); }
+kn_status Engine::query_async() {
+    if (use_tree_) return tree_query();
+    return check(launch_query(query_buffers(), stream_), "query");
+}
+
+kn_status Engine::tree_query() {
+    kn_status st;
+    const size_t need = tree_workspace_bytes(n_);
+    if (tree_ws_bytes_ < need) {
+        if (tree_ws_) (void)hipFree(tree_ws_);
+        tree_ws_ = nullptr;
+        tree_ws_bytes_ = 0;
+        if ((st = check(hipMalloc(&tree_ws_, need), "hipMalloc(tree)")) != KN_OK) return st;
+        tree_ws_bytes_ = need;
+    }
+    TreeView t = tree_view(tree_ws_, n_);
+    if ((st = check(launch_tree_leaves(sorted_, geom_, t, stream_), "tree leaves")) != KN_OK) return st;
+    unsigned L = 0;
+    if (n_ > 0) {
+        if ((st = check(hipMemcpyAsync(&L, t.info, sizeof(L), hipMemcpyDeviceToHost, stream_), "D2H leaves")) != KN_OK)
+            return st;
+        if ((st = check(hipStreamSynchronize(stream_), "tree sync")) != KN_OK) return st;
+    }
+    const size_t nb = tree_node_bytes((int)L);
+    if (tree_nodes_bytes_ < nb) {
+        if (tree_nodes_) (void)hipFree(tree_nodes_);
+        tree_nodes_ = nullptr;
+        tree_nodes_bytes_ = 0;
+        if ((st = check(hipMalloc(&tree_nodes_, nb), "hipMalloc(tree nodes)")) != KN_OK) return st;
+        tree_nodes_bytes_ = nb;
+    }
+    tree_leaves_ = (int)L;
+    tree_attach_nodes(t, tree_nodes_, (int)L);
+    if ((st = check(launch_tree_nodes(t, stream_), "tree nodes")) != KN_OK) return st;
+    TreeQuery q{};
+    q.k = cfg_.k;
+    q.n_queries = n_;
+    q.out_idx = out_idx_;
+    q.out_dist = out_dist_;
+    q.counters = counters_;
+    return check(launch_tree_query(t, q, stream_), "tree query");
+}
 
 kn_status Engine::occupancy(double* w) {
     unsigned long long s = 0;
@@ -198,24 +241,39 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     kn_status st;
     if (!src && n > 0) return fail(KN_ERR_INVALID_ARGUMENT, "null points");
     if ((st = allocate(n)) != KN_OK) return st;
+    bool refined = false;
     for (int round = 0;; ++round) {
         if (n > 0 && (st = check(hipMemcpyAsync(points_, src, (size_t)n * 12, kind, stream_), "copy points")) != KN_OK)
             return st;
         (void)hipEventRecord(ev_[0], stream_);
         points3_valid_ = false;
-        if ((st = build_async()) != KN_OK) return st;
+        // adaptive: probe grids are binned without the in-cell order (see launch_cell_sort)
+        BuildBuffers b = build_buffers();
+        if (cfg_.adaptive) b.deterministic = 0;
+        if ((st = check(launch_build(b, stream_), "build")) != KN_OK) return st;
         (void)hipEventRecord(ev_[1], stream_);
         if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
         (void)hipEventElapsedTime(&ms_build_, ev_[0], ev_[1]);
-        if (!cfg_.adaptive || round == 3 || n == 0) break;
+        if (!cfg_.adaptive || n == 0) break;
         double w = 0.0;
-        if ((st = occupancy(&w)) != KN_OK) return st;
         int nd[3];
-        if (!refine_dims(ap_.dims, w, cfg_.k, cfg_.points_per_cell, n, nd)) break;
+        if (round < 3 && (st = occupancy(&w)) != KN_OK) return st;
+        if (round == 3 || !refine_dims(ap_.dims, w, cfg_.k, cfg_.points_per_cell, n, nd)) {
+            if (cfg_.deterministic &&
+                (st = check(launch_cell_sort(cell_start_, geom_, n, sorted_, perm_, bin_tmp_, stream_), "cell sort")) != KN_OK)
+                return st;
+            break;
+        }
         if (cfg_.verbose)
             fprintf(stderr, "kn: cell occupancy %.1f -> grid %dx%dx%d\n", w, nd[0], nd[1], nd[2]);
         if ((st = allocate(n, nd, true)) != KN_OK) return st;
+        refined = true;
     }
+    // A grid that had to be refined serves a cloud whose density varies too much for one cell
+    // size (900K clustered, K=16: grid query 7.5 ms, tree 1.6 ms + 0.27 ms build; surfaces
+    // 1.27 vs 0.96 + 0.27; profiles/diag_r2_tree.jsonl): the tree path takes it.
+    use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined));
+    if (use_tree_ && graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
     built_ = true;
     return KN_OK;
@@ -295,6 +353,16 @@ kn_status Engine::set_k(int k) {
 kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     if (!built_) return fail(KN_ERR_STATE, "run_graph() before prepare()");
     kn_status st;
+    if (use_tree_) {  // eager steps (see launch_graph)
+        (void)hipEventRecord(ev_[0], stream_);
+        if ((st = launch_graph(iters)) != KN_OK) return st;
+        (void)hipEventRecord(ev_[1], stream_);
+        if ((st = check(hipEventSynchronize(ev_[1]), "graph sync")) != KN_OK) return st;
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, ev_[0], ev_[1]);
+        if (ms_per_iter) *ms_per_iter = iters > 0 ? ms / iters : 0.f;
+        return KN_OK;
+    }
     if (!graph_) {
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
@@ -324,6 +392,16 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
 kn_status Engine::launch_graph(int iters) {
     if (!built_) return fail(KN_ERR_STATE, "launch_graph() before prepare()");
     kn_status st;
+    if (use_tree_) {
+        // the tree build reads its leaf count back (sizes the node buffer): eager steps
+        for (int i = 0; i < iters; ++i) {
+            if ((st = build_async()) != KN_OK) return st;
+            if ((st = query_async()) != KN_OK) return st;
+        }
+        solved_ = true;
+        stored_valid_ = points3_valid_ = false;
+        return KN_OK;
+    }
     if (!graph_) {
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;

@@ -14,6 +14,7 @@
 
 #include "knearests.h"
 #include "kn/kernels.h"
+#include "kn/tree.h"
 
 namespace kn {
 
@@ -28,6 +29,7 @@ struct EngineConfig {
     int use_tiles = 1;
     int with_distances = 1;
     int adaptive = 1;  // refine the grid when cells are over-occupied (clusters, surfaces)
+    int algo = 0;      // query structure: 0 auto (tree when the adaptive grid was refined), 1 grid, 2 tree
 };
 
 class Engine {
@@ -74,6 +76,8 @@ public:
     int num_cells() const { return C_; }
     float ms_build() const { return ms_build_; }
     float ms_solve() const { return ms_solve_; }
+    bool uses_tree() const { return use_tree_; }
+    int tree_leaves() const { return tree_leaves_; }
 
     // raw device pointers (C API struct fields)
     float4* d_sorted() const { return sorted_; }
@@ -91,6 +95,8 @@ private:
     kn_status occupancy(double* w);
     kn_status build_async();
     kn_status query_async();
+    // Morton-leaf tree over the built grid's points (one host sync: the leaf count) + its query
+    kn_status tree_query();
     QueryBuffers query_buffers() const;
     BuildBuffers build_buffers() const;
     void release();
@@ -128,6 +134,12 @@ private:
     bool points3_valid_ = false;
     bool built_ = false, solved_ = false, stored_valid_ = false;
     unsigned last_fallback_ = ~0u;  // fallback-list length of the last eager solve (~0: unknown)
+    bool use_tree_ = false;         // chosen at prepare (EngineConfig::algo)
+    void* tree_ws_ = nullptr;
+    size_t tree_ws_bytes_ = 0;
+    void* tree_nodes_ = nullptr;
+    size_t tree_nodes_bytes_ = 0;
+    int tree_leaves_ = 0;
     float ms_build_ = 0.f, ms_solve_ = 0.f;
 };
 

@@ -14,6 +14,7 @@
 
 #include "kn/kernels.h"
 #include "kn/route.h"
+#include "kn/tree.h"
 #include "../host/host.hpp"
 #include "../runtime/engine.hpp"
 
@@ -149,6 +150,64 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     KN_CHECK_HIP(kn::launch_query(q, s));
     if (!with_dist) out_dist = torch::empty({0}, sorted.options());
     return {out_idx, out_dist, counters, uncert, fallback};
+}
+
+// Morton-leaf tree over a built grid's points (kn/tree.h): (workspace, node buffer, leaf count).
+// One host sync (the leaf count sizes the node buffer).
+py::tuple tree_build(torch::Tensor sorted, torch::Tensor geom) {
+    TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
+                "sorted must be a (N,4) float32 GPU tensor");
+    TORCH_CHECK(geom.is_cuda() && geom.numel() == 16, "geom must be a 16-int GPU tensor");
+    const c10::DeviceGuard guard(sorted.device());
+    const int n = (int)sorted.size(0);
+    auto u8 = sorted.options().dtype(torch::kUInt8);
+    auto ws = torch::empty({(int64_t)kn::tree_workspace_bytes(n)}, u8);
+    kn::TreeView t = kn::tree_view(ws.data_ptr(), n);
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_tree_leaves(reinterpret_cast<const float4*>(sorted.data_ptr<float>()),
+                                        reinterpret_cast<const kn::GridGeom*>(geom.data_ptr<int>()), t, s));
+    unsigned L = 0;
+    if (n > 0) {
+        KN_CHECK_HIP(hipMemcpyAsync(&L, t.info, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        KN_CHECK_HIP(hipStreamSynchronize(s));
+    }
+    auto nodes = torch::empty({(int64_t)kn::tree_node_bytes((int)L)}, u8);
+    kn::tree_attach_nodes(t, nodes.data_ptr(), (int)L);
+    KN_CHECK_HIP(kn::launch_tree_nodes(t, s));
+    return py::make_tuple(ws, nodes, (int64_t)L);
+}
+
+std::vector<torch::Tensor> tree_query(torch::Tensor ws, torch::Tensor nodes, int64_t leaves, int64_t n, int64_t k,
+                                      int64_t n_queries, c10::optional<torch::Tensor> id_map, bool with_dist,
+                                      int64_t flags) {
+    TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kUInt8, "ws must be a tree_build workspace");
+    TORCH_CHECK(n >= 0 && (size_t)ws.numel() >= kn::tree_workspace_bytes((int)n), "workspace too small for n");
+    TORCH_CHECK(nodes.is_cuda() && (size_t)nodes.numel() >= kn::tree_node_bytes((int)leaves), "node buffer too small");
+    TORCH_CHECK(n == 0 || (leaves >= 1 && leaves <= n), "bad leaf count");
+    TORCH_CHECK(k >= 1 && k <= 128, "k must be in [1, 128]");
+    TORCH_CHECK(n_queries >= 0 && n_queries <= n, "n_queries out of range");
+    const c10::DeviceGuard guard(ws.device());
+    kn::TreeView t = kn::tree_view(ws.data_ptr(), (int)n);
+    kn::tree_attach_nodes(t, nodes.data_ptr(), (int)leaves);
+    auto i32 = ws.options().dtype(torch::kInt32);
+    auto out_idx = torch::empty({n_queries, k}, i32);
+    torch::Tensor out_dist = torch::empty({with_dist ? n_queries : 0, with_dist ? k : 0}, ws.options().dtype(torch::kFloat32));
+    auto counters = torch::empty({kn::kNumCounters}, i32);
+    kn::TreeQuery q{};
+    q.k = (int)k;
+    q.n_queries = (int)n_queries;
+    if (id_map.has_value()) {
+        TORCH_CHECK(id_map->is_cuda() && id_map->scalar_type() == torch::kInt32 && id_map->numel() >= n,
+                    "id_map must be an int32 GPU tensor with >= N entries");
+        q.id_map = reinterpret_cast<const unsigned*>(id_map->data_ptr<int>());
+    }
+    q.out_idx = reinterpret_cast<unsigned*>(out_idx.data_ptr<int>());
+    q.out_dist = with_dist ? out_dist.data_ptr<float>() : nullptr;
+    q.counters = reinterpret_cast<unsigned*>(counters.data_ptr<int>());
+    q.flags = (int)flags;
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_tree_query(t, q, s));
+    return {out_idx, out_dist, counters};
 }
 
 py::dict auto_params(int64_t n, int64_t k, double ppc, std::vector<int64_t> tile, int64_t halo,
@@ -548,6 +607,20 @@ torch::Tensor steady_flag(torch::Tensor local, torch::Tensor metas, int64_t rank
     return flag;
 }
 
+void cell_sort(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor perm, torch::Tensor geom) {
+    TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4, "sorted must be (N,4) GPU");
+    TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
+    TORCH_CHECK(perm.is_cuda() && perm.numel() == sorted.size(0), "perm must match sorted");
+    TORCH_CHECK(geom.is_cuda() && geom.numel() == 16, "geom must be a 16-int GPU tensor");
+    const c10::DeviceGuard guard(sorted.device());
+    auto tmp = torch::empty_like(sorted);
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_cell_sort(cell_start.data_ptr<int>(), reinterpret_cast<const kn::GridGeom*>(geom.data_ptr<int>()),
+                                      (int)sorted.size(0), reinterpret_cast<float4*>(sorted.data_ptr<float>()),
+                                      reinterpret_cast<unsigned*>(perm.data_ptr<int>()),
+                                      reinterpret_cast<float4*>(tmp.data_ptr<float>()), s));
+}
+
 // occupancy-adaptive grid: sum over cells of count^2 (int64, on device, no sync)
 torch::Tensor occupancy(torch::Tensor cell_start) {
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32 && cell_start.is_contiguous() &&
@@ -585,7 +658,7 @@ torch::Tensor local_meta(torch::Tensor points) {
 class PyEngine {
 public:
     PyEngine(int64_t k, double ppc, std::vector<int64_t> tile, int64_t halo, bool deterministic, bool use_tiles,
-             bool with_dist, int64_t device, bool adaptive) {
+             bool with_dist, int64_t device, bool adaptive, int64_t algo) {
         kn::EngineConfig c;
         c.k = (int)k;
         c.points_per_cell = (float)ppc;
@@ -594,6 +667,7 @@ public:
         c.deterministic = deterministic ? 1 : 0;
         c.use_tiles = use_tiles ? 1 : 0;
         c.adaptive = adaptive ? 1 : 0;
+        c.algo = (int)algo;
         c.with_distances = with_dist ? 1 : 0;
         c.device = (int)device;
         e_ = std::make_unique<kn::Engine>(c);
@@ -635,6 +709,8 @@ public:
         d["dims"] = std::vector<int>{e_->dims()[0], e_->dims()[1], e_->dims()[2]};
         d["ms_build"] = e_->ms_build();
         d["ms_solve"] = e_->ms_solve();
+        d["algo"] = e_->uses_tree() ? "tree" : "grid";
+        d["tree_leaves"] = e_->tree_leaves();
         return d;
     }
 
@@ -643,11 +719,12 @@ private:
 };
 
 std::vector<int64_t> debug_words(bool reset) {
-    unsigned b[4], q[4], r[4];
+    unsigned b[4], q[4], r[4], t[4];
     KN_CHECK_HIP(kn::debug_words_build(b, reset));
     KN_CHECK_HIP(kn::debug_words_query(q, reset));
     KN_CHECK_HIP(kn::debug_words_route(r, reset));
-    return {b[0], b[1], b[2], b[3], q[0], q[1], q[2], q[3], r[0], r[1], r[2], r[3]};
+    KN_CHECK_HIP(kn::debug_words_tree(t, reset));
+    return {b[0], b[1], b[2], b[3], q[0], q[1], q[2], q[3], r[0], r[1], r[2], r[3], t[0], t[1], t[2], t[3]};
 }
 
 // ---- CPU (host) components ----------------------------------------------------------
@@ -736,6 +813,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("exact_grid") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
+    m.def("tree_build", &tree_build, "Morton-leaf tree over a grid's sorted points: (workspace, nodes, leaves)",
+          py::arg("sorted"), py::arg("geom"));
+    m.def("tree_query", &tree_query, "kNN through a tree_build result: (idx, d2, counters)", py::arg("ws"),
+          py::arg("nodes"), py::arg("leaves"), py::arg("n"), py::arg("k"), py::arg("n_queries"), py::arg("id_map") = py::none(),
+          py::arg("with_dist") = true, py::arg("flags") = 0);
+    m.def("cell_sort", &cell_sort, "in-cell order by original index (deterministic layout) of a built grid");
     m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");
     m.def("refine_dims", &refine_dims, "finer grid dims for an over-occupied grid, or None");
     m.def("local_meta", &local_meta, "multi-GPU: {lo[3], hi[3], n, 0} of the local points (float64, on device)");
@@ -762,10 +845,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")
-        .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t, bool>(),
+        .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t, bool, int64_t>(),
              py::arg("k") = 16, py::arg("points_per_cell") = 0.0, py::arg("tile") = std::vector<int64_t>{},
              py::arg("halo") = 0, py::arg("deterministic") = true, py::arg("use_tiles") = true,
-             py::arg("with_dist") = true, py::arg("device") = 0, py::arg("adaptive") = true)
+             py::arg("with_dist") = true, py::arg("device") = 0, py::arg("adaptive") = true,
+             py::arg("algo") = 0)
         .def("prepare", &PyEngine::prepare)
         .def("prepare_async", &PyEngine::prepare_async)
         .def("solve", &PyEngine::solve)

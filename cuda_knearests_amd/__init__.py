@@ -13,11 +13,11 @@ Layout:
 """
 from ._ext import load as _load_ext
 from .models.knearests import KNearests
-from .ops.knn_ops import Grid, Plan, build_grid, check_knn, knn, knn_cpu, normalize_1000, query, read_xyz, to_stored_space, write_xyz
+from .ops.knn_ops import Grid, Plan, build_grid, build_tree, check_knn, knn, knn_cpu, normalize_1000, query, read_xyz, to_stored_space, write_xyz
 
 __version__ = "0.1.0"
 
 __all__ = [
-    "KNearests", "Grid", "Plan", "build_grid", "query", "knn", "knn_cpu", "check_knn",
+    "KNearests", "Grid", "Plan", "build_grid", "build_tree", "query", "knn", "knn_cpu", "check_knn",
     "read_xyz", "write_xyz", "normalize_1000", "to_stored_space", "__version__",
 ]

@@ -28,7 +28,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
-KERNELS = ["kernels/build.hip", "kernels/query.hip", "kernels/route.hip"]
+KERNELS = ["kernels/build.hip", "kernels/query.hip", "kernels/route.hip", "kernels/tree.hip"]
 HOST = ["host/host.cpp"]
 RUNTIME = ["runtime/engine.cpp", "runtime/api.cpp"]
 MULTI = "runtime/multi.cpp"  # C-API multi-GPU runtime: libknearests.so only (links RCCL)

@@ -32,9 +32,14 @@ from .._ext import load
 class KNearests:
     def __init__(self, k: int = 50, device: str | torch.device = "cuda", points_per_cell: float = 0.0,
                  tile=(), halo: int = 0, deterministic: bool = True, use_tiles: bool = True,
-                 with_distances: bool = True, verbose: bool = False):
+                 with_distances: bool = True, verbose: bool = False, algo: str = "auto"):
         if not 1 <= int(k) <= 128:
             raise ValueError("k must be in [1, 128]")
+        if algo not in ("auto", "grid", "tree"):
+            raise ValueError("algo must be 'auto', 'grid' or 'tree'")
+        # query structure: the uniform grid, the Morton-leaf tree, or auto (the tree when the
+        # occupancy-adaptive grid had to be refined: clusters, surfaces)
+        self.algo = algo if use_tiles else "grid"
         self.k = int(k)
         self.device = torch.device(device)
         self.points_per_cell = float(points_per_cell)
@@ -100,12 +105,13 @@ class KNearests:
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
         idx, d2, info = ops.query(self.grid, self.k, use_tiles=self.use_tiles,
-                                  with_dist=self.with_distances, return_info=True)
+                                  with_dist=self.with_distances, return_info=True, algo=self.algo)
         t1.record()
         t1.synchronize()
         self.timings["ms_solve"] = t0.elapsed_time(t1)
         c = info["counters"].cpu()
-        self.info = {"exact_path": int(c[0]), "uncertified": int(c[1]), "dense_tiles": int(c[2])}
+        algo = self.grid.extra.get("algo", "grid") if self.algo == "auto" else self.algo
+        self.info = {"exact_path": int(c[0]), "uncertified": int(c[1]), "dense_tiles": int(c[2]), "algo": algo}
         self.neighbors, self.distances = idx, d2
         if self.verbose:
             print(f"kn_solve: {self.timings['ms_solve']:.3f} msec ({self.info})", file=sys.stderr)
@@ -141,12 +147,13 @@ class KNearests:
         if not capture:
             g = ops.build_grid(pts, self.k, plan=self.plan(pts.size(0)), deterministic=self.deterministic)
             self.neighbors, self.distances = ops.query(g, self.k, use_tiles=self.use_tiles,
-                                                       with_dist=self.with_distances)
+                                                       with_dist=self.with_distances, algo=self.algo)
             self.grid = g
             return self
         if self._graph is None or self._graph_n != pts.size(0):
             self._graph = load().Engine(self.k, self.points_per_cell, list(self.tile), self.halo,
-                                        self.deterministic, self.use_tiles, True, self.device.index or 0)
+                                        self.deterministic, self.use_tiles, True, self.device.index or 0,
+                                        True, {"auto": 0, "grid": 1, "tree": 2}[self.algo])
             self._graph_n = pts.size(0)
             self._graph.prepare(pts)  # eager first build: decides the (occupancy-adaptive) grid
         # the engine keeps its own copy of the input, so every step re-uploads (D2D) + replays

@@ -83,28 +83,66 @@ def build_grid(points: torch.Tensor, k: int = 16, plan: Optional[Plan] = None,
         plan = Plan.auto(n, k, points_per_cell, extent=extent)
     C = load()
     bx = list(map(float, box)) if box is not None else None
-    s, cs, perm, geom = C.build(points, list(plan.dims), bool(deterministic), bx)
-    for _ in range(3 if adaptive and n > 0 else 0):
+    probe = adaptive and n > 0
+    # probe grids skip the in-cell order (a clustered cloud's first grid has cells of thousands
+    # of points); the final grid is ordered once
+    s, cs, perm, geom = C.build(points, list(plan.dims), bool(deterministic) and not probe, bx)
+    refined = False
+    for _ in range(3 if probe else 0):
         w = int(C.occupancy(cs).item()) / n
         dims = C.refine_dims(list(plan.dims), w, int(k), float(points_per_cell), n)
         if dims is None:
             break
         plan = Plan(list(dims), list(plan.tile), plan.halo, plan.lds_capacity, plan.lds_bytes)
-        s, cs, perm, geom = C.build(points, list(plan.dims), bool(deterministic), bx)
-    return Grid(s, cs, perm, geom, plan, n)
+        s, cs, perm, geom = C.build(points, list(plan.dims), False, bx)
+        refined = True
+    if probe and deterministic:
+        C.cell_sort(s, cs, perm, geom)
+    # a grid that had to be refined serves a density one cell size cannot: query("auto") takes
+    # the Morton-leaf tree (same rule as kn::Engine, csrc/runtime/engine.cpp)
+    return Grid(s, cs, perm, geom, plan, n, {"algo": "tree" if refined else "grid"})
+
+
+def build_tree(grid: Grid) -> tuple:
+    """Morton-leaf box tree over the grid's points (``kn/tree.h``), cached on the grid: the
+    density-adaptive query structure for clouds one cell size cannot serve (clusters, scans).
+    Returns ``(workspace, nodes, leaves)``; one host sync (the leaf count)."""
+    t = grid.extra.get("tree")
+    if t is None:
+        t = tuple(load().tree_build(grid.sorted, grid.geom))
+        grid.extra["tree"] = t
+    return t
 
 
 def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[torch.Tensor] = None,
           complete: Optional[Sequence[float]] = None, use_tiles: bool = True, with_dist: bool = True,
-          return_info: bool = False, flags: int = 0):
+          return_info: bool = False, flags: int = 0, algo: str = "grid"):
     """kNN of the grid's points (original index < n_queries) against all grid points.
 
-    Returns ``(idx, d2)`` (+ ``info`` dict with the device counters and the uncertified
-    query list when ``return_info``). ``idx`` values are original indices, or ``id_map[...]``.
+    ``algo``: ``"grid"`` (LDS-tiled grid kernels + exact fallback), ``"tree"`` (Morton-leaf tree,
+    :func:`build_tree`; not with ``complete``) or ``"auto"`` (the grid's ``plan`` choice, see
+    :func:`build_grid`). Returns ``(idx, d2)`` (+ ``info`` dict with the device counters and the
+    uncertified query list when ``return_info``). ``idx`` values are original indices, or
+    ``id_map[...]``.
     """
     if not 1 <= k <= 128:
         raise ValueError("k must be in [1, 128]")
+    if algo == "auto":
+        algo = grid.extra.get("algo", "grid")
     nq = grid.n if n_queries is None else int(n_queries)
+    if algo == "tree":
+        if complete is not None:
+            raise ValueError("the tree path serves complete (single-GPU) point sets only")
+        ws, nodes, leaves = build_tree(grid)
+        idx, d2, counters = load().tree_query(ws, nodes, leaves, grid.n, int(k), nq, id_map, bool(with_dist),
+                                              int(flags) & 1)
+        if return_info:
+            return idx, (d2 if with_dist else None), {"counters": counters,
+                                                      "uncertified": counters.new_zeros(0),
+                                                      "exact_path": None}
+        return idx, (d2 if with_dist else None)
+    if algo != "grid":
+        raise ValueError(f"unknown algo {algo!r}")
     comp = list(complete) if complete is not None else [-INF, -INF, -INF, INF, INF, INF]
     p = grid.plan
     halo, cap = p.halo, p.lds_capacity
@@ -118,10 +156,13 @@ def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[
 
 
 def knn(points: torch.Tensor, k: int = 16, points_per_cell: float = 0.0, deterministic: bool = True,
-        use_tiles: bool = True, with_dist: bool = True, adaptive: bool = True):
-    """All-points k-nearest neighbours on the GPU. Returns ``(idx int32 (N,k), d2 float32 (N,k))``."""
+        use_tiles: bool = True, with_dist: bool = True, adaptive: bool = True, algo: str = "auto"):
+    """All-points k-nearest neighbours on the GPU. Returns ``(idx int32 (N,k), d2 float32 (N,k))``.
+    ``algo``: "auto" (grid, or the tree when the adaptive grid had to be refined), "grid", "tree"."""
     g = build_grid(points, k, points_per_cell=points_per_cell, deterministic=deterministic, adaptive=adaptive)
-    return query(g, k, use_tiles=use_tiles, with_dist=with_dist)
+    if not use_tiles:
+        algo = "grid"
+    return query(g, k, use_tiles=use_tiles, with_dist=with_dist, algo=algo)
 
 
 def to_stored_space(idx: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:

@@ -11,7 +11,7 @@ from cuda_knearests_amd.utils import dataset
 class KnConfig(C.Structure):
     _fields_ = [("k", C.c_int), ("points_per_cell", C.c_float), ("tile", C.c_int * 3), ("halo", C.c_int),
                 ("deterministic", C.c_int), ("device", C.c_int), ("verbose", C.c_int), ("exact_only", C.c_int),
-                ("fixed_grid", C.c_int)]
+                ("fixed_grid", C.c_int), ("algo", C.c_int)]
 
 
 class KnProblem(C.Structure):

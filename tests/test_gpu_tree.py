@@ -1,0 +1,127 @@
+"""GPU tests of the Morton-leaf tree path (csrc/kernels/tree.hip, kn/tree.h) against the kd-tree
+oracle: bitwise-equal distances, ids distinct / not self / reproducing their distance
+(cuda_knearests_amd/utils/check.py), on the clouds the grid cannot adapt to and on the
+reference's uniform ones."""
+import pytest
+import torch
+
+import cuda_knearests_amd as kn
+from cuda_knearests_amd.utils import clustered_cloud, surface_cloud, uniform_cloud
+from cuda_knearests_amd.utils.check import assert_knn_exact
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(p, idx, d2, k, n_queries=None):
+    nq = p.size(0) if n_queries is None else n_queries
+    pc = p.cpu()
+    oi, od = kn.knn_cpu(pc, k, "kdtree")
+    idx, d2 = idx.cpu(), d2.cpu()
+    assert idx.shape == (nq, k)
+    mism = (d2 != od[:nq]).any(1)
+    assert int(mism.sum()) == 0, f"{int(mism.sum())} rows differ; first {int(mism.nonzero()[0, 0])}"
+    assert_knn_exact(pc, torch.arange(nq), idx, d2, od[:nq])
+
+
+@pytest.mark.parametrize("k,gen", [(1, "uniform"), (8, "clustered"), (16, "uniform"), (16, "clustered"),
+                                   (16, "surface"), (32, "clustered"), (50, "clustered"), (64, "surface"),
+                                   (100, "clustered")])
+def test_tree_vs_oracle(cuda, k, gen):
+    mk = {"uniform": uniform_cloud, "clustered": clustered_cloud, "surface": surface_cloud}[gen]
+    p = mk(40000, seed=600 + k).to(cuda)
+    g = kn.build_grid(p, k, adaptive=True)
+    idx, d2, info = kn.query(g, k, algo="tree", return_info=True)
+    _check(p, idx, d2, k)
+    if k <= 64:
+        # near-ties and visit-cap overflows only: the exact finish is a small minority
+        assert int(info["counters"][0]) < p.size(0) // 20
+
+
+@pytest.mark.parametrize("k", [1, 16, 50])
+def test_tree_forced_exact_finish(cuda, k):
+    # flags bit 0 sends every query through the exact traversal (the rare branch, covered)
+    p = clustered_cloud(20000, seed=700 + k).to(cuda)
+    g = kn.build_grid(p, k, adaptive=True)
+    idx, d2, info = kn.query(g, k, algo="tree", return_info=True, flags=1)
+    assert int(info["counters"][0]) == p.size(0)
+    _check(p, idx, d2, k)
+    i2, e2 = kn.query(g, k, algo="tree")
+    assert torch.equal(idx, i2) and torch.equal(d2, e2)
+
+
+def test_tree_matches_grid_bitwise(cuda):
+    # same arithmetic, same tie rule (d2, id): identical output to the grid path
+    p = uniform_cloud(50000, seed=801, device=cuda)
+    g = kn.build_grid(p, 16)
+    i1, e1 = kn.query(g, 16)
+    i2, e2 = kn.query(g, 16, algo="tree")
+    assert torch.equal(i1, i2) and torch.equal(e1, e2)
+
+
+def test_tree_duplicates_tiny_and_subsets(cuda):
+    p = uniform_cloud(3000, seed=9)
+    p = torch.cat([p, p, p[:100]]).to(cuda)  # exact duplicates: d2 = 0 ties
+    g = kn.build_grid(p, 8)
+    idx, d2 = kn.query(g, 8, algo="tree")
+    _check(p, idx, d2, 8)
+    for n in (1, 2, 3, 9, 17, 63, 64, 65, 129):
+        q = uniform_cloud(n, seed=n, device=cuda)
+        g = kn.build_grid(q, 8)
+        idx, d2 = kn.query(g, 8, algo="tree")
+        _check(q, idx, d2, 8)
+    # queries = a prefix of the original indices, ids through an id map
+    p = clustered_cloud(30000, seed=11).to(cuda)
+    g = kn.build_grid(p, 16, adaptive=True)
+    idx, d2 = kn.query(g, 16, n_queries=12345, algo="tree")
+    _check(p, idx, d2, 16, n_queries=12345)
+    id_map = torch.arange(p.size(0), device=cuda, dtype=torch.int32) * 3
+    i2, e2 = kn.query(g, 16, n_queries=12345, id_map=id_map, algo="tree")
+    assert torch.equal(i2, idx * 3) and torch.equal(e2, d2)
+
+
+def test_tree_single_point_cluster(cuda):
+    # 20K points on one spot plus a sparse background: every Morton code of the cluster collides
+    g0 = torch.Generator().manual_seed(5)
+    core = 500 + 1e-3 * torch.randn((20000, 3), generator=g0)
+    bg = 1000 * torch.rand((2000, 3), generator=g0)
+    p = torch.cat([core, bg]).to(cuda)
+    g = kn.build_grid(p, 16, adaptive=True)
+    idx, d2 = kn.query(g, 16, algo="tree")
+    _check(p, idx, d2, 16)
+
+
+@pytest.mark.parametrize("gen,expect", [("clustered", "tree"), ("uniform", "grid")])
+def test_engine_auto_algo(cuda, gen, expect):
+    # kn::Engine (C API runtime): the tree when the adaptive grid was refined; steps through
+    # launch_graph (eager for the tree: the leaf count sizes its node buffer) stay exact
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    p = (clustered_cloud if gen == "clustered" else uniform_cloud)(40000, seed=31).to(cuda)
+    e = C.Engine(16)
+    e.prepare(p)
+    e.solve()
+    assert e.info()["algo"] == expect
+    idx, d2 = e.results(cuda)
+    _check(p, idx, d2, 16)
+    e.prepare_async(p)
+    e.launch_graph(2)
+    e.sync()
+    i2, e2 = e.results(cuda)
+    assert torch.equal(i2, idx) and torch.equal(e2, d2)
+    # forced structures agree bit for bit
+    for algo in (1, 2):
+        f = C.Engine(16, algo=algo)
+        f.prepare(p)
+        f.solve()
+        i3, e3 = f.results(cuda)
+        assert torch.equal(e3, d2)
+
+
+def test_knearests_model_tree(cuda):
+    p = clustered_cloud(30000, seed=41).to(cuda)
+    m = kn.KNearests(k=16, device=cuda).prepare(p).solve()
+    assert m.info["algo"] == "tree"
+    _check(p, m.neighbors, m.distances, 16)
+    m.step(p, capture=True)
+    _check(p, m.neighbors, m.distances, 16)
