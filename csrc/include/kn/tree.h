@@ -6,17 +6,18 @@
 // overflow the LDS budget. The tree path adapts to any density:
 //
 //   build:  30-bit Morton code of every point (cubic quantisation of the grid's domain) ->
-//           radix sort (hipCUB) -> points gathered into Morton order -> leaves of <= 64
-//           consecutive points (one wave), cut at the curve's large jumps -> leaf boxes (wave DPP
-//           reductions) -> implicit complete binary tree of boxes over the leaves (heap index,
-//           root 1, leaf l = node P + l), reduced bottom-up 6 levels per launch in LDS.
-//   query:  one wave per leaf, lanes = the leaf's 64 points. Wave-uniform near-first traversal
+//           radix sort (hipCUB) -> points gathered into Morton order -> leaves = the maximal
+//           binary-prefix (radix) nodes of <= 32 points -> leaf boxes (wave DPP reductions) ->
+//           implicit complete binary tree of boxes over the leaves (heap index, root 1, leaf l =
+//           node P + l), reduced bottom-up 6 levels per launch in LDS.
+//   query:  one wave per 64 consecutive points of the Morton order (lanes = queries).
+//           Wave-uniform near-first traversal
 //           (a node is entered when ANY lane's box distance is within its own K-th bound);
 //           every visited leaf is staged once in the wave's LDS slice and streamed to all
 //           lanes (broadcast reads) into the same packed-key / v_med3_u32 register top-K as the
 //           grid kernels, key slot = (visit index, point in leaf). Exact re-rank of the kept
 //           slots by (d2, id) and certification against the truncation floor; uncertified
-//           queries (near-ties, > 64 visited leaves) go to a list finished by a wave-per-query
+//           queries (near-ties, > 256 visited leaves) go to a list finished by a wave-per-query
 //           exact traversal with threshold compaction (same semantics as the grid's exact
 //           kernel, so results are identical to the oracle's).
 //
@@ -31,7 +32,7 @@
 
 namespace kn {
 
-constexpr int kTreeLeaf = 64;
+constexpr int kTreeLeaf = 32;  // points per leaf (at most)
 
 // A tree: one workspace (carved by tree_view) plus a node buffer sized from the leaf count.
 struct TreeView {
@@ -49,8 +50,6 @@ struct TreeView {
     size_t sort_temp_bytes;
     float4* nlo;          // 2P node boxes (lower corner; heap index, root 1, leaf l = node P + l)
     float4* nhi;          // 2P upper corners; empty padded leaves: lo = +inf, hi = -inf
-    float4* slo;          // 4L sub-boxes: points [16 r, 16 r + 16) of leaf l at 4 l + r
-    float4* shi;
     int n, L, P;          // points, leaves, P = next power of two >= L
 };
 

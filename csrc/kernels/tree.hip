@@ -19,9 +19,11 @@ namespace kn {
 namespace {
 
 constexpr unsigned SENT = 0xFFFFFFFFu;
-constexpr int kVisitBits = 7;                 // key slot = visit index (7 bits) | point in leaf (6 bits)
+constexpr int kLeafBits = 5;                  // kTreeLeaf = 32 points per leaf
+constexpr int kVisitBits = 8;                 // key slot = visit index (8 bits) | point in leaf (5 bits)
 constexpr int kMaxVisit = 1 << kVisitBits;    // leaves a wave may visit before its queries go exact
-constexpr unsigned kMask = (1u << (kVisitBits + 6)) - 1u;
+constexpr unsigned kMask = (1u << (kVisitBits + kLeafBits)) - 1u;
+static_assert((1 << kLeafBits) == kTreeLeaf, "leaf size");
 constexpr int kStack = 64;                    // traversal stack (depth <= log2(P) + 1)
 constexpr int kTCap = 256;                    // exact-finish candidate buffer per wave (u64 keys)
 constexpr int kSortPasses = 3;                // odd-even passes of the exact re-rank (then checked)
@@ -35,8 +37,6 @@ struct TArgs {
     const unsigned* leaf_start;  // L + 1
     const float4* nlo;
     const float4* nhi;
-    const float4* slo;  // 4 sub-boxes per leaf (points [16 r, 16 r + 16) of the leaf)
-    const float4* shi;
     unsigned* list;
     float* thr;
     int n, L, P;
@@ -98,12 +98,12 @@ __global__ void gather_kernel(const float4* __restrict__ in, const unsigned* __r
     if (i < n) out[i] = in[src[i]];
 }
 
-// Leaf boundaries. Fixed 64-point runs of the Morton order straddle the curve's jumps: a run that
-// crosses the boundary of a large octree node holds points from two far-apart corners and gets a
-// huge box (every wave nearby then visits it, and its own queries need two regions). A cut is
-// forced at b when the jump between b-1 and b (highest differing code bit) is 2+ octree levels
-// coarser than the local spacing on both sides (the jumps across 8 points before and after);
-// segments between cuts are split into ceil(len / 64) near-equal leaves.
+// Leaf boundaries: leaves are the maximal binary-prefix (radix) nodes of the sorted Morton codes
+// holding <= kTreeLeaf points -- boxes of aspect <= 2 that never straddle a jump of the curve
+// (fixed runs of the Morton order do: measured ~2x the candidates per query). Positions b-1 and b
+// are in different leaves iff their lowest common prefix node holds more than kTreeLeaf points;
+// its extent is found by two binary searches inside the kTreeLeaf + 1 window around b. Runs of
+// equal codes (one finest cell) longer than a leaf are chunked by leaf_flag_kernel.
 __device__ __forceinline__ int hibit(unsigned x) { return x ? 31 - __builtin_clz(x) : -1; }
 
 __global__ void cut_kernel(const unsigned* __restrict__ c, int n, unsigned* __restrict__ flag) {
@@ -111,10 +111,24 @@ __global__ void cut_kernel(const unsigned* __restrict__ c, int n, unsigned* __re
     if (b >= n) return;
     unsigned f = 1u;
     if (b > 0) {
-        const int jump = hibit(c[b - 1] ^ c[b]);
-        const int ja = b >= 8 ? hibit(c[b - 8] ^ c[b - 1]) : -1;
-        const int jb = b + 8 <= n ? hibit(c[b] ^ c[b + 7]) : -1;
-        f = (jump >= 0 && jump >= max(ja, jb) + 6) ? 1u : 0u;
+        const unsigned x = c[b - 1] ^ c[b];
+        f = 0u;
+        if (x) {
+            const int sh = hibit(x) + 1;
+            const unsigned p = c[b] >> sh;
+            int lo = max(0, b - 1 - kTreeLeaf), hi = b - 1;  // first index with prefix p
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((c[mid] >> sh) == p) hi = mid; else lo = mid + 1;
+            }
+            const int s0 = lo;
+            lo = b; hi = min(n, b + kTreeLeaf + 1);  // first index past the prefix
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if ((c[mid] >> sh) == p) lo = mid + 1; else hi = mid;
+            }
+            f = (lo - s0 > kTreeLeaf) ? 1u : 0u;
+        }
     }
     flag[b] = f;
 }
@@ -132,7 +146,7 @@ __global__ void starts_kernel(const unsigned* __restrict__ flag, const unsigned*
     }
 }
 
-// flag[b] = b starts a leaf: segment [s, e) splits at s + floor(j len / c), c = ceil(len / 64)
+// flag[b] = b starts a leaf: segment [s, e) splits at s + floor(j len / c), c = ceil(len / kTreeLeaf)
 __global__ void leaf_flag_kernel(const unsigned* __restrict__ incl, const unsigned* __restrict__ seg_start, int n,
                                  unsigned* __restrict__ flag) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -144,25 +158,9 @@ __global__ void leaf_flag_kernel(const unsigned* __restrict__ incl, const unsign
     flag[b] = (j * len / c == o) ? 1u : 0u;
 }
 
-// 16-lane row reduction (every lane of the row gets the row's result)
-__device__ __forceinline__ unsigned row_min_u32(unsigned x) {
-    x = kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false));
-    x = kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false));
-    x = kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false));
-    return kn_umin(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_MIRROR, 0xF, 0xF, false));
-}
-__device__ __forceinline__ unsigned row_max_u32(unsigned x) {
-    x = kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_1032, 0xF, 0xF, false));
-    x = kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_QUAD_2301, 0xF, 0xF, false));
-    x = kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_HALF_MIRROR, 0xF, 0xF, false));
-    return kn_umax(x, (unsigned)__builtin_amdgcn_update_dpp((int)x, (int)x, KN_DPP_ROW_MIRROR, 0xF, 0xF, false));
-}
-
-// One wave per leaf (P leaves: the padded ones get empty boxes): the leaf box (node P + leaf) and
-// its 4 sub-boxes of 16 points (empty sub-groups: empty boxes).
+// One wave per leaf (P leaves: the padded ones get empty boxes).
 __global__ __launch_bounds__(256) void leaf_box_kernel(const float4* __restrict__ pts, const unsigned* __restrict__ leaf_start,
-                                                       int L, int P, float4* __restrict__ nlo, float4* __restrict__ nhi,
-                                                       float4* __restrict__ slo, float4* __restrict__ shi) {
+                                                       int L, int P, float4* __restrict__ nlo, float4* __restrict__ nhi) {
     const int leaf = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (leaf >= P) return;
     if (leaf >= L) {
@@ -175,22 +173,12 @@ __global__ __launch_bounds__(256) void leaf_box_kernel(const float4* __restrict_
     const unsigned i = leaf_start[leaf] + lane;
     const bool v = i < leaf_start[leaf + 1];
     const float4 p = v ? pts[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const unsigned ox = v ? ordf(p.x) : SENT, oy = v ? ordf(p.y) : SENT, oz = v ? ordf(p.z) : SENT;
-    const unsigned px = v ? ordf(p.x) : 0u, py = v ? ordf(p.y) : 0u, pz = v ? ordf(p.z) : 0u;
-    const unsigned lx = row_min_u32(ox), ly = row_min_u32(oy), lz = row_min_u32(oz);
-    const unsigned hx = row_max_u32(px), hy = row_max_u32(py), hz = row_max_u32(pz);
-    if ((lane & 15) == 0) {
-        const bool any = lx != SENT;  // the row holds at least one point
-        const size_t o = 4 * (size_t)leaf + (lane >> 4);
-        slo[o] = any ? make_float4(unordf(lx), unordf(ly), unordf(lz), 0.f) : make_float4(INFINITY, INFINITY, INFINITY, 0.f);
-        shi[o] = any ? make_float4(unordf(hx), unordf(hy), unordf(hz), 0.f)
-                     : make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-    }
-    const unsigned wlx = wave_min_u32(lx), wly = wave_min_u32(ly), wlz = wave_min_u32(lz);
-    const unsigned whx = wave_max_u32(hx), why = wave_max_u32(hy), whz = wave_max_u32(hz);
+    const unsigned lx = wave_min_u32(v ? ordf(p.x) : SENT), hx = wave_max_u32(v ? ordf(p.x) : 0u);
+    const unsigned ly = wave_min_u32(v ? ordf(p.y) : SENT), hy = wave_max_u32(v ? ordf(p.y) : 0u);
+    const unsigned lz = wave_min_u32(v ? ordf(p.z) : SENT), hz = wave_max_u32(v ? ordf(p.z) : 0u);
     if (lane == 0) {
-        nlo[P + leaf] = make_float4(unordf(wlx), unordf(wly), unordf(wlz), 0.f);
-        nhi[P + leaf] = make_float4(unordf(whx), unordf(why), unordf(whz), 0.f);
+        nlo[P + leaf] = make_float4(unordf(lx), unordf(ly), unordf(lz), 0.f);
+        nhi[P + leaf] = make_float4(unordf(hx), unordf(hy), unordf(hz), 0.f);
     }
 }
 
@@ -218,7 +206,7 @@ __global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, 
     }
 }
 
-// ---- query: one wave per leaf, lanes = the leaf's points ---------------------------------------
+// ---- query: one wave per 64 consecutive points of the Morton order (lanes = queries) -------------
 template <int KT, int M>
 __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     constexpr int KM = KT + M + 1;  // + 1: the query itself enters its own list at d2 = 0
@@ -226,14 +214,14 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     __shared__ int s_visit[4][kMaxVisit];  // first point of each visited leaf
     __shared__ int s_stack[4][kStack];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int leaf = xcd_remap(blockIdx.x, gridDim.x) * 4 + wid;
-    if (leaf >= a.L) return;
+    const int w = xcd_remap(blockIdx.x, gridDim.x) * 4 + wid;
+    const int base = w * 64;
+    if (base >= a.n) return;
     float4* buf = s_pts[wid];
     int* vis = s_visit[wid];
     int* stk = s_stack[wid];
-    const int base = (int)a.leaf_start[leaf];
-    const int qcnt = (int)a.leaf_start[leaf + 1] - base;
-    // lanes past the leaf's last point duplicate it (same candidate stream, never written back)
+    const int qcnt = min(64, a.n - base);
+    // lanes past the last point duplicate it (same candidate stream, never written back)
     const unsigned qpos = (unsigned)(base + min(lane, qcnt - 1));
     const float4 qp = a.pts[KN_IDX(qpos, (unsigned)a.n, 401)];
     const unsigned qw = __float_as_uint(qp.w);
@@ -248,38 +236,38 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     int nv = 0;
     bool over = false;
 
-    // stage leaf lf in the wave's LDS slice and stream its points to every lane
+    // stage leaf lf in the wave's LDS slice and stream its points to every lane (broadcast reads)
     auto visit = [&](int lf) __attribute__((always_inline)) {
         const int b = (int)a.leaf_start[lf];
         const int cnt = (int)a.leaf_start[lf + 1] - b;
         if (lane < cnt) buf[lane] = a.pts[KN_IDX(b + lane, a.n, 402)];
         if (lane == 0) vis[nv] = b;
         __builtin_amdgcn_wave_barrier();
-        const int sb = nv << 6;
-        // 16-point sub-groups no lane's bound reaches are skipped
-        for (int r = 0; r * 16 < cnt; ++r) {
-            const unsigned last = keys[KM - 1];
-            const float ub = last == SENT ? INFINITY : __uint_as_float(last | kMask);
-            const float bd = box_d2(qx, qy, qz, a.slo[4 * lf + r], a.shi[4 * lf + r]);
-            if (!__builtin_amdgcn_ballot_w64(live && bd * kShrink <= ub)) continue;
-            const int j1 = min(cnt, 16 * r + 16);
+        const int sb = nv << kLeafBits;
 #pragma unroll 4
-            for (int j = 16 * r; j < j1; ++j) {
-                const float4 c = buf[j];
-                nnet += topk_push(keys, cand_key(c, qx, qy, qz, ~kMask, sb + j, 0));
-            }
+        for (int j = 0; j < cnt; ++j) {
+            const float4 c = buf[j];
+            nnet += topk_push(keys, cand_key(c, qx, qy, qz, ~kMask, sb + j, 0));
         }
         ++nv;
         __builtin_amdgcn_wave_barrier();
     };
-    visit(leaf);
-
-    // wave-uniform near-first traversal from the root (P == 1: the root is this leaf)
-    int sp = 0;
-    if (a.P > 1) {
-        if (lane == 0) stk[0] = 1;
-        sp = 1;
+    // the leaves holding the wave's own 64 points first: every lane starts the traversal with a
+    // bound from ~64 nearby candidates (small leaves alone leave the early bounds loose, and a
+    // loose bound of any lane opens nodes for the whole wave)
+    int l0 = 0, l1 = a.L - 1;
+    while (l0 < l1) {  // last leaf starting at or before base
+        const int mid = (l0 + l1 + 1) >> 1;
+        if ((int)a.leaf_start[mid] <= base) l0 = mid; else l1 = mid - 1;
     }
+    l1 = l0;
+    while (l1 + 1 < a.L && (int)a.leaf_start[l1 + 1] < base + qcnt) ++l1;
+    for (int lf = l0; lf <= l1 && nv < kMaxVisit; ++lf) visit(lf);
+
+    // wave-uniform near-first traversal from the root: a node is entered when any live lane's
+    // box distance is within its bound (the (K+M+1)-th key, rounded up)
+    int sp = 1;
+    if (lane == 0) stk[0] = 1;
     __builtin_amdgcn_wave_barrier();
     while (sp > 0) {
         --sp;
@@ -289,9 +277,10 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
         if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
         if (node >= a.P) {
-            if (node - a.P == leaf) continue;
+            const int lf = node - a.P;
+            if (lf >= l0 && lf <= l1) continue;  // visited first
             if (nv == kMaxVisit) { over = true; break; }
-            visit(node - a.P);
+            visit(lf);
             continue;
         }
         const int c0 = 2 * node;
@@ -323,7 +312,7 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         unsigned long long v = ~0ull;
         if (key != SENT) {
             const unsigned slot = key & kMask;
-            const unsigned pidx = (unsigned)vis[slot >> 6] + (slot & 63u);
+            const unsigned pidx = (unsigned)vis[slot >> kLeafBits] + (slot & ((1u << kLeafBits) - 1u));
             if (pidx != qpos) {
                 const float4 c = a.pts[KN_IDX(pidx, (unsigned)a.n, 403)];
                 const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
@@ -555,17 +544,13 @@ TreeView tree_view(void* ws, int n) {
     return t;
 }
 
-size_t tree_node_bytes(int L) {
-    return (2 * (size_t)tree_pow2(std::max(L, 1)) * 2 + 4 * (size_t)std::max(L, 1) * 2) * sizeof(float4);
-}
+size_t tree_node_bytes(int L) { return 2 * (size_t)tree_pow2(std::max(L, 1)) * 2 * sizeof(float4); }
 
 void tree_attach_nodes(TreeView& t, void* nodes, int L) {
     t.L = L;
     t.P = tree_pow2(std::max(L, 1));
     t.nlo = static_cast<float4*>(nodes);
     t.nhi = t.nlo + 2 * (size_t)t.P;
-    t.slo = t.nhi + 2 * (size_t)t.P;
-    t.shi = t.slo + 4 * (size_t)std::max(L, 1);
 }
 
 hipError_t launch_tree_leaves(const float4* in, const GridGeom* geom, const TreeView& t, hipStream_t s) {
@@ -592,7 +577,7 @@ hipError_t launch_tree_leaves(const float4* in, const GridGeom* geom, const Tree
 hipError_t launch_tree_nodes(const TreeView& t, hipStream_t s) {
     if (t.n <= 0) return hipSuccess;
     if (!t.nlo || t.L < 1) return hipErrorInvalidValue;
-    leaf_box_kernel<<<cdiv(t.P, 4), 256, 0, s>>>(t.pts, t.leaf_start, t.L, t.P, t.nlo, t.nhi, t.slo, t.shi);
+    leaf_box_kernel<<<cdiv(t.P, 4), 256, 0, s>>>(t.pts, t.leaf_start, t.L, t.P, t.nlo, t.nhi);
     for (int m = t.P; m > 1; m /= std::min(m, 64))
         node_box_kernel<<<m / std::min(m, 64), 64, 0, s>>>(t.nlo, t.nhi, m);
     return hipGetLastError();
@@ -604,12 +589,12 @@ hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t 
     if (e != hipSuccess || t.n == 0 || q.n_queries == 0) return e;
     if (!t.nlo || t.L < 1) return hipErrorInvalidValue;
     TArgs a{};
-    a.pts = t.pts; a.leaf_start = t.leaf_start; a.nlo = t.nlo; a.nhi = t.nhi; a.slo = t.slo; a.shi = t.shi; a.list = t.list; a.thr = t.thr;
+    a.pts = t.pts; a.leaf_start = t.leaf_start; a.nlo = t.nlo; a.nhi = t.nhi; a.list = t.list; a.thr = t.thr;
     a.n = t.n; a.L = t.L; a.P = t.P; a.k = q.k; a.n_queries = q.n_queries; a.id_map = q.id_map;
     a.row_of = nullptr; a.out_idx = q.out_idx; a.out_dist = q.out_dist; a.counters = q.counters;
     a.flags = q.flags;
     constexpr int M = 2;
-    const unsigned grid = cdiv(t.L, 4);
+    const unsigned grid = cdiv(cdiv(t.n, 64), 4);
     const int k = q.k;
     bool all = false;
     if (k <= 4) knn_tree_kernel<4, M><<<grid, 256, 0, s>>>(a);
