@@ -294,11 +294,20 @@ def run_loopback_bench(args) -> dict:
     dev = torch.device("cuda", 0)
     W = args.loopback
     shares = []
-    for r in range(W):
-        blo, bhi = SpatialDecomposition(W, (0.0,) * 3, (1000.0,) * 3).rank_box(r)
-        u = uniform_cloud(args.n, seed=args.seed + 7919 * r, device=dev, lo=0.0, hi=1.0)
-        shares.append((u * torch.tensor([bhi[a] - blo[a] for a in range(3)], device=dev)
-                       + torch.tensor(blo, device=dev)).contiguous())
+    if args.gen == "uniform" and not args.xyz:
+        for r in range(W):
+            blo, bhi = SpatialDecomposition(W, (0.0,) * 3, (1000.0,) * 3).rank_box(r)
+            u = uniform_cloud(args.n, seed=args.seed + 7919 * r, device=dev, lo=0.0, hi=1.0)
+            shares.append((u * torch.tensor([bhi[a] - blo[a] for a in range(3)], device=dev)
+                           + torch.tensor(blo, device=dev)).contiguous())
+    else:
+        # one W x n cloud of the requested distribution, dealt to the ranks in input order (not
+        # spatially): the routing (count-balanced boxes by default) redistributes it
+        n1 = args.n
+        args.n = n1 * W
+        cloud = make_cloud(args, dev)
+        args.n = n1
+        shares = [c.contiguous() for c in cloud.chunk(W)]
     log(f"loopback: {W} ranks x {args.n} points")
     times = []
 
@@ -329,8 +338,12 @@ def run_loopback_bench(args) -> dict:
             checked += c["checked"]
         chk = {"checked": checked, "bad_rows": bad}
     st = out[0].stats
-    return {"t": dt, "n_total": args.n * W, "check": chk,
-            "stats": {k: st[k] for k in ("n_halo", "halo_width", "rounds", "grid")}}
+    owned = [r.stats["n_owned"] for r in out]
+    halo = [r.stats["n_halo"] for r in out]
+    return {"t": dt, "n_total": sum(s.size(0) for s in shares), "check": chk,
+            "stats": {**{k: st[k] for k in ("n_halo", "halo_width", "rounds", "grid")},
+                      "owned_max_over_mean": max(owned) / (sum(owned) / len(owned)),
+                      "halo_frac_max": max(h / max(1, o) for h, o in zip(halo, owned))}}
 
 
 def run_cpu_oracle(args) -> dict:

@@ -22,12 +22,25 @@ struct RouteParams {
     int id_offset;  // global id of this rank's first point (route_scatter with ids == nullptr)
     float box_lo[kRouteMaxWorld][3];  // rank boxes (same formula as SpatialDecomposition.rank_box)
     float box_hi[kRouteMaxWorld][3];
+    // Count-balanced decomposition (balanced = 1): the owner comes from kd splits instead of the
+    // equal-volume grid formula -- x splits, then y splits per x slab, then z splits per (x, y)
+    // column, each set chosen at global quantiles (SpatialDecomposition.splits, the same layout):
+    //   xs[0..px]                       (xs[0] = lo, xs[px] = hi)
+    //   ys[ix * (py + 1) + j], j <= py
+    //   zs[(ix + px * iy) * (pz + 1) + j], j <= pz
+    int balanced;
+    float xs[kRouteMaxWorld + 1];
+    float ys[2 * kRouteMaxWorld];
+    float zs[2 * kRouteMaxWorld];
 };
+// floats in a splits array for decomposition grid g (kd layout above)
+inline int route_split_count(const int g[3]) { return (g[0] + 1) + g[0] * (g[1] + 1) + g[0] * g[1] * (g[2] + 1); }
 
 // Device-side plan header (doubles) written by launch_route_plan for the host's one sync:
-constexpr int kPlanHdr = 16;
+constexpr int kPlanHdr = 24;
 // [0..2] global lo  [3..5] global hi  [6] h (certification halo)  [7] h_send  [8] n_total
 // [9] id offset of this rank  [10] 1 if the halo covers the whole domain  [11] domain diagonal
+// [12..14] this rank's box lo  [15..17] its box hi
 
 // Receive-side table: source s's segment starts at seg[s], holds own[s] owned rows then its
 // halo rows; owned rows of all sources go first (own_pref), then halo rows (halo_pref).
@@ -73,8 +86,9 @@ hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int 
 // Writes the RouteParams for decomposition `grid` (px*py*pz == world) and the plan header:
 // global domain, h = halo_factor x expected K-th neighbour radius of the whole cloud, the
 // send width (h plus rounding slack; the whole domain once h reaches its diagonal), id offset.
+// splits: optional device array (route_split_count(grid) floats): count-balanced boxes.
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
-                             double halo_factor, RouteParams* p, double* hdr, hipStream_t s);
+                             double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s);
 // Local meta of a rank's share: out = {lo[3], hi[3], n, 0} (doubles; +-inf box when n == 0).
 // words: kBBoxWords scratch words (kn/kernels.h). One all_gather of `out` gives the global
 // domain and the id offsets.

@@ -30,6 +30,17 @@ constexpr int kRT = 256;                      // threads per routing block
 constexpr int kRounds = kRouteItems / kRT;    // points per thread
 
 __device__ __forceinline__ int route_owner(const RouteParams& p, float x, float y, float z) {
+    if (p.balanced) {
+        // kd splits: the number of inner splits <= the coordinate on each level (a point on a
+        // split belongs to the upper box), as SpatialDecomposition.owner
+        const int px = p.grid[0], py = p.grid[1], pz = p.grid[2];
+        int ix = 0, iy = 0, iz = 0;
+        for (int j = 1; j < px; ++j) ix += p.xs[j] <= x ? 1 : 0;
+        for (int j = 1; j < py; ++j) iy += p.ys[ix * (py + 1) + j] <= y ? 1 : 0;
+        const int col = ix + px * iy;
+        for (int j = 1; j < pz; ++j) iz += p.zs[col * (pz + 1) + j] <= z ? 1 : 0;
+        return ix + px * (iy + py * iz);
+    }
     const float v[3] = {x, y, z};
     int c[3];
 #pragma unroll
@@ -225,8 +236,8 @@ __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restr
 // One thread: global domain, halo width, rank boxes and id offset from the gathered metas.
 // Formulas follow SpatialDecomposition / DistributedKNearests (parallel/*.py) in double.
 __global__ void route_plan_kernel(const double* __restrict__ metas, int world, int rank, int gx, int gy, int gz,
-                                  int k, double halo_factor, RouteParams* __restrict__ p,
-                                  double* __restrict__ hdr) {
+                                  int k, double halo_factor, const float* __restrict__ splits,
+                                  RouteParams* __restrict__ p, double* __restrict__ hdr) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     double lo[3], hi[3];
     double ntot = 0.0, off = 0.0;
@@ -268,24 +279,47 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     const float hf = (float)hs;
     p->h2 = hf * hf;
     p->id_offset = (int)off;
+    p->balanced = splits ? 1 : 0;
+    const int nxs = gx + 1, nys = gx * (gy + 1), nzs = gx * gy * (gz + 1);
+    for (int j = 0; j < kRouteMaxWorld + 1; ++j) p->xs[j] = (splits && j < nxs) ? splits[j] : 0.f;
+    for (int j = 0; j < 2 * kRouteMaxWorld; ++j) p->ys[j] = (splits && j < nys) ? splits[nxs + j] : 0.f;
+    for (int j = 0; j < 2 * kRouteMaxWorld; ++j) p->zs[j] = (splits && j < nzs) ? splits[nxs + nys + j] : 0.f;
+    double own_lo[3] = {0, 0, 0}, own_hi[3] = {0, 0, 0};
     for (int r = 0; r < world; ++r) {
         const int c[3] = {r % gx, (r / gx) % gy, r / (gx * gy)};
+        double blo[3], bhi[3];
+        if (splits) {
+            const int col = c[0] + gx * c[1];
+            blo[0] = p->xs[c[0]];
+            bhi[0] = p->xs[c[0] + 1];
+            blo[1] = p->ys[c[0] * (gy + 1) + c[1]];
+            bhi[1] = p->ys[c[0] * (gy + 1) + c[1] + 1];
+            blo[2] = p->zs[col * (gz + 1) + c[2]];
+            bhi[2] = p->zs[col * (gz + 1) + c[2] + 1];
+        } else {
+            for (int a = 0; a < 3; ++a) {
+                const double w = (hi[a] - lo[a]) / g[a];
+                blo[a] = __dadd_rn(lo[a], __dmul_rn((double)c[a], w));
+                bhi[a] = c[a] == g[a] - 1 ? hi[a] : __dadd_rn(lo[a], __dmul_rn((double)(c[a] + 1), w));
+            }
+        }
         for (int a = 0; a < 3; ++a) {
-            const double w = (hi[a] - lo[a]) / g[a];
-            p->box_lo[r][a] = (float)__dadd_rn(lo[a], __dmul_rn((double)c[a], w));
-            p->box_hi[r][a] = (float)(c[a] == g[a] - 1 ? hi[a] : __dadd_rn(lo[a], __dmul_rn((double)(c[a] + 1), w)));
+            p->box_lo[r][a] = (float)blo[a];
+            p->box_hi[r][a] = (float)bhi[a];
+            if (r == rank) { own_lo[a] = blo[a]; own_hi[a] = bhi[a]; }
         }
     }
     for (int r = world; r < kRouteMaxWorld; ++r)  // unused slots: defined bytes (plans compare equal)
         for (int a = 0; a < 3; ++a) p->box_lo[r][a] = p->box_hi[r][a] = 0.f;
     for (int a = 0; a < 3; ++a) { hdr[a] = lo[a]; hdr[3 + a] = hi[a]; }
+    for (int a = 0; a < 3; ++a) { hdr[12 + a] = own_lo[a]; hdr[15 + a] = own_hi[a]; }
     hdr[6] = h;
     hdr[7] = hs;
     hdr[8] = ntot;
     hdr[9] = off;
     hdr[10] = full ? 1.0 : 0.0;
     hdr[11] = diag;
-    for (int i = 12; i < kPlanHdr; ++i) hdr[i] = 0.0;
+    for (int i = 18; i < kPlanHdr; ++i) hdr[i] = 0.0;
 }
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
@@ -368,10 +402,11 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
 }
 
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
-                             double halo_factor, RouteParams* p, double* hdr, hipStream_t s) {
+                             double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s) {
     if (world < 1 || world > kRouteMaxWorld || grid[0] * grid[1] * grid[2] != world || rank < 0 || rank >= world)
         return hipErrorInvalidValue;
-    route_plan_kernel<<<1, 64, 0, s>>>(metas, world, rank, grid[0], grid[1], grid[2], k, halo_factor, p, hdr);
+    route_plan_kernel<<<1, 64, 0, s>>>(metas, world, rank, grid[0], grid[1], grid[2], k, halo_factor, splits, p,
+                                       hdr);
     return hipGetLastError();
 }
 

@@ -159,7 +159,7 @@ kn_status solve_round(kn_multi* m, double hf, std::vector<Round>& rd, bool* done
         RankState& R = m->r[i];
         KN_M(hipSetDevice(R.dev));
         KN_M(hipMemcpyAsync(R.metas, metas.data(), metas.size() * sizeof(double), hipMemcpyHostToDevice, R.s));
-        KN_M(kn::launch_route_plan(R.metas, W, i, grid, k, hf, R.plan, R.hdr, R.s));
+        KN_M(kn::launch_route_plan(R.metas, W, i, grid, k, hf, nullptr, R.plan, R.hdr, R.s));
         KN_M(kn::launch_route_count(R.pts, R.n, R.plan, W, R.bc, R.totals, R.s));
         KN_M(hipMemcpyAsync(&tot[(size_t)2 * W * i], R.totals, 2 * W * sizeof(int), hipMemcpyDeviceToHost, R.s));
         if (i == 0) KN_M(hipMemcpyAsync(hdr.data(), R.hdr, kn::kPlanHdr * sizeof(double), hipMemcpyDeviceToHost, R.s));

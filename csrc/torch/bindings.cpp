@@ -250,7 +250,8 @@ torch::Tensor to_stored_space(torch::Tensor out_orig, torch::Tensor perm) {
 
 // ---- multi-GPU routing (csrc/kernels/route.hip) -------------------------------------
 kn::RouteParams route_params(const std::vector<double>& lo, const std::vector<double>& hi,
-                             const std::vector<int64_t>& grid, const std::vector<double>& boxes, double h) {
+                             const std::vector<int64_t>& grid, const std::vector<double>& boxes, double h,
+                             const c10::optional<std::vector<double>>& splits = c10::nullopt) {
     TORCH_CHECK(lo.size() == 3 && hi.size() == 3 && grid.size() == 3, "lo/hi/grid must have 3 entries");
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld, "world size must be in [1, 64]");
@@ -272,6 +273,18 @@ kn::RouteParams route_params(const std::vector<double>& lo, const std::vector<do
             p.box_lo[r][a] = (float)boxes[6 * r + a];
             p.box_hi[r][a] = (float)boxes[6 * r + 3 + a];
         }
+    if (splits.has_value()) {
+        const int g[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
+        TORCH_CHECK((int)splits->size() == kn::route_split_count(g), "splits do not match the grid");
+        const int nxs = g[0] + 1, nys = g[0] * (g[1] + 1);
+        p.balanced = 1;
+        for (int j = 0; j < (int)splits->size(); ++j) {
+            const float v = (float)(*splits)[j];
+            if (j < nxs) p.xs[j] = v;
+            else if (j < nxs + nys) p.ys[j - nxs] = v;
+            else p.zs[j - nxs - nys] = v;
+        }
+    }
     return p;
 }
 
@@ -323,28 +336,38 @@ torch::Tensor route_scatter_impl(const torch::Tensor& points, const c10::optiona
 
 // -> (scanned block counts, totals (world, 2) = owned / halo rows per destination)
 std::vector<torch::Tensor> route_count(torch::Tensor points, std::vector<double> lo, std::vector<double> hi,
-                                       std::vector<int64_t> grid, std::vector<double> boxes, double h) {
+                                       std::vector<int64_t> grid, std::vector<double> boxes, double h,
+                                       c10::optional<std::vector<double>> splits) {
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
-    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h);
+    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h, splits);
     auto dp = upload_params(p, points.device());
     return route_count_impl(points, params_ptr(dp), p.world);
 }
 
 torch::Tensor route_scatter(torch::Tensor points, torch::Tensor ids, std::vector<double> lo, std::vector<double> hi,
                             std::vector<int64_t> grid, std::vector<double> boxes, double h, torch::Tensor block_offsets,
-                            torch::Tensor totals, int64_t rows) {
+                            torch::Tensor totals, int64_t rows, c10::optional<std::vector<double>> splits) {
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
-    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h);
+    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h, splits);
     auto dp = upload_params(p, points.device());
     return route_scatter_impl(points, ids, params_ptr(dp), p.world, block_offsets, totals, rows);
+}
+
+const float* splits_ptr(const c10::optional<torch::Tensor>& splits, const std::vector<int64_t>& grid) {
+    if (!splits.has_value()) return nullptr;
+    const int g[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
+    TORCH_CHECK(splits->is_cuda() && splits->scalar_type() == torch::kFloat32 && splits->is_contiguous() &&
+                    splits->numel() == kn::route_split_count(g),
+                "splits must be a contiguous float32 GPU tensor in the kd layout of the grid");
+    return splits->data_ptr<float>();
 }
 
 // Device-side plan from the all-gathered metas (world x 8 float64, on device): no host sync.
 // -> (plan (uint8 RouteParams on device), header (16,) float64 on device, see kn::kPlanHdr)
 std::vector<torch::Tensor> route_plan(torch::Tensor metas, int64_t rank, std::vector<int64_t> grid, int64_t k,
-                                      double halo_factor) {
+                                      double halo_factor, c10::optional<torch::Tensor> splits) {
     TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
                     metas.numel() % 8 == 0,
                 "metas must be a contiguous (world*8,) float64 GPU tensor");
@@ -356,7 +379,7 @@ std::vector<torch::Tensor> route_plan(torch::Tensor metas, int64_t rank, std::ve
     const int g[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor,
-                                       reinterpret_cast<kn::RouteParams*>(plan.data_ptr<uint8_t>()),
+                                       splits_ptr(splits, grid), reinterpret_cast<kn::RouteParams*>(plan.data_ptr<uint8_t>()),
                                        hdr.data_ptr<double>(), s));
     return {plan, hdr};
 }
@@ -389,7 +412,7 @@ torch::Tensor route_scatter_dev(torch::Tensor points, c10::optional<torch::Tenso
 // -> (plan, sync, scanned block counts, send (cap, 4))
 std::vector<torch::Tensor> route_begin(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor metas,
                                        int64_t rank, std::vector<int64_t> grid, int64_t k, double halo_factor,
-                                       int64_t cap) {
+                                       int64_t cap, c10::optional<torch::Tensor> splits) {
     check_points(points, true);
     TORCH_CHECK(cap >= 0 && cap < INT32_MAX, "cap out of range");
     TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
@@ -415,7 +438,8 @@ std::vector<torch::Tensor> route_begin(torch::Tensor points, c10::optional<torch
     int* totals = sync.data_ptr<int>() + 2 * kn::kPlanHdr;
     const int g[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-    KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor, pp,
+    KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor,
+                                       splits_ptr(splits, grid), pp,
                                        reinterpret_cast<double*>(sync.data_ptr<int>()), s));
     KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, pp, world, bc.data_ptr<int>(), totals, s));
     KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, world, bc.data_ptr<int>(), totals,
@@ -510,7 +534,7 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
                                       std::vector<int64_t> recv_halo, int64_t rank, std::vector<int64_t> grid,
                                       std::vector<double> hdr, int64_t k, double ppc, bool deterministic,
                                       int64_t exact_grid = 0) {
-    TORCH_CHECK(grid.size() == 3 && hdr.size() >= 12, "grid must have 3 entries, hdr >= 12");
+    TORCH_CHECK(grid.size() == 3 && hdr.size() >= 18, "grid must have 3 entries, hdr >= 18");
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world == (int64_t)recv_own.size(), "grid does not match the source table");
     auto pg = route_unpack_split(recv, self_rows, recv_own, recv_halo, rank);
@@ -522,10 +546,9 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     std::vector<double> complete(6), box(6);
     std::vector<double> ext(3);
     for (int a = 0; a < 3; ++a) {
+        // the rank's box (equal-volume or count-balanced) as the plan kernel computed it
         const double lo = hdr[a], hi = hdr[3 + a];
-        const double w = (hi - lo) / (double)grid[a];
-        const double blo = lo + (double)c[a] * w;
-        const double bhi = c[a] == grid[a] - 1 ? hi : lo + (double)(c[a] + 1) * w;
+        const double blo = hdr[12 + a], bhi = hdr[15 + a];
         const double inf = std::numeric_limits<double>::infinity();
         complete[a] = full ? -inf : (c[a] == 0 ? -inf : blo - h);
         complete[3 + a] = full ? inf : (c[a] == grid[a] - 1 ? inf : bhi + h);
@@ -822,8 +845,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");
     m.def("refine_dims", &refine_dims, "finer grid dims for an over-occupied grid, or None");
     m.def("local_meta", &local_meta, "multi-GPU: {lo[3], hi[3], n, 0} of the local points (float64, on device)");
-    m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts");
-    m.def("route_plan", &route_plan, "multi-GPU: device-side routing plan from the gathered metas (no host sync)");
+    m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts",
+          py::arg("points"), py::arg("lo"), py::arg("hi"), py::arg("grid"), py::arg("boxes"), py::arg("h"),
+          py::arg("splits") = py::none());
+    m.def("route_plan", &route_plan, "multi-GPU: device-side routing plan from the gathered metas (no host sync)",
+          py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"), py::arg("halo_factor"),
+          py::arg("splits") = py::none());
     m.def("route_count_dev", &route_count_dev, "multi-GPU: route_count with the device plan");
     m.def("route_scatter_dev", &route_scatter_dev, "multi-GPU: route_scatter with the device plan (ids=None: offset + i)",
           py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("world"), py::arg("block_offsets"),
@@ -831,7 +858,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("route_begin", &route_begin,
           "multi-GPU: plan + counts + scatter (self-last layout, cap rows) enqueued in one call",
           py::arg("points"), py::arg("ids"), py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"),
-          py::arg("halo_factor"), py::arg("cap"));
+          py::arg("halo_factor"), py::arg("cap"), py::arg("splits") = py::none());
     m.def("query_external", &query_external,
           "multi-GPU query forwarding: exact K nearest of external points among a local grid");
     m.def("steady_flag", &steady_flag, "multi-GPU: on-device check of a sync-free steady-state step");
@@ -842,7 +869,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("exact_grid") = 0);
     m.def("route_unpack_split", &route_unpack_split,
           "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
-    m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer");
+    m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer",
+          py::arg("points"), py::arg("ids"), py::arg("lo"), py::arg("hi"), py::arg("grid"), py::arg("boxes"),
+          py::arg("h"), py::arg("block_offsets"), py::arg("totals"), py::arg("rows"), py::arg("splits") = py::none());
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")
         .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t, bool, int64_t>(),

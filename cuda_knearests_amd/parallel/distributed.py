@@ -34,11 +34,12 @@ from typing import Optional
 import torch
 
 from ..ops import knn_ops as ops
-from .decomposition import SpatialDecomposition, factor3
+from .decomposition import SpatialDecomposition, balanced_splits, factor3
 from .transport import HostStagedTransport, TorchDistTransport
 
 INF = math.inf
-HDR = 16  # doubles in the device plan header (kn::kPlanHdr, csrc/include/kn/route.h)
+HDR = 24  # doubles in the device plan header (kn::kPlanHdr, csrc/include/kn/route.h)
+META_I32 = 16  # one rank's meta (8 float64) as int32 words
 
 
 def _pack(points: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
@@ -101,8 +102,14 @@ class DistributedKNearests:
     # tail ~1e-13 per query for +4 % halo points per rank.
     def __init__(self, k: int = 16, group=None, halo_factor: float = 2.5, points_per_cell: float = 0.0,
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
-                 transport=None, device_plan: bool = True, timeout_s: Optional[float] = None):
+                 transport=None, device_plan: bool = True, timeout_s: Optional[float] = None,
+                 balance: str = "count"):
         self.k = int(k)
+        if balance not in ("count", "volume"):
+            raise ValueError("balance must be 'count' or 'volume'")
+        # rank boxes: "count" = kd splits at global quantiles (every rank ~N/world points, also
+        # for clustered clouds), "volume" = equal-volume slices of the domain
+        self.balance = balance
         self.group = group
         self.halo_factor = float(halo_factor)
         self.points_per_cell = float(points_per_cell)
@@ -124,7 +131,7 @@ class DistributedKNearests:
         # metas followed by an all-to-all of the counts. Checked exactly on the host: if any
         # rank's meta changed, the step re-plans with the new metas (one extra round trip).
         self.speculative = True
-        self._spec = None  # (metas on device, metas on host (world, 8) f64, grid)
+        self._spec = None  # (metas on device, metas on host (world, 8) f64, grid, kd splits or None)
         # Steady state (no host synchronisation at all): once a full step has been validated, the
         # next steps assume the same metas and counts, enqueue everything with the known split
         # sizes, and verify the assumption ON THE DEVICE (own meta and send counts unchanged, no
@@ -176,6 +183,18 @@ class DistributedKNearests:
         lo, hi, _ = self.meta(points)
         return lo, hi
 
+    def _splits(self, points: torch.Tensor, metas: torch.Tensor, grid) -> Optional[torch.Tensor]:
+        """Count-balanced kd splits for ``grid`` from this step's points (collective; on the
+        points' device, no host sync), or None for equal-volume boxes / one rank."""
+        if self.balance != "count" or self.world == 1:
+            return None
+        m = metas.view(-1, 8)
+        lo, hi = m[:, 0:3].min(0).values, m[:, 3:6].max(0).values
+        bad = ~(torch.isfinite(lo) & torch.isfinite(hi))
+        lo = torch.where(bad, torch.zeros_like(lo), lo)  # empty global cloud: the unit box
+        hi = torch.where(bad, torch.ones_like(hi), hi)
+        return balanced_splits(points, lo, hi, grid, self.comm.all_gather_cat)
+
     def _use_native(self, points: torch.Tensor) -> bool:
         return points.is_cuda if self.native_route is None else bool(self.native_route)
 
@@ -187,7 +206,7 @@ class DistributedKNearests:
             C = ops.load()
             lo, hi = list(dec.lo), list(dec.hi)
             boxes = dec.boxes()
-            bc, totals = C.route_count(points, lo, hi, list(dec.grid), boxes, float(h_send))
+            bc, totals = C.route_count(points, lo, hi, list(dec.grid), boxes, float(h_send), dec.splits)
             recv_tot = torch.empty_like(totals)
             self.comm.all_to_all_single(recv_tot, totals)
             both = torch.cat([totals, recv_tot]).cpu()  # host sync 2 (send + receive splits)
@@ -195,7 +214,7 @@ class DistributedKNearests:
             recv_own = [int(a) for a, _ in both[self.world:].tolist()]
             recv_halo = [int(b) for _, b in both[self.world:].tolist()]
             send = C.route_scatter(points, ids, lo, hi, list(dec.grid), boxes, float(h_send), bc, totals,
-                                   sum(send_counts))
+                                   sum(send_counts), dec.splits)
             recv = self._a2a(send, send_counts, [a + b for a, b in zip(recv_own, recv_halo)])
             pts, gids = C.route_unpack(recv, recv_own, recv_halo)
             return pts, gids, sum(recv_own)
@@ -245,10 +264,11 @@ class DistributedKNearests:
         local = C.local_meta(points)
         spec = self._spec if (world > 1 and self.speculative) else None
         if spec is not None:
-            metas, grid = spec[0], spec[2]
+            metas, grid, splits = spec[0], spec[2], spec[3]
         else:
             metas = self.comm.all_gather_cat(local) if world > 1 else local  # (world*8,) f64, on device
             grid = self._grid or factor3(world, (1.0, 1.0, 1.0))
+            splits = self._splits(points, metas, grid)
         hf = self.halo_factor
         nh = 2 * HDR
         src_pts, src_ids = points, (ids.to(torch.int32).contiguous() if ids is not None else None)
@@ -258,26 +278,28 @@ class DistributedKNearests:
             rounds += 1
             while True:
                 cap = max(self._send_cap, int(src_pts.size(0) * (1.0 + self.send_headroom)) + 1024)
-                plan, sync, bc, send = C.route_begin(src_pts, src_ids, metas, rank, list(grid), self.k, hf, cap)
+                plan, sync, bc, send = C.route_begin(src_pts, src_ids, metas, rank, list(grid), self.k, hf, cap,
+                                                     splits)
                 totals = sync[nh:nh + 2 * world]
                 if spec is not None:
                     # one all-gather of {meta, counts}; the rows this rank receives are column
                     # `rank` of every source's counts
-                    row = nh // 2 + 2 * world  # int32 per rank: 8 f64 meta + 2*world counts
+                    row = META_I32 + 2 * world  # int32 per rank: 8 f64 meta + 2*world counts
                     gathered = self.comm.all_gather_cat(torch.cat([local.view(torch.int32), totals]))
                     mark(("enqueued", time.perf_counter()))
                     host = torch.cat([sync[:nh], gathered]).cpu()
                     mark(("synced", time.perf_counter()))
                     g = host[nh:].view(world, row)
-                    new_metas = g[:, :16].contiguous().view(torch.float64)
+                    new_metas = g[:, :META_I32].contiguous().view(torch.float64)
                     if not torch.equal(new_metas, spec[1]):
                         # a rank's cloud changed: re-plan with this step's metas (on device)
-                        metas = gathered.view(world, row)[:, :16].contiguous().view(torch.float64).flatten()
+                        metas = gathered.view(world, row)[:, :META_I32].contiguous().view(torch.float64).flatten()
+                        splits = self._splits(points, metas, grid)
                         spec = self._spec = None
                         continue
                     gl = g.tolist()
-                    rt = [v for d in range(world) for v in gl[d][16 + 2 * rank:18 + 2 * rank]]
-                    hv = host[:nh].view(torch.float64).tolist() + gl[rank][16:] + rt
+                    rt = [v for d in range(world) for v in gl[d][META_I32 + 2 * rank:META_I32 + 2 + 2 * rank]]
+                    hv = host[:nh].view(torch.float64).tolist() + gl[rank][META_I32:] + rt
                     meta_host = spec[1]
                 else:
                     if world > 1:  # rows to receive land in the tail of the same sync buffer
@@ -295,13 +317,14 @@ class DistributedKNearests:
                 if want == tuple(grid):
                     break
                 grid = want  # domain shape changed: re-plan with the matching decomposition
+                splits = self._splits(points, metas, grid)
             self._grid = tuple(grid)
             if world > 1 and rounds == 1:
-                self._spec = (metas, meta_host, tuple(grid))
+                self._spec = (metas, meta_host, tuple(grid), splits)
             spec = None  # growth rounds re-route with the normal exchange
             h, hs, full = hv[6], hv[7], hv[10] != 0.0
-            tot = [int(x) for x in hv[16:16 + 2 * world]]
-            rtot = [int(x) for x in hv[16 + 2 * world:16 + 4 * world]] if world > 1 else tot
+            tot = [int(x) for x in hv[HDR:HDR + 2 * world]]
+            rtot = [int(x) for x in hv[HDR + 2 * world:HDR + 4 * world]] if world > 1 else tot
             send_counts = [tot[2 * d] + tot[2 * d + 1] for d in range(world)]
             recv_own = [rtot[2 * d] for d in range(world)]
             recv_halo = [rtot[2 * d + 1] for d in range(world)]
@@ -333,7 +356,7 @@ class DistributedKNearests:
             n_fwd = 0
             if not done and self.forward:
                 # targeted second round: only the uncertified queries travel (query forwarding)
-                n_fwd = self._forward_round(hv, grid, pts, gids, idx, d2, counters, local_grid)
+                n_fwd = self._forward_round(hv, grid, pts, gids, idx, d2, counters, local_grid, splits)
                 rounds += 1
                 done = True
             if done:
@@ -345,7 +368,7 @@ class DistributedKNearests:
         if rounds == 1 and not full and self.steady:
             # validated single-round step: the steady-state assumption for the next ones
             self._steady = {
-                "metas": metas, "grid": tuple(grid), "hdr": hv[:HDR], "cap": int(send.size(0)),
+                "metas": metas, "grid": tuple(grid), "hdr": hv[:HDR], "cap": int(send.size(0)), "splits": splits,
                 "tot": torch.tensor(tot, dtype=torch.int32, device=points.device),
                 "send_counts": send_counts, "recv_own": recv_own, "recv_halo": recv_halo,
                 "cross_send": cross_send, "cross_recv": cross_recv, "x": x,
@@ -357,7 +380,7 @@ class DistributedKNearests:
             self._steady = None
         return DistResult(own_ids, idx, d2, stats)
 
-    def _forward_round(self, hv, grid, pts, gids, idx, d2, counters, local_grid) -> int:
+    def _forward_round(self, hv, grid, pts, gids, idx, d2, counters, local_grid, splits=None) -> int:
         """Query forwarding for the uncertified queries of a round (targeted second round,
         replaces re-routing every owned point with a doubled halo). Each uncertified query q
         with local K-th distance r (an upper bound of the true one: the local set is a subset)
@@ -376,7 +399,7 @@ class DistributedKNearests:
         qg = gids[U]
         r2 = d2[U, k - 1] if n_unc else d2.new_empty(0)
         lo, hi = tuple(hv[0:3]), tuple(hv[3:6])
-        dec = SpatialDecomposition(world, lo, hi, tuple(grid))
+        dec = SpatialDecomposition(world, lo, hi, tuple(grid), splits.tolist() if splits is not None else None)
         # conservative box test: the float32 box arithmetic may not miss a rank
         r2c = torch.where(torch.isfinite(r2), r2 * (1.0 + 1e-5) + 1e-6, torch.full_like(r2, INF))
         masks = []
@@ -449,7 +472,7 @@ class DistributedKNearests:
         src_ids = ids.to(torch.int32).contiguous() if ids is not None else None
         local = C.local_meta(points)
         plan, sync, bc, send = C.route_begin(points, src_ids, st["metas"], rank, list(st["grid"]), self.k,
-                                             self.halo_factor, st["cap"])
+                                             self.halo_factor, st["cap"], st["splits"])
         totals = sync[nh:nh + 2 * world]
         x = st["x"]
         if world > 1:
@@ -547,6 +570,10 @@ class DistributedKNearests:
             off = sum(counts[: self.rank])
             ids = torch.arange(off, off + points.size(0), dtype=torch.int32, device=dev)
         dec = SpatialDecomposition(self.world, lo, hi)
+        if self.balance == "count" and self.world > 1:
+            sp = balanced_splits(points, torch.tensor(lo, dtype=torch.float64), torch.tensor(hi, dtype=torch.float64),
+                                 dec.grid, self.comm.all_gather_cat)
+            dec = SpatialDecomposition(self.world, lo, hi, dec.grid, sp.tolist())
         n_total = sum(counts)
         vol = max(1e-30, (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]))
         h = self.halo_factor * ops.expected_kth_radius(n_total, self.k, vol)

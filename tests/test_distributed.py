@@ -113,7 +113,33 @@ def test_decomposition_factors():
     assert cb[0] == float("-inf") and cb[3] == 510.0
 
 
-def _loopback_check(world, k, gen, device, native, n=6000, halo_factor=1.6, scatter="mod"):
+def test_balanced_splits_kd_layout():
+    # count-balanced kd splits: every point lies in its owner's box, every box holds ~N/world
+    from cuda_knearests_amd.parallel import SpatialDecomposition
+    from cuda_knearests_amd.parallel.decomposition import balanced_splits, split_count
+    from cuda_knearests_amd.utils import clustered_cloud
+
+    pts = clustered_cloud(40000, seed=3)
+    lo, hi = pts.min(0).values.double(), pts.max(0).values.double()
+    for grid in [(2, 2, 2), (2, 1, 1), (3, 2, 1), (1, 1, 4)]:
+        world = grid[0] * grid[1] * grid[2]
+        sp = balanced_splits(pts, lo, hi, grid, lambda t: t)
+        assert sp.dtype == torch.float32 and sp.numel() == split_count(grid)
+        d = SpatialDecomposition(world, tuple(lo.tolist()), tuple(hi.tolist()), grid, sp.tolist())
+        o = d.owner(pts)
+        cnt = torch.bincount(o, minlength=world).double()
+        assert float(cnt.max() / cnt.mean()) < 1.05, (grid, cnt.tolist())
+        for r in range(world):
+            blo, bhi = d.rank_box(r)
+            m = o == r
+            assert bool(((pts[m] >= torch.tensor(blo)) & (pts[m] <= torch.tensor(bhi))).all())
+    # equal-volume boxes of the same clustered cloud are far from balanced
+    dv = SpatialDecomposition(8, tuple(lo.tolist()), tuple(hi.tolist()), (2, 2, 2))
+    cv = torch.bincount(dv.owner(pts), minlength=8).double()
+    assert float(cv.max() / cv.mean()) > 1.3
+
+
+def _loopback_check(world, k, gen, device, native, n=6000, halo_factor=1.6, scatter="mod", balance="count"):
     """Run the distributed solve on `world` virtual ranks (threads, LoopbackTransport) and
     compare the union of the per-rank results with the single-process kd-tree oracle."""
     import cuda_knearests_amd as kn
@@ -126,7 +152,7 @@ def _loopback_check(world, k, gen, device, native, n=6000, halo_factor=1.6, scat
 
     def fn(t):
         m = owner == t.rank
-        dk = DistributedKNearests(k=k, halo_factor=halo_factor, transport=t, native_route=native)
+        dk = DistributedKNearests(k=k, halo_factor=halo_factor, transport=t, native_route=native, balance=balance)
         r = dk.solve(cloud[m].contiguous().to(device), ids[m].contiguous().to(device))
         return r.ids.cpu(), r.neighbors.cpu(), r.d2.cpu(), r.stats
 
@@ -146,6 +172,16 @@ def _loopback_check(world, k, gen, device, native, n=6000, halo_factor=1.6, scat
 @pytest.mark.parametrize("world,gen", [(3, "uniform"), (8, "clustered")])
 def test_loopback_cpu_matches_single(world, gen):
     _loopback_check(world, 8, gen, "cpu", native=False)
+
+
+def test_loopback_cpu_clustered_balanced_owners():
+    # clustered cloud over 8 ranks: exact, and count-balanced boxes keep max/mean owned <= 1.3
+    out = _loopback_check(8, 16, "clustered", "cpu", native=False, n=16000)
+    own = torch.tensor([s["n_owned"] for *_, s in out], dtype=torch.float64)
+    assert float(own.max() / own.mean()) <= 1.3, own.tolist()
+    outv = _loopback_check(8, 16, "clustered", "cpu", native=False, n=16000, balance="volume")
+    ownv = torch.tensor([s["n_owned"] for *_, s in outv], dtype=torch.float64)
+    assert float(ownv.max() / ownv.mean()) > float(own.max() / own.mean())
 
 
 def test_loopback_cpu_growth_round():

@@ -46,6 +46,45 @@ def test_native_router_matches_torch(cuda, ext, world, h):
     assert torch.equal(gids, exp[:, 3].contiguous().view(torch.int32))
 
 
+@pytest.mark.parametrize("world", [2, 8, 12])
+def test_native_router_balanced_matches_torch(cuda, ext, world):
+    # count-balanced kd boxes: the native router's owner / halo decisions == the torch reference
+    from cuda_knearests_amd.parallel.decomposition import balanced_splits
+    from cuda_knearests_amd.utils import clustered_cloud
+
+    n = 50_000
+    p = clustered_cloud(n, seed=world).to(cuda)
+    ids = torch.arange(n, dtype=torch.int32, device=cuda)
+    lo_t, hi_t = p.min(0).values.double(), p.max(0).values.double()
+    lo, hi = tuple(lo_t.tolist()), tuple(hi_t.tolist())
+    grid = SpatialDecomposition(world, lo, hi).grid
+    sp = balanced_splits(p, lo_t, hi_t, grid, lambda t: t)
+    dec = SpatialDecomposition(world, lo, hi, grid, sp.tolist())
+    hs = halo_send_width(12.0, lo, hi)
+    ref, cnt = route_rows_torch(dec, p, ids, hs)
+    own = cnt[:, 0].double()
+    assert float(own.max() / own.mean()) < 1.05
+    bc, totals = ext.route_count(p, list(lo), list(hi), list(grid), dec.boxes(), hs, dec.splits)
+    assert torch.equal(totals, cnt)
+    send = ext.route_scatter(p, ids, list(lo), list(hi), list(grid), dec.boxes(), hs, bc, totals, ref.size(0),
+                             dec.splits)
+    assert torch.equal(send.view(torch.int32), ref.view(torch.int32))
+    # device plan with the same splits: same boxes (and this rank's box in the header)
+    metas = ext.local_meta(p).repeat(world).contiguous()
+    plan, hdr = ext.route_plan(metas, world - 1, list(grid), 16, 2.5, sp)
+    blo, bhi = dec.rank_box(world - 1)
+    assert hdr[12:18].cpu().tolist() == list(blo) + list(bhi)
+    bc2, totals2 = ext.route_count_dev(p, plan, world)
+    assert torch.equal(totals2[:, 0], cnt[:, 0])
+
+
+def test_loopback_gpu_clustered_balanced(cuda):
+    # 8 virtual ranks, clustered cloud: exact, and the count-balanced boxes hold max/mean <= 1.3
+    out = _loopback_check(8, 16, "clustered", cuda, native=True, n=40000, scatter="random")
+    own = torch.tensor([s["n_owned"] for *_, s in out], dtype=torch.float64)
+    assert float(own.max() / own.mean()) <= 1.3, own.tolist()
+
+
 @pytest.mark.parametrize("world,k,gen", [(2, 16, "uniform"), (4, 8, "clustered"), (8, 16, "uniform"), (8, 50, "uniform")])
 def test_loopback_gpu_matches_single(cuda, world, k, gen):
     _loopback_check(world, k, gen, cuda, native=True, n=30000, scatter="random")
@@ -229,7 +268,7 @@ def test_route_begin_self_last(cuda, ext, world, rank):
     metas = ext.local_meta(p).repeat(world).contiguous()  # every rank "has" the same box
     grid = list(factor3(world, (1.0, 1.0, 1.0)))
     plan, sync, bc, send = ext.route_begin(p, ids, metas, rank, grid, 16, 2.5, world * n + 1024)
-    hdr, totals = sync[:32].view(torch.float64), sync[32:32 + 2 * world].view(world, 2)
+    hdr, totals = sync[:48].view(torch.float64), sync[48:48 + 2 * world].view(world, 2)
     plan2, hdr2 = ext.route_plan(metas, rank, grid, 16, 2.5)
     assert torch.equal(plan, plan2) and torch.equal(hdr, hdr2)
     bc2, totals2 = ext.route_count_dev(p, plan2, world)
