@@ -140,9 +140,22 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     const int tx = tile % a.ntx, ty = (tile / a.ntx) % a.nty, tz = tile / (a.ntx * a.nty);
     const int tx0 = tx * a.TX, ty0 = ty * a.TY, tz0 = tz * a.TZ;
     const int tx1 = min(a.X, tx0 + a.TX), ty1 = min(a.Y, ty0 + a.TY), tz1 = min(a.Z, tz0 + a.TZ);
-    const int sx0 = max(0, tx0 - a.H), sx1 = min(a.X, tx1 + a.H);
-    const int sy0 = max(0, ty0 - a.H), sy1 = min(a.Y, ty1 + a.H);
-    const int sz0 = max(0, tz0 - a.H), sz1 = min(a.Z, tz1 + a.H);
+    // Staged block: the tile + H rings, clipped to the grid. With the whole-block lane walk
+    // (kFull, K > 40) a block that would be clipped at a domain face is SHIFTED inward instead:
+    // the same number of cells (so the same LDS plan), but the tile's boundary queries -- whose
+    // K-th ball is a half/quarter/eighth ball up to 2x the interior radius -- reach T + 2H - 1
+    // cells inward instead of H and certify on the tile path instead of the exact kernel.
+    int sx0, sx1, sy0, sy1, sz0, sz1;
+    if constexpr (kFull) {
+        const int wx = a.TX + 2 * a.H, wy = a.TY + 2 * a.H, wz = a.TZ + 2 * a.H;
+        sx0 = max(0, min(tx0 - a.H, a.X - wx)); sx1 = min(a.X, sx0 + wx);
+        sy0 = max(0, min(ty0 - a.H, a.Y - wy)); sy1 = min(a.Y, sy0 + wy);
+        sz0 = max(0, min(tz0 - a.H, a.Z - wz)); sz1 = min(a.Z, sz0 + wz);
+    } else {
+        sx0 = max(0, tx0 - a.H); sx1 = min(a.X, tx1 + a.H);
+        sy0 = max(0, ty0 - a.H); sy1 = min(a.Y, ty1 + a.H);
+        sz0 = max(0, tz0 - a.H); sz1 = min(a.Z, tz1 + a.H);
+    }
     const int nxs = sx1 - sx0, nys = sy1 - sy0, nzs = sz1 - sz0;
     const int nrows = nys * nzs;
     const int cbs = nxs + 1;

@@ -1,5 +1,6 @@
 // api.cpp -- C API (knearests.h) on top of kn::Engine.
 // Reference: knearests.cu:235-466 (kn_prepare / kn_solve / kn_free / getters / stats).
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -52,6 +53,21 @@ kn::EngineConfig to_engine(const kn_config* c) {
 }
 }  // namespace
 
+// Log level from the environment, shared with the Python package (utils.get_logger):
+// KN_LOG = DEBUG -> 2 (debug), INFO -> 1 (timings, as the reference's IF_VERBOSE), WARNING /
+// ERROR -> 0; KN_VERBOSE=<int> overrides. `dflt` when neither is set.
+static int env_verbosity(int dflt) {
+    if (const char* v = std::getenv("KN_VERBOSE")) return std::atoi(v);
+    if (const char* l = std::getenv("KN_LOG")) {
+        std::string s(l);
+        for (auto& ch : s) ch = (char)std::toupper((unsigned char)ch);
+        if (s == "DEBUG") return 2;
+        if (s == "INFO") return 1;
+        if (s == "WARNING" || s == "WARN" || s == "ERROR" || s == "CRITICAL") return 0;
+    }
+    return dflt;
+}
+
 extern "C" {
 
 void kn_set_last_error_internal(const char* msg) { g_err = msg ? msg : ""; }
@@ -61,7 +77,7 @@ kn_config kn_default_config(void) {
     std::memset(&c, 0, sizeof(c));
     c.k = KN_DEFAULT_K;
     c.deterministic = 1;
-    c.verbose = 0;
+    c.verbose = env_verbosity(0);
     return c;
 }
 
@@ -83,8 +99,7 @@ kn_problem* kn_prepare_ex(const kn_float3* points, int numpoints, const kn_confi
 
 kn_problem* kn_prepare(const kn_float3* points, int numpoints) {
     kn_config c = kn_default_config();
-    c.verbose = 1;  // reference prints its timings (IF_VERBOSE, params.h:6)
-    if (const char* v = std::getenv("KN_VERBOSE")) c.verbose = std::atoi(v);
+    c.verbose = env_verbosity(1);  // reference prints its timings (IF_VERBOSE, params.h:6)
     return kn_prepare_ex(points, numpoints, &c);
 }
 

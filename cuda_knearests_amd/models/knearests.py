@@ -18,6 +18,7 @@ replays it afterwards (the bench path).
 """
 from __future__ import annotations
 
+import logging
 import sys
 import time
 from typing import Optional
@@ -27,6 +28,9 @@ import torch
 
 from ..ops import knn_ops as ops
 from .._ext import load
+from ..utils import get_logger
+
+_log = get_logger()
 
 
 class KNearests:
@@ -48,7 +52,10 @@ class KNearests:
         self.deterministic = bool(deterministic)
         self.use_tiles = bool(use_tiles)
         self.with_distances = bool(with_distances)
+        # verbose=True logs the reference's timing lines at WARNING (always shown); otherwise
+        # they are INFO records of the "knearests" logger (env KN_LOG=INFO shows them)
         self.verbose = verbose
+        self._lvl = logging.WARNING if verbose else logging.INFO
         self.grid: Optional[ops.Grid] = None
         self.points: Optional[torch.Tensor] = None
         self.neighbors: Optional[torch.Tensor] = None
@@ -86,8 +93,8 @@ class KNearests:
         t1.record()
         t1.synchronize()
         self.timings["ms_build"] = t0.elapsed_time(t1)
-        if self.verbose:
-            print(f"kn_firstbuild: {self.timings['ms_build']:.3f} msec", file=sys.stderr)
+        _log.log(self._lvl, "kn_firstbuild: %.3f msec (grid %s, algo %s)", self.timings["ms_build"],
+                 self.grid.plan.dims, self.grid.extra.get("algo", "grid"))
         return self
 
     def solve(self) -> "KNearests":
@@ -100,6 +107,7 @@ class KNearests:
             self.timings["ms_solve"] = (time.perf_counter() - t) * 1e3
             self.neighbors, self.distances = idx, d2
             self.info = {"uncertified": int(unc.numel()), "exact_path": 0}
+            _log.log(self._lvl, "kn_solve (cpu): %.3f msec (%s)", self.timings["ms_solve"], self.info)
             return self
         t0 = torch.cuda.Event(enable_timing=True)
         t1 = torch.cuda.Event(enable_timing=True)
@@ -113,8 +121,10 @@ class KNearests:
         algo = self.grid.extra.get("algo", "grid") if self.algo == "auto" else self.algo
         self.info = {"exact_path": int(c[0]), "uncertified": int(c[1]), "dense_tiles": int(c[2]), "algo": algo}
         self.neighbors, self.distances = idx, d2
-        if self.verbose:
-            print(f"kn_solve: {self.timings['ms_solve']:.3f} msec ({self.info})", file=sys.stderr)
+        _log.log(self._lvl, "kn_solve: %.3f msec (%s)", self.timings["ms_solve"], self.info)
+        if self.info["exact_path"] > max(1024, self.grid.n // 100):
+            _log.warning("kn_solve: %d of %d queries took the exact path (strongly non-uniform cloud?)",
+                         self.info["exact_path"], self.grid.n)
         return self
 
     def set_k(self, k: int) -> "KNearests":

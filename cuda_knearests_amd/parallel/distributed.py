@@ -35,7 +35,10 @@ import torch
 
 from ..ops import knn_ops as ops
 from .decomposition import SpatialDecomposition, balanced_splits, factor3
+from ..utils import get_logger
 from .transport import HostStagedTransport, TorchDistTransport
+
+_log = get_logger("knearests.dist")
 
 INF = math.inf
 HDR = 24  # doubles in the device plan header (kn::kPlanHdr, csrc/include/kn/route.h)
@@ -293,6 +296,7 @@ class DistributedKNearests:
                     new_metas = g[:, :META_I32].contiguous().view(torch.float64)
                     if not torch.equal(new_metas, spec[1]):
                         # a rank's cloud changed: re-plan with this step's metas (on device)
+                        _log.info("rank %d: speculative routing plan stale (a rank's meta changed), re-planning", rank)
                         metas = gathered.view(world, row)[:, :META_I32].contiguous().view(torch.float64).flatten()
                         splits = self._splits(points, metas, grid)
                         spec = self._spec = None
@@ -316,6 +320,7 @@ class DistributedKNearests:
                 want = factor3(world, tuple(max(hi[a] - lo[a], 1e-30) for a in range(3)))
                 if want == tuple(grid):
                     break
+                _log.info("rank %d: domain shape asks for rank grid %s (was %s), re-planning", rank, want, tuple(grid))
                 grid = want  # domain shape changed: re-plan with the matching decomposition
                 splits = self._splits(points, metas, grid)
             self._grid = tuple(grid)
@@ -331,6 +336,7 @@ class DistributedKNearests:
             need = sum(send_counts)
             self._send_cap = max(self._send_cap, need + need // 8 + 1024)
             if need > send.size(0):  # did not fit: route_begin wrote nothing, scatter again
+                _log.debug("rank %d: send buffer %d < %d rows, re-scattering", rank, send.size(0), need)
                 send = C.route_scatter_dev(src_pts, src_ids, plan, world, bc, totals, need, rank)
             cross_send = [0 if d == rank else send_counts[d] for d in range(world)]
             cross_recv = [0 if d == rank else recv_own[d] + recv_halo[d] for d in range(world)]
@@ -357,14 +363,17 @@ class DistributedKNearests:
             if not done and self.forward:
                 # targeted second round: only the uncertified queries travel (query forwarding)
                 n_fwd = self._forward_round(hv, grid, pts, gids, idx, d2, counters, local_grid, splits)
+                _log.info("rank %d: %d uncertified queries (all ranks) answered by query forwarding", rank, n_fwd)
                 rounds += 1
                 done = True
             if done:
                 break
             hf *= 2.0
+            _log.info("rank %d: uncertified queries, growth round %d with halo factor %.3g", rank, rounds + 1, hf)
             src_pts, src_ids = own_pts, own_ids
         stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
                  "grid": tuple(grid), "forwarded": n_fwd}
+        _log.debug("rank %d: step %s", rank, stats)
         if rounds == 1 and not full and self.steady:
             # validated single-round step: the steady-state assumption for the next ones
             self._steady = {
@@ -559,6 +568,8 @@ class DistributedKNearests:
                     if res.stats.get("graph"):  # graph buffers are reused by the next replay
                         res = DistResult(res.ids.clone(), res.neighbors.clone(), res.d2.clone(), res.stats)
                     return res
+                _log.info("rank %d: steady-state step invalid (routing changed or uncertified query), "
+                          "re-solving the full way", self.rank)
                 self._steady = None  # assumption failed or a query is uncertified: the full way
                 self._graph = None
             return self._solve_native(points, ids)

@@ -118,14 +118,18 @@ class DeviceTimer:
 
 
 def get_logger(name: str = "knearests") -> logging.Logger:
-    """Leveled logger; level from env ``KN_LOG`` (DEBUG/INFO/WARNING)."""
-    log = logging.getLogger(name)
-    if not log.handlers:
+    """Leveled logger of the package (``knearests`` or a ``knearests.*`` child). The level comes
+    from env ``KN_LOG`` (DEBUG / INFO / WARNING / ERROR, default WARNING); the same variable sets
+    the native library's verbosity (``kn_default_config``: DEBUG -> 2, INFO -> 1)."""
+    root = logging.getLogger("knearests")
+    if not root.handlers:
         h = logging.StreamHandler(sys.stderr)
         h.setFormatter(logging.Formatter("[%(name)s %(levelname)s] %(message)s"))
-        log.addHandler(h)
-        log.setLevel(os.environ.get("KN_LOG", "WARNING").upper())
-    return log
+        root.addHandler(h)
+        lvl = os.environ.get("KN_LOG", "WARNING").upper()
+        root.setLevel(lvl if lvl in ("DEBUG", "INFO", "WARNING", "ERROR", "CRITICAL") else "WARNING")
+        root.propagate = False  # one line per record even when the application configures logging
+    return logging.getLogger(name)
 
 
 def emit_json(obj: dict, file=sys.stdout) -> None:

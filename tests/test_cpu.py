@@ -135,3 +135,44 @@ def test_cpp_unit_cpu_under_asan_ubsan():
     r = subprocess.run([str(exe), "cpu"], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+def test_kn_log_levels(monkeypatch):
+    """KN_LOG drives the package logger (solve lines at INFO) and the native verbosity
+    (kn_default_config().verbose: DEBUG -> 2, INFO -> 1, WARNING -> 0)."""
+    import logging
+
+    from cuda_knearests_amd import KNearests
+    from cuda_knearests_amd.utils import get_logger, uniform_cloud
+
+    records = []
+
+    class H(logging.Handler):
+        def emit(self, r):
+            records.append(r)
+
+    log = get_logger()
+    h = H()
+    log.addHandler(h)
+    old = log.level
+    try:
+        log.setLevel(logging.INFO)
+        KNearests(k=4, device="cpu").prepare(uniform_cloud(500, seed=1)).solve()
+        assert any("kn_solve" in r.getMessage() for r in records)
+        records.clear()
+        log.setLevel(logging.WARNING)
+        KNearests(k=4, device="cpu").prepare(uniform_cloud(500, seed=1)).solve()
+        assert not any("kn_solve" in r.getMessage() for r in records)
+    finally:
+        log.removeHandler(h)
+        log.setLevel(old)
+    from test_capi import KnConfig  # the ctypes mirror of kn_config (size-checked there)
+
+    from cuda_knearests_amd._ext import load_capi
+
+    lib = load_capi()
+    lib.kn_default_config.restype = KnConfig
+    for val, want in (("DEBUG", 2), ("info", 1), ("WARNING", 0)):
+        monkeypatch.setenv("KN_LOG", val)
+        monkeypatch.delenv("KN_VERBOSE", raising=False)
+        assert lib.kn_default_config().verbose == want, val
