@@ -72,6 +72,15 @@ struct BuildBuffers {
     // optional fixed domain (multi-GPU ranks): if use_box, bbox is not computed
     int use_box;
     float box_lo[3], box_hi[3];
+    // optional: words (<= 64) the build zeroes on the device (the following query's counters,
+    // so the step needs no memset node; then QueryBuffers::counters_zeroed = 1)
+    unsigned* zero_words;
+    int n_zero_words;
+    // optional global-id mode (multi-GPU ranks, query.hip row_of): every stored point's w becomes
+    // gids[local index] | 0x80000000 on non-owned points (local index >= n_owned); perm keeps the
+    // local index. Fused into the bucket sort (non-deterministic bucketed build), else one extra pass.
+    const int* gids;
+    int n_owned;
 };
 
 size_t scan_block_count(int num_cells);
@@ -120,6 +129,7 @@ struct QueryBuffers {
     int use_tiles;            // 0: exact ring walk for every query (debug / reference path)
     int flags;                // 1: force the exact re-scan for every query (tests); 2: stream kernel;
                               // 4: LDS-staged tile kernel (neither: env KN_QUERY_ALGO / default)
+    int counters_zeroed;      // 1: the preceding build zeroed `counters` (no memset here)
     int exact_grid;           // workgroups of the fallback launch; 0 = default (sized for long
                               // lists). The engine passes a small grid when the previous solve's
                               // list was short (the launch then costs ~3 us less).

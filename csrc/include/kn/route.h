@@ -65,7 +65,8 @@ int route_block_count(int n);
 // block_counts: 2*world*route_block_count(n) ints (column-major, scanned in place);
 // totals: 2*world ints = (owned, halo) rows per destination.
 hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int world, int* block_counts,
-                              int* totals, hipStream_t s);
+                              int* totals, hipStream_t s,
+                              unsigned* partials = nullptr);
 // ids == nullptr: global id = p->id_offset + local index.
 // self_last < 0: segments in destination order 0..world-1. self_last = rank: the other
 // destinations in order, then the rank's own segment at the end (kept out of the collective).
@@ -95,6 +96,11 @@ hipError_t launch_route_plan(const double* metas, int world, int rank, const int
 hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* out, hipStream_t s);
 // Steady-state check of a sync-free distributed step, one wave: flag[0] = (this rank's meta or
 // send counts differ from the planned ones) + (any uncertified query). No host involvement.
+// Steady step check with the share's bbox taken from route_count's partials (route_block_count(n)
+// blocks x 6 words, [a * nb + block]) instead of a local_meta pass.
+hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const double* planned_meta, const int* totals,
+                                       const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
+                                       hipStream_t stream);
 hipError_t launch_steady_flag(const double* local, const double* planned_meta, const int* totals,
                               const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                               hipStream_t s);

@@ -17,6 +17,7 @@
 #include <cstdlib>
 
 #include "kn/kernels.h"
+#include "kn/route.h"
 #include "kn/wave.h"
 
 namespace kn {
@@ -337,13 +338,16 @@ hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hip
 // ---- bucketed binning ---------------------------------------------------------------
 // A1: per-(bucket, block) counts with LDS atomics, table column = bucket (bucket-major, so the
 // exclusive scan of the table gives every block its write offset inside every bucket).
-__global__ __launch_bounds__(256) void bucket_count_kernel(const float* __restrict__ pts, int n, GeomSrc src,
+__global__ __launch_bounds__(1024) void bucket_count_kernel(const float* __restrict__ pts, int n, GeomSrc src,
                                                            GridGeom* __restrict__ gout, int shift,
                                                            int nbuckets, int nblocks, int per_block,
-                                                           int* __restrict__ table) {
+                                                           int* __restrict__ table, unsigned* __restrict__ zero_words,
+                                                           int n_zero_words) {
     extern __shared__ int hist[];
     __shared__ GridGeom gs;
-    for (int j = threadIdx.x; j < nbuckets; j += 256) hist[j] = 0;
+    // the step's query counters, zeroed here instead of by a separate memset node
+    if (blockIdx.x == 0 && (int)threadIdx.x < n_zero_words) zero_words[threadIdx.x] = 0u;
+    for (int j = threadIdx.x; j < nbuckets; j += blockDim.x) hist[j] = 0;
     if (threadIdx.x < 64) {  // every block derives the geometry; block 0 publishes it
         GridGeom t;
         if (src.use_box) write_geom(&t, src.lo, src.hi, src.dims);
@@ -356,16 +360,16 @@ __global__ __launch_bounds__(256) void bucket_count_kernel(const float* __restri
     __syncthreads();
     const GridGeom g = gs;
     const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
-    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
         atomicAdd(&hist[cell_of(g, p) >> shift], 1);
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < nbuckets; j += 256) table[(size_t)j * nblocks + blockIdx.x] = hist[j];
+    for (int j = threadIdx.x; j < nbuckets; j += blockDim.x) table[(size_t)j * nblocks + blockIdx.x] = hist[j];
 }
 
 // A3: every point to its bucket's segment of bin_tmp as {x, y, z, bits(original index)}
-__global__ __launch_bounds__(256) void bucket_scatter_kernel(const float* __restrict__ pts, int n,
+__global__ __launch_bounds__(1024) void bucket_scatter_kernel(const float* __restrict__ pts, int n,
                                                              const GridGeom* __restrict__ gp, int shift,
                                                              int nbuckets, int nblocks, int per_block,
                                                              const int* __restrict__ tscan,
@@ -382,14 +386,14 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const float* __rest
             if (j0 + j < nbt) { pre[j0 + j] = run; run += tsums[j0 + j]; }
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < nbuckets; j += 256) {
+    for (int j = threadIdx.x; j < nbuckets; j += blockDim.x) {
         const size_t t = (size_t)j * nblocks + blockIdx.x;
         cur[j] = tscan[t] + pre[t / kScanItems];
     }
     __syncthreads();
     const GridGeom g = *gp;
     const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
-    for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
         const int pos = atomicAdd(&cur[cell_of(g, p) >> shift], 1);
         tmp[KN_IDX(pos, n, 104)] = make_float4(p[0], p[1], p[2], __uint_as_float((unsigned)i));
@@ -405,7 +409,8 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
                                                           const int* __restrict__ tsums, int num_cells,
                                                           int* __restrict__ cell_start,
                                                           float4* __restrict__ sorted,
-                                                          unsigned* __restrict__ perm) {
+                                                          unsigned* __restrict__ perm,
+                                                          const int* __restrict__ gids, int n_owned) {
     extern __shared__ int cur[];  // 2^shift cells
     __shared__ int wsum[4];
     __shared__ int seg[2];
@@ -462,8 +467,16 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
         const float4 v = tmp[KN_IDX(k, n, 105)];
         const float p[3] = {v.x, v.y, v.z};
         const int pos = atomicAdd(&cur[cell_of(g, p) - c0], 1);
-        sorted[KN_IDX(pos, n, 107)] = v;
-        perm[pos] = __float_as_uint(v.w);
+        const unsigned local = __float_as_uint(v.w);
+        float4 o = v;
+        if (gids) {  // global-id mode (see BuildBuffers::gids)
+            // (A/B: carrying the ids through the bucket scatter instead -- a second scattered store
+            // stream -- cost 4 us more at 900K than this gather)
+            const unsigned gid = (unsigned)gids[KN_IDX(local, (unsigned)n, 108)];
+            o.w = __uint_as_float((gid & 0x7FFFFFFFu) | ((int)local >= n_owned ? 0x80000000u : 0u));
+        }
+        sorted[KN_IDX(pos, n, 107)] = o;
+        perm[pos] = local;
     }
 }
 
@@ -509,20 +522,35 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
             src.nbb = bbox_block_count(n);
         }
         const size_t T = (size_t)bp.nbuckets * bp.nblocks;
-        bucket_count_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
-            b.points, n, src, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count);
+        // global ids fused into the sort unless the in-cell order pass follows (it orders by w)
+        const bool fuse_gid = b.gids && !b.deterministic;
+        // streaming blocks of 1024 threads: ~220 blocks at 900K points is one block per CU, so
+        // the LDS-atomic loops need 16 waves per CU to hide their latency (KN_BIN_THREADS A/B)
+        static const int bin_threads = [] {
+            const char* v = std::getenv("KN_BIN_THREADS");
+            const int t = v ? std::atoi(v) : 1024;
+            return (t == 256 || t == 512 || t == 1024) ? t : 1024;
+        }();
+        bucket_count_kernel<<<bp.nblocks, bin_threads, bp.nbuckets * sizeof(int), s>>>(
+            b.points, n, src, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count, b.zero_words,
+            b.n_zero_words);
         const unsigned nbt = (unsigned)scan_block_count((int)T);
         scan_blocks_kernel<<<nbt, 256, 0, s>>>(b.cell_count, (int)T, b.cell_scan, b.block_sums);
-        bucket_scatter_kernel<<<bp.nblocks, 256, bp.nbuckets * sizeof(int), s>>>(
+        bucket_scatter_kernel<<<bp.nblocks, bin_threads, bp.nbuckets * sizeof(int), s>>>(
             b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_scan, b.block_sums,
             (int)nbt, b.bin_tmp);
         bucket_sort_kernel<<<bp.nbuckets, 256, (1u << bp.shift) * sizeof(int), s>>>(
             b.bin_tmp, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, b.cell_scan, b.block_sums, C, b.cell_start,
-            b.sorted, b.perm);
-        if (b.deterministic) return launch_cell_sort(b.cell_start, b.geom, n, b.sorted, b.perm, b.bin_tmp, s);
+            b.sorted, b.perm, fuse_gid ? b.gids : nullptr, b.n_owned);
+        if (b.deterministic && (e = launch_cell_sort(b.cell_start, b.geom, n, b.sorted, b.perm, b.bin_tmp, s)) != hipSuccess)
+            return e;
+        if (b.gids && !fuse_gid) return launch_global_w(b.sorted, b.perm, b.gids, n, b.n_owned, s);
         return hipGetLastError();
     }
     // global-atomic binning (fallback)
+    if (b.zero_words && b.n_zero_words > 0 &&
+        (e = hipMemsetAsync(b.zero_words, 0, (size_t)b.n_zero_words * sizeof(unsigned), s)) != hipSuccess)
+        return e;
     if (b.use_box) {
         geom_box_kernel<<<1, 64, 0, s>>>(b.box_lo[0], b.box_lo[1], b.box_lo[2], b.box_hi[0],
                                          b.box_hi[1], b.box_hi[2], b.dims[0], b.dims[1],
@@ -543,6 +571,10 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
                                                       b.perm);
     if (b.deterministic)
         cell_sort_kernel<<<cdiv(C, 256), 256, 0, s>>>(b.cell_start, C, b.sorted, b.perm);
+    if (b.gids) {
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return launch_global_w(b.sorted, b.perm, b.gids, n, b.n_owned, s);
+    }
     return hipGetLastError();
 }
 

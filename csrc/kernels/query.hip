@@ -1522,8 +1522,9 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     // distances collide within one truncation ulp (~2^-(23-SB)); M=3 makes that ~1e-7/query.
     constexpr int M = 2;
     const int X = q.dims[0], Y = q.dims[1], Z = q.dims[2];
-    hipError_t e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (!q.counters_zeroed && (e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s)) != hipSuccess)
+        return e;
     if (q.n == 0 || q.n_queries == 0) return hipSuccess;
     // the register-resident tile path covers K <= 64; larger K use the exact ring walk
     const bool tiles = q.use_tiles && KT <= 64;

@@ -70,20 +70,36 @@ __device__ __forceinline__ unsigned long long route_halo(const RouteParams& p, f
     return m;
 }
 
+__device__ __forceinline__ unsigned meta_ord(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float meta_unord(unsigned u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// partials (optional): the block's bbox as 6 words at partials[a * nb + block] (the encoding of
+// launch_bbox_partials) -- the steady-state step checks its share's bbox from these instead of a
+// separate pass over the points (steady_flag_partials_kernel)
 __global__ __launch_bounds__(kRT) void route_count_kernel(const float* __restrict__ pts, int n,
                                                           const RouteParams* __restrict__ pp,
-                                                          int* __restrict__ block_counts, int nb) {
+                                                          int* __restrict__ block_counts, int nb,
+                                                          unsigned* __restrict__ partials) {
     const RouteParams& p = *pp;
     __shared__ int cnt[2 * kRouteMaxWorld];
+    __shared__ unsigned red[6][kRT / 64];
     const int cols = 2 * p.world;
     for (int c = threadIdx.x; c < cols; c += kRT) cnt[c] = 0;
     __syncthreads();
+    unsigned bw[6] = {0u, 0u, 0u, 0u, 0u, 0u};  // max of ~ord(min) / ord(max); 0 = empty
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
         const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
         if (i < n) {
             const size_t i3 = 3 * (size_t)i;  // 64-bit: 3*i overflows int above 715M points
             const float x = pts[i3], y = pts[i3 + 1], z = pts[i3 + 2];
+            bw[0] = max(bw[0], ~meta_ord(x)); bw[1] = max(bw[1], ~meta_ord(y)); bw[2] = max(bw[2], ~meta_ord(z));
+            bw[3] = max(bw[3], meta_ord(x)); bw[4] = max(bw[4], meta_ord(y)); bw[5] = max(bw[5], meta_ord(z));
             const int o = route_owner(p, x, y, z);
             atomicAdd(&cnt[2 * o], 1);
             unsigned long long m = route_halo(p, x, y, z, o);
@@ -94,8 +110,21 @@ __global__ __launch_bounds__(kRT) void route_count_kernel(const float* __restric
             }
         }
     }
+    if (partials) {
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const unsigned v = wave_max_u32(bw[a]);
+            if (lane == 0) red[a][wid] = v;
+        }
+    }
     __syncthreads();
     for (int c = threadIdx.x; c < cols; c += kRT) block_counts[(size_t)c * nb + blockIdx.x] = cnt[c];
+    if (partials && threadIdx.x < 6) {
+        unsigned v = red[threadIdx.x][0];
+        for (int w = 1; w < kRT / 64; ++w) v = max(v, red[threadIdx.x][w]);
+        partials[(size_t)threadIdx.x * nb + blockIdx.x] = v;
+    }
 }
 
 // One workgroup per column: exclusive scan of the column's nb block counts; total -> totals[c].
@@ -327,14 +356,6 @@ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 // ---- local meta of a rank's share: {lo[3], hi[3], n, 0} as doubles ---------------------
 // (replaces a strided torch.aminmax over dim 0, which costs ~0.34 ms at 900K points)
-__device__ __forceinline__ unsigned meta_ord(float f) {
-    const unsigned u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float meta_unord(unsigned u) {
-    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
-}
-
 // words: the per-block partials of launch_bbox_partials (build.hip), same encoding
 __global__ void meta_finalize_kernel(const unsigned* __restrict__ partials, int nblocks, int n,
                                      double* __restrict__ out) {
@@ -377,15 +398,62 @@ __global__ void steady_flag_kernel(const double* __restrict__ local, const doubl
     if (lane == 0) flag[0] = (any ? 1 : 0) + (counters[1] != 0u ? 1 : 0);
 }
 
+// Steady-state check from the routing pass's bbox partials (route_count_kernel): this share's
+// {lo, hi, n} against the planned meta (the same double conversion as meta_finalize_kernel), the
+// send counts against the planned ones, and no uncertified query.
+__global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsigned* __restrict__ partials, int nb, int n,
+                                            const double* __restrict__ planned, const int* __restrict__ totals,
+                                            const int* __restrict__ ptotals, int nt,
+                                            const unsigned* __restrict__ counters, int* __restrict__ flag) {
+    // block-wide reduction of the nb x 6 partials (1024 threads: one pass at ~900K points)
+    __shared__ unsigned red[6][16];
+    __shared__ unsigned words_s[6];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nbr = n > 0 ? nb : 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        unsigned v = 0u;
+        for (int b = threadIdx.x; b < nbr; b += blockDim.x) v = max(v, partials[(size_t)a * nb + b]);
+        v = wave_max_u32(v);
+        if (lane == 0) red[a][wid] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        unsigned v = 0u;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v = max(v, red[threadIdx.x][w]);
+        words_s[threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (wid != 0) return;
+    unsigned words[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) words[a] = words_s[a];
+    bool diff = false;
+    if (lane < 8) {
+        unsigned wt = words[0];
+#pragma unroll
+        for (int a = 1; a < 6; ++a) wt = (lane == a) ? words[a] : wt;
+        double v;
+        if (lane < 3) v = n > 0 ? (double)meta_unord(~wt) : (double)INFINITY;
+        else if (lane < 6) v = n > 0 ? (double)meta_unord(wt) : -(double)INFINITY;
+        else if (lane == 6) v = (double)n;
+        else v = 0.0;
+        diff = v != planned[lane];  // a NaN never matches
+    }
+    for (int i = lane; i < nt; i += 64) diff |= totals[i] != ptotals[i];
+    const bool any = __builtin_amdgcn_ballot_w64(diff) != 0ull;
+    if (lane == 0) flag[0] = (any ? 1 : 0) + (counters[1] != 0u ? 1 : 0);
+}
+
 }  // namespace
 
 int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
 
 hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int world, int* block_counts,
-                              int* totals, hipStream_t s) {
+                              int* totals, hipStream_t s, unsigned* partials) {
     if (world < 1 || world > kRouteMaxWorld) return hipErrorInvalidValue;
     const int nb = route_block_count(n);
-    route_count_kernel<<<nb, kRT, 0, s>>>(pts, n, p, block_counts, nb);
+    route_count_kernel<<<nb, kRT, 0, s>>>(pts, n, p, block_counts, nb, partials);
     route_scan_kernel<<<2 * world, kRT, 0, s>>>(block_counts, nb, totals);
     return hipGetLastError();
 }
@@ -430,6 +498,14 @@ hipError_t launch_steady_flag(const double* local, const double* planned_meta, c
                               const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                               hipStream_t s) {
     steady_flag_kernel<<<1, 64, 0, s>>>(local, planned_meta, totals, planned_totals, n_totals, counters, flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const double* planned_meta, const int* totals,
+                                       const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
+                                       hipStream_t s) {
+    steady_flag_partials_kernel<<<1, 1024, 0, s>>>(partials, route_block_count(n), n, planned_meta, totals,
+                                                 planned_totals, n_totals, counters, flag);
     return hipGetLastError();
 }
 

@@ -180,10 +180,21 @@ QueryBuffers Engine::query_buffers() const {
     return q;
 }
 
-kn_status Engine::build_async() { return check(launch_build(build_buffers(), stream_), "build"); }
-kn_status Engine::query_async() {
+// fused_step: build + grid query in one stream-ordered step (the captured graph): the build's
+// first binning kernel zeroes the query counters, so the step has no memset node
+kn_status Engine::build_async(bool fused_step) {
+    BuildBuffers b = build_buffers();
+    if (fused_step && !use_tree_) {
+        b.zero_words = counters_;
+        b.n_zero_words = kNumCounters;
+    }
+    return check(launch_build(b, stream_), "build");
+}
+kn_status Engine::query_async(bool fused_step) {
     if (use_tree_) return tree_query();
-    return check(launch_query(query_buffers(), stream_), "query");
+    QueryBuffers q = query_buffers();
+    q.counters_zeroed = fused_step ? 1 : 0;
+    return check(launch_query(q, stream_), "query");
 }
 
 kn_status Engine::tree_query() {
@@ -366,8 +377,8 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     if (!graph_) {
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
-        kn_status s1 = build_async();
-        kn_status s2 = query_async();
+        kn_status s1 = build_async(true);
+        kn_status s2 = query_async(true);
         hipError_t e = hipStreamEndCapture(stream_, &g);
         if (s1 != KN_OK) return s1;
         if (s2 != KN_OK) return s2;
@@ -405,8 +416,8 @@ kn_status Engine::launch_graph(int iters) {
     if (!graph_) {
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
-        kn_status s1 = build_async();
-        kn_status s2 = query_async();
+        kn_status s1 = build_async(true);
+        kn_status s2 = query_async(true);
         hipError_t e = hipStreamEndCapture(stream_, &g);
         if (s1 != KN_OK) return s1;
         if (s2 != KN_OK) return s2;

@@ -93,8 +93,8 @@ private:
     kn_status allocate(int n, const int* dims_override = nullptr, bool refined = false);
     kn_status prepare_from(const float* src, int n, hipMemcpyKind kind);
     kn_status occupancy(double* w);
-    kn_status build_async();
-    kn_status query_async();
+    kn_status build_async(bool fused_step = false);
+    kn_status query_async(bool fused_step = false);
     // Morton-leaf tree over the built grid's points (one host sync: the leaf count) + its query
     kn_status tree_query();
     QueryBuffers query_buffers() const;

@@ -42,8 +42,9 @@ void check_points(const torch::Tensor& p, bool cuda) {
 // geom tensor: 16 x int32 (64 bytes) holding a kn::GridGeom
 static_assert(sizeof(kn::GridGeom) <= 64, "GridGeom must fit in 64 bytes");
 
-std::vector<torch::Tensor> build(torch::Tensor points, std::vector<int64_t> dims, bool deterministic,
-                                 c10::optional<std::vector<double>> box) {
+std::vector<torch::Tensor> build_impl(torch::Tensor points, std::vector<int64_t> dims, bool deterministic,
+                                      c10::optional<std::vector<double>> box, const int* gids = nullptr,
+                                      int n_owned = 0, unsigned* zero_words = nullptr, int n_zero_words = 0) {
     check_points(points, true);
     TORCH_CHECK(dims.size() == 3 && dims[0] > 0 && dims[1] > 0 && dims[2] > 0, "dims must be 3 positive ints");
     const c10::DeviceGuard guard(points.device());
@@ -84,9 +85,18 @@ std::vector<torch::Tensor> build(torch::Tensor points, std::vector<int64_t> dims
         b.use_box = 1;
         for (int a = 0; a < 3; ++a) { b.box_lo[a] = (float)(*box)[a]; b.box_hi[a] = (float)(*box)[3 + a]; }
     }
+    b.gids = gids;
+    b.n_owned = n_owned;
+    b.zero_words = zero_words;
+    b.n_zero_words = n_zero_words;
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_build(b, s));
     return {sorted, cell_start, perm, geom};
+}
+
+std::vector<torch::Tensor> build(torch::Tensor points, std::vector<int64_t> dims, bool deterministic,
+                                 c10::optional<std::vector<double>> box) {
+    return build_impl(points, dims, deterministic, box);
 }
 
 std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom,
@@ -94,7 +104,8 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                                  c10::optional<torch::Tensor> id_map, std::vector<double> complete,
                                  std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
                                  bool use_tiles, bool with_dist, int64_t flags,
-                                 c10::optional<torch::Tensor> row_of, int64_t exact_grid = 0) {
+                                 c10::optional<torch::Tensor> row_of, int64_t exact_grid = 0,
+                                 c10::optional<torch::Tensor> zeroed_counters = c10::nullopt) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
@@ -110,7 +121,10 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     torch::Tensor out_dist;
     if (with_dist) out_dist = torch::empty({n_queries, k}, sorted.options());
     auto fallback = torch::empty({std::max(1, n)}, i32);
-    auto counters = torch::empty({kn::kNumCounters}, i32);
+    // zeroed_counters: kNumCounters int32 words the preceding build zeroed on the device
+    torch::Tensor counters = zeroed_counters.has_value() ? *zeroed_counters : torch::empty({kn::kNumCounters}, i32);
+    TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == torch::kInt32 && counters.numel() == kn::kNumCounters,
+                "counters must be kNumCounters int32 GPU words");
     auto uncert = torch::empty({std::max<int64_t>(1, n_queries)}, i32);
     kn::QueryBuffers q{};
     q.sorted = reinterpret_cast<const float4*>(sorted.data_ptr<float>());
@@ -143,6 +157,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     q.use_tiles = use_tiles ? 1 : 0;
     q.flags = (int)flags;
     q.exact_grid = (int)exact_grid;
+    q.counters_zeroed = zeroed_counters.has_value() ? 1 : 0;
     TORCH_CHECK(lds_capacity >= 64 && lds_capacity % 64 == 0 && lds_capacity <= 8192,
                 "lds_capacity must be a multiple of 64 in [64, 8192]");
     TORCH_CHECK(kn::query_lds_bytes(q.tile, q.halo, q.lds_capacity) <= 160 * 1024, "tile plan exceeds 160 KiB LDS");
@@ -533,7 +548,8 @@ std::vector<torch::Tensor> route_unpack_split(torch::Tensor recv, torch::Tensor 
 std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_rows, std::vector<int64_t> recv_own,
                                       std::vector<int64_t> recv_halo, int64_t rank, std::vector<int64_t> grid,
                                       std::vector<double> hdr, int64_t k, double ppc, bool deterministic,
-                                      int64_t exact_grid = 0) {
+                                      int64_t exact_grid = 0, bool adaptive = false,
+                                      c10::optional<std::vector<int64_t>> dims_hint = c10::nullopt) {
     TORCH_CHECK(grid.size() == 3 && hdr.size() >= 18, "grid must have 3 entries, hdr >= 18");
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world == (int64_t)recv_own.size(), "grid does not match the source table");
@@ -560,19 +576,41 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     float fext[3] = {(float)ext[0], (float)ext[1], (float)ext[2]};
     const int th[3] = {0, 0, 0};
     const kn::AutoParams ap = kn::auto_params((int)npts, (int)k, (float)ppc, th, 0, fext);
-    const std::vector<int64_t> dims = {ap.dims[0], ap.dims[1], ap.dims[2]};
-    auto g = build(pg[0], dims, deterministic, box);
+    std::vector<int64_t> dims = {ap.dims[0], ap.dims[1], ap.dims[2]};
+    if (dims_hint.has_value()) {
+        TORCH_CHECK(dims_hint->size() == 3 && (*dims_hint)[0] > 0 && (*dims_hint)[1] > 0 && (*dims_hint)[2] > 0,
+                    "dims_hint must be 3 positive ints");
+        dims = *dims_hint;  // the validated step's (possibly refined) grid: no occupancy sync
+    }
     // global-id mode: the stored points carry their global ids (halo bit on non-owned points), so
-    // the query epilogue writes ids without a random gather through the id table
-    const int64_t nst = g[0].size(0);
-    KN_CHECK_HIP(kn::launch_global_w(reinterpret_cast<float4*>(g[0].data_ptr<float>()),
-                                     reinterpret_cast<const unsigned*>(g[2].data_ptr<int>()), pg[1].data_ptr<int>(),
-                                     (int)nst, (int)n_owned,
-                                     c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+    // the query epilogue writes ids without a random gather through the id table. The build writes
+    // them (fused into its bucket sort) and zeroes the query counters (no memset node).
+    auto counters = torch::empty({kn::kNumCounters}, pg[1].options());
+    auto g = build_impl(pg[0], dims, deterministic, box, pg[1].data_ptr<int>(), (int)n_owned,
+                        reinterpret_cast<unsigned*>(counters.data_ptr<int>()), kn::kNumCounters);
+    if (adaptive && !dims_hint.has_value() && npts > 0) {
+        // occupancy-adaptive local grid (as kn::Engine::prepare_from): while the mean occupancy of a
+        // point's cell is far above a Poisson grid's, re-bin finer (<= 3 rounds); the tile / halo /
+        // LDS plan stays that of the target density. One host read per round (full steps only).
+        const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+        auto occ = torch::empty({1}, pg[1].options().dtype(torch::kInt64));
+        for (int round = 0; round < 3; ++round) {
+            const int C = (int)(dims[0] * dims[1] * dims[2]);
+            KN_CHECK_HIP(kn::launch_cell_occupancy(g[1].data_ptr<int>(), C,
+                                                   reinterpret_cast<unsigned long long*>(occ.data_ptr<int64_t>()), s));
+            const double w = (double)occ.cpu().item<int64_t>() / (double)npts;
+            const int cur[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
+            int nd[3];
+            if (!kn::refine_dims(cur, w, (int)k, (float)ppc, (int)npts, nd)) break;
+            dims = {nd[0], nd[1], nd[2]};
+            g = build_impl(pg[0], dims, deterministic, box, pg[1].data_ptr<int>(), (int)n_owned,
+                           reinterpret_cast<unsigned*>(counters.data_ptr<int>()), kn::kNumCounters);
+        }
+    }
     auto q = query(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
-                   ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid);
+                   ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid, counters);
     // + the local grid (global-id mode) and the uncertified list, for query forwarding
-    auto dims_t = torch::tensor({ap.dims[0], ap.dims[1], ap.dims[2]}, torch::kInt64);
+    auto dims_t = torch::tensor({dims[0], dims[1], dims[2]}, torch::kInt64);
     return {pg[0], pg[1], q[0], q[1], q[2], g[0], g[1], g[3], g[2], q[3], dims_t};
 }
 
@@ -627,6 +665,62 @@ torch::Tensor steady_flag(torch::Tensor local, torch::Tensor metas, int64_t rank
                                         totals.data_ptr<int>(), planned_totals.data_ptr<int>(), (int)totals.numel(),
                                         reinterpret_cast<const unsigned*>(counters.data_ptr<int>()),
                                         flag.data_ptr<int>(), s));
+    return flag;
+}
+
+// Pre-collective half of a steady-state step: counts + scatter with the validated step's plan
+// (no re-planning; the plan kernel is a serial one-thread pass) and this share's bbox partials
+// taken by the counting pass. -> (totals (2*world,) int32, send (cap, 4), partials)
+std::vector<torch::Tensor> route_steady(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor plan,
+                                        int64_t world, int64_t cap, int64_t rank) {
+    check_points(points, true);
+    TORCH_CHECK(plan.is_cuda() && plan.numel() == (int64_t)sizeof(kn::RouteParams), "plan must be a route plan");
+    TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld && rank >= 0 && rank < world, "bad world / rank");
+    TORCH_CHECK(cap >= 0 && cap < INT32_MAX, "cap out of range");
+    const c10::DeviceGuard guard(points.device());
+    const int n = (int)points.size(0);
+    const int* idp = nullptr;
+    if (ids.has_value()) {
+        TORCH_CHECK(ids->is_cuda() && ids->scalar_type() == torch::kInt32 && ids->numel() == n && ids->is_contiguous(),
+                    "ids must be a contiguous int32 GPU tensor of N entries");
+        idp = ids->data_ptr<int>();
+    }
+    auto i32 = points.options().dtype(torch::kInt32);
+    const int nb = kn::route_block_count(n);
+    auto totals = torch::empty({2 * world}, i32);
+    auto bc = torch::empty({2 * world * (int64_t)nb}, i32);
+    auto partials = torch::empty({6 * (int64_t)nb}, i32);
+    auto send = torch::empty({cap, 4}, points.options());
+    const auto* pp = reinterpret_cast<const kn::RouteParams*>(plan.data_ptr<uint8_t>());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, pp, (int)world, bc.data_ptr<int>(),
+                                        totals.data_ptr<int>(), s, reinterpret_cast<unsigned*>(partials.data_ptr<int>())));
+    KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, (int)world, bc.data_ptr<int>(),
+                                          totals.data_ptr<int>(), reinterpret_cast<float4*>(send.data_ptr<float>()),
+                                          (int)cap, (int)rank, s));
+    return {totals, send, partials};
+}
+
+// Steady-state check from route_steady's partials: (1,) int32, non-zero = the share's meta or send
+// counts differ from the validated step's, or a query is uncertified
+torch::Tensor steady_flag_partials(torch::Tensor partials, int64_t n, torch::Tensor metas, int64_t rank,
+                                   torch::Tensor totals, torch::Tensor planned_totals, torch::Tensor counters) {
+    TORCH_CHECK(partials.is_cuda() && partials.scalar_type() == torch::kInt32 &&
+                    partials.numel() == 6 * (int64_t)kn::route_block_count((int)n), "partials of route_steady");
+    TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.numel() >= 8 * (rank + 1) &&
+                    metas.is_contiguous(), "metas: (world*8,) f64 GPU");
+    TORCH_CHECK(totals.is_cuda() && planned_totals.is_cuda() && totals.scalar_type() == torch::kInt32 &&
+                    planned_totals.scalar_type() == torch::kInt32 && totals.numel() == planned_totals.numel() &&
+                    totals.is_contiguous() && planned_totals.is_contiguous(), "totals: matching int32 GPU tensors");
+    TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == torch::kInt32 && counters.numel() >= 2, "counters");
+    const c10::DeviceGuard guard(partials.device());
+    auto flag = torch::empty({1}, counters.options());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_steady_flag_partials(reinterpret_cast<const unsigned*>(partials.data_ptr<int>()), (int)n,
+                                                 metas.data_ptr<double>() + 8 * rank, totals.data_ptr<int>(),
+                                                 planned_totals.data_ptr<int>(), (int)totals.numel(),
+                                                 reinterpret_cast<const unsigned*>(counters.data_ptr<int>()),
+                                                 flag.data_ptr<int>(), s));
     return flag;
 }
 
@@ -833,7 +927,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("k"), py::arg("n_queries"),
           py::arg("id_map"), py::arg("complete"), py::arg("tile"), py::arg("halo"), py::arg("lds_capacity"),
           py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0, py::arg("row_of") = py::none(),
-          py::arg("exact_grid") = 0);
+          py::arg("exact_grid") = 0, py::arg("zeroed_counters") = py::none());
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     m.def("tree_build", &tree_build, "Morton-leaf tree over a grid's sorted points: (workspace, nodes, leaves)",
@@ -862,11 +956,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("query_external", &query_external,
           "multi-GPU query forwarding: exact K nearest of external points among a local grid");
     m.def("steady_flag", &steady_flag, "multi-GPU: on-device check of a sync-free steady-state step");
+    m.def("route_steady", &route_steady,
+          "multi-GPU steady step: counts + scatter with a validated plan, share bbox partials on the way");
+    m.def("steady_flag_partials", &steady_flag_partials,
+          "multi-GPU: steady-step check with the share bbox from route_steady's partials");
     m.def("dist_local", &dist_local,
           "multi-GPU: unpack + local grid build + owned-point queries from the plan header, one call",
           py::arg("recv"), py::arg("self_rows"), py::arg("recv_own"), py::arg("recv_halo"), py::arg("rank"),
           py::arg("grid"), py::arg("hdr"), py::arg("k"), py::arg("ppc"), py::arg("deterministic"),
-          py::arg("exact_grid") = 0);
+          py::arg("exact_grid") = 0, py::arg("adaptive") = false, py::arg("dims_hint") = py::none());
     m.def("route_unpack_split", &route_unpack_split,
           "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer",

@@ -106,8 +106,11 @@ class DistributedKNearests:
     def __init__(self, k: int = 16, group=None, halo_factor: float = 2.5, points_per_cell: float = 0.0,
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
                  transport=None, device_plan: bool = True, timeout_s: Optional[float] = None,
-                 balance: str = "count"):
+                 balance: str = "count", adaptive: bool = True):
         self.k = int(k)
+        # occupancy-adaptive local grids (GPU): a rank whose share is clustered re-bins finer, as
+        # the 1-GPU engine does; steady steps reuse the validated step's grid (no extra sync)
+        self.adaptive = bool(adaptive)
         if balance not in ("count", "volume"):
             raise ValueError("balance must be 'count' or 'volume'")
         # rank boxes: "count" = kd splits at global quantiles (every rank ~N/world points, also
@@ -349,7 +352,7 @@ class DistributedKNearests:
             # local_solve with SpatialDecomposition's boxes)
             pts, gids, idx, d2, counters, *local_grid = C.dist_local(
                 recv, send[x:x + send_counts[rank]], recv_own, recv_halo, rank, list(grid), hv[:HDR], self.k,
-                self.points_per_cell, self.deterministic)
+                self.points_per_cell, self.deterministic, 0, self.adaptive)
             mark(("local_enqueued", time.perf_counter()))
             n_owned = sum(recv_own)
             if rounds == 1:
@@ -372,12 +375,15 @@ class DistributedKNearests:
             _log.info("rank %d: uncertified queries, growth round %d with halo factor %.3g", rank, rounds + 1, hf)
             src_pts, src_ids = own_pts, own_ids
         stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
-                 "grid": tuple(grid), "forwarded": n_fwd}
+                 "grid": tuple(grid), "forwarded": n_fwd, "exact_path": int(counters[0].item()),
+                 "local_dims": tuple(int(v) for v in local_grid[5].tolist())}
         _log.debug("rank %d: step %s", rank, stats)
         if rounds == 1 and not full and self.steady:
             # validated single-round step: the steady-state assumption for the next ones
             self._steady = {
                 "metas": metas, "grid": tuple(grid), "hdr": hv[:HDR], "cap": int(send.size(0)), "splits": splits,
+                "plan": plan,  # the validated route plan (steady steps do not re-plan)
+                "dims": [int(v) for v in local_grid[5].tolist()],  # the local grid (maybe refined)
                 "tot": torch.tensor(tot, dtype=torch.int32, device=points.device),
                 "send_counts": send_counts, "recv_own": recv_own, "recv_halo": recv_halo,
                 "cross_send": cross_send, "cross_recv": cross_recv, "x": x,
@@ -477,12 +483,9 @@ class DistributedKNearests:
         st = self._steady
         C = ops.load()
         world, rank = self.world, self.rank
-        nh = 2 * HDR
         src_ids = ids.to(torch.int32).contiguous() if ids is not None else None
-        local = C.local_meta(points)
-        plan, sync, bc, send = C.route_begin(points, src_ids, st["metas"], rank, list(st["grid"]), self.k,
-                                             self.halo_factor, st["cap"], st["splits"])
-        totals = sync[nh:nh + 2 * world]
+        # counts + scatter with the validated plan; the share's bbox comes from the counting pass
+        totals, send, partials = C.route_steady(points, src_ids, st["plan"], world, st["cap"], rank)
         x = st["x"]
         if world > 1:
             recv = self._a2a(send[:x], st["cross_send"], st["cross_recv"])
@@ -491,8 +494,9 @@ class DistributedKNearests:
         sc = st["send_counts"][rank]
         pts, gids, idx, d2, counters, *_ = C.dist_local(recv, send[x:x + sc], st["recv_own"], st["recv_halo"],
                                                         rank, list(st["grid"]), st["hdr"], self.k,
-                                                        self.points_per_cell, self.deterministic, st["exact_grid"])
-        flag = C.steady_flag(local, st["metas"], rank, totals, st["tot"], counters)
+                                                        self.points_per_cell, self.deterministic, st["exact_grid"],
+                                                        False, st["dims"])
+        flag = C.steady_flag_partials(partials, points.size(0), st["metas"], rank, totals, st["tot"], counters)
         if world > 1:
             self.comm.all_reduce_max(flag)
         return gids[:sum(st["recv_own"])], idx, d2, flag

@@ -26,21 +26,30 @@ class CollectiveError(RuntimeError):
 
 
 class TorchDistTransport:
-    """``timeout_s``: every collective is issued asynchronously and waited for at most that long
-    (failure detection inside the library, independent of the process group's own timeout).
-    GPU collectives complete on the device stream, so a device-side hang is caught by the
-    group's watchdog (``TORCH_NCCL_ASYNC_ERROR_HANDLING``, on by default) instead; this timeout
-    covers the host side of every collective and all of a CPU (gloo) one."""
+    """``timeout_s``: failure detection inside the library, independent of the process group's
+    own timeout. On a CPU backend (gloo) every collective is issued asynchronously and waited for
+    at most that long. On RCCL ("nccl") collectives stay stream-ordered and never block the host:
+    ``Work.wait(timeout)`` would make the CPU thread poll the collective to completion, which
+    serialises the sync-free steady-state steps. A device-side hang or a dead peer is then caught
+    by the group's watchdog (``TORCH_NCCL_ASYNC_ERROR_HANDLING``, on by default, aborts the
+    process after the group's timeout); errors the call raises become ``CollectiveError``."""
 
     def __init__(self, group=None, timeout_s: Optional[float] = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.timeout_s = timeout_s
+        self.stream_ordered = dist.get_backend(group) == "nccl"
 
     def _run(self, name: str, fn):
         if self.timeout_s is None:
             fn(False)
+            return
+        if self.stream_ordered:
+            try:
+                fn(False)
+            except Exception as e:  # noqa: BLE001 - report which collective and rank
+                raise CollectiveError(f"rank {self.rank}: {name} failed: {e}") from e
             return
         import datetime
 

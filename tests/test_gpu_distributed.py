@@ -390,3 +390,42 @@ def test_steady_state_async_steps(cuda, world):
         ids = i3.long()
         assert torch.equal(d3, od[ids])
         assert_knn_exact(moved, ids, n3, d3, od[ids])
+
+
+def test_adaptive_local_grid_clustered(cuda):
+    """Clustered shares: the occupancy-adaptive local grid (as the 1-GPU engine's) re-bins the
+    dense ranks finer, sends fewer queries to the exact path than the fixed grid, stays exact,
+    and the steady (sync-free) step reuses the validated step's grid bit for bit."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+    from cuda_knearests_amd.utils import clustered_cloud
+
+    n, k, world = 60000, 16, 4
+    cloud = clustered_cloud(n, seed=5)
+    owner = torch.arange(n) % world
+    _, od = kn.knn_cpu(cloud, k, "kdtree")
+
+    def run(adaptive):
+        def body(t):
+            m = owner == t.rank
+            ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
+            dk = DistributedKNearests(k=k, transport=t, adaptive=adaptive)
+            r0 = dk.solve(cloud[m].contiguous().to(cuda), ids)
+            r1 = dk.solve(cloud[m].contiguous().to(cuda), ids, async_=True)
+            ok = r1.valid()
+            return (r0.ids.cpu(), r0.neighbors.cpu(), r0.d2.cpu(), r1.neighbors.cpu(), r1.d2.cpu(), ok,
+                    r0.stats)
+        return run_loopback(world, body)
+
+    fixed, adapt = run(False), run(True)
+    for out in (fixed, adapt):
+        for i0, n0, d0, n1, d1, ok, _ in out:
+            ids = i0.long()
+            assert torch.equal(d0, od[ids])
+            assert_knn_exact(cloud, ids, n0, d0, od[ids])
+            assert ok and torch.equal(n0, n1) and torch.equal(d0, d1)
+    ex_fixed = sum(o[-1]["exact_path"] for o in fixed)
+    ex_adapt = sum(o[-1]["exact_path"] for o in adapt)
+    refined = [o[-1]["local_dims"] != f[-1]["local_dims"] for o, f in zip(adapt, fixed)]
+    assert any(refined), [o[-1]["local_dims"] for o in adapt]
+    assert ex_adapt <= ex_fixed, (ex_adapt, ex_fixed)
