@@ -113,6 +113,7 @@ struct QueryBuffers {
     int dims[3];
     int k;
     int n_queries;            // points with original index < n_queries are queries
+    int q_lo;                 // ... and >= q_lo (query ranges; out row = original index - q_lo)
     const unsigned* id_map;   // optional: output id = id_map[original index]
     const unsigned* row_of;   // optional: global-id mode -- each stored point's w is its global id
                               // (| 0x80000000 on non-query halo points) and a query's output row

@@ -35,13 +35,13 @@ __device__ __forceinline__ bool pair_less(float da, unsigned ia, float db, unsig
 constexpr unsigned kHaloBit = 0x80000000u;
 template <class A>
 __device__ __forceinline__ bool w_live(const A& a, unsigned w) {
-    return a.row_of ? !(w & kHaloBit) : (int)w < a.n_queries;
+    return a.row_of ? !(w & kHaloBit) : ((int)w >= a.q_lo && (int)w < a.n_queries);
 }
 template <class A>
 __device__ __forceinline__ unsigned w_id(const A& a, unsigned w) { return a.row_of ? (w & ~kHaloBit) : w; }
 template <class A>
 __device__ __forceinline__ unsigned w_row(const A& a, unsigned w, unsigned sidx) {
-    return a.row_of ? a.row_of[KN_IDX(sidx, (unsigned)a.n, 231)] : w;
+    return a.row_of ? a.row_of[KN_IDX(sidx, (unsigned)a.n, 231)] : w - (unsigned)a.q_lo;
 }
 template <class A>
 __device__ __forceinline__ unsigned out_id(const A& a, unsigned id) {

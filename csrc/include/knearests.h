@@ -126,6 +126,11 @@ void kn_print_stats(kn_problem *kn);
 kn_config kn_default_config(void);
 kn_problem *kn_prepare_ex(const kn_float3 *points, int numpoints, const kn_config *cfg);
 kn_status kn_solve_ex(kn_problem *kn);
+/* Queries of the original indices [first, first + count) only: count x K original-space ids
+ * (row = original index - first) into host buffers, squared distances too when out_d2 != NULL.
+ * The whole N x K result is never allocated on the device, so clouds whose result does not fit
+ * next to the grid are solved in batches. */
+kn_status kn_solve_range(kn_problem *kn, int first, int count, unsigned int *out_ids, float *out_d2);
 kn_status kn_set_k(kn_problem *kn, int k);                 /* re-solve with another K, no rebuild */
 float *kn_get_distances(kn_problem *kn);                   /* N x K squared distances, stored space */
 unsigned int *kn_get_neighbors(kn_problem *kn);            /* N x K, original space (row = original id) */

@@ -62,6 +62,7 @@ struct TileArgs {
     int X, Y, Z;
     int k;
     int n_queries;
+    int q_lo;                // local mode: queries are original indices [q_lo, n_queries), row = w - q_lo
     const unsigned* id_map;
     const unsigned* row_of;  // non-null: global-id mode (see w_live / w_id / w_row)
     CompleteBox complete;
@@ -1272,6 +1273,7 @@ struct ExactArgs {
     int X, Y, Z;
     int k;
     int n_queries;
+    int q_lo;                // local mode: queries are original indices [q_lo, n_queries), row = w - q_lo
     const unsigned* id_map;
     const unsigned* row_of;
     CompleteBox complete;
@@ -1525,13 +1527,13 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     hipError_t e = hipSuccess;
     if (!q.counters_zeroed && (e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s)) != hipSuccess)
         return e;
-    if (q.n == 0 || q.n_queries == 0) return hipSuccess;
+    if (q.n == 0 || q.n_queries <= q.q_lo) return hipSuccess;
     // the register-resident tile path covers K <= 64; larger K use the exact ring walk
     const bool tiles = q.use_tiles && KT <= 64;
     if (tiles) {
         TileArgs a;
         a.sorted = q.sorted; a.cell_start = q.cell_start; a.geom = q.geom; a.n = q.n;
-        a.X = X; a.Y = Y; a.Z = Z; a.k = q.k; a.n_queries = q.n_queries; a.id_map = q.id_map;
+        a.X = X; a.Y = Y; a.Z = Z; a.k = q.k; a.n_queries = q.n_queries; a.q_lo = q.q_lo; a.id_map = q.id_map;
         a.row_of = q.row_of;
         a.complete = q.complete; a.out_idx = q.out_idx; a.out_dist = q.out_dist;
         a.fallback_list = q.fallback_list; a.counters = q.counters;
@@ -1570,7 +1572,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     }
     ExactArgs b;
     b.sorted = q.sorted; b.cell_start = q.cell_start; b.geom = q.geom; b.n = q.n;
-    b.X = X; b.Y = Y; b.Z = Z; b.k = q.k; b.n_queries = q.n_queries; b.id_map = q.id_map;
+    b.X = X; b.Y = Y; b.Z = Z; b.k = q.k; b.n_queries = q.n_queries; b.q_lo = q.q_lo; b.id_map = q.id_map;
     b.row_of = q.row_of;
     b.complete = q.complete; b.out_idx = q.out_idx; b.out_dist = q.out_dist;
     b.list = tiles ? q.fallback_list : nullptr;
@@ -1608,7 +1610,7 @@ hipError_t launch_query_external(const QueryBuffers& q, const float4* ext, int n
     if (n_ext == 0) return hipSuccess;
     ExactArgs b{};
     b.sorted = q.sorted; b.cell_start = q.cell_start; b.geom = q.geom; b.n = q.n;
-    b.X = q.dims[0]; b.Y = q.dims[1]; b.Z = q.dims[2]; b.k = q.k; b.n_queries = n_ext;
+    b.X = q.dims[0]; b.Y = q.dims[1]; b.Z = q.dims[2]; b.k = q.k; b.n_queries = n_ext; b.q_lo = 0;
     b.id_map = q.id_map; b.row_of = q.row_of;
     for (int a = 0; a < 3; ++a) { b.complete.lo[a] = -INFINITY; b.complete.hi[a] = INFINITY; }
     b.out_idx = q.out_idx; b.out_dist = q.out_dist;

@@ -42,6 +42,7 @@ struct TArgs {
     int n, L, P;
     int k;
     int n_queries;
+    int q_lo;  // always 0: the tree path serves whole solves (ranges use the grid kernels)
     const unsigned* id_map;
     const unsigned* row_of;  // always null: local mode of w_live / w_id / w_row / out_id
     unsigned* out_idx;
@@ -590,7 +591,7 @@ hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t 
     if (!t.nlo || t.L < 1) return hipErrorInvalidValue;
     TArgs a{};
     a.pts = t.pts; a.leaf_start = t.leaf_start; a.nlo = t.nlo; a.nhi = t.nhi; a.list = t.list; a.thr = t.thr;
-    a.n = t.n; a.L = t.L; a.P = t.P; a.k = q.k; a.n_queries = q.n_queries; a.id_map = q.id_map;
+    a.n = t.n; a.L = t.L; a.P = t.P; a.k = q.k; a.n_queries = q.n_queries; a.q_lo = 0; a.id_map = q.id_map;
     a.row_of = nullptr; a.out_idx = q.out_idx; a.out_dist = q.out_dist; a.counters = q.counters;
     a.flags = q.flags;
     constexpr int M = 2;

@@ -117,6 +117,35 @@ kn_status kn_solve_ex(kn_problem* kn) {
 
 void kn_solve(kn_problem* kn) { (void)kn_solve_ex(kn); }
 
+kn_status kn_solve_range(kn_problem* kn, int first, int count, unsigned int* out_ids, float* out_d2) {
+    kn::Engine* e = eng(kn);
+    if (!e) { g_err = "null problem"; return KN_ERR_INVALID_ARGUMENT; }
+    if (count < 0 || first < 0 || (long long)first + count > (long long)e->n()) {
+        g_err = "query range outside [0, N)";
+        return KN_ERR_INVALID_ARGUMENT;
+    }
+    if (count > 0 && !out_ids) { g_err = "null output"; return KN_ERR_INVALID_ARGUMENT; }
+    if (count == 0) return KN_OK;
+    const size_t nk = (size_t)count * e->k();
+    unsigned* d_idx = nullptr;
+    float* d_d2 = nullptr;
+    kn_status s = KN_OK;
+    if (hipMalloc(&d_idx, nk * sizeof(unsigned)) != hipSuccess ||
+        (out_d2 && hipMalloc(&d_d2, nk * sizeof(float)) != hipSuccess)) {
+        g_err = "hipMalloc(query range)";
+        s = KN_ERR_DEVICE;
+    }
+    if (s == KN_OK && (s = e->solve_range(first, count, d_idx, d_d2)) != KN_OK) g_err = e->error();
+    if (s == KN_OK && (hipMemcpy(out_ids, d_idx, nk * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess ||
+                       (out_d2 && hipMemcpy(out_d2, d_d2, nk * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess))) {
+        g_err = "D2H (query range)";
+        s = KN_ERR_DEVICE;
+    }
+    if (d_idx) (void)hipFree(d_idx);
+    if (d_d2) (void)hipFree(d_d2);
+    return s;
+}
+
 kn_status kn_set_k(kn_problem* kn, int k) {
     kn::Engine* e = eng(kn);
     if (!e) { g_err = "null problem"; return KN_ERR_INVALID_ARGUMENT; }

@@ -119,11 +119,9 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
                      (void**)&dist_stored_, (void**)&points3_})
         if (*q) { (void)hipFree(*q); *q = nullptr; }
+    // the N x K outputs are allocated on the first whole solve (ensure_outputs): a caller that
+    // only solves query ranges (solve_range, kn_solve_range) never holds them
     const size_t nk = std::max<size_t>(1, (size_t)n * cfg_.k);
-    if ((st = check(hipMalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
-    if (cfg_.with_distances &&
-        (st = check(hipMalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
-        return st;
     n_ = n;
     C_ = C;
     built_ = solved_ = stored_valid_ = points3_valid_ = false;
@@ -307,9 +305,41 @@ kn_status Engine::upload_device(const float* d_pts, int n) {
     return KN_OK;
 }
 
+kn_status Engine::ensure_outputs() {
+    const size_t nk = std::max<size_t>(1, (size_t)n_ * cfg_.k);
+    kn_status st;
+    if (!out_idx_ && (st = check(hipMalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
+    if (cfg_.with_distances && !out_dist_ &&
+        (st = check(hipMalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
+        return st;
+    return KN_OK;
+}
+
+// Queries of the original indices [first, first + count) only, rows written to caller device
+// buffers (count x K ids in original space, optional distances). The whole-solve outputs are
+// never allocated, so a cloud whose N x K result does not fit next to the grid is solved in
+// batches. Grid kernels (also for clouds the tree path serves).
+kn_status Engine::solve_range(int first, int count, unsigned* d_idx, float* d_dist) {
+    if (!built_) return fail(KN_ERR_STATE, "solve_range() before prepare()");
+    if (first < 0 || count < 0 || (long long)first + count > (long long)n_)
+        return fail(KN_ERR_INVALID_ARGUMENT, "query range outside [0, N)");
+    if (count > 0 && !d_idx) return fail(KN_ERR_INVALID_ARGUMENT, "null output buffer");
+    if (count == 0) return KN_OK;
+    QueryBuffers q = query_buffers();
+    q.q_lo = first;
+    q.n_queries = first + count;
+    q.out_idx = d_idx;
+    q.out_dist = d_dist;
+    q.exact_grid = 0;
+    kn_status st;
+    if ((st = check(launch_query(q, stream_), "query range")) != KN_OK) return st;
+    return check(hipStreamSynchronize(stream_), "query range sync");
+}
+
 kn_status Engine::solve() {
     if (!built_) return fail(KN_ERR_STATE, "solve() before prepare()");
     kn_status st;
+    if ((st = ensure_outputs()) != KN_OK) return st;
     (void)hipEventRecord(ev_[2], stream_);
     if ((st = query_async()) != KN_OK) return st;
     (void)hipEventRecord(ev_[3], stream_);
@@ -350,12 +380,6 @@ kn_status Engine::set_k(int k) {
     }
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_, (void**)&dist_stored_})
         if (*q) { (void)hipFree(*q); *q = nullptr; }
-    const size_t nk = std::max<size_t>(1, (size_t)n_ * k);
-    kn_status st;
-    if ((st = check(hipMalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
-    if (cfg_.with_distances &&
-        (st = check(hipMalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
-        return st;
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     solved_ = stored_valid_ = false;
     return KN_OK;
@@ -364,6 +388,7 @@ kn_status Engine::set_k(int k) {
 kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     if (!built_) return fail(KN_ERR_STATE, "run_graph() before prepare()");
     kn_status st;
+    if ((st = ensure_outputs()) != KN_OK) return st;  // not inside the capture
     if (use_tree_) {  // eager steps (see launch_graph)
         (void)hipEventRecord(ev_[0], stream_);
         if ((st = launch_graph(iters)) != KN_OK) return st;
@@ -403,6 +428,7 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
 kn_status Engine::launch_graph(int iters) {
     if (!built_) return fail(KN_ERR_STATE, "launch_graph() before prepare()");
     kn_status st;
+    if ((st = ensure_outputs()) != KN_OK) return st;  // not inside the capture
     if (use_tree_) {
         // the tree build reads its leaf count back (sizes the node buffer): eager steps
         for (int i = 0; i < iters; ++i) {

@@ -47,6 +47,9 @@ public:
     // rebuilds the grid itself). Re-plans (and drops the graph) only when n changes.
     kn_status upload_device(const float* d_pts, int n);
     kn_status solve();
+    // Queries [first, first + count) only, into caller device buffers (count x K; d_dist may be
+    // null): batched solves of clouds whose whole N x K result does not fit on the device.
+    kn_status solve_range(int first, int count, unsigned* d_idx, float* d_dist);
     kn_status set_k(int k);
     // Capture build+solve into a graph once, then replay it `iters` times (bench path).
     kn_status run_graph(int iters, float* ms_per_iter);
@@ -93,6 +96,7 @@ private:
     kn_status allocate(int n, const int* dims_override = nullptr, bool refined = false);
     kn_status prepare_from(const float* src, int n, hipMemcpyKind kind);
     kn_status occupancy(double* w);
+    kn_status ensure_outputs();
     kn_status build_async(bool fused_step = false);
     kn_status query_async(bool fused_step = false);
     // Morton-leaf tree over the built grid's points (one host sync: the leaf count) + its query

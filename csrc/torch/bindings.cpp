@@ -105,7 +105,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                                  std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
                                  bool use_tiles, bool with_dist, int64_t flags,
                                  c10::optional<torch::Tensor> row_of, int64_t exact_grid = 0,
-                                 c10::optional<torch::Tensor> zeroed_counters = c10::nullopt) {
+                                 c10::optional<torch::Tensor> zeroed_counters = c10::nullopt, int64_t q_lo = 0) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
@@ -115,11 +115,14 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     TORCH_CHECK(cell_start.numel() == dims[0] * dims[1] * dims[2] + 1, "cell_start size does not match dims");
     const int n = (int)sorted.size(0);
     TORCH_CHECK(n_queries >= 0 && n_queries <= n, "n_queries out of range");
+    // query range [q_lo, n_queries) of original indices (local id mode only); rows = n_queries - q_lo
+    TORCH_CHECK(q_lo >= 0 && q_lo <= n_queries && (q_lo == 0 || !row_of.has_value()), "bad query range");
     const c10::DeviceGuard guard(sorted.device());
     auto i32 = sorted.options().dtype(torch::kInt32);
-    auto out_idx = torch::empty({n_queries, k}, i32);
+    const int64_t rows = n_queries - q_lo;
+    auto out_idx = torch::empty({rows, k}, i32);
     torch::Tensor out_dist;
-    if (with_dist) out_dist = torch::empty({n_queries, k}, sorted.options());
+    if (with_dist) out_dist = torch::empty({rows, k}, sorted.options());
     auto fallback = torch::empty({std::max(1, n)}, i32);
     // zeroed_counters: kNumCounters int32 words the preceding build zeroed on the device
     torch::Tensor counters = zeroed_counters.has_value() ? *zeroed_counters : torch::empty({kn::kNumCounters}, i32);
@@ -135,6 +138,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     for (int a = 0; a < 3; ++a) q.dims[a] = (int)dims[a];
     q.k = (int)k;
     q.n_queries = (int)n_queries;
+    q.q_lo = (int)q_lo;
     if (id_map.has_value()) {
         TORCH_CHECK(id_map->is_cuda() && id_map->scalar_type() == torch::kInt32 && id_map->numel() >= n,
                     "id_map must be an int32 GPU tensor with >= N entries");
@@ -814,6 +818,18 @@ public:
                     e_->error());
         return {idx, d2};
     }
+    // queries [first, first + count) only, (count, K) ids (original space) + squared distances
+    std::vector<torch::Tensor> solve_range(int64_t first, int64_t count, torch::Device dev) {
+        TORCH_CHECK(first >= 0 && count >= 0 && first + count <= e_->n(), "query range outside [0, N)");
+        const int64_t k = e_->k();
+        auto opt = torch::TensorOptions().device(dev);
+        auto idx = torch::empty({count, k}, opt.dtype(torch::kInt32));
+        auto d2 = torch::empty({count, k}, opt.dtype(torch::kFloat32));
+        TORCH_CHECK(e_->solve_range((int)first, (int)count, reinterpret_cast<unsigned*>(idx.data_ptr<int>()),
+                                    d2.data_ptr<float>()) == KN_OK,
+                    e_->error());
+        return {idx, d2};
+    }
     std::vector<int64_t> counters() {
         unsigned c[kn::kNumCounters];
         TORCH_CHECK(e_->counters(c) == KN_OK, e_->error());
@@ -927,7 +943,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("k"), py::arg("n_queries"),
           py::arg("id_map"), py::arg("complete"), py::arg("tile"), py::arg("halo"), py::arg("lds_capacity"),
           py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0, py::arg("row_of") = py::none(),
-          py::arg("exact_grid") = 0, py::arg("zeroed_counters") = py::none());
+          py::arg("exact_grid") = 0, py::arg("zeroed_counters") = py::none(), py::arg("q_lo") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     m.def("tree_build", &tree_build, "Morton-leaf tree over a grid's sorted points: (workspace, nodes, leaves)",
@@ -983,6 +999,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
         .def("sync", &PyEngine::sync)
         .def("results", &PyEngine::results)
+        .def("solve_range", &PyEngine::solve_range, py::arg("first"), py::arg("count"), py::arg("device"))
         .def("counters", &PyEngine::counters)
         .def("info", &PyEngine::info);
     m.def("debug_words", &debug_words, "checked builds: first OOB report {code, index, limit, hi} of build and query kernels",

@@ -127,6 +127,19 @@ class KNearests:
                          self.info["exact_path"], self.grid.n)
         return self
 
+    def solve_range(self, first: int, count: int):
+        """Neighbours of the points with original index in [first, first + count) only: ``(ids,
+        d2)`` of shape (count, K), row r = point first + r (extension; the C API's
+        kn_solve_range). The whole-cloud N x K result is never allocated, so a cloud whose result
+        does not fit next to its grid is solved in batches."""
+        if self.grid is None:
+            raise RuntimeError("solve_range() before prepare() (GPU)")
+        first, count = int(first), int(count)
+        if first < 0 or count < 0 or first + count > self.grid.n:
+            raise ValueError("query range outside [0, N)")
+        return ops.query(self.grid, self.k, n_queries=first + count, use_tiles=self.use_tiles,
+                         with_dist=self.with_distances, algo="grid", first=first)
+
     def set_k(self, k: int) -> "KNearests":
         """Re-solve with another K without rebuilding the grid (extension)."""
         if not 1 <= int(k) <= 128:

@@ -116,8 +116,11 @@ def build_tree(grid: Grid) -> tuple:
 
 def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[torch.Tensor] = None,
           complete: Optional[Sequence[float]] = None, use_tiles: bool = True, with_dist: bool = True,
-          return_info: bool = False, flags: int = 0, algo: str = "grid"):
-    """kNN of the grid's points (original index < n_queries) against all grid points.
+          return_info: bool = False, flags: int = 0, algo: str = "grid", first: int = 0):
+    """kNN of the grid's points (original index in [first, n_queries)) against all grid points.
+
+    ``first`` > 0 solves a query range (grid kernels; row r = original index first + r): batched
+    solves of clouds whose whole N x K result does not fit next to the grid.
 
     ``algo``: ``"grid"`` (LDS-tiled grid kernels + exact fallback), ``"tree"`` (Morton-leaf tree,
     :func:`build_tree`; not with ``complete``) or ``"auto"`` (the grid's ``plan`` choice, see
@@ -130,6 +133,8 @@ def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[
     if algo == "auto":
         algo = grid.extra.get("algo", "grid")
     nq = grid.n if n_queries is None else int(n_queries)
+    if first:
+        algo = "grid"  # query ranges run on the grid kernels
     if algo == "tree":
         if complete is not None:
             raise ValueError("the tree path serves complete (single-GPU) point sets only")
@@ -148,7 +153,7 @@ def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[
     halo, cap = p.halo, p.lds_capacity
     idx, d2, counters, uncert, fallback = load().query(grid.sorted, grid.cell_start, grid.geom, list(p.dims), int(k), nq,
                                              id_map, comp, list(p.tile), int(halo), int(cap), bool(use_tiles),
-                                             bool(with_dist), int(flags))
+                                             bool(with_dist), int(flags), None, 0, None, int(first))
     if return_info:
         return idx, (d2 if with_dist else None), {"counters": counters, "uncertified": uncert,
                                                   "exact_path": fallback}

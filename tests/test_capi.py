@@ -136,6 +136,43 @@ def test_capi_reference_flow():
     assert torch.allclose(d, od, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.gpu
+def test_capi_solve_range_batches():
+    """kn_solve_range: the cloud solved in query batches (no N x K device result) equals the
+    whole solve row for row (original-space ids and distances)."""
+    import torch
+
+    import cuda_knearests_amd as kn
+
+    lib = _lib()
+    lib.kn_solve_range.argtypes = [C.POINTER(KnProblem), C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    lib.kn_get_neighbors.restype = C.POINTER(C.c_uint)
+    lib.kn_get_neighbors.argtypes = [C.POINTER(KnProblem)]
+    libc = C.CDLL(None)
+    n, k = 25000, 12
+    rng = np.random.default_rng(3)
+    pts = (rng.random((n, 3), dtype=np.float32) * 1000).astype(np.float32)
+    cfg = lib.kn_default_config()
+    cfg.k = k
+    prob = lib.kn_prepare_ex(pts.ctypes.data, n, C.byref(cfg))
+    assert prob, lib.kn_last_error()
+    ids = np.empty((n, k), dtype=np.uint32)
+    d2 = np.empty((n, k), dtype=np.float32)
+    for first in range(0, n, 7000):  # uneven last batch
+        cnt = min(7000, n - first)
+        assert lib.kn_solve_range(prob, first, cnt, ids[first:].ctypes.data, d2[first:].ctypes.data) == 0, \
+            lib.kn_last_error()
+    assert lib.kn_solve_range(prob, n - 5, 10, ids.ctypes.data, None) != 0  # out of range
+    assert lib.kn_solve_ex(prob) == 0
+    g = lib.kn_get_neighbors(prob)
+    whole = np.ctypeslib.as_array(g, shape=(n * k,)).reshape(n, k).copy()
+    libc.free(g)
+    lib.kn_free(C.pointer(prob))
+    assert np.array_equal(ids, whole)
+    _, od = kn.knn_cpu(torch.from_numpy(pts), k, "kdtree")
+    assert torch.equal(torch.from_numpy(d2), od)
+
+
 def _multi_lib():
     lib = _lib()
     lib.kn_prepare_multi.restype = C.c_void_p

@@ -363,3 +363,23 @@ def test_beyond_int32_point_offsets(cuda):
         assert float((e * e).sum()) == pytest.approx(float(d2[q, 0]), rel=1e-6), q
     del p, g, idx, d2
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k", [8, 50])
+def test_solve_range_matches_whole_solve(cuda, k):
+    """Query ranges (kn_solve_range / KNearests.solve_range / Engine.solve_range): batches of
+    original indices give the whole solve's rows bit for bit, also for a tree-path cloud (ranges
+    run on the grid kernels)."""
+    from cuda_knearests_amd._ext import load
+
+    for gen in (uniform_cloud, clustered_cloud):
+        p = gen(40000, seed=k, device=cuda)
+        m = kn.KNearests(k=k, device=cuda).prepare(p).solve()
+        whole_i, whole_d = m.neighbors.cpu(), m.distances.cpu()
+        parts = [m.solve_range(f, min(9000, p.size(0) - f)) for f in range(0, p.size(0), 9000)]
+        assert torch.equal(torch.cat([a for a, _ in parts]).cpu(), whole_i)
+        assert torch.equal(torch.cat([b for _, b in parts]).cpu(), whole_d)
+        e = load().Engine(k)
+        e.prepare(p)
+        ri, rd = e.solve_range(12345, 6000, cuda)  # before any whole solve: no N x K buffers
+        assert torch.equal(ri.cpu(), whole_i[12345:18345]) and torch.equal(rd.cpu(), whole_d[12345:18345])
