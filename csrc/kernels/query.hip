@@ -1552,7 +1552,13 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             const size_t dyn = ((size_t)a.max_rows * a.cb_stride + (size_t)a.TY * a.TZ + 1) * sizeof(int);
             if constexpr (KT <= 64) knn_stream_kernel<KT, M><<<nt, kWG, dyn, s>>>(a);
         } else {
-        const size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity);
+        // KN_LDS_EXTRA (bytes, diagnostics): pad the workgroup's LDS to measure how the query
+        // kernel responds to fewer resident workgroups per CU
+        static const size_t lds_extra = [] {
+            const char* v = std::getenv("KN_LDS_EXTRA");
+            return v ? (size_t)std::max(0, std::atoi(v)) : (size_t)0;
+        }();
+        const size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity) + lds_extra;
         static bool attr_set = false;
         if (!attr_set) {
             if constexpr (KT <= 64) {
