@@ -131,9 +131,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     int* rowbase = cb + a.max_rows * a.cb_stride;
     int* qpref = rowbase + a.max_rows + 1;  // TY*TZ + 1 entries
     int* misc = qpref + a.TY * a.TZ + 1;
-    // per-wave buffers of the cooperative re-scan, 16-B aligned after misc (query_lds_bytes)
-    unsigned long long* cbuf = reinterpret_cast<unsigned long long*>(
-        (reinterpret_cast<uintptr_t>(misc + 4) + 15) & ~(uintptr_t)15);
 
     const GridGeom g = *a.geom;
     const int ntiles = a.ntx * a.nty * a.ntz;
@@ -725,14 +722,20 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         // per-wave LDS buffer, then sorted and written as above. More than kCoopCap such
         // points (heavy duplication) leave the query to the exact kernel.
         bool prec_fail = last != SENT && !(dK2 <= __uint_as_float(last & HIMASK));
-        for (unsigned long long om = __builtin_amdgcn_ballot_w64(prec_fail && act); om; om &= om - 1) {
+        // The wave's re-scan buffer lives in the unused tail of the staged-point area (slots
+        // [S, cap)): no LDS is reserved for this rare path, which keeps the workgroup's LDS (and
+        // so the workgroups per CU) at the staging's. A wave whose slice does not fit leaves
+        // the query to the exact kernel (prec_fail stays set).
+        constexpr int kCoopSlots = kCoopCap * 8 / (int)sizeof(float4);
+        const bool coop_ok = S + (wid + 1) * kCoopSlots <= a.cap;
+        for (unsigned long long om = __builtin_amdgcn_ballot_w64(prec_fail && act && coop_ok); om; om &= om - 1) {
             const int L = __builtin_ctzll(om);
             auto rl = [&](int v) { return __builtin_amdgcn_readlane(v, L); };
             auto rlf = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), L)); };
             const int qsL = rl(qslot);
             const float qxL = rlf(qx), qyL = rlf(qy), qzL = rlf(qz), thr = rlf(dK2);
             const int x0 = rl(rx0), x1 = rl(rx1), y0 = rl(ry0), y1 = rl(ry1), z0 = rl(rz0), z1 = rl(rz1);
-            unsigned long long* buf = cbuf + wid * kCoopCap;
+            unsigned long long* buf = reinterpret_cast<unsigned long long*>(pts + S) + wid * kCoopCap;
             const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
             int cnt = 0;
             for (int z = z0; z <= z1; ++z) {
@@ -1604,8 +1607,7 @@ size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity) {
     b += (size_t)(rows + 1) * 4;
     b += (size_t)(tile[1] * tile[2] + 1) * 4;
     b += 16;
-    b = (b + 15) & ~(size_t)15;
-    b += (size_t)kWaves * kCoopCap * 8;  // cooperative re-scan buffers
+    b = (b + 15) & ~(size_t)15;  // (cooperative re-scan buffers: the staged area's unused tail)
     return b;
 }
 
@@ -1671,7 +1673,12 @@ hipError_t launch_to_stored_space(const unsigned* out_orig, const unsigned* perm
 // negligible for near-uniform clouds while keeping the 4x4x4/H2 plan at ~31 KB per workgroup,
 // i.e. 5 workgroups (20 waves) per CU instead of 4 with a power-of-two 2048.
 int lds_capacity_for(double staged) {
-    double c = staged + 5.0 * std::sqrt(std::max(staged, 1.0)) + 64.0;
+    // KN_LDS_SD: slack in standard deviations of the staged count (default 5; sweeps)
+    static const double sd = [] {
+        const char* v = std::getenv("KN_LDS_SD");
+        return v ? std::max(0.0, std::atof(v)) : 5.0;
+    }();
+    double c = staged + sd * std::sqrt(std::max(staged, 1.0)) + 64.0;
     int cap = ((int)std::ceil(c) + 63) & ~63;
     return std::max(128, std::min(cap, 8192));
 }

@@ -945,6 +945,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0, py::arg("row_of") = py::none(),
           py::arg("exact_grid") = 0, py::arg("zeroed_counters") = py::none(), py::arg("q_lo") = 0);
     m.def("auto_params", &auto_params, "grid / tile plan");
+    m.def(
+        "query_lds_bytes",
+        [](std::vector<int64_t> tile, int64_t halo, int64_t cap) {
+            TORCH_CHECK(tile.size() == 3, "tile must have 3 entries");
+            const int t[3] = {(int)tile[0], (int)tile[1], (int)tile[2]};
+            return (int64_t)kn::query_lds_bytes(t, (int)halo, (int)cap);
+        },
+        "LDS bytes per workgroup of the tile query kernel for a plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     m.def("tree_build", &tree_build, "Morton-leaf tree over a grid's sorted points: (workspace, nodes, leaves)",
           py::arg("sorted"), py::arg("geom"));
