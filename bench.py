@@ -228,6 +228,7 @@ def run_dist(args) -> dict:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         steps.append(dk.solve(pts, partitioned=part, async_=not args.sync_steps))
+    t_enq = time.perf_counter() - t0  # host time to enqueue the steps (~dt: the host is the bound)
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
@@ -277,7 +278,8 @@ def run_dist(args) -> dict:
     nt = torch.tensor([pts.size(0)], device=cdev, dtype=torch.int64)
     dist.all_reduce(nt)
     out = {"t": float(t.item()), "stats": res.stats if res else {}, "check": chk, "n_total": int(nt.item()),
-           "rank": rank, "world": world, "invalid_async_steps": invalid}
+           "rank": rank, "world": world, "invalid_async_steps": invalid,
+           "host_enqueue_ms_per_step": t_enq * 1e3 / max(1, args.steps)}
     dist.barrier()
     dist.destroy_process_group()
     return out
@@ -431,7 +433,8 @@ def main() -> int:
         extra = {"halo_width": r["stats"].get("halo_width"), "n_halo_rank0": r["stats"].get("n_halo"),
                  "rounds": r["stats"].get("rounds"), "rank_grid": r["stats"].get("grid"), "layout": args.layout,
                  "steady_async": bool(r["stats"].get("steady")) and not args.sync_steps,
-                 "invalid_async_steps": r["invalid_async_steps"], "path": "distributed"}
+                 "invalid_async_steps": r["invalid_async_steps"], "path": "distributed",
+                 "host_enqueue_ms_per_step": round(r["host_enqueue_ms_per_step"], 4)}
     else:
         r = run_native(args) if args.path == "native" else run_single(args)
         n_gpus = 1

@@ -4,6 +4,9 @@
 //   knn_cli --uniform N | --blue N | --clustered N [options]
 // options: --k K  --ppc X  --tile a,b,c  --halo H  --exact  --nondet  --no-check  --json
 //          --save file.kng  --out neighbours.txt  --repeat R
+//          --batch B   solve in query batches of B points (kn_solve_range: no N x K device result)
+//          --multi D   spatial split over D ranks (kn_prepare_multi / kn_solve_multi; rank i on
+//                      device i mod the device count, so D > devices runs virtual ranks)
 //
 // Flow: device report -> load -> kn_prepare_ex + kn_solve_ex (timed) -> kn_print_stats ->
 // stored-space getters -> remap to original ids (reference :155-160) -> permutation
@@ -44,7 +47,7 @@ int main(int argc, char** argv) {
     cfg.k = KN_DEFAULT_K;
     cfg.verbose = 1;
     std::string path, gen, save, out;
-    int gen_n = 0, repeat = 1;
+    int gen_n = 0, repeat = 1, batch = 0, multi = 0;
     bool check = true, json = false, exact = false;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -64,9 +67,12 @@ int main(int argc, char** argv) {
         else if (a == "--save") save = next();
         else if (a == "--out") out = next();
         else if (a == "--repeat") repeat = std::max(1, atoi(next()));
+        else if (a == "--batch") batch = std::max(0, atoi(next()));
+        else if (a == "--multi") multi = std::max(0, atoi(next()));
         else if (a == "-h" || a == "--help") {
             fprintf(stderr, "usage: %s points.xyz | --uniform N | --blue N | --clustered N [--k K] [--ppc X] "
-                            "[--tile a,b,c] [--halo H] [--exact] [--nondet] [--no-check] [--json] [--save f] [--out f]\n", argv[0]);
+                            "[--tile a,b,c] [--halo H] [--exact] [--nondet] [--no-check] [--json] [--save f] [--out f] "
+                            "[--repeat R] [--batch B] [--multi D]\n", argv[0]);
             return 0;
         } else path = a;
     }
@@ -93,34 +99,73 @@ int main(int argc, char** argv) {
         (void)hipFree(p);
     }
     std::vector<uint32_t> neighbors((size_t)n * K);
-    double t0 = now_ms();
-    kn_problem* kn = kn_prepare_ex(reinterpret_cast<const kn_float3*>(pts.data()), n, &cfg);
-    if (!kn) { fprintf(stderr, "kn_prepare failed: %s\n", kn_last_error()); return 1; }
-    for (int r = 0; r < repeat; ++r)
-        if (kn_solve_ex(kn) != KN_OK) { fprintf(stderr, "kn_solve failed: %s\n", kn_last_error()); return 1; }
-    const double t1 = now_ms();
-    fprintf(stderr, "knn subgpu: %.3f ms (prepare + %d solve)\n", t1 - t0, repeat);
-    kn_print_stats(kn);
-    kn_stats st;
-    kn_get_stats(kn, &st);
-    unsigned* knn = kn_get_knearests(kn);
-    unsigned* perm = kn_get_permutation(kn);
-    if (!knn || !perm) { fprintf(stderr, "getter failed: %s\n", kn_last_error()); return 1; }
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < K; ++j) {
-            const unsigned v = knn[(size_t)i * K + j];
-            neighbors[(size_t)perm[i] * K + j] = (v == 0xFFFFFFFFu) ? v : perm[v];
-        }
+    kn_stats st{};
     bool ok = true;
-    {   // permutation bijection (reference :162-168)
-        std::vector<unsigned> p(perm, perm + n);
-        std::sort(p.begin(), p.end());
-        for (int i = 0; i < n; ++i) if (p[i] != (unsigned)i) { ok = false; fprintf(stderr, "ERROR: permutation is not a bijection\n"); break; }
+    double t0 = now_ms();
+    if (multi > 0) {
+        // spatial split over `multi` ranks from this one process (extension)
+        int nd = 0;
+        if (hipGetDeviceCount(&nd) != hipSuccess || nd < 1) nd = 1;
+        std::vector<int> devs(multi);
+        for (int r = 0; r < multi; ++r) devs[r] = r % nd;
+        kn_multi* m = kn_prepare_multi(reinterpret_cast<const kn_float3*>(pts.data()), n, devs.data(), multi, &cfg);
+        if (!m) { fprintf(stderr, "kn_prepare_multi failed: %s\n", kn_last_error()); return 1; }
+        for (int r = 0; r < repeat; ++r)
+            if (kn_solve_multi(m) != KN_OK) { fprintf(stderr, "kn_solve_multi failed: %s\n", kn_last_error()); return 1; }
+        fprintf(stderr, "knn multi: %.3f ms (prepare + %d solve)\n", now_ms() - t0, repeat);
+        int ranks = 0, rounds = 0, halo = 0, rccl = 0;
+        kn_get_multi_info(m, &ranks, &rounds, &halo, &rccl);
+        fprintf(stderr, "ranks %d, rounds %d, halo points %d, transport %s\n", ranks, rounds, halo,
+                rccl ? "RCCL" : "device copies");
+        unsigned* nb = kn_get_neighbors_multi(m);
+        if (!nb) { fprintf(stderr, "getter failed: %s\n", kn_last_error()); return 1; }
+        std::copy(nb, nb + (size_t)n * K, neighbors.begin());
+        free(nb);
+        kn_free_multi(&m);
+        st.num_points = n;
+        st.k = K;
+    } else {
+        kn_problem* kn = kn_prepare_ex(reinterpret_cast<const kn_float3*>(pts.data()), n, &cfg);
+        if (!kn) { fprintf(stderr, "kn_prepare failed: %s\n", kn_last_error()); return 1; }
+        if (batch > 0) {
+            // query batches straight into original-space rows (no N x K device result)
+            for (int r = 0; r < repeat; ++r)
+                for (int first = 0; first < n; first += batch) {
+                    const int cnt = std::min(batch, n - first);
+                    if (kn_solve_range(kn, first, cnt, neighbors.data() + (size_t)first * K, nullptr) != KN_OK) {
+                        fprintf(stderr, "kn_solve_range failed: %s\n", kn_last_error());
+                        return 1;
+                    }
+                }
+            fprintf(stderr, "knn batches: %.3f ms (prepare + %d x %d batches of <= %d)\n", now_ms() - t0, repeat,
+                    (n + batch - 1) / batch, batch);
+        } else {
+            for (int r = 0; r < repeat; ++r)
+                if (kn_solve_ex(kn) != KN_OK) { fprintf(stderr, "kn_solve failed: %s\n", kn_last_error()); return 1; }
+            const double t1 = now_ms();
+            fprintf(stderr, "knn subgpu: %.3f ms (prepare + %d solve)\n", t1 - t0, repeat);
+            kn_print_stats(kn);
+            kn_get_stats(kn, &st);
+            unsigned* knn = kn_get_knearests(kn);
+            unsigned* perm = kn_get_permutation(kn);
+            if (!knn || !perm) { fprintf(stderr, "getter failed: %s\n", kn_last_error()); return 1; }
+            for (int i = 0; i < n; ++i)
+                for (int j = 0; j < K; ++j) {
+                    const unsigned v = knn[(size_t)i * K + j];
+                    neighbors[(size_t)perm[i] * K + j] = (v == 0xFFFFFFFFu) ? v : perm[v];
+                }
+            {   // permutation bijection (reference :162-168)
+                std::vector<unsigned> p(perm, perm + n);
+                std::sort(p.begin(), p.end());
+                for (int i = 0; i < n; ++i)
+                    if (p[i] != (unsigned)i) { ok = false; fprintf(stderr, "ERROR: permutation is not a bijection\n"); break; }
+            }
+            free(perm);
+            free(knn);
+        }
+        if (!save.empty() && kn_save(kn, save.c_str()) != KN_OK) fprintf(stderr, "save failed: %s\n", kn_last_error());
+        kn_free(&kn);
     }
-    free(perm);
-    free(knn);
-    if (!save.empty() && kn_save(kn, save.c_str()) != KN_OK) fprintf(stderr, "save failed: %s\n", kn_last_error());
-    kn_free(&kn);
     if (!out.empty()) {
         FILE* f = fopen(out.c_str(), "w");
         if (f) {

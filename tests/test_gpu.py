@@ -220,6 +220,16 @@ def test_cli_reference_flow(cuda):
     assert '"ok": true' in r.stdout
 
 
+@pytest.mark.parametrize("mode", [["--batch", "7000"], ["--multi", "4"]])
+def test_cli_batches_and_multi_rank(cuda, mode):
+    """knn_cli --batch (kn_solve_range) and --multi (kn_prepare_multi: 4 ranks, virtual on one
+    GPU) on the reference fixture, checked against the kd-tree oracle by the CLI itself."""
+    r = subprocess.run([str(REPO / "bin" / "knn_cli"), str(dataset("pts20K.xyz")), "--k", "16", "--json"] + mode,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert '"ok": true' in r.stdout
+
+
 @pytest.mark.parametrize("k", [16, 50])
 def test_halo1_certification_and_fallback(cuda, k):
     """force a 1-ring halo -> many tile queries cannot be certified and must be
