@@ -108,6 +108,9 @@ struct TileArgs {
 constexpr int kWin = 3;
 constexpr int kCoopCap = 128;  // per-wave LDS buffer of the cooperative re-scan (u64 keys)
 constexpr int kQueryForceRescan = 1;
+// fallback-list entry flag: the query's output row holds K real candidates (their K-th squared
+// distance is an upper bound the exact kernel seeds its threshold with); stored indices < 2^31
+constexpr unsigned kSeedBit = 0x80000000u;
 constexpr int kQueryAlgoStream = 2;
 constexpr int kQueryAlgoTile = 4;
 constexpr int kQueryAlgoLane = 8;
@@ -907,7 +910,14 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 #endif
         if (!geo_ok) {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
-            a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx;
+#if KN_WINDOW_RERANK
+            // the row already holds K real candidates: their K-th distance bounds the true one,
+            // and the exact kernel starts its walk with it (kSeedBit)
+            const bool seed = a.out_dist && nfound >= k && dK2 < INFINITY;
+#else
+            const bool seed = false;
+#endif
+            a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx | (seed ? kSeedBit : 0u);
         }
     }
 }
@@ -1317,8 +1327,10 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
     const int k = a.k;
     for (int t = blockIdx.x * 4 + wid; t < total; t += gridDim.x * 4) {
         // external queries (multi-GPU forwarding): a point of another rank, self = same global id
-        const unsigned sidx = a.ext ? ~0u : (unsigned)__builtin_amdgcn_readfirstlane(
+        const unsigned entry = a.ext ? ~0u : (unsigned)__builtin_amdgcn_readfirstlane(
             (int)(a.list ? a.list[KN_IDX(t, a.n, 311)] : (unsigned)t));
+        const bool seeded = !a.ext && a.list && (entry & kSeedBit) && a.out_dist;
+        const unsigned sidx = a.ext ? ~0u : (entry & ~kSeedBit);
         const float4 qp = a.ext ? a.ext[t] : a.sorted[KN_IDX(sidx, (unsigned)a.n, 312)];
         const unsigned qw = __float_as_uint(qp.w);
         if (!a.ext && !w_live(a, qw)) continue;
@@ -1328,6 +1340,13 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
         const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
         int cnt = 0;            // keys in buf (uniform)
         float thr = INFINITY;   // current K-th distance bound (uniform)
+        if (seeded) {
+            // the tile kernel's K-th distance for this row (K real points within it): every true
+            // neighbour passes d2 <= thr from the first shell on, rows are cut by the ball at once
+            const float s0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
+                a.out_dist[KN_IDX((size_t)qorig * (size_t)k + (size_t)(k - 1), (size_t)a.n_queries * k, 317)])));
+            if (s0 >= 0.f && s0 < INFINITY) thr = s0;
+        }
         // sort buf[0, cnt), keep the first min(cnt, k), thr = K-th distance once K are held
         auto compact = [&]() __attribute__((always_inline)) {
             __builtin_amdgcn_wave_barrier();
