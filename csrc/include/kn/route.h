@@ -59,6 +59,18 @@ struct UnpackTable {
     int halo_pref[kRouteMaxWorld];
 };
 
+// Direct placement of the self segment (steady-state steps, split sizes known): the rank's own
+// owned / halo rows go straight to their local rows -- owned row j at own_base + j, halo row j
+// at halo_base + j of the (rows, 3) points / (rows,) global ids the local build reads -- instead of
+// into the send buffer and through the unpack.
+struct SelfPlace {
+    float* pts;
+    int* gids;
+    int own_base;   // sum of recv_own over the sources before this rank
+    int halo_base;  // n_own + sum of recv_halo over the sources before this rank
+    int rows;       // local rows (bounds checks)
+};
+
 int route_block_count(int n);
 // Every launcher reads the routing parameters from DEVICE memory (`p`), so the whole
 // meta -> plan -> count chain is enqueued without a host round trip. `world` = p->world.
@@ -75,7 +87,8 @@ hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int
 // before the host knows the sizes.
 hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams* p, int world,
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
-                                int self_last, hipStream_t s);
+                                int self_last, hipStream_t s,
+                                const SelfPlace* self_place = nullptr);
 // rows = t.rows_cross + rows of the self buffer (self_rows may be null when t.self < 0)
 // sorted[i].w = gid[perm[i]] | (perm[i] >= n_owned ? 0x80000000 : 0): prepares a rank's grid
 // for the query kernels' global-id mode (QueryBuffers::row_of = perm).

@@ -159,10 +159,11 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
                                                             const int* __restrict__ block_offsets, int nb,
                                                             const int* __restrict__ totals,
                                                             float4* __restrict__ send, int send_rows,
-                                                            int self_last) {
+                                                            int self_last, SelfPlace sp) {
     __shared__ int base[2 * kRouteMaxWorld];            // block's next row of every column
     __shared__ int wcnt[kRT / 64][2 * kRouteMaxWorld];  // per-wave counts of the current round
     __shared__ int overflow;
+    __shared__ int seg_self;                            // first row of the self segment
     const RouteParams& p = *pp;
     const int cols = 2 * p.world;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -174,9 +175,12 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
             const int own = totals[2 * d], halo = totals[2 * d + 1];
             base[2 * d] = seg + block_offsets[(size_t)(2 * d) * nb + blockIdx.x];
             base[2 * d + 1] = seg + own + block_offsets[(size_t)(2 * d + 1) * nb + blockIdx.x];
+            if (d == self_last) seg_self = seg;
             seg += own + halo;
         }
-        overflow = seg > send_rows;  // same decision in every block: nothing is written
+        // same decision in every block: nothing is written. With direct self placement the
+        // self segment does not occupy the send buffer.
+        overflow = (sp.pts ? seg_self : seg) > send_rows;
     }
     __syncthreads();
     if (overflow) return;
@@ -216,7 +220,19 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
                     int off = base[c];
                     for (int w = 0; w < wid; ++w) off += wcnt[w][c];
                     off += __builtin_popcountll((po ? bo : bh) & lt);
-                    send[KN_IDX(off, send_rows, 401)] = row;
+                    if (sp.pts && d == self_last) {
+                        // the rank's own segment straight to its local rows (what the unpack
+                        // would compute): owned first over all sources, halo after
+                        const int j = off - seg_self;
+                        const int loc = po ? sp.own_base + j : sp.halo_base + (j - totals[2 * d]);
+                        const size_t l3 = 3 * (size_t)KN_IDX(loc, sp.rows, 403);
+                        sp.pts[l3] = x;
+                        sp.pts[l3 + 1] = y;
+                        sp.pts[l3 + 2] = z;
+                        sp.gids[loc] = gid;
+                    } else {
+                        send[KN_IDX(off, send_rows, 401)] = row;
+                    }
                 }
             }
         }
@@ -460,12 +476,17 @@ hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int
 
 hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const RouteParams* p, int world,
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
-                                int self_last, hipStream_t s) {
+                                int self_last, hipStream_t s, const SelfPlace* self_place) {
     if (world < 1 || world > kRouteMaxWorld || self_last >= world) return hipErrorInvalidValue;
+    SelfPlace sp{};
+    if (self_place) {
+        if (self_last < 0 || !self_place->pts || !self_place->gids) return hipErrorInvalidValue;
+        sp = *self_place;
+    }
     const int nb = route_block_count(n);
     if (n > 0)
         route_scatter_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, block_offsets, nb, totals, send, send_rows,
-                                                self_last);
+                                                self_last, sp);
     return hipGetLastError();
 }
 

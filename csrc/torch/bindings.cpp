@@ -553,11 +553,42 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
                                       std::vector<int64_t> recv_halo, int64_t rank, std::vector<int64_t> grid,
                                       std::vector<double> hdr, int64_t k, double ppc, bool deterministic,
                                       int64_t exact_grid = 0, bool adaptive = false,
-                                      c10::optional<std::vector<int64_t>> dims_hint = c10::nullopt) {
+                                      c10::optional<std::vector<int64_t>> dims_hint = c10::nullopt,
+                                      c10::optional<torch::Tensor> pre_pts = c10::nullopt,
+                                      c10::optional<torch::Tensor> pre_gids = c10::nullopt) {
     TORCH_CHECK(grid.size() == 3 && hdr.size() >= 18, "grid must have 3 entries, hdr >= 18");
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world == (int64_t)recv_own.size(), "grid does not match the source table");
-    auto pg = route_unpack_split(recv, self_rows, recv_own, recv_halo, rank);
+    std::vector<torch::Tensor> pg;
+    if (pre_pts.has_value()) {
+        // the self segment is already in place (route_steady with `place`): unpack only the rows
+        // received from the other sources into the same local arrays
+        TORCH_CHECK(pre_gids.has_value(), "pre_pts needs pre_gids");
+        TORCH_CHECK(rank >= 0 && rank < world, "bad rank");
+        kn::UnpackTable t{};
+        t.world = (int)world;
+        int64_t seg = 0, own = 0, halo = 0;
+        for (int64_t src = 0; src < world; ++src) {
+            t.seg[src] = (int)seg;
+            t.own[src] = (int)recv_own[src];
+            t.own_pref[src] = (int)own;
+            t.halo_pref[src] = (int)halo;
+            if (src != rank) seg += recv_own[src] + recv_halo[src];
+            own += recv_own[src];
+            halo += recv_halo[src];
+        }
+        t.n_own = (int)own;
+        t.rows_cross = (int)seg;
+        t.self = (int)rank;
+        TORCH_CHECK(seg == recv.size(0) && pre_pts->size(0) == own + halo && pre_gids->numel() == own + halo,
+                    "source table does not add up to the received / local rows");
+        KN_CHECK_HIP(kn::launch_route_unpack(reinterpret_cast<const float4*>(recv.data_ptr<float>()), nullptr,
+                                             (int)seg, t, pre_pts->data_ptr<float>(), pre_gids->data_ptr<int>(),
+                                             c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+        pg = {*pre_pts, *pre_gids};
+    } else {
+        pg = route_unpack_split(recv, self_rows, recv_own, recv_halo, rank);
+    }
     int64_t n_owned = 0;
     for (auto v : recv_own) n_owned += v;
     const double h = hdr[6], hs = hdr[7];
@@ -676,7 +707,8 @@ torch::Tensor steady_flag(torch::Tensor local, torch::Tensor metas, int64_t rank
 // (no re-planning; the plan kernel is a serial one-thread pass) and this share's bbox partials
 // taken by the counting pass. -> (totals (2*world,) int32, send (cap, 4), partials)
 std::vector<torch::Tensor> route_steady(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor plan,
-                                        int64_t world, int64_t cap, int64_t rank) {
+                                        int64_t world, int64_t cap, int64_t rank,
+                                        c10::optional<std::vector<int64_t>> place = c10::nullopt) {
     check_points(points, true);
     TORCH_CHECK(plan.is_cuda() && plan.numel() == (int64_t)sizeof(kn::RouteParams), "plan must be a route plan");
     TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld && rank >= 0 && rank < world, "bad world / rank");
@@ -699,6 +731,19 @@ std::vector<torch::Tensor> route_steady(torch::Tensor points, c10::optional<torc
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, pp, (int)world, bc.data_ptr<int>(),
                                         totals.data_ptr<int>(), s, reinterpret_cast<unsigned*>(partials.data_ptr<int>())));
+    if (place.has_value()) {
+        // place = [own_base, halo_base, local rows]: the self segment goes straight to the local
+        // (rows, 3) points / global ids (SelfPlace); send holds only the other destinations' rows
+        TORCH_CHECK(place->size() == 3 && (*place)[2] >= 0 && (*place)[2] < INT32_MAX, "place = [own_base, halo_base, rows]");
+        auto lpts = torch::empty({(*place)[2], 3}, points.options());
+        auto lgids = torch::empty({(*place)[2]}, i32);
+        kn::SelfPlace sp{lpts.data_ptr<float>(), lgids.data_ptr<int>(), (int)(*place)[0], (int)(*place)[1],
+                         (int)(*place)[2]};
+        KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, (int)world, bc.data_ptr<int>(),
+                                              totals.data_ptr<int>(), reinterpret_cast<float4*>(send.data_ptr<float>()),
+                                              (int)cap, (int)rank, s, &sp));
+        return {totals, send, partials, lpts, lgids};
+    }
     KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, (int)world, bc.data_ptr<int>(),
                                           totals.data_ptr<int>(), reinterpret_cast<float4*>(send.data_ptr<float>()),
                                           (int)cap, (int)rank, s));
@@ -981,14 +1026,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "multi-GPU query forwarding: exact K nearest of external points among a local grid");
     m.def("steady_flag", &steady_flag, "multi-GPU: on-device check of a sync-free steady-state step");
     m.def("route_steady", &route_steady,
-          "multi-GPU steady step: counts + scatter with a validated plan, share bbox partials on the way");
+          "multi-GPU steady step: counts + scatter with a validated plan, share bbox partials on the way",
+          py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("world"), py::arg("cap"), py::arg("rank"),
+          py::arg("place") = py::none());
     m.def("steady_flag_partials", &steady_flag_partials,
           "multi-GPU: steady-step check with the share bbox from route_steady's partials");
     m.def("dist_local", &dist_local,
           "multi-GPU: unpack + local grid build + owned-point queries from the plan header, one call",
           py::arg("recv"), py::arg("self_rows"), py::arg("recv_own"), py::arg("recv_halo"), py::arg("rank"),
           py::arg("grid"), py::arg("hdr"), py::arg("k"), py::arg("ppc"), py::arg("deterministic"),
-          py::arg("exact_grid") = 0, py::arg("adaptive") = false, py::arg("dims_hint") = py::none());
+          py::arg("exact_grid") = 0, py::arg("adaptive") = false, py::arg("dims_hint") = py::none(),
+          py::arg("pre_pts") = py::none(), py::arg("pre_gids") = py::none());
     m.def("route_unpack_split", &route_unpack_split,
           "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer",

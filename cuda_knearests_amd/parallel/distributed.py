@@ -387,6 +387,8 @@ class DistributedKNearests:
                 "tot": torch.tensor(tot, dtype=torch.int32, device=points.device),
                 "send_counts": send_counts, "recv_own": recv_own, "recv_halo": recv_halo,
                 "cross_send": cross_send, "cross_recv": cross_recv, "x": x,
+                # direct placement of the own segment in steady steps: [own_base, halo_base, rows]
+                "place": [sum(recv_own[:rank]), n_owned + sum(recv_halo[:rank]), n_owned + sum(recv_halo)],
                 "n": int(points.size(0)), "ids": ids is not None, "stats": dict(stats),
                 # fallback launch sized from the validated step's list (short list: 256 WGs)
                 "exact_grid": 256 if int(counters[0].item()) < 4096 else 0,
@@ -484,18 +486,20 @@ class DistributedKNearests:
         C = ops.load()
         world, rank = self.world, self.rank
         src_ids = ids.to(torch.int32).contiguous() if ids is not None else None
-        # counts + scatter with the validated plan; the share's bbox comes from the counting pass
-        totals, send, partials = C.route_steady(points, src_ids, st["plan"], world, st["cap"], rank)
+        # counts + scatter with the validated plan; the share's bbox comes from the counting pass,
+        # and the rank's own segment goes straight to its local rows (no send-buffer copy, no
+        # unpack of it): only rows received from other ranks are unpacked
+        totals, send, partials, lpts, lgids = C.route_steady(points, src_ids, st["plan"], world, st["cap"], rank,
+                                                             st["place"])
         x = st["x"]
         if world > 1:
             recv = self._a2a(send[:x], st["cross_send"], st["cross_recv"])
         else:
             recv = send[:0]
-        sc = st["send_counts"][rank]
-        pts, gids, idx, d2, counters, *_ = C.dist_local(recv, send[x:x + sc], st["recv_own"], st["recv_halo"],
+        pts, gids, idx, d2, counters, *_ = C.dist_local(recv, send[:0], st["recv_own"], st["recv_halo"],
                                                         rank, list(st["grid"]), st["hdr"], self.k,
                                                         self.points_per_cell, self.deterministic, st["exact_grid"],
-                                                        False, st["dims"])
+                                                        False, st["dims"], lpts, lgids)
         flag = C.steady_flag_partials(partials, points.size(0), st["metas"], rank, totals, st["tot"], counters)
         if world > 1:
             self.comm.all_reduce_max(flag)
