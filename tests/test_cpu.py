@@ -176,3 +176,23 @@ def test_kn_log_levels(monkeypatch):
         monkeypatch.setenv("KN_LOG", val)
         monkeypatch.delenv("KN_VERBOSE", raising=False)
         assert lib.kn_default_config().verbose == want, val
+
+
+def test_python_cli_cpu(tmp_path):
+    """python -m cuda_knearests_amd: the reference driver flow from Python (CPU grid solver),
+    checked against the kd-tree oracle, rows written in original order."""
+    import json
+    import subprocess
+    import sys
+
+    from cuda_knearests_amd.utils import REPO, dataset
+
+    out = tmp_path / "nb.txt"
+    r = subprocess.run([sys.executable, "-m", "cuda_knearests_amd", str(dataset("pts20K.xyz")), "--k", "8",
+                        "--device", "cpu", "--check", "--json", "--out", str(out)],
+                       capture_output=True, text=True, timeout=300, cwd=str(REPO))
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["ok"] and line["n"] == 20626
+    rows = out.read_text().splitlines()
+    assert len(rows) == 20626 and len(rows[0].split()) == 8

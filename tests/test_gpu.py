@@ -393,3 +393,11 @@ def test_solve_range_matches_whole_solve(cuda, k):
         e.prepare(p)
         ri, rd = e.solve_range(12345, 6000, cuda)  # before any whole solve: no N x K buffers
         assert torch.equal(ri.cpu(), whole_i[12345:18345]) and torch.equal(rd.cpu(), whole_d[12345:18345])
+
+
+def test_python_cli_gpu_batches(cuda, tmp_path):
+    r = subprocess.run([sys.executable, "-m", "cuda_knearests_amd", str(dataset("pts20K.xyz")), "--k", "16",
+                        "--check", "--json", "--batch", "6000"],
+                       capture_output=True, text=True, timeout=300, cwd=str(REPO))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert '"ok": true' in r.stdout
