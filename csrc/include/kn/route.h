@@ -53,6 +53,7 @@ struct UnpackTable {
     int n_own;
     int rows_cross;  // rows in recv; rows past it come from the self buffer
     int self;        // source whose segment is the self buffer (-1: none)
+    int out_rows;    // rows of the output arrays (0: the rows processed; bounds checks only)
     int seg[kRouteMaxWorld];
     int own[kRouteMaxWorld];
     int own_pref[kRouteMaxWorld];

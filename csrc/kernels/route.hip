@@ -269,7 +269,7 @@ __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restr
         v = recv[j];
     }
     const int out = (o < t.own[lo]) ? t.own_pref[lo] + o : t.n_own + t.halo_pref[lo] + (o - t.own[lo]);
-    const int oo = KN_IDX(out, rows, 402);
+    const int oo = KN_IDX(out, t.out_rows > 0 ? t.out_rows : rows, 402);
     const size_t o3 = 3 * (size_t)oo;
     pts[o3] = v.x;
     pts[o3 + 1] = v.y;

@@ -580,6 +580,7 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
         t.n_own = (int)own;
         t.rows_cross = (int)seg;
         t.self = (int)rank;
+        t.out_rows = (int)(own + halo);  // only the cross rows are processed; outputs span all
         TORCH_CHECK(seg == recv.size(0) && pre_pts->size(0) == own + halo && pre_gids->numel() == own + halo,
                     "source table does not add up to the received / local rows");
         KN_CHECK_HIP(kn::launch_route_unpack(reinterpret_cast<const float4*>(recv.data_ptr<float>()), nullptr,
