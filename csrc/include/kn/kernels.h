@@ -137,6 +137,10 @@ struct QueryBuffers {
 };
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);
+// Complete-box certification of `rows` finished rows (row r = local point r of `pts`, N x 3):
+// uncertified rows are appended to uncert_list and counted in counters[1].
+hipError_t launch_certify_rows(const float* pts, int rows, int k, const float* out_dist, const CompleteBox& cb,
+                               const GridGeom* geom, unsigned* counters, unsigned* uncert_list, hipStream_t stream);
 // Exact K nearest of EXTERNAL points {x, y, z, bits(global id)} among the grid's points (multi-GPU
 // query forwarding): row t of q.out_idx / q.out_dist; a point with the query's global id is
 // skipped (self). Uses q.sorted / cell_start / geom / dims / k / row_of / counters.

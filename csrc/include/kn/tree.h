@@ -44,7 +44,7 @@ struct TreeView {
     unsigned* flag;       // n scratch
     unsigned* incl;       // n scratch
     unsigned* codes;      // 2n Morton codes (sort double buffer)
-    unsigned* vals;       // 2n source indices
+    unsigned* vals;       // 2n source indices; after the build vals[0, n) maps tree point -> input index
     unsigned* info;       // [0] = L after launch_tree_leaves (device)
     void* sort_temp;      // hipCUB temp storage (sort / scan)
     size_t sort_temp_bytes;
@@ -68,6 +68,8 @@ struct TreeQuery {
     int k;
     int n_queries;            // points whose w < n_queries are queries
     const unsigned* id_map;   // optional output id map (as QueryBuffers::id_map)
+    const unsigned* row_of;   // optional global-id mode (as QueryBuffers::row_of: w = global id |
+                              // halo bit, output row = row_of[stored index]; multi-GPU ranks)
     unsigned* out_idx;        // n_queries x k, row = original index
     float* out_dist;          // optional
     unsigned* counters;       // kNumCounters words: [0] exact-finish queries, [2] waves over the

@@ -1488,6 +1488,26 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
     }
 }
 
+// Complete-box certification of finished rows (multi-GPU ranks on the tree path, whose kernels
+// search the whole local point set): row r (= local point r) is certified when its K-th squared
+// distance lies inside the rank's complete box margin; otherwise it is listed for the
+// query-forwarding round (counters[1], uncert_list), as the grid kernels list theirs.
+__global__ void certify_rows_kernel(const float* __restrict__ pts, int rows, int k, const float* __restrict__ out_dist,
+                                    CompleteBox cb, const GridGeom* __restrict__ geom, unsigned* __restrict__ counters,
+                                    unsigned* __restrict__ uncert_list) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const float dk = out_dist[(size_t)r * k + (k - 1)];  // INFINITY when fewer than K were found
+    const float x = pts[3 * (size_t)r], y = pts[3 * (size_t)r + 1], z = pts[3 * (size_t)r + 2];
+    const float m = fminf(fminf(complete_margin(cb, x, 0), complete_margin(cb, y, 1)), complete_margin(cb, z, 2)) -
+                    geom->eps;
+    const bool cert = (m == INFINITY) || (m > 0.f && dk <= m * m);
+    if (!cert) {
+        const unsigned pos = atomicAdd(counters + 1, 1u);
+        uncert_list[KN_IDX(pos, (unsigned)rows, 318)] = (unsigned)r;
+    }
+}
+
 __global__ void invert_perm_kernel(const unsigned* __restrict__ perm, int n, unsigned* __restrict__ inv) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) inv[perm[i]] = (unsigned)i;
@@ -1631,6 +1651,13 @@ size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity) {
 }
 
 KN_DEFINE_DEBUG_READER(debug_words_query)
+
+hipError_t launch_certify_rows(const float* pts, int rows, int k, const float* out_dist, const CompleteBox& cb,
+                               const GridGeom* geom, unsigned* counters, unsigned* uncert_list, hipStream_t s) {
+    if (rows < 0 || k < 1 || !out_dist) return hipErrorInvalidValue;
+    if (rows > 0) certify_rows_kernel<<<cdiv(rows, 256), 256, 0, s>>>(pts, rows, k, out_dist, cb, geom, counters, uncert_list);
+    return hipGetLastError();
+}
 
 hipError_t launch_query_external(const QueryBuffers& q, const float4* ext, int n_ext, hipStream_t s) {
     if (q.k <= 0 || q.k > 128 || n_ext < 0) return hipErrorInvalidValue;

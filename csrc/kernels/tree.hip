@@ -44,7 +44,8 @@ struct TArgs {
     int n_queries;
     int q_lo;  // always 0: the tree path serves whole solves (ranges use the grid kernels)
     const unsigned* id_map;
-    const unsigned* row_of;  // always null: local mode of w_live / w_id / w_row / out_id
+    const unsigned* row_of;  // null: local mode of w_live / w_id / w_row / out_id; else global-id mode
+    const unsigned* src;     // tree point -> input (grid slot) index: row_of is indexed by grid slot
     unsigned* out_idx;
     float* out_dist;
     unsigned* counters;
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         if (lane == 0) atomicAdd(a.counters + 6, nets);
     }
     if (live && cert) {
-        const unsigned row = w_row(a, qw, qpos);
+        const unsigned row = w_row(a, qw, a.row_of ? a.src[KN_IDX(qpos, (unsigned)a.n, 419)] : qpos);
 #pragma unroll
         for (int j = 0; j < KT; ++j) {
             if (j < k) {
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
             __builtin_amdgcn_wave_barrier();
         }
         compact();
-        const unsigned row = w_row(a, qw, qpos);
+        const unsigned row = w_row(a, qw, a.row_of ? a.src[KN_IDX(qpos, (unsigned)a.n, 419)] : qpos);
         for (int j = lane; j < k; j += 64) {
             const size_t o = KN_IDX((size_t)row * (size_t)k + j, (size_t)a.n_queries * k, 415);
             const unsigned long long v = (j < cnt) ? buf[j] : ~0ull;
@@ -563,7 +564,12 @@ hipError_t launch_tree_leaves(const float4* in, const GridGeom* geom, const Tree
     hipcub::DoubleBuffer<unsigned> kb(t.codes, t.codes + n), vb(t.vals, t.vals + n);
     size_t bytes = t.sort_temp_bytes;
     if ((e = hipcub::DeviceRadixSort::SortPairs(t.sort_temp, bytes, kb, vb, n, 0, 30, s)) != hipSuccess) return e;
-    gather_kernel<<<cdiv(n, 256), 256, 0, s>>>(in, vb.Current(), n, t.pts);
+    // vals[0, n) = the input index of every tree point after the build (queries in global-id mode
+    // map a tree point to its grid slot with it: TArgs::src)
+    if (vb.Current() != t.vals &&
+        (e = hipMemcpyAsync(t.vals, vb.Current(), (size_t)n * sizeof(unsigned), hipMemcpyDeviceToDevice, s)) != hipSuccess)
+        return e;
+    gather_kernel<<<cdiv(n, 256), 256, 0, s>>>(in, t.vals, n, t.pts);
     cut_kernel<<<cdiv(n, 256), 256, 0, s>>>(kb.Current(), n, t.flag);
     bytes = t.sort_temp_bytes;
     if ((e = hipcub::DeviceScan::InclusiveSum(t.sort_temp, bytes, t.flag, t.incl, n, s)) != hipSuccess) return e;
@@ -592,7 +598,7 @@ hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t 
     TArgs a{};
     a.pts = t.pts; a.leaf_start = t.leaf_start; a.nlo = t.nlo; a.nhi = t.nhi; a.list = t.list; a.thr = t.thr;
     a.n = t.n; a.L = t.L; a.P = t.P; a.k = q.k; a.n_queries = q.n_queries; a.q_lo = 0; a.id_map = q.id_map;
-    a.row_of = nullptr; a.out_idx = q.out_idx; a.out_dist = q.out_dist; a.counters = q.counters;
+    a.row_of = q.row_of; a.src = t.vals; a.out_idx = q.out_idx; a.out_dist = q.out_dist; a.counters = q.counters;
     a.flags = q.flags;
     constexpr int M = 2;
     const unsigned grid = cdiv(cdiv(t.n, 64), 4);

@@ -173,7 +173,14 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
 
 // Morton-leaf tree over a built grid's points (kn/tree.h): (workspace, node buffer, leaf count).
 // One host sync (the leaf count sizes the node buffer).
+std::tuple<torch::Tensor, torch::Tensor, int64_t> tree_build_impl(torch::Tensor sorted, torch::Tensor geom);
+
 py::tuple tree_build(torch::Tensor sorted, torch::Tensor geom) {
+    auto r = tree_build_impl(sorted, geom);
+    return py::make_tuple(std::get<0>(r), std::get<1>(r), std::get<2>(r));
+}
+
+std::tuple<torch::Tensor, torch::Tensor, int64_t> tree_build_impl(torch::Tensor sorted, torch::Tensor geom) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(geom.is_cuda() && geom.numel() == 16, "geom must be a 16-int GPU tensor");
@@ -193,12 +200,12 @@ py::tuple tree_build(torch::Tensor sorted, torch::Tensor geom) {
     auto nodes = torch::empty({(int64_t)kn::tree_node_bytes((int)L)}, u8);
     kn::tree_attach_nodes(t, nodes.data_ptr(), (int)L);
     KN_CHECK_HIP(kn::launch_tree_nodes(t, s));
-    return py::make_tuple(ws, nodes, (int64_t)L);
+    return {ws, nodes, (int64_t)L};
 }
 
 std::vector<torch::Tensor> tree_query(torch::Tensor ws, torch::Tensor nodes, int64_t leaves, int64_t n, int64_t k,
                                       int64_t n_queries, c10::optional<torch::Tensor> id_map, bool with_dist,
-                                      int64_t flags) {
+                                      int64_t flags, c10::optional<torch::Tensor> row_of = c10::nullopt) {
     TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kUInt8, "ws must be a tree_build workspace");
     TORCH_CHECK(n >= 0 && (size_t)ws.numel() >= kn::tree_workspace_bytes((int)n), "workspace too small for n");
     TORCH_CHECK(nodes.is_cuda() && (size_t)nodes.numel() >= kn::tree_node_bytes((int)leaves), "node buffer too small");
@@ -219,6 +226,11 @@ std::vector<torch::Tensor> tree_query(torch::Tensor ws, torch::Tensor nodes, int
         TORCH_CHECK(id_map->is_cuda() && id_map->scalar_type() == torch::kInt32 && id_map->numel() >= n,
                     "id_map must be an int32 GPU tensor with >= N entries");
         q.id_map = reinterpret_cast<const unsigned*>(id_map->data_ptr<int>());
+    }
+    if (row_of.has_value()) {
+        TORCH_CHECK(row_of->is_cuda() && row_of->scalar_type() == torch::kInt32 && row_of->numel() >= n,
+                    "row_of must be an int32 GPU tensor with >= N entries");
+        q.row_of = reinterpret_cast<const unsigned*>(row_of->data_ptr<int>());
     }
     q.out_idx = reinterpret_cast<unsigned*>(out_idx.data_ptr<int>());
     q.out_dist = with_dist ? out_dist.data_ptr<float>() : nullptr;
@@ -555,7 +567,8 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
                                       int64_t exact_grid = 0, bool adaptive = false,
                                       c10::optional<std::vector<int64_t>> dims_hint = c10::nullopt,
                                       c10::optional<torch::Tensor> pre_pts = c10::nullopt,
-                                      c10::optional<torch::Tensor> pre_gids = c10::nullopt) {
+                                      c10::optional<torch::Tensor> pre_gids = c10::nullopt,
+                                      int64_t use_tree = -1) {
     TORCH_CHECK(grid.size() == 3 && hdr.size() >= 18, "grid must have 3 entries, hdr >= 18");
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world == (int64_t)recv_own.size(), "grid does not match the source table");
@@ -624,6 +637,7 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     auto counters = torch::empty({kn::kNumCounters}, pg[1].options());
     auto g = build_impl(pg[0], dims, deterministic, box, pg[1].data_ptr<int>(), (int)n_owned,
                         reinterpret_cast<unsigned*>(counters.data_ptr<int>()), kn::kNumCounters);
+    bool refined = false;
     if (adaptive && !dims_hint.has_value() && npts > 0) {
         // occupancy-adaptive local grid (as kn::Engine::prepare_from): while the mean occupancy of a
         // point's cell is far above a Poisson grid's, re-bin finer (<= 3 rounds); the tile / halo /
@@ -641,13 +655,35 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
             dims = {nd[0], nd[1], nd[2]};
             g = build_impl(pg[0], dims, deterministic, box, pg[1].data_ptr<int>(), (int)n_owned,
                            reinterpret_cast<unsigned*>(counters.data_ptr<int>()), kn::kNumCounters);
+            refined = true;
         }
+    }
+    // use_tree: -1 auto (the local grid had to be refined: a share too non-uniform for one cell
+    // size, as kn::Engine decides on one GPU), 0 grid, 1 tree
+    const bool tree = use_tree < 0 ? refined : use_tree != 0;
+    auto dims_t = torch::tensor({dims[0], dims[1], dims[2]}, torch::kInt64);
+    auto tree_t = torch::tensor({(int64_t)(tree ? 1 : 0)}, torch::kInt64);
+    if (tree && npts > 0) {
+        // Morton-leaf tree over the local grid's points in global-id mode (owned points are the
+        // queries), then the complete-box certification the grid kernels do inline: uncertified
+        // rows go to the forwarding round
+        auto tb = tree_build_impl(g[0], g[3]);
+        auto tq = tree_query(std::get<0>(tb), std::get<1>(tb), std::get<2>(tb), npts, k, n_owned, c10::nullopt, true,
+                             0, g[2]);
+        auto uncert = torch::empty({std::max<int64_t>(1, n_owned)}, pg[1].options());
+        kn::CompleteBox cb;
+        for (int a = 0; a < 3; ++a) { cb.lo[a] = (float)complete[a]; cb.hi[a] = (float)complete[3 + a]; }
+        KN_CHECK_HIP(kn::launch_certify_rows(pg[0].data_ptr<float>(), (int)n_owned, (int)k, tq[1].data_ptr<float>(), cb,
+                                             reinterpret_cast<const kn::GridGeom*>(g[3].data_ptr<int>()),
+                                             reinterpret_cast<unsigned*>(tq[2].data_ptr<int>()),
+                                             reinterpret_cast<unsigned*>(uncert.data_ptr<int>()),
+                                             c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+        return {pg[0], pg[1], tq[0], tq[1], tq[2], g[0], g[1], g[3], g[2], uncert, dims_t, tree_t};
     }
     auto q = query(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
                    ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid, counters);
     // + the local grid (global-id mode) and the uncertified list, for query forwarding
-    auto dims_t = torch::tensor({dims[0], dims[1], dims[2]}, torch::kInt64);
-    return {pg[0], pg[1], q[0], q[1], q[2], g[0], g[1], g[3], g[2], q[3], dims_t};
+    return {pg[0], pg[1], q[0], q[1], q[2], g[0], g[1], g[3], g[2], q[3], dims_t, tree_t};
 }
 
 // Exact K nearest of external points (multi-GPU query forwarding) among a global-id-mode local
@@ -1004,7 +1040,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("sorted"), py::arg("geom"));
     m.def("tree_query", &tree_query, "kNN through a tree_build result: (idx, d2, counters)", py::arg("ws"),
           py::arg("nodes"), py::arg("leaves"), py::arg("n"), py::arg("k"), py::arg("n_queries"), py::arg("id_map") = py::none(),
-          py::arg("with_dist") = true, py::arg("flags") = 0);
+          py::arg("with_dist") = true, py::arg("flags") = 0, py::arg("row_of") = py::none());
     m.def("cell_sort", &cell_sort, "in-cell order by original index (deterministic layout) of a built grid");
     m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");
     m.def("refine_dims", &refine_dims, "finer grid dims for an over-occupied grid, or None");
@@ -1037,7 +1073,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("recv"), py::arg("self_rows"), py::arg("recv_own"), py::arg("recv_halo"), py::arg("rank"),
           py::arg("grid"), py::arg("hdr"), py::arg("k"), py::arg("ppc"), py::arg("deterministic"),
           py::arg("exact_grid") = 0, py::arg("adaptive") = false, py::arg("dims_hint") = py::none(),
-          py::arg("pre_pts") = py::none(), py::arg("pre_gids") = py::none());
+          py::arg("pre_pts") = py::none(), py::arg("pre_gids") = py::none(), py::arg("use_tree") = -1);
     m.def("route_unpack_split", &route_unpack_split,
           "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer",

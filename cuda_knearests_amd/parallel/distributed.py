@@ -376,7 +376,8 @@ class DistributedKNearests:
             src_pts, src_ids = own_pts, own_ids
         stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
                  "grid": tuple(grid), "forwarded": n_fwd, "exact_path": int(counters[0].item()),
-                 "local_dims": tuple(int(v) for v in local_grid[5].tolist())}
+                 "local_dims": tuple(int(v) for v in local_grid[5].tolist()),
+                 "local_tree": bool(local_grid[6].item())}
         _log.debug("rank %d: step %s", rank, stats)
         if rounds == 1 and not full and self.steady:
             # validated single-round step: the steady-state assumption for the next ones
@@ -384,6 +385,7 @@ class DistributedKNearests:
                 "metas": metas, "grid": tuple(grid), "hdr": hv[:HDR], "cap": int(send.size(0)), "splits": splits,
                 "plan": plan,  # the validated route plan (steady steps do not re-plan)
                 "dims": [int(v) for v in local_grid[5].tolist()],  # the local grid (maybe refined)
+                "use_tree": int(local_grid[6].item()),  # the local solve ran the tree path
                 "tot": torch.tensor(tot, dtype=torch.int32, device=points.device),
                 "send_counts": send_counts, "recv_own": recv_own, "recv_halo": recv_halo,
                 "cross_send": cross_send, "cross_recv": cross_recv, "x": x,
@@ -499,7 +501,7 @@ class DistributedKNearests:
         pts, gids, idx, d2, counters, *_ = C.dist_local(recv, send[:0], st["recv_own"], st["recv_halo"],
                                                         rank, list(st["grid"]), st["hdr"], self.k,
                                                         self.points_per_cell, self.deterministic, st["exact_grid"],
-                                                        False, st["dims"], lpts, lgids)
+                                                        False, st["dims"], lpts, lgids, st["use_tree"])
         flag = C.steady_flag_partials(partials, points.size(0), st["metas"], rank, totals, st["tot"], counters)
         if world > 1:
             self.comm.all_reduce_max(flag)
