@@ -2,27 +2,29 @@
 
 The reference is single-GPU (knearests.cu has no streams, devices or collectives).
 Here: one process per GPU, ``torch.distributed`` with backend ``"nccl"`` (= RCCL over xGMI on
-ROCm) or ``"gloo"`` (CPU ranks, used by the tests). Per solve:
+ROCm) or ``"gloo"`` (CPU ranks, used by the tests). DESIGN.md §5 has the full picture.
 
-1. **meta** -- one ``all_gather`` of {local bbox, point count} (8 doubles per rank) gives the
-   global domain, the total N (halo width) and every rank's id offset; one host sync.
-2. **route** -- every point is sent to its OWNER rank (the box of a px*py*pz decomposition that
-   contains it) and, as a HALO copy, to every rank whose box is within ``h`` of it, in ONE
-   ``all_to_all_single`` of float4 rows {x, y, z, bits(global id)}. GPU ranks build the send
-   buffer with the native router (``csrc/kernels/route.hip``: per-block counts -> scan ->
-   ballot-ranked scatter, deterministic order); the (owned, halo) counts per destination are
-   exchanged first (a tiny all-to-all, one host sync for both directions' split sizes).
-   ``h`` = ``halo_factor`` x the expected K-th neighbour radius of the whole cloud.
-3. **local solve** on owned + halo points (GPU: grid build over the rank's box + the LDS-tiled
-   HIP query kernel; CPU: the native grid solver). Queries = owned points; neighbour ids are
-   mapped to global ids on the device; every query is certified against the rank's *complete
-   box* (own box grown by h, unbounded on domain faces).
-4. **growth round** (rare): if any rank has an uncertified query (its K-th distance reaches past
-   the complete box) one all-reduce says so, ``h`` doubles and the halo is re-routed.
+Full (validating) step, GPU ranks:
+1. **meta + plan** -- the local bbox/count is all-gathered (speculatively: the previous step's
+   metas plan the routing and this step's metas travel with the counts in one all-gather);
+   ``route_begin`` computes on the device the global domain, the halo width ``h`` (halo_factor x
+   the expected K-th neighbour radius), the rank boxes (count-balanced kd splits by default) and
+   routes every point to its OWNER and, as HALO copies, to every rank whose box is within ``h``.
+   One host sync reads the split sizes.
+2. **route** -- one ``all_to_all_single`` of float4 rows {x, y, z, bits(global id)} (self-last
+   layout: the rank's own rows never enter the collective).
+3. **local solve** (``dist_local``) -- occupancy-adaptive local grid over the rank's box + halo,
+   owned points are the queries, global ids written by the build; the grid kernels, or the tree
+   path when the local grid had to be refined; every query certified against the rank's
+   *complete box* (own box grown by h, unbounded on domain faces).
+4. **forwarding round** (rare) -- uncertified queries go to the ranks within their K-th distance
+   and are answered there (exact in one round).
 
+Steady state (after a validated single-round step): no host synchronisation at all -- cached
+plan, the own segment placed straight into the local rows, an on-device check of the step's
+assumptions all-reduced into a flag that is read asynchronously (``DistResult.valid``).
 xGMI is point-to-point: with 2x2x2 ranks every rank neighbours all 7 others, so the single
-all-to-all-v keeps all 7 links busy at once; per step there are 3 small host syncs (meta,
-counts, certification flag) and one bulk collective.
+all-to-all keeps all 7 links busy at once.
 """
 from __future__ import annotations
 
