@@ -490,7 +490,13 @@ hipError_t launch_cell_sort(const int* cell_start, const GridGeom* geom, int n, 
 
 bool bin_plan(int n, int num_cells, BinPlan* out) {
     if (n <= 0 || num_cells <= 0) return false;
-    const int nblocks = std::max(1, std::min((int)cdiv((size_t)n, 4096), 1024));
+    // points per streaming block (KN_BIN_ITEMS, A/B): fewer -> more blocks, more bucket columns
+    static const int items = [] {
+        const char* v = std::getenv("KN_BIN_ITEMS");
+        const int t = v ? std::atoi(v) : 4096;
+        return (t >= 512 && t <= 65536) ? t : 4096;
+    }();
+    const int nblocks = std::max(1, std::min((int)cdiv((size_t)n, (size_t)items), 1024));
     const int per_block = (int)(cdiv(cdiv((size_t)n, nblocks), 256) * 256);
     for (int shift = 8; shift <= 14; ++shift) {
         const long long nbuckets = ((long long)num_cells + (1ll << shift) - 1) >> shift;
