@@ -152,9 +152,11 @@ class DistributedKNearests:
         self.forward = True
         # hipGraph replay of the steady step (torch.cuda.CUDAGraph), opt-in: KN_DIST_GRAPH=1 or
         # graph_steady = True. Replayed rows live in the graph's static buffers until the next
-        # solve. Off by default: back-to-back replays of the captured step at 900K points faulted
-        # once on MI355X (illegal address) while separately synchronised replays and the eager
-        # steady step did not; not yet root-caused.
+        # solve. At world 1 (RCCL) 200 back-to-back replays are valid and bit-identical to the
+        # eager steady step on the release and the bounds-checked builds, host enqueue 0.14 ->
+        # 0.06 ms per step (profiles/ab_r2_dist_graph.txt; an early round-2 version faulted once
+        # in this mode). Not the default because capturing RCCL collectives (world > 1) cannot
+        # be exercised on a one-GPU box.
         self.graph_steady = None
         self._graph = None
 

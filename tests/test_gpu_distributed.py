@@ -429,3 +429,24 @@ def test_adaptive_local_grid_clustered(cuda):
     refined = [o[-1]["local_dims"] != f[-1]["local_dims"] for o, f in zip(adapt, fixed)]
     assert any(refined), [o[-1]["local_dims"] for o in adapt]
     assert ex_adapt <= ex_fixed, (ex_adapt, ex_fixed)
+
+
+def test_rccl_world1_graph_replay(cuda):
+    """Steady distributed steps replayed from a hipGraph (torch.cuda.CUDAGraph, opt-in
+    graph_steady / KN_DIST_GRAPH=1): back-to-back replays without host synchronisation are all
+    valid and give the eager steady step's rows bit for bit."""
+    import subprocess
+    import sys
+
+    from cuda_knearests_amd.utils import REPO
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONPATH=str(REPO), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               RANK="0", WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, str(REPO / "scripts" / "diag_dist_graph.py"), "60", "200000"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "graph True valid True same rows as eager True" in r.stdout
