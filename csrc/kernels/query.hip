@@ -1564,7 +1564,10 @@ template <int KT>
 hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     // margin slots beyond K: a query is lost to the exact path only if the K-th and (K+M)-th
     // distances collide within one truncation ulp (~2^-(23-SB)); M=3 makes that ~1e-7/query.
-    constexpr int M = 2;
+#ifndef KN_TOPK_MARGIN
+#define KN_TOPK_MARGIN 2
+#endif
+    constexpr int M = KN_TOPK_MARGIN;
     const int X = q.dims[0], Y = q.dims[1], Z = q.dims[2];
     hipError_t e = hipSuccess;
     if (!q.counters_zeroed && (e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s)) != hipSuccess)
