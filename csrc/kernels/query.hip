@@ -491,20 +491,23 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             [&](int s0, int s1) {
                 int s = s0;
                 if constexpr (LANE) {
-                    // divergent per-lane walk: KN_LANE_UNROLL gathers in flight per lane
+                    // divergent per-lane walk: kUnroll gathers in flight per lane (the K=50 bucket
+                    // runs 1: 900K 0.946 -> 0.923 ms query, K=64 and K=16 lose with 1,
+                    // profiles/ab_r2_lane_unroll.txt)
+                    constexpr int kUnroll = (KT > 40 && KT <= 50) ? 1 : KN_LANE_UNROLL;
                     if constexpr (kStats) {
                         st_rows += (s1 > s0) ? 1u : 0u;
                         st_cand += (unsigned)max(0, s1 - s0);
                     }
-                    for (; s + KN_LANE_UNROLL <= s1; s += KN_LANE_UNROLL) {
-                        float4 p[KN_LANE_UNROLL];
-                        unsigned kk[KN_LANE_UNROLL];
+                    for (; s + kUnroll <= s1; s += kUnroll) {
+                        float4 p[kUnroll];
+                        unsigned kk[kUnroll];
 #pragma unroll
-                        for (int u = 0; u < KN_LANE_UNROLL; ++u) p[u] = pts[s + u];
+                        for (int u = 0; u < kUnroll; ++u) p[u] = pts[s + u];
 #pragma unroll
-                        for (int u = 0; u < KN_LANE_UNROLL; ++u) kk[u] = cand_key_v(p[u], qx, qy, qz, HIMASK, s + u);
+                        for (int u = 0; u < kUnroll; ++u) kk[u] = cand_key_v(p[u], qx, qy, qz, HIMASK, s + u);
 #pragma unroll
-                        for (int u = 0; u < KN_LANE_UNROLL; ++u) {
+                        for (int u = 0; u < kUnroll; ++u) {
                             const unsigned i0 = topk_push<KM>(keys, kk[u]);
                             if constexpr (kStats) st_ins += i0;
                         }
