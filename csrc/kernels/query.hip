@@ -491,10 +491,11 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             [&](int s0, int s1) {
                 int s = s0;
                 if constexpr (LANE) {
-                    // divergent per-lane walk: kUnroll gathers in flight per lane (the K=50 bucket
-                    // runs 1: 900K 0.946 -> 0.923 ms query, K=64 and K=16 lose with 1,
-                    // profiles/ab_r2_lane_unroll.txt)
-                    constexpr int kUnroll = (KT > 40 && KT <= 50) ? 1 : KN_LANE_UNROLL;
+                    // divergent per-lane walk: kUnroll gathers in flight per lane, per K bucket from
+                    // interleaved A/Bs at 900K (profiles/ab_r2_lane_unroll.txt): 3 for K <= 40
+                    // (vs 2: K=8 -3.8 %, 16 -1.5 %, 24 -3.6 %, 32 -1 to -3 %, 40 -3.1 %), 1 for
+                    // the K=50 bucket (-2.4 %), 2 for K=64 (1 and 3 lose or tie)
+                    constexpr int kUnroll = KT <= 40 ? 3 : (KT <= 50 ? 1 : KN_LANE_UNROLL);
                     if constexpr (kStats) {
                         st_rows += (s1 > s0) ? 1u : 0u;
                         st_cand += (unsigned)max(0, s1 - s0);
