@@ -105,7 +105,10 @@ struct TileArgs {
 #ifndef KN_WINDOW_RERANK
 #define KN_WINDOW_RERANK 1
 #endif
-constexpr int kWin = 3;
+#ifndef KN_WIN
+#define KN_WIN 2
+#endif
+constexpr int kWin = KN_WIN;  // exact re-rank window: same-bucket neighbours within +-kWin
 constexpr int kCoopCap = 128;  // per-wave LDS buffer of the cooperative re-scan (u64 keys)
 constexpr int kQueryForceRescan = 1;
 // fallback-list entry flag: the query's output row holds K real candidates (their K-th squared
