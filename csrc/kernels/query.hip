@@ -106,7 +106,7 @@ struct TileArgs {
 #define KN_WINDOW_RERANK 1
 #endif
 #ifndef KN_WIN
-#define KN_WIN 2
+#define KN_WIN 1
 #endif
 constexpr int kWin = KN_WIN;  // exact re-rank window: same-bucket neighbours within +-kWin
 constexpr int kCoopCap = 128;  // per-wave LDS buffer of the cooperative re-scan (u64 keys)
