@@ -182,6 +182,10 @@ AutoParams auto_params(int n, int k, float points_per_cell, const int* tile_hint
 // {site code, index, limit, index high word}; all 0xFFFFFFFF in release builds.
 hipError_t debug_words_build(unsigned out[4], bool reset);
 hipError_t debug_words_query(unsigned out[4], bool reset);
+// -DKN_PHASES=1 builds: wave cycles of knn_tile_kernel per phase, summed over waves:
+// {stage (+ the kernel tail), chunk setup, scan (hot loop), re-rank, certify, chunks, waves, -}.
+// Other builds: hipErrorNotSupported.
+hipError_t debug_phase_cycles(unsigned long long out[8], bool reset);
 
 size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity);
 int lds_capacity_for(double staged_points);

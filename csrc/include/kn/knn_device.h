@@ -135,6 +135,19 @@ __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key
     return 0u;
 }
 
+// Branch-free insertion (bulk flushes of the collect-mode queue, where some lane of the wave
+// almost always improves, so a ballot test would only add an instruction).
+// The med3 chain is issued in descending slot order as VOLATILE asm, so each new[j] is written
+// over old[j] after old[j] fed new[j+1]: the list is updated in place. Left to the scheduler,
+// the independent med3s were reordered and the allocator kept a second copy of the list
+// (K=50: 118 -> 169 VGPRs, i.e. 2 instead of 3 waves per SIMD).
+template <int KM>
+__device__ __forceinline__ void topk_insert(unsigned (&keys)[KM], unsigned key) {
+#pragma unroll
+    for (int j = KM - 1; j > 0; --j)
+        asm volatile("v_med3_u32 %0, %1, %2, %0" : "+v"(keys[j]) : "v"(keys[j - 1]), "v"(key));
+    asm volatile("v_min_u32 %0, %0, %1" : "+v"(keys[0]) : "v"(key));
+}
 
 // Wave-wide sum (DPP within rows of 16, then the 4 row totals).
 __device__ __forceinline__ unsigned wave_sum_u32(unsigned x) {

@@ -69,7 +69,12 @@ struct SelfPlace {
     int* gids;
     int own_base;   // sum of recv_own over the sources before this rank
     int halo_base;  // n_own + sum of recv_halo over the sources before this rank
-    int rows;       // local rows (bounds checks)
+    int rows;       // local rows: every write is checked against it
+    // the planned size of the self segment (validated step): a step whose own / halo counts for
+    // this rank differ writes NOTHING (its rows would land at other offsets, possibly past
+    // `rows`); the steady flag, which compares every count with the plan, rejects the step
+    int own_cnt;
+    int halo_cnt;
 };
 
 int route_block_count(int n);

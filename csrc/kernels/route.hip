@@ -181,6 +181,8 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
         // same decision in every block: nothing is written. With direct self placement the
         // self segment does not occupy the send buffer.
         overflow = (sp.pts ? seg_self : seg) > send_rows;
+        if (sp.pts && (totals[2 * self_last] != sp.own_cnt || totals[2 * self_last + 1] != sp.halo_cnt))
+            overflow = 1;  // self segment differs from the plan: placing it could overrun `rows`
     }
     __syncthreads();
     if (overflow) return;
@@ -225,6 +227,7 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
                         // would compute): owned first over all sources, halo after
                         const int j = off - seg_self;
                         const int loc = po ? sp.own_base + j : sp.halo_base + (j - totals[2 * d]);
+                        if (loc < 0 || loc >= sp.rows) continue;  // unreachable after the prologue check
                         const size_t l3 = 3 * (size_t)KN_IDX(loc, sp.rows, 403);
                         sp.pts[l3] = x;
                         sp.pts[l3 + 1] = y;

@@ -109,7 +109,9 @@ kn_status kn_solve_ex(kn_problem* kn) {
     kn_status s = e->solve();
     // reference semantics: d_knearests holds the stored-space result after kn_solve
     // (knearests.cu:329-364); the engine solves in original space, one remap kernel converts
-    if (s == KN_OK && !e->d_knn_stored()) s = KN_ERR_DEVICE;
+    // (N*K ids + N inverse permutation). Non-fatal: if that buffer does not fit, the solve still
+    // succeeded, d_knearests stays NULL and the getters convert on demand.
+    if (s == KN_OK && !e->d_knn_stored()) g_err = "kn_solve: stored-space d_knearests not materialised: " + e->error();
     if (s != KN_OK) g_err = e->error();
     sync_fields(kn);
     return s;

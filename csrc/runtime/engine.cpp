@@ -37,7 +37,6 @@ void Engine::release() {
     if (out_dist_) { (void)hipFree(out_dist_); out_dist_ = nullptr; }
     if (inv_perm_) { (void)hipFree(inv_perm_); inv_perm_ = nullptr; }
     if (knn_stored_) { (void)hipFree(knn_stored_); knn_stored_ = nullptr; }
-    if (dist_stored_) { (void)hipFree(dist_stored_); dist_stored_ = nullptr; }
     if (points3_) { (void)hipFree(points3_); points3_ = nullptr; }
     if (tree_ws_) { (void)hipFree(tree_ws_); tree_ws_ = nullptr; }
     if (tree_nodes_) { (void)hipFree(tree_nodes_); tree_nodes_ = nullptr; }
@@ -117,7 +116,7 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
     occ_ = carve<unsigned long long>(p, 1);
     // outputs
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
-                     (void**)&dist_stored_, (void**)&points3_})
+                     (void**)&points3_})
         if (*q) { (void)hipFree(*q); *q = nullptr; }
     // the N x K outputs are allocated on the first whole solve (ensure_outputs): a caller that
     // only solves query ranges (solve_range, kn_solve_range) never holds them
@@ -281,6 +280,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     // A grid that had to be refined serves a cloud whose density varies too much for one cell
     // size (900K clustered, K=16: grid query 7.5 ms, tree 1.6 ms + 0.27 ms build; surfaces
     // 1.27 vs 0.96 + 0.27; profiles/diag_r2_tree.jsonl): the tree path takes it.
+    refined_ = refined;
     use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined));
     if (use_tree_ && graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
@@ -378,7 +378,7 @@ kn_status Engine::set_k(int k) {
         ap_.lds_capacity = lds_capacity_for(staged);
         ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity);
     }
-    for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_, (void**)&dist_stored_})
+    for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_})
         if (*q) { (void)hipFree(*q); *q = nullptr; }
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     solved_ = stored_valid_ = false;
@@ -482,16 +482,15 @@ kn_status Engine::counters(unsigned out[kNumCounters]) {
 unsigned* Engine::d_knn_stored() {
     if (!solved_) return nullptr;
     if (stored_valid_) return knn_stored_;
+    // ids only: the reference exposes no distances (knearests.h:3-16), so the stored-space
+    // distance copy is made on demand by get_distances_stored()
     const size_t nk = std::max<size_t>(1, (size_t)n_ * cfg_.k);
     if (!inv_perm_ && check(hipMalloc(&inv_perm_, std::max<size_t>(1, n_) * sizeof(unsigned)), "hipMalloc(inv)") != KN_OK)
         return nullptr;
     if (!knn_stored_ && check(hipMalloc(&knn_stored_, nk * sizeof(unsigned)), "hipMalloc(knn_stored)") != KN_OK)
         return nullptr;
-    if (out_dist_ && !dist_stored_ && check(hipMalloc(&dist_stored_, nk * sizeof(float)), "hipMalloc(dist_stored)") != KN_OK)
-        return nullptr;
     if (check(launch_invert_perm(perm_, n_, inv_perm_, stream_), "invert perm") != KN_OK) return nullptr;
-    if (check(launch_to_stored_space(out_idx_, perm_, inv_perm_, n_, cfg_.k, knn_stored_, out_dist_,
-                                     dist_stored_, stream_),
+    if (check(launch_to_stored_space(out_idx_, perm_, inv_perm_, n_, cfg_.k, knn_stored_, nullptr, nullptr, stream_),
               "to stored space") != KN_OK)
         return nullptr;
     if (check(hipStreamSynchronize(stream_), "sync") != KN_OK) return nullptr;
@@ -543,8 +542,18 @@ unsigned* Engine::get_knearests_stored() {
 }
 float* Engine::get_distances_stored() {
     if (!out_dist_) { fail(KN_ERR_STATE, "distances disabled"); return nullptr; }
-    if (!d_knn_stored()) return nullptr;
-    return d2h(dist_stored_, (size_t)n_ * cfg_.k, stream_);
+    if (!d_knn_stored()) return nullptr;  // also builds inv_perm_
+    // stored-space distances: a temporary device buffer, freed before returning
+    const size_t nk = (size_t)n_ * cfg_.k;
+    float* tmp = nullptr;
+    if (check(hipMalloc(&tmp, std::max<size_t>(1, nk) * sizeof(float)), "hipMalloc(dist_stored)") != KN_OK) return nullptr;
+    float* out = nullptr;
+    // the id half rewrites knn_stored_ with the values it already holds
+    if (check(launch_to_stored_space(out_idx_, perm_, inv_perm_, n_, cfg_.k, knn_stored_, out_dist_, tmp, stream_),
+              "to stored space") == KN_OK)
+        out = d2h(tmp, nk, stream_);
+    (void)hipFree(tmp);
+    return out;
 }
 unsigned* Engine::get_neighbors_original() {
     if (!solved_) { fail(KN_ERR_STATE, "not solved"); return nullptr; }
@@ -585,7 +594,11 @@ kn_status Engine::stats(kn_stats* out, std::vector<int>* hist) {
 
 namespace {
 constexpr unsigned kMagicV1 = 0x4b4e4731;  // "KNG1": {magic, n, dims[3], k}
-constexpr unsigned kMagic = 0x4b4e4732;    // "KNG2": + {tile[3], halo, lds_capacity, refined}
+constexpr unsigned kMagic = 0x4b4e4732;    // "KNG2": + {tile[3], halo, lds_capacity, flags}
+// KNG2 flags word: bit 0 = the plan words are valid, bit 1 = the grid was refined (the cloud's
+// density varies: algo auto serves it with the tree path)
+constexpr int kPlanValid = 1, kPlanRefined = 2;
+constexpr size_t kMaxLdsBytes = 160 * 1024;  // gfx950 LDS per workgroup
 }  // namespace
 
 kn_status Engine::save(const char* path) {
@@ -602,7 +615,8 @@ kn_status Engine::save(const char* path) {
     // the tile / halo / LDS plan travels with the grid: a refined (occupancy-adaptive) grid keeps
     // the plan of the target density, which allocate() cannot re-derive from n / C
     const int hdr[12] = {(int)kMagic, n_, ap_.dims[0], ap_.dims[1], ap_.dims[2], cfg_.k,
-                         ap_.tile[0], ap_.tile[1], ap_.tile[2], ap_.halo, ap_.lds_capacity, 1};
+                         ap_.tile[0], ap_.tile[1], ap_.tile[2], ap_.halo, ap_.lds_capacity,
+                         kPlanValid | (refined_ ? kPlanRefined : 0)};
     f.write((const char*)hdr, sizeof(hdr));
     f.write((const char*)&g, sizeof(g));
     f.write((const char*)s.data(), s.size() * sizeof(float4));
@@ -648,13 +662,27 @@ Engine* Engine::load(const char* path, const EngineConfig& cfg, std::string* err
     Engine* e = new Engine(c);
     const int dims[3] = {hdr[2], hdr[3], hdr[4]};
     if (e->allocate(n, dims) != KN_OK) { if (err) *err = e->error(); delete e; return nullptr; }
-    if (v2 && hdr[11] && c.k == hdr[5]) {
-        // same K: restore the saved plan (refined grids keep the target density's LDS plan)
-        for (int a = 0; a < 3; ++a) e->ap_.tile[a] = std::max(1, hdr[6 + a]);
-        e->ap_.halo = std::max(1, hdr[9]);
-        e->ap_.lds_capacity = std::max(128, std::min(hdr[10], 8192));
+    if (v2 && (hdr[11] & kPlanValid) && c.k == hdr[5]) {
+        // same K: restore the saved plan (refined grids keep the target density's LDS plan);
+        // a plan the device cannot launch (corrupt / hostile file) is rejected here, not at the
+        // first query launch
+        int tile[3];
+        for (int a = 0; a < 3; ++a) tile[a] = hdr[6 + a];
+        const bool sane = tile[0] >= 1 && tile[1] >= 1 && tile[2] >= 1 && tile[0] <= 64 && tile[1] <= 64 &&
+                          tile[2] <= 64 && hdr[9] >= 1 && hdr[9] <= 16 && hdr[10] >= 64 && hdr[10] <= 8192;
+        if (!sane || query_lds_bytes(tile, hdr[9], hdr[10]) > kMaxLdsBytes) {
+            if (err) *err = "corrupt file: query plan exceeds the device's LDS";
+            delete e;
+            return nullptr;
+        }
+        for (int a = 0; a < 3; ++a) e->ap_.tile[a] = tile[a];
+        e->ap_.halo = hdr[9];
+        e->ap_.lds_capacity = hdr[10];
         e->ap_.lds_bytes = query_lds_bytes(e->ap_.tile, e->ap_.halo, e->ap_.lds_capacity);
     }
+    // the refined state travels with the grid: algo auto serves a refined grid with the tree
+    e->refined_ = v2 && (hdr[11] & kPlanRefined);
+    e->use_tree_ = c.use_tiles && (c.algo == 2 || (c.algo == 0 && e->refined_));
     bool ok = hipMemcpy(e->geom_, &g, sizeof(g), hipMemcpyHostToDevice) == hipSuccess &&
               (n == 0 || hipMemcpy(e->sorted_, s.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice) == hipSuccess) &&
               (n == 0 || hipMemcpy(e->perm_, perm.data(), (size_t)n * sizeof(unsigned), hipMemcpyHostToDevice) == hipSuccess) &&

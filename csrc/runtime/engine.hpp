@@ -133,12 +133,12 @@ private:
     float* out_dist_ = nullptr;
     unsigned* inv_perm_ = nullptr;
     unsigned* knn_stored_ = nullptr;
-    float* dist_stored_ = nullptr;
     float* points3_ = nullptr;  // stored-order float3 copy of sorted_ (reference d_stored_points)
     bool points3_valid_ = false;
     bool built_ = false, solved_ = false, stored_valid_ = false;
     unsigned last_fallback_ = ~0u;  // fallback-list length of the last eager solve (~0: unknown)
     bool use_tree_ = false;         // chosen at prepare (EngineConfig::algo)
+    bool refined_ = false;          // the occupancy-adaptive grid was refined (saved with the grid)
     void* tree_ws_ = nullptr;
     size_t tree_ws_bytes_ = 0;
     void* tree_nodes_ = nullptr;

@@ -769,13 +769,15 @@ std::vector<torch::Tensor> route_steady(torch::Tensor points, c10::optional<torc
     KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, pp, (int)world, bc.data_ptr<int>(),
                                         totals.data_ptr<int>(), s, reinterpret_cast<unsigned*>(partials.data_ptr<int>())));
     if (place.has_value()) {
-        // place = [own_base, halo_base, local rows]: the self segment goes straight to the local
-        // (rows, 3) points / global ids (SelfPlace); send holds only the other destinations' rows
-        TORCH_CHECK(place->size() == 3 && (*place)[2] >= 0 && (*place)[2] < INT32_MAX, "place = [own_base, halo_base, rows]");
+        // place = [own_base, halo_base, local rows, planned own, planned halo]: the self segment
+        // goes straight to the local (rows, 3) points / global ids (SelfPlace); send holds only the
+        // other destinations' rows. A self segment of another size than planned writes nothing.
+        TORCH_CHECK(place->size() == 5 && (*place)[2] >= 0 && (*place)[2] < INT32_MAX,
+                    "place = [own_base, halo_base, rows, own_cnt, halo_cnt]");
         auto lpts = torch::empty({(*place)[2], 3}, points.options());
         auto lgids = torch::empty({(*place)[2]}, i32);
         kn::SelfPlace sp{lpts.data_ptr<float>(), lgids.data_ptr<int>(), (int)(*place)[0], (int)(*place)[1],
-                         (int)(*place)[2]};
+                         (int)(*place)[2], (int)(*place)[3], (int)(*place)[4]};
         KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, (int)world, bc.data_ptr<int>(),
                                               totals.data_ptr<int>(), reinterpret_cast<float4*>(send.data_ptr<float>()),
                                               (int)cap, (int)rank, s, &sp));
@@ -932,6 +934,13 @@ public:
 private:
     std::unique_ptr<kn::Engine> e_;
 };
+
+// -DKN_PHASES=1 builds: knn_tile_kernel wave cycles per phase (kn/kernels.h); empty otherwise
+std::vector<int64_t> debug_phase_cycles(bool reset) {
+    unsigned long long v[8];
+    if (kn::debug_phase_cycles(v, reset) != hipSuccess) return {};
+    return std::vector<int64_t>(v, v + 8);
+}
 
 std::vector<int64_t> debug_words(bool reset) {
     unsigned b[4], q[4], r[4], t[4];
@@ -1095,6 +1104,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("solve_range", &PyEngine::solve_range, py::arg("first"), py::arg("count"), py::arg("device"))
         .def("counters", &PyEngine::counters)
         .def("info", &PyEngine::info);
+    m.def("debug_phase_cycles", &debug_phase_cycles, "KN_PHASES builds: query-kernel wave cycles per phase",
+          py::arg("reset") = false);
     m.def("debug_words", &debug_words, "checked builds: first OOB report {code, index, limit, hi} of build and query kernels",
           py::arg("reset") = false);
 #if defined(KN_CHECKED) && KN_CHECKED

@@ -28,6 +28,7 @@ all-to-all keeps all 7 links busy at once.
 """
 from __future__ import annotations
 
+import collections
 import math
 import time
 from dataclasses import dataclass
@@ -92,7 +93,9 @@ class DistResult:
     event: Optional[object] = None
 
     def valid(self) -> bool:
-        """True when the rows are final (waits for the step's flag; no-op for synchronous steps)."""
+        """True when the rows are final (waits for the step's flag; no-op for synchronous steps).
+        Reading it never changes the solver's state: which path the next step takes is decided
+        inside solve() from the flags of earlier steps, identically on every rank."""
         if self.flag is None:
             return True
         if self.event is not None:
@@ -159,6 +162,12 @@ class DistributedKNearests:
         # be exercised on a one-GPU box.
         self.graph_steady = None
         self._graph = None
+        # asynchronous steady results not yet checked by the solver. Before the next steady step
+        # all but the newest are checked (their steps are long done, so this rarely waits, and it
+        # bounds the host's lead to ~2 steps): an invalid one drops the steady plan. The flags
+        # are all-reduced and every rank checks the same steps at the same call, so all ranks
+        # take the same path (a caller's own valid() calls decide nothing).
+        self._pending = collections.deque()
 
     # ------------------------------------------------------------------ helpers ------
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
@@ -393,8 +402,10 @@ class DistributedKNearests:
                 "tot": torch.tensor(tot, dtype=torch.int32, device=points.device),
                 "send_counts": send_counts, "recv_own": recv_own, "recv_halo": recv_halo,
                 "cross_send": cross_send, "cross_recv": cross_recv, "x": x,
-                # direct placement of the own segment in steady steps: [own_base, halo_base, rows]
-                "place": [sum(recv_own[:rank]), n_owned + sum(recv_halo[:rank]), n_owned + sum(recv_halo)],
+                # direct placement of the own segment in steady steps: [own_base, halo_base, rows,
+                # planned own count, planned halo count] (a different self count writes nothing)
+                "place": [sum(recv_own[:rank]), n_owned + sum(recv_halo[:rank]), n_owned + sum(recv_halo),
+                          tot[2 * rank], tot[2 * rank + 1]],
                 "n": int(points.size(0)), "ids": ids is not None, "stats": dict(stats),
                 # fallback launch sized from the validated step's list (short list: 256 WGs)
                 "exact_grid": 256 if int(counters[0].item()) < 4096 else 0,
@@ -557,6 +568,18 @@ class DistributedKNearests:
         stats["graph"] = self._graph is not None and self._use_graph(points)
         return DistResult(gid, idx, d2, stats, flag=host, event=ev)
 
+    def _drop_steady(self) -> None:
+        _log.info("rank %d: steady-state step invalid (routing changed or uncertified query), "
+                  "the next step takes the full path", self.rank)
+        self._steady = None
+        self._graph = None
+        self._pending.clear()
+
+    def _check_pending(self, keep: int) -> None:
+        while len(self._pending) > keep:
+            if not self._pending.popleft().valid():
+                self._drop_steady()
+
     # -------------------------------------------------------------------- solve ------
     def solve(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None,
               partitioned: bool = False, domain=None, async_: bool = False) -> DistResult:
@@ -575,17 +598,18 @@ class DistributedKNearests:
             # outcomes (the all-reduced flags), so it is never decided from local data alone -- a
             # rank whose share changed still runs the steady step and its on-device check fails
             if self.steady and self._steady is not None:
+                self._check_pending(keep=1 if async_ else 0)
+            if self.steady and self._steady is not None:
                 res = self._solve_steady(points, ids)
                 if async_:
+                    self._pending.append(res)
                     return res
                 if res.valid():
                     if res.stats.get("graph"):  # graph buffers are reused by the next replay
                         res = DistResult(res.ids.clone(), res.neighbors.clone(), res.d2.clone(), res.stats)
                     return res
-                _log.info("rank %d: steady-state step invalid (routing changed or uncertified query), "
-                          "re-solving the full way", self.rank)
-                self._steady = None  # assumption failed or a query is uncertified: the full way
-                self._graph = None
+                self._drop_steady()  # assumption failed or a query is uncertified: the full way
+            self._pending.clear()  # a full step replaces the plan the pending steps ran with
             return self._solve_native(points, ids)
         dev = points.device
         lo, hi, counts = self.meta(points)
