@@ -114,7 +114,9 @@ __device__ __forceinline__ unsigned cand_key_v(const float4& p, float qx, float 
     const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
     const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     unsigned key;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(key) : "v"(himask), "v"(__float_as_uint(d2)), "v"((unsigned)s));
+    // himask is wave-uniform: an SGPR operand (a VGPR constraint re-materialised it with a v_mov
+    // per candidate inside the unrolled loop)
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(key) : "s"(himask), "v"(__float_as_uint(d2)), "v"((unsigned)s));
     return key;
 }
 
@@ -133,20 +135,6 @@ __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key
         return 1u;
     }
     return 0u;
-}
-
-// Branch-free insertion (bulk flushes of the collect-mode queue, where some lane of the wave
-// almost always improves, so a ballot test would only add an instruction).
-// The med3 chain is issued in descending slot order as VOLATILE asm, so each new[j] is written
-// over old[j] after old[j] fed new[j+1]: the list is updated in place. Left to the scheduler,
-// the independent med3s were reordered and the allocator kept a second copy of the list
-// (K=50: 118 -> 169 VGPRs, i.e. 2 instead of 3 waves per SIMD).
-template <int KM>
-__device__ __forceinline__ void topk_insert(unsigned (&keys)[KM], unsigned key) {
-#pragma unroll
-    for (int j = KM - 1; j > 0; --j)
-        asm volatile("v_med3_u32 %0, %1, %2, %0" : "+v"(keys[j]) : "v"(keys[j - 1]), "v"(key));
-    asm volatile("v_min_u32 %0, %0, %1" : "+v"(keys[0]) : "v"(key));
 }
 
 // Wave-wide sum (DPP within rows of 16, then the 4 row totals).

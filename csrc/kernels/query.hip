@@ -77,7 +77,6 @@ struct TileArgs {
     int cb_stride;  // max staged cells per row + 1
     int max_rows;
     int flags;      // kQueryForceRescan: every query takes the exact re-scan (tests)
-    int qoff;       // byte offset of the collect queues in dynamic LDS (KN_COLLECT)
 };
 
 #ifndef KN_STAGE_ROWS
@@ -109,36 +108,19 @@ struct TileArgs {
 #ifndef KN_WIN
 #define KN_WIN 1
 #endif
-#ifndef KN_TOPK_MARGIN
-#define KN_TOPK_MARGIN 2
-#endif
-#define KN_TOPK_MARGIN_DEF KN_TOPK_MARGIN
 constexpr int kWin = KN_WIN;  // exact re-rank window: same-bucket neighbours within +-kWin
-// Collect-then-select lane walk (KN_COLLECT=1, default; round 3). Measured on MI355X
-// (csrc/tools/valu_rate.hip, profiles/valu_rate_r3.jsonl): FP32 add/mul/fma and integer
-// add/and/or/mov issue in 2 cycles per wave64 instruction (with >= 2 waves per SIMD), but
-// v_med3_u32, v_min/max, v_bfi_b32, shifts and v_cndmask take 4. The med3 top-K insertion
-// (K+M+1 med3 per candidate, paid by every lane for every candidate because of SIMT) was ~75 %
-// of the hot loop's cycles. Collect mode decouples it: the lane walk only computes d2 and
-// appends the candidate's LDS slot to a lane-private LDS queue when d2 <= the lane's bound
-// (an R-ball holding ~kCollectLambda points at the tile's density, then the list's own bound
-// once it is full); the queue is inserted in bulk when any lane's queue fills and at the end.
-#ifndef KN_COLLECT
-#define KN_COLLECT 1
-#endif
-#ifndef KN_COLLECT_LAM_SCALE
-#define KN_COLLECT_LAM_SCALE 1.0f
-#endif
-template <int KT>
-struct CollectPlan {
-    static constexpr int KM = KT + KN_TOPK_MARGIN_DEF + 1;
-    // per-lane queue entries (u16 LDS slots)
-    static constexpr int cap = KT <= 16 ? 24 : (KT <= 40 ? 32 : 48);
-    // expected points inside the bound's ball: P(Poisson(lambda) < KM) ~ 1e-4
-    static constexpr float lambda = (float)KM + 3.75f * (KT <= 8 ? 3.3f : KT <= 16 ? 4.36f : KT <= 24 ? 5.2f
-                                                     : KT <= 32 ? 5.9f : KT <= 40 ? 6.6f : KT <= 50 ? 7.3f : 8.2f) + 7.f;
-};
-constexpr size_t collect_queue_bytes(int cap) { return (size_t)kWaves * 64 * cap * 2; }
+// Round-3 A/Bs of the lane walk that LOST against this kernel (900K uniform, interleaved in
+// process, identical rows; profiles/ab_r3_lane_variants.jsonl, profiles/ab_r3_collect.jsonl):
+//  * collect-then-select (d2-only scan + per-lane LDS queue of candidate slots, bulk med3
+//    insertion): K=16 0.30 -> 0.49 ms. The ballot-gated insertion already skips ~45 % of the
+//    candidate steps (98 networks per 64-query chunk for ~172 steps, checked-build counters),
+//    so the queue saved less than its LDS traffic and the lost workgroup slot cost.
+//  * fast re-rank (rows straight from the keys unless two adjacent keys share a truncation
+//    bucket): 2 % of the lanes have such a pair, and the cooperative sort they fall back to
+//    costs more than the window pass saves (K=16 +4 %, K=50 2.2x).
+//  * software-pipelined lane gathers: +0-3 %. R-capped lane bound (Poisson-quantile ball at the
+//    tile density): K=16 +6 %, K=50 +8 %.
+
 constexpr int kCoopCap = 128;  // per-wave LDS buffer of the cooperative re-scan (u64 keys)
 constexpr int kQueryForceRescan = 1;
 // fallback-list entry flag: the query's output row holds K real candidates (their K-th squared
@@ -320,12 +302,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 
     const unsigned MASK = (1u << a.slot_bits) - 1u;
     const unsigned HIMASK = ~MASK;
-#if KN_COLLECT
-    // collect bound: radius^3 of a ball holding kCollectLambda points at the staged block's
-    // density (S points in nxs*nys*nzs cells): r^3 = 3 lambda V / (4 pi S)
-    const float coll_r3 = (CollectPlan<KT>::lambda * KN_COLLECT_LAM_SCALE) * ((float)(nxs * nys * nzs) * g.cell[0] * g.cell[1] * g.cell[2]) /
-                          (4.18879020f * (float)S);
-#endif
 
     // ---- 4. query chunks: 64 queries per wave ------------------------------------------
     // Lanes past the tile's last query duplicate that query (identical candidate tests, so
@@ -559,152 +535,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         // SGPRs in the hot loop
         unsigned st_rows = 0, st_cand = 0, st_ins = 0;
         KN_PH_MARK(kPhScan);
-#if KN_COLLECT
-        if constexpr (LANE) {
-            using CP = CollectPlan<KT>;
-            constexpr int C = CP::cap;
-#ifndef KN_COLLECT_U
-#define KN_COLLECT_U 3
-#endif
-#ifndef KN_COLLECT_FU
-#define KN_COLLECT_FU 2
-#endif
-            constexpr int U = KN_COLLECT_U;  // gathers in flight per lane
-            // lane-private queue of u16 LDS slots, entry j at u16 index j*64 + (lane%32)*2 +
-            // lane/32: lanes l and l+32 share a dword but sit in different 32-lane LDS groups
-            unsigned short* qb = reinterpret_cast<unsigned short*>(smem + a.qoff) + (size_t)wid * C * 64 +
-                                 (((lane & 31) << 1) | (lane >> 5));
-            // the lane's bound: the tile-density ball, grown by 2^(1/3) per axis on which it
-            // crosses the grid's faces (no points beyond them: a half ball needs 2x the volume)
-            float thr;
-            {
-                float r = cbrtf(coll_r3);
-                float f = 1.f;
-                const float qc[3] = {qx, qy, qz};
-#pragma unroll
-                for (int ax = 0; ax < 3; ++ax) {
-                    const float lo = g.origin[ax], hi = g.origin[ax] + (float)g.dims[ax] * g.cell[ax];
-                    f *= (qc[ax] - lo < r || hi - qc[ax] < r) ? 1.2599211f : 1.f;
-                }
-                r *= f;
-                thr = r * r;
-            }
-            int cnt = 0, ncol = 0;
-            auto flush = [&]() {
-                // bulk insertion of the queued slots (2 per step: their LDS reads overlap)
-                for (int j = 0; __builtin_amdgcn_ballot_w64(j < cnt); j += KN_COLLECT_FU) {
-                    unsigned sq[KN_COLLECT_FU];
-                    float4 pq[KN_COLLECT_FU];
-#pragma unroll
-                    for (int u = 0; u < KN_COLLECT_FU; ++u) sq[u] = j + u < cnt ? (unsigned)qb[(j + u) * 64] : 0u;
-#pragma unroll
-                    for (int u = 0; u < KN_COLLECT_FU; ++u) pq[u] = pts[KN_IDX(sq[u], (unsigned)S, 216)];
-#pragma unroll
-                    for (int u = 0; u < KN_COLLECT_FU; ++u)
-                        topk_insert<KM>(keys, j + u < cnt ? cand_key_v(pq[u], qx, qy, qz, HIMASK, (int)sq[u]) : SENT);
-                }
-                if constexpr (kStats) st_ins += (unsigned)cnt;
-                ncol += cnt;
-                cnt = 0;
-                // the list's own bound once it is full (it only shrinks)
-                const unsigned last = keys[KM - 1];
-                if (last != SENT) thr = fminf(thr, __uint_as_float(last | MASK));
-            };
-            auto body = [&](int s0, int s1) {
-                if constexpr (kStats) {
-                    st_rows += (s1 > s0) ? 1u : 0u;
-                    st_cand += (unsigned)max(0, s1 - s0);
-                }
-                // one flush site (U candidates per step, the row's tail masked): a second
-                // inlined copy of the insertion network costs registers
-                for (int sl = s0; sl < s1; sl += U) {
-                    if (__builtin_amdgcn_ballot_w64(cnt > C - U)) flush();  // lanes still in this row
-                    float4 p[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) p[u] = pts[min(sl + u, s1 - 1)];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        // same arithmetic as cand_key_v: d2 <= thr here <=> the key passes at the flush
-                        const float dx = p[u].x - qx, dy = p[u].y - qy, dz = p[u].z - qz;
-                        const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                        qb[KN_IDX(cnt, C, 217) * 64] = (unsigned short)(sl + u);  // kept only if counted
-                        cnt += (sl + u < s1 && d2 <= thr) ? 1 : 0;
-                    }
-                }
-            };
-            // LDS slot range [s0, s1) of cells [x0, x1] of staged row (y, z); empty if x0 > x1
-            auto lane_span = [&](int y, int z, int x0, int x1) {
-                int2 sp = make_int2(0, 0);
-                if (x0 <= x1) {
-                    const int r = y + nys * z;
-                    const int rb = rowbase[r] - cb[r * cbs];
-                    sp.x = rb + cb[r * cbs + x0];
-                    sp.y = KN_IDX(rb + cb[r * cbs + x1 + 1], S + 1, 212);
-                }
-                return sp;
-            };
-            // Pass 0: the bounded collection. Pass 1 (rare): lanes whose ball held fewer than
-            // K + 1 points (a local density far below the tile's) start over with no bound --
-            // the list's own bound takes over after the first flush, as the plain lane walk.
-            for (int pass = 0; pass < 2; ++pass) {
-                const bool run = pass == 0 ? live : (live && ncol < a.k + 1 && thr != INFINITY);
-                if (!__builtin_amdgcn_ballot_w64(run)) break;
-                if (pass == 1 && run) {
-#pragma unroll
-                    for (int j = 0; j < KM; ++j) keys[j] = SENT;
-                    thr = INFINITY;
-                    ncol = 0;
-                }
-                // rows of the lane's region centre-out; an axis loop ends at the first offset
-                // magnitude no lane reaches on either side (slab distance grows, thr shrinks)
-                for (int tz_ = 0; tz_ < 2 * nzs; ++tz_) {
-                    const int mz = (tz_ + 1) >> 1;
-                    const int z = cz + ((tz_ & 1) ? mz : -mz);
-                    if (tz_ & 1) {
-                        bool reach = false;
-                        if (run) {
-                            if (cz + mz <= rz1) { const float d = slab_dist(g, 2, qz, sz0 + cz + mz, sz0 + cz + mz); reach |= d * d <= thr; }
-                            if (cz - mz >= rz0) { const float d = slab_dist(g, 2, qz, sz0 + cz - mz, sz0 + cz - mz); reach |= d * d <= thr; }
-                        }
-                        if (!__builtin_amdgcn_ballot_w64(reach)) break;
-                    }
-                    const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
-                    const float dz2 = dzb * dzb;
-                    const bool zin = run && z >= rz0 && z <= rz1 && dz2 <= thr;
-                    if (!__builtin_amdgcn_ballot_w64(zin)) continue;
-                    for (int ty_ = 0; ty_ < 2 * nys; ++ty_) {
-                        const int my = (ty_ + 1) >> 1;
-                        const int y = cy + ((ty_ & 1) ? my : -my);
-                        if (ty_ & 1) {
-                            bool reach = false;
-                            if (zin) {
-                                if (cy + my <= ry1) { const float d = slab_dist(g, 1, qy, sy0 + cy + my, sy0 + cy + my); reach |= fmaf(d, d, dz2) <= thr; }
-                                if (cy - my >= ry0) { const float d = slab_dist(g, 1, qy, sy0 + cy - my, sy0 + cy - my); reach |= fmaf(d, d, dz2) <= thr; }
-                            }
-                            if (!__builtin_amdgcn_ballot_w64(reach)) break;
-                        }
-                        const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
-                        const float dyz2 = fmaf(dyb, dyb, dz2);
-                        int lx0 = 0, lx1 = -1;
-                        if (zin && y >= ry0 && y <= ry1 && dyz2 <= thr) {
-                            if (thr == INFINITY) {
-                                lx0 = rx0; lx1 = rx1;
-                            } else {
-                                const float rr = sqrtf(thr - dyz2) * 1.000001f + g.eps;
-                                lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
-                                lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
-                            }
-                        }
-                        if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
-                        const int2 sp = lane_span(y, z, lx0, lx1);
-                        body(sp.x, sp.y);
-                    }
-                }
-                flush();
-            }
-        }
-#endif
-        if constexpr (!(LANE && KN_COLLECT))
         scan_region(
             [&]() {
                 const unsigned last = keys[KM - 1];
@@ -1833,12 +1663,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             const char* v = std::getenv("KN_LDS_EXTRA");
             return v ? (size_t)std::max(0, std::atoi(v)) : (size_t)0;
         }();
-        size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity);
-        a.qoff = (int)lds;
-#if KN_COLLECT
-        if (query_algo(q.flags, q.k) == kAlgoLane) lds += collect_queue_bytes(CollectPlan<KT>::cap);
-#endif
-        lds += lds_extra;
+        const size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity) + lds_extra;
         static bool attr_set = false;
         if (!attr_set) {
             if constexpr (KT <= 64) {

@@ -7,6 +7,10 @@
 //          --batch B   solve in query batches of B points (kn_solve_range: no N x K device result)
 //          --multi D   spatial split over D ranks (kn_prepare_multi / kn_solve_multi; rank i on
 //                      device i mod the device count, so D > devices runs virtual ranks)
+//          --api-bench R  host-to-host timing of the reference API, R timed iterations after one
+//                      warm-up: kn_prepare(host points) -> kn_solve -> kn_get_knearests ->
+//                      kn_get_permutation -> free / kn_free (the reference's "knn subgpu" timer
+//                      plus its getters, test_knearests.cu:136-153); one JSON line, medians
 //
 // Flow: device report -> load -> kn_prepare_ex + kn_solve_ex (timed) -> kn_print_stats ->
 // stored-space getters -> remap to original ids (reference :155-160) -> permutation
@@ -47,7 +51,7 @@ int main(int argc, char** argv) {
     cfg.k = KN_DEFAULT_K;
     cfg.verbose = 1;
     std::string path, gen, save, out;
-    int gen_n = 0, repeat = 1, batch = 0, multi = 0;
+    int gen_n = 0, repeat = 1, batch = 0, multi = 0, api_bench = 0;
     bool check = true, json = false, exact = false;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -69,10 +73,11 @@ int main(int argc, char** argv) {
         else if (a == "--repeat") repeat = std::max(1, atoi(next()));
         else if (a == "--batch") batch = std::max(0, atoi(next()));
         else if (a == "--multi") multi = std::max(0, atoi(next()));
+        else if (a == "--api-bench") api_bench = std::max(1, atoi(next()));
         else if (a == "-h" || a == "--help") {
             fprintf(stderr, "usage: %s points.xyz | --uniform N | --blue N | --clustered N [--k K] [--ppc X] "
                             "[--tile a,b,c] [--halo H] [--exact] [--nondet] [--no-check] [--json] [--save f] [--out f] "
-                            "[--repeat R] [--batch B] [--multi D]\n", argv[0]);
+                            "[--repeat R] [--batch B] [--multi D] [--api-bench R]\n", argv[0]);
             return 0;
         } else path = a;
     }
@@ -97,6 +102,39 @@ int main(int argc, char** argv) {
         void* p = nullptr;
         (void)hipMalloc(&p, 4);
         (void)hipFree(p);
+    }
+    if (api_bench > 0) {
+        // host-to-host reference-API cost: every iteration uploads the points, builds, solves,
+        // converts to the reference's stored index space and copies both results back
+        cfg.verbose = 0;
+        std::vector<double> tp, ts, tk, tm, tt;
+        for (int it = 0; it <= api_bench; ++it) {
+            const double a0 = now_ms();
+            kn_problem* kn = kn_prepare_ex(reinterpret_cast<const kn_float3*>(pts.data()), n, &cfg);
+            if (!kn) { fprintf(stderr, "kn_prepare failed: %s\n", kn_last_error()); return 1; }
+            const double a1 = now_ms();
+            if (kn_solve_ex(kn) != KN_OK) { fprintf(stderr, "kn_solve failed: %s\n", kn_last_error()); return 1; }
+            const double a2 = now_ms();
+            unsigned* knn = kn_get_knearests(kn);
+            const double a3 = now_ms();
+            unsigned* perm = kn_get_permutation(kn);
+            const double a4 = now_ms();
+            if (!knn || !perm) { fprintf(stderr, "getter failed: %s\n", kn_last_error()); return 1; }
+            free(knn);
+            free(perm);
+            kn_free(&kn);
+            const double a5 = now_ms();
+            if (it == 0) continue;  // warm-up (first allocations, code objects)
+            tp.push_back(a1 - a0); ts.push_back(a2 - a1); tk.push_back(a3 - a2); tm.push_back(a4 - a3);
+            tt.push_back(a5 - a0);
+        }
+        auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+        const double h2d = 12.0 * n / 1e6, d2h = (4.0 * n * K + 4.0 * n) / 1e6;
+        printf("{\"mode\": \"api_host_to_host\", \"n\": %d, \"k\": %d, \"iters\": %d, \"ms_prepare\": %.4f, "
+               "\"ms_solve\": %.4f, \"ms_get_knearests\": %.4f, \"ms_get_permutation\": %.4f, \"ms_total\": %.4f, "
+               "\"h2d_mb\": %.2f, \"d2h_mb\": %.2f, \"queries_per_s\": %.4g}\n",
+               n, K, api_bench, med(tp), med(ts), med(tk), med(tm), med(tt), h2d, d2h, n / (med(tt) * 1e-3));
+        return 0;
     }
     std::vector<uint32_t> neighbors((size_t)n * K);
     kn_stats st{};

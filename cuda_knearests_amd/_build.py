@@ -37,7 +37,10 @@ RCCL_OK = os.path.exists(os.path.join(ROCM, "include", "rccl", "rccl.h"))
 CXX = os.environ.get("CXX", "g++")
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-D__HIP_PLATFORM_AMD__=1"]
 # device code: hipcc for gfx950 only
-HIPFLAGS = COMMON + [f"--offload-arch={ARCH}", "-x", "hip", "-munsafe-fp-atomics",
+# -fno-slp-vectorize: the SLP vectorizer packs pairs of scalar f32 sub/mul/fma into v_pk_*_f32,
+# which issue in 4 cycles per wave64 instruction on gfx950 where the scalar forms take 2
+# (profiles/valu_rate_r3.txt), plus the v_mov pairing: a loss in VALU-bound kernels.
+HIPFLAGS = COMMON + [f"--offload-arch={ARCH}", "-x", "hip", "-munsafe-fp-atomics", "-fno-slp-vectorize",
                      "-Wno-unused-result", "-Wno-unused-value"]
 # host-only code (runtime, oracles, bindings, tools): the system C++ compiler + HIP headers
 HOSTFLAGS = COMMON + [f"-I{ROCM}/include", "-fopenmp", "-Wall", "-Wno-unused-result",
