@@ -5,11 +5,16 @@
 // background, scans): dense cells hold hundreds of points, sparse queries need many rings, tiles
 // overflow the LDS budget. The tree path adapts to any density:
 //
-//   build:  30-bit Morton code of every point (cubic quantisation of the grid's domain) ->
-//           radix sort (hipCUB) -> points gathered into Morton order -> leaves = the maximal
-//           binary-prefix (radix) nodes of <= 32 points -> leaf boxes (wave DPP reductions) ->
-//           implicit complete binary tree of boxes over the leaves (heap index, root 1, leaf l =
-//           node P + l), reduced bottom-up 6 levels per launch in LDS.
+//   build:  the grid's points (already grouped by cell) in the Morton order of their CELLS,
+//           without sorting: 8^3-cell bricks numbered by the Morton code of their brick
+//           coordinates, one exclusive scan of the brick counts, one workgroup per brick scans
+//           its 512 cells in Morton order and copies their point runs -> leaves = the maximal
+//           binary-prefix (radix) nodes of <= 32 points (runs of one cell chunked) -> leaf
+//           boxes (wave DPP reductions) -> implicit complete binary tree of boxes over P = pow2
+//           >= n leaf slots (heap index, root 1, leaf l = node P + l; nodes past the leaf count
+//           are never written nor entered), reduced bottom-up 6 levels per launch in LDS.
+//           Every launch is sized from n and the grid dims alone and the leaf count stays on
+//           the device: the whole tree step is stream-ordered and graph-capturable.
 //   query:  one wave per 64 consecutive points of the Morton order (lanes = queries).
 //           Wave-uniform near-first traversal
 //           (a node is entered when ANY lane's box distance is within its own K-th bound);
@@ -34,7 +39,7 @@ namespace kn {
 
 constexpr int kTreeLeaf = 32;  // points per leaf (at most)
 
-// A tree: one workspace (carved by tree_view) plus a node buffer sized from the leaf count.
+// A tree: one workspace (carved by tree_view) plus a node buffer sized from n.
 struct TreeView {
     float4* pts;          // n points in Morton order {x, y, z, w} (w copied from the input)
     unsigned* leaf_start; // L + 1 leaf boundaries (<= 64 points per leaf)
@@ -43,26 +48,36 @@ struct TreeView {
     float* thr;           // n: their distance bound
     unsigned* flag;       // n scratch
     unsigned* incl;       // n scratch
-    unsigned* codes;      // 2n Morton codes (sort double buffer)
-    unsigned* vals;       // 2n source indices; after the build vals[0, n) maps tree point -> input index
-    unsigned* info;       // [0] = L after launch_tree_leaves (device)
-    void* sort_temp;      // hipCUB temp storage (sort / scan)
-    size_t sort_temp_bytes;
+    unsigned long long* codes;  // n: the Morton code of each tree point's cell
+    unsigned* vals;       // n: input (grid slot) index of each tree point
+    unsigned* info;       // [0] = L after launch_tree_leaves (device; the query kernels read it)
+    float4* tmp_pts;      // n: points in cell order (before the sub-cell order)
+    unsigned* tmp_vals;   // n
+    unsigned* cell_code;  // n: Morton code of each point's cell
+    uint2* cell_span;     // n: tree range [first, end) of each point's cell
+    unsigned* bcount;     // padded brick space + 1: brick counts, scanned in place to bases
+    unsigned* scan_sums;  // block sums of the device scans
+    size_t nbricks_pad;   // 8^bb brick slots (bb = ceil(log2(max bricks per axis)))
+    int nbricks[3];       // bricks per axis
+    int dims[3];          // grid dims
     float4* nlo;          // 2P node boxes (lower corner; heap index, root 1, leaf l = node P + l)
-    float4* nhi;          // 2P upper corners; empty padded leaves: lo = +inf, hi = -inf
-    int n, L, P;          // points, leaves, P = next power of two >= L
+    float4* nhi;          // 2P upper corners
+    int n, P;             // points, P = next power of two >= n (leaf slots)
 };
 
-size_t tree_workspace_bytes(int n);
-TreeView tree_view(void* ws, int n);
-// Phase 1 (stream-ordered): Morton codes of `in` (n points {x, y, z, w}, typically the grid's
-// sorted array) over the grid's domain, sort, gather, leaf boundaries; the leaf count lands in
-// t.info[0]. The caller reads it (one host sync) to size the node buffer.
-hipError_t launch_tree_leaves(const float4* in, const GridGeom* geom, const TreeView& t, hipStream_t s);
-size_t tree_node_bytes(int L);
-void tree_attach_nodes(TreeView& t, void* nodes, int L);
+// dims: the grid's dims (host copy of GridGeom::dims)
+size_t tree_workspace_bytes(int n, const int dims[3]);
+TreeView tree_view(void* ws, int n, const int dims[3]);
+// Phase 1 (stream-ordered, no host sync): the grid's sorted points in the Morton order of their
+// cells, leaf boundaries; the leaf count lands in t.info[0] on the device.
+hipError_t launch_tree_leaves(const float4* in, const int* cell_start, const GridGeom* geom, const TreeView& t,
+                              hipStream_t s);
+size_t tree_node_bytes(int n);
+void tree_attach_nodes(TreeView& t, void* nodes);
 // Phase 2: leaf boxes and the implicit tree's node boxes.
 hipError_t launch_tree_nodes(const TreeView& t, hipStream_t s);
+// Diagnostics: the leaf count (one host sync).
+hipError_t tree_leaf_count(const TreeView& t, unsigned* L, hipStream_t s);
 
 struct TreeQuery {
     int k;

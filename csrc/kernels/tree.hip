@@ -8,7 +8,6 @@
 
 #include <algorithm>
 #include <cmath>
-#include <hipcub/hipcub.hpp>
 
 #include "kn/knn_device.h"
 #include "kn/tree.h"
@@ -39,7 +38,8 @@ struct TArgs {
     const float4* nhi;
     unsigned* list;
     float* thr;
-    int n, L, P;
+    const unsigned* Lp;  // device leaf count (written by the build: no host read, graph-capturable)
+    int n, P, logP;      // P = the node buffer's leaf capacity (power of two >= n)
     int k;
     int n_queries;
     int q_lo;  // always 0: the tree path serves whole solves (ranges use the grid kernels)
@@ -77,27 +77,200 @@ __device__ __forceinline__ float box_d2(float qx, float qy, float qz, const floa
     return fmaf(dz, dz, fmaf(dy, dy, dx * dx));
 }
 
-// Cubic quantisation of the grid's domain to 1024 steps per axis (cells of a finer level stay
-// cubes, so the implicit octree's boxes are balanced).
-__global__ void morton_kernel(const float4* __restrict__ in, int n, const GridGeom* __restrict__ geom,
-                              unsigned* __restrict__ codes, unsigned* __restrict__ vals) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const GridGeom g = *geom;
-    const float ext = fmaxf(fmaxf(g.cell[0] * g.dims[0], g.cell[1] * g.dims[1]), g.cell[2] * g.dims[2]);
-    const float s = ext > 0.f ? 1024.f / ext : 0.f;
-    const float4 p = in[i];
-    const int qx = clampi((int)((p.x - g.origin[0]) * s), 0, 1023);
-    const int qy = clampi((int)((p.y - g.origin[1]) * s), 0, 1023);
-    const int qz = clampi((int)((p.z - g.origin[2]) * s), 0, 1023);
-    codes[i] = spread10(qx) | (spread10(qy) << 1) | (spread10(qz) << 2);
-    vals[i] = (unsigned)i;
+// ---- build: Morton order of the grid's CELLS, no sort ------------------------------------------
+// The input is the grid's sorted array: points already grouped by cell (x-fastest). The tree order
+// is the Morton order of the cells: cells are grouped in 8x8x8 bricks, bricks are numbered by
+// the Morton code of their brick coordinates (a padded power-of-two brick space) and the cells of
+// a brick by their 9-bit in-brick Morton code, so (brick code << 9 | cell code) IS the cell's
+// Morton code. One exclusive scan over the brick counts places every brick; one workgroup per
+// brick scans its 512 cells in Morton order and copies their point runs. Counting, no sorting:
+// replaces the round-2 30-bit radix sort of point codes (hipCUB) and needs no host round trip.
+constexpr int kBrickBits = 3;            // 8 cells per brick axis
+constexpr int kBrickCells = 1 << (3 * kBrickBits);
+
+__device__ __forceinline__ unsigned compact3(unsigned v) {  // inverse of spread10
+    v &= 0x09249249u;
+    v = (v | (v >> 2)) & 0x030C30C3u;
+    v = (v | (v >> 4)) & 0x0300F00Fu;
+    v = (v | (v >> 8)) & 0x030000FFu;
+    v = (v | (v >> 16)) & 0x000003FFu;
+    return v;
 }
 
-__global__ void gather_kernel(const float4* __restrict__ in, const unsigned* __restrict__ src, int n,
-                              float4* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = in[src[i]];
+// One 64-thread workgroup per real brick: lane = one (y, z) row of the brick's 8x8 rows; the
+// brick's point count lands at its Morton slot of the (pre-zeroed) padded count array.
+__global__ __launch_bounds__(64) void brick_count_kernel(const int* __restrict__ cell_start, const GridGeom* __restrict__ geom,
+                                                         int nbx, int nby, unsigned* __restrict__ bcount) {
+    const GridGeom g = *geom;
+    const int b = blockIdx.x, bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
+    const int lane = threadIdx.x;
+    const int y = by * 8 + (lane & 7), z = bz * 8 + (lane >> 3);
+    const int x0 = bx * 8, x1 = min(g.dims[0], x0 + 8);
+    unsigned c = 0;
+    if (y < g.dims[1] && z < g.dims[2]) {
+        const size_t row = ((size_t)z * g.dims[1] + y) * g.dims[0];
+        c = (unsigned)(cell_start[row + x1] - cell_start[row + x0]);
+    }
+    c = wave_sum_u32(c);
+    if (lane == 0) bcount[spread10(bx) | (spread10(by) << 1) | (spread10(bz) << 2)] = c;
+}
+
+// One 256-thread workgroup per real brick: in-brick Morton scan of the 512 cell counts, then every
+// point of the brick to its cell's tree range (thread per point, cell found by binary search),
+// in input order within the cell: tmp_pts / tmp_vals (input index), the cell's Morton code and
+// tree range [first, end) per point (subcell_rank_kernel orders the cell).
+__global__ __launch_bounds__(256) void brick_scatter_kernel(const float4* __restrict__ in, const int* __restrict__ cell_start,
+                                                            const GridGeom* __restrict__ geom, int nbx, int nby,
+                                                            const unsigned* __restrict__ bbase, float4* __restrict__ tmp_pts,
+                                                            unsigned* __restrict__ tmp_vals, unsigned* __restrict__ cell_code,
+                                                            uint2* __restrict__ cell_span) {
+    __shared__ int s_base[kBrickCells + 1];
+    __shared__ int s_start[kBrickCells];
+    __shared__ int s_wsum[4];
+    const GridGeom g = *geom;
+    const int b = blockIdx.x, bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
+    const unsigned bcode = spread10(bx) | (spread10(by) << 1) | (spread10(bz) << 2);
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    int cnt[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int m = 2 * t + h;  // a thread owns two consecutive Morton slots
+        const int x = bx * 8 + (int)compact3((unsigned)m), y = by * 8 + (int)compact3((unsigned)m >> 1),
+                  z = bz * 8 + (int)compact3((unsigned)m >> 2);
+        cnt[h] = 0;
+        int st = 0;
+        if (x < g.dims[0] && y < g.dims[1] && z < g.dims[2]) {
+            const size_t c = ((size_t)z * g.dims[1] + y) * g.dims[0] + x;
+            st = cell_start[c];
+            cnt[h] = cell_start[c + 1] - st;
+        }
+        s_start[m] = st;
+    }
+    const int tsum = cnt[0] + cnt[1];
+    const int incl = wave_inclusive_scan_add(tsum);
+    if (lane == 63) s_wsum[wid] = incl;
+    __syncthreads();
+    int off = incl - tsum;
+    for (int w = 0; w < wid; ++w) off += s_wsum[w];
+    s_base[2 * t] = off;
+    s_base[2 * t + 1] = off + cnt[0];
+    if (t == 255) s_base[kBrickCells] = off + tsum;
+    __syncthreads();
+    const int total = s_base[kBrickCells];
+    const unsigned out0 = bbase[bcode];
+    for (int j = t; j < total; j += 256) {
+        int lo = 0, hi = kBrickCells - 1;  // last slot whose base <= j (the non-empty cell holding j)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_base[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        const unsigned src = (unsigned)(s_start[lo] + (j - s_base[lo]));
+        const unsigned dst = out0 + (unsigned)j;
+        tmp_pts[dst] = in[src];
+        tmp_vals[dst] = src;
+        cell_code[dst] = (bcode << (3 * kBrickBits)) | (unsigned)lo;  // the cell's Morton code (<= 30 bits)
+        cell_span[dst] = make_uint2(out0 + (unsigned)s_base[lo], out0 + (unsigned)s_base[lo + 1]);
+    }
+}
+
+// Within a cell, points follow the Morton order of their 8x8x8 sub-cell (ties: input order), so
+// leaves may split a dense cell into compact parts (cell-granular leaves cost the tree query
+// ~20 %). One thread per point ranks it by counting over its cell's points: sum of count^2 work
+// (~8n for an occupancy-adaptive grid), spread evenly over the points -- done per brick, the
+// few bricks holding a cluster's core serialised it (230 us at 900K clustered).
+__device__ __forceinline__ unsigned subcell_code(const GridGeom& g, const float4& p, unsigned cc) {
+    const int cx = (int)compact3(cc), cy = (int)compact3(cc >> 1), cz = (int)compact3(cc >> 2);
+    const int sx = clampi((int)((p.x - (g.origin[0] + cx * g.cell[0])) * g.inv_cell[0] * 8.f), 0, 7);
+    const int sy = clampi((int)((p.y - (g.origin[1] + cy * g.cell[1])) * g.inv_cell[1] * 8.f), 0, 7);
+    const int sz = clampi((int)((p.z - (g.origin[2] + cz * g.cell[2])) * g.inv_cell[2] * 8.f), 0, 7);
+    return spread10((unsigned)sx) | (spread10((unsigned)sy) << 1) | (spread10((unsigned)sz) << 2);
+}
+__global__ __launch_bounds__(256) void subcell_rank_kernel(const float4* __restrict__ tmp_pts, const unsigned* __restrict__ tmp_vals,
+                                                           const unsigned* __restrict__ cell_code, const uint2* __restrict__ cell_span,
+                                                           const GridGeom* __restrict__ geom, int n, float4* __restrict__ pts,
+                                                           unsigned* __restrict__ vals, unsigned long long* __restrict__ codes) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const GridGeom g = *geom;
+    const unsigned cc = cell_code[j];
+    const uint2 sp = cell_span[j];
+    const float4 p = tmp_pts[j];
+    const unsigned sc = subcell_code(g, p, cc);
+    unsigned r = 0;
+    if (sp.y - sp.x > 1)
+        for (unsigned i = sp.x; i < sp.y; ++i) {
+            const unsigned si = subcell_code(g, tmp_pts[i], cc);
+            r += (si < sc || (si == sc && i < (unsigned)j)) ? 1u : 0u;
+        }
+    const unsigned dst = sp.x + r;
+    pts[dst] = p;
+    vals[dst] = tmp_vals[j];
+    codes[dst] = ((unsigned long long)cc << 9) | sc;
+}
+
+// ---- device-wide scan of u32 (block sums -> one-workgroup scan of the sums -> block scans) ------
+constexpr int kTScanItems = 4096;  // 256 threads x 16
+__global__ __launch_bounds__(256) void tscan_sums_kernel(const unsigned* __restrict__ in, int n, unsigned* __restrict__ sums) {
+    const int base = blockIdx.x * kTScanItems;
+    unsigned s = 0;
+    for (int i = base + threadIdx.x; i < min(n, base + kTScanItems); i += 256) s += in[i];
+    __shared__ unsigned ws[4];
+    s = wave_sum_u32(s);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+__global__ __launch_bounds__(1024) void tscan_top_kernel(unsigned* __restrict__ sums, int nb) {
+    __shared__ unsigned wsum[16];
+    __shared__ unsigned carry_s;
+    if (threadIdx.x == 0) carry_s = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int base = 0; base < nb; base += 1024) {
+        const int i = base + threadIdx.x;
+        const unsigned v = (i < nb) ? sums[i] : 0u;
+        const unsigned incl = (unsigned)wave_inclusive_scan_add((int)v);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        unsigned woff = 0;
+        for (int w = 0; w < wid; ++w) woff += wsum[w];
+        const unsigned carry = carry_s;
+        if (i < nb) sums[i] = carry + woff + incl - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry_s = carry + woff + incl;
+        __syncthreads();
+    }
+}
+// out = scan(in) with the block offsets from tscan_top (inclusive or exclusive); in may == out
+__global__ __launch_bounds__(256) void tscan_apply_kernel(const unsigned* __restrict__ in, int n, const unsigned* __restrict__ sums,
+                                                          unsigned* __restrict__ out, int inclusive) {
+    constexpr int I = kTScanItems / 256;
+    const int base = blockIdx.x * kTScanItems + threadIdx.x * I;
+    unsigned v[I];
+#pragma unroll
+    for (int j = 0; j < I; ++j) v[j] = (base + j < n) ? in[base + j] : 0u;
+    unsigned s = 0;
+#pragma unroll
+    for (int j = 0; j < I; ++j) { const unsigned x = v[j]; v[j] = inclusive ? s + x : s; s += x; }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned incl = (unsigned)wave_inclusive_scan_add((int)s);
+    __shared__ unsigned wsum[4];
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    unsigned off = sums[blockIdx.x] + incl - s;
+    for (int w = 0; w < wid; ++w) off += wsum[w];
+#pragma unroll
+    for (int j = 0; j < I; ++j)
+        if (base + j < n) out[base + j] = v[j] + off;
+}
+inline unsigned cdiv_(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
+hipError_t tscan(const unsigned* in, int n, unsigned* out, unsigned* sums, bool inclusive, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const unsigned nb = cdiv_((size_t)n, kTScanItems);
+    tscan_sums_kernel<<<nb, 256, 0, s>>>(in, n, sums);
+    tscan_top_kernel<<<1, 1024, 0, s>>>(sums, (int)nb);
+    tscan_apply_kernel<<<nb, 256, 0, s>>>(in, n, sums, out, inclusive ? 1 : 0);
+    return hipGetLastError();
 }
 
 // Leaf boundaries: leaves are the maximal binary-prefix (radix) nodes of the sorted Morton codes
@@ -106,28 +279,30 @@ __global__ void gather_kernel(const float4* __restrict__ in, const unsigned* __r
 // are in different leaves iff their lowest common prefix node holds more than kTreeLeaf points;
 // its extent is found by two binary searches inside the kTreeLeaf + 1 window around b. Runs of
 // equal codes (one finest cell) longer than a leaf are chunked by leaf_flag_kernel.
-__device__ __forceinline__ int hibit(unsigned x) { return x ? 31 - __builtin_clz(x) : -1; }
+__device__ __forceinline__ int hibit(unsigned long long x) { return x ? 63 - __builtin_clzll(x) : -1; }
 
-__global__ void cut_kernel(const unsigned* __restrict__ c, int n, unsigned* __restrict__ flag) {
+// codes: 64-bit Morton codes of each point's sub-cell (3 bits per brick level, 9 in-brick cell
+// bits, 9 sub-cell bits: > 32 bits for any grid of more than one brick level)
+__global__ void cut_kernel(const unsigned long long* __restrict__ c, int n, unsigned* __restrict__ flag) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= n) return;
     unsigned f = 1u;
     if (b > 0) {
-        const unsigned x = c[b - 1] ^ c[b];
+        const unsigned long long x = c[b - 1] ^ c[b];
         f = 0u;
         if (x) {
             const int sh = hibit(x) + 1;
-            const unsigned p = c[b] >> sh;
+            const unsigned long long p = sh >= 64 ? 0ull : c[b] >> sh;
             int lo = max(0, b - 1 - kTreeLeaf), hi = b - 1;  // first index with prefix p
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if ((c[mid] >> sh) == p) hi = mid; else lo = mid + 1;
+                if ((sh >= 64 ? 0ull : c[mid] >> sh) == p) hi = mid; else lo = mid + 1;
             }
             const int s0 = lo;
             lo = b; hi = min(n, b + kTreeLeaf + 1);  // first index past the prefix
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if ((c[mid] >> sh) == p) lo = mid + 1; else hi = mid;
+                if ((sh >= 64 ? 0ull : c[mid] >> sh) == p) lo = mid + 1; else hi = mid;
             }
             f = (lo - s0 > kTreeLeaf) ? 1u : 0u;
         }
@@ -160,38 +335,49 @@ __global__ void leaf_flag_kernel(const unsigned* __restrict__ incl, const unsign
     flag[b] = (j * len / c == o) ? 1u : 0u;
 }
 
-// One wave per leaf (P leaves: the padded ones get empty boxes).
+// One wave per leaf, grid-stride over the device leaf count (leaves past it are never read:
+// the traversal and node_box_kernel test a node's first leaf against L instead).
 __global__ __launch_bounds__(256) void leaf_box_kernel(const float4* __restrict__ pts, const unsigned* __restrict__ leaf_start,
-                                                       int L, int P, float4* __restrict__ nlo, float4* __restrict__ nhi) {
-    const int leaf = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (leaf >= P) return;
-    if (leaf >= L) {
+                                                       const unsigned* __restrict__ Lp, int P, float4* __restrict__ nlo,
+                                                       float4* __restrict__ nhi) {
+    const int L = (int)*Lp, lane = threadIdx.x & 63;
+    for (int leaf = blockIdx.x * 4 + (threadIdx.x >> 6); leaf < L; leaf += gridDim.x * 4) {
+        const unsigned i = leaf_start[leaf] + lane;
+        const bool v = i < leaf_start[leaf + 1];
+        const float4 p = v ? pts[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const unsigned lx = wave_min_u32(v ? ordf(p.x) : SENT), hx = wave_max_u32(v ? ordf(p.x) : 0u);
+        const unsigned ly = wave_min_u32(v ? ordf(p.y) : SENT), hy = wave_max_u32(v ? ordf(p.y) : 0u);
+        const unsigned lz = wave_min_u32(v ? ordf(p.z) : SENT), hz = wave_max_u32(v ? ordf(p.z) : 0u);
         if (lane == 0) {
-            nlo[P + leaf] = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
-            nhi[P + leaf] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+            nlo[P + leaf] = make_float4(unordf(lx), unordf(ly), unordf(lz), 0.f);
+            nhi[P + leaf] = make_float4(unordf(hx), unordf(hy), unordf(hz), 0.f);
         }
-        return;
     }
-    const unsigned i = leaf_start[leaf] + lane;
-    const bool v = i < leaf_start[leaf + 1];
-    const float4 p = v ? pts[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const unsigned lx = wave_min_u32(v ? ordf(p.x) : SENT), hx = wave_max_u32(v ? ordf(p.x) : 0u);
-    const unsigned ly = wave_min_u32(v ? ordf(p.y) : SENT), hy = wave_max_u32(v ? ordf(p.y) : 0u);
-    const unsigned lz = wave_min_u32(v ? ordf(p.z) : SENT), hz = wave_max_u32(v ? ordf(p.z) : 0u);
-    if (lane == 0) {
-        nlo[P + leaf] = make_float4(unordf(lx), unordf(ly), unordf(lz), 0.f);
-        nhi[P + leaf] = make_float4(unordf(hx), unordf(hy), unordf(hz), 0.f);
-    }
+}
+
+// First leaf of heap node v (root 1, leaves at [P, 2P), P = 2^logP). Nodes whose first leaf is
+// at or past the leaf count L are empty; they are never written, never entered.
+__device__ __forceinline__ int first_leaf(int v, int logP) {
+    const int d = 31 - __builtin_clz((unsigned)v);
+    return (v << (logP - d)) - (1 << logP);
 }
 
 // Nodes [m, 2m) -> their ancestors up to log2(min(m, 64)) levels, one 64-thread workgroup per
 // group of min(m, 64) siblings, in LDS.
-__global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, float4* __restrict__ nhi, int m) {
+__global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, float4* __restrict__ nhi, int m,
+                                                      int logP, const unsigned* __restrict__ Lp) {
     __shared__ float4 slo[64], shi[64];
     const int t = threadIdx.x;
     const int cnt = min(m, 64);
     int nb = m + blockIdx.x * cnt;
-    if (t < cnt) { slo[t] = nlo[nb + t]; shi[t] = nhi[nb + t]; }
+    const int L = (int)*Lp;
+    if (first_leaf(nb, logP) >= L) return;  // the whole group is past the last leaf
+    if (t < cnt) {
+        // empty nodes (first leaf >= L) were never written: read as empty boxes
+        const bool e = first_leaf(nb + t, logP) >= L;
+        slo[t] = e ? make_float4(INFINITY, INFINITY, INFINITY, 0.f) : nlo[nb + t];
+        shi[t] = e ? make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f) : nhi[nb + t];
+    }
     __syncthreads();
     for (int c = cnt; c > 1; c >>= 1) {
         const int h = c >> 1;
@@ -257,13 +443,14 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     // the leaves holding the wave's own 64 points first: every lane starts the traversal with a
     // bound from ~64 nearby candidates (small leaves alone leave the early bounds loose, and a
     // loose bound of any lane opens nodes for the whole wave)
-    int l0 = 0, l1 = a.L - 1;
+    const int L = (int)*a.Lp;
+    int l0 = 0, l1 = L - 1;
     while (l0 < l1) {  // last leaf starting at or before base
         const int mid = (l0 + l1 + 1) >> 1;
         if ((int)a.leaf_start[mid] <= base) l0 = mid; else l1 = mid - 1;
     }
     l1 = l0;
-    while (l1 + 1 < a.L && (int)a.leaf_start[l1 + 1] < base + qcnt) ++l1;
+    while (l1 + 1 < L && (int)a.leaf_start[l1 + 1] < base + qcnt) ++l1;
     for (int lf = l0; lf <= l1 && nv < kMaxVisit; ++lf) visit(lf);
 
     // wave-uniform near-first traversal from the root: a node is entered when any live lane's
@@ -286,8 +473,9 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             continue;
         }
         const int c0 = 2 * node;
+        // the left child shares the node's first leaf (non-empty); the right one may lie past L
         const float b0 = box_d2(qx, qy, qz, a.nlo[c0], a.nhi[c0]);
-        const float b1 = box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]);
+        const float b1 = first_leaf(c0 + 1, a.logP) < L ? box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]) : INFINITY;
         const bool need0 = __builtin_amdgcn_ballot_w64(live && b0 < INFINITY && b0 * kShrink <= ub) != 0;
         const bool need1 = __builtin_amdgcn_ballot_w64(live && b1 < INFINITY && b1 * kShrink <= ub) != 0;
         // nearer child (for most live lanes) on top of the stack
@@ -413,6 +601,7 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int total = all ? a.n : (int)a.counters[0];
     const int k = a.k;
+    const int L = (int)*a.Lp;
     for (int t = blockIdx.x * 4 + wid; t < total; t += gridDim.x * 4) {
         const unsigned qpos = all ? (unsigned)t : (unsigned)__builtin_amdgcn_readfirstlane((int)a.list[KN_IDX(t, a.n, 411)]);
         const float4 qp = a.pts[KN_IDX(qpos, (unsigned)a.n, 412)];
@@ -469,7 +658,7 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
             }
             const int c0 = 2 * node;
             const float b0 = box_d2(qx, qy, qz, a.nlo[c0], a.nhi[c0]);
-            const float b1 = box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]);
+            const float b1 = first_leaf(c0 + 1, a.logP) < L ? box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]) : INFINITY;
             const bool need0 = b0 < INFINITY && b0 * kShrink <= thr;
             const bool need1 = b1 < INFINITY && b1 * kShrink <= thr;
             const bool first0 = b0 <= b1;
@@ -498,14 +687,6 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 inline size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-size_t sort_temp_bytes(int n) {
-    size_t bytes = 0, b2 = 0;
-    hipcub::DoubleBuffer<unsigned> kb(nullptr, nullptr), vb(nullptr, nullptr);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, n, 0, 30);
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, b2, (const unsigned*)nullptr, (unsigned*)nullptr, n);
-    return std::max(bytes, b2);
-}
-
 }  // namespace
 
 static int tree_pow2(int L) {
@@ -513,19 +694,39 @@ static int tree_pow2(int L) {
     while (P < L) P <<= 1;
     return P;
 }
+static int tree_log2(int P) { return 31 - __builtin_clz((unsigned)P); }
 
-size_t tree_workspace_bytes(int n) {
+// padded brick space of a grid: (8^bb entries, bricks per axis)
+static size_t brick_space(const int dims[3], int nb3[3]) {
+    int m = 1;
+    for (int a = 0; a < 3; ++a) {
+        nb3[a] = std::max(1, (dims[a] + 7) / 8);
+        m = std::max(m, nb3[a]);
+    }
+    const size_t side = (size_t)tree_pow2(m);
+    return side * side * side;
+}
+
+size_t tree_workspace_bytes(int n, const int dims[3]) {
     if (n <= 0) return 256;
+    int nb3[3];
+    const size_t NB = brick_space(dims, nb3);
+    const size_t sums = cdiv(std::max<size_t>(n, NB), kTScanItems) + 1;
     size_t b = align256((size_t)n * 16);         // pts
     b += 2 * align256(((size_t)n + 1) * 4);      // leaf_start, seg_start
     b += 4 * align256((size_t)n * 4);            // list, thr, flag, incl
-    b += 2 * align256((size_t)n * 8);            // codes, vals (double buffers)
+    b += align256((size_t)n * 8);                // codes (u64)
+    b += align256((size_t)n * 4);                // vals
     b += align256(16);                           // info
-    b += align256(sort_temp_bytes(n));
+    b += align256((size_t)n * 16);               // tmp_pts
+    b += 2 * align256((size_t)n * 4);            // tmp_vals, cell_code
+    b += align256((size_t)n * 8);                // cell_span
+    b += align256((NB + 1) * 4);                 // brick counts -> bases
+    b += align256(sums * 4);                     // scan block sums
     return b;
 }
 
-TreeView tree_view(void* ws, int n) {
+TreeView tree_view(void* ws, int n, const int dims[3]) {
     TreeView t{};
     t.n = std::max(n, 0);
     if (n <= 0) return t;
@@ -538,55 +739,62 @@ TreeView tree_view(void* ws, int n) {
     t.thr = reinterpret_cast<float*>(take((size_t)n * 4));
     t.flag = reinterpret_cast<unsigned*>(take((size_t)n * 4));
     t.incl = reinterpret_cast<unsigned*>(take((size_t)n * 4));
-    t.codes = reinterpret_cast<unsigned*>(take((size_t)n * 8));
-    t.vals = reinterpret_cast<unsigned*>(take((size_t)n * 8));
+    t.codes = reinterpret_cast<unsigned long long*>(take((size_t)n * 8));
+    t.vals = reinterpret_cast<unsigned*>(take((size_t)n * 4));
     t.info = reinterpret_cast<unsigned*>(take(16));
-    t.sort_temp_bytes = sort_temp_bytes(n);
-    t.sort_temp = take(t.sort_temp_bytes);
+    t.tmp_pts = reinterpret_cast<float4*>(take((size_t)n * 16));
+    t.tmp_vals = reinterpret_cast<unsigned*>(take((size_t)n * 4));
+    t.cell_code = reinterpret_cast<unsigned*>(take((size_t)n * 4));
+    t.cell_span = reinterpret_cast<uint2*>(take((size_t)n * 8));
+    for (int a = 0; a < 3; ++a) t.dims[a] = dims[a];
+    t.nbricks_pad = brick_space(dims, t.nbricks);
+    t.bcount = reinterpret_cast<unsigned*>(take((t.nbricks_pad + 1) * 4));
+    t.scan_sums = reinterpret_cast<unsigned*>(take((cdiv(std::max<size_t>(n, t.nbricks_pad), kTScanItems) + 1) * 4));
     return t;
 }
 
-size_t tree_node_bytes(int L) { return 2 * (size_t)tree_pow2(std::max(L, 1)) * 2 * sizeof(float4); }
+// the node buffer holds a tree over P = pow2 >= n leaf slots: every possible leaf count (a leaf
+// holds >= 1 point) fits without knowing L on the host
+size_t tree_node_bytes(int n) { return 2 * (size_t)tree_pow2(std::max(n, 1)) * 2 * sizeof(float4); }
 
-void tree_attach_nodes(TreeView& t, void* nodes, int L) {
-    t.L = L;
-    t.P = tree_pow2(std::max(L, 1));
+void tree_attach_nodes(TreeView& t, void* nodes) {
+    t.P = tree_pow2(std::max(t.n, 1));
     t.nlo = static_cast<float4*>(nodes);
     t.nhi = t.nlo + 2 * (size_t)t.P;
 }
 
-hipError_t launch_tree_leaves(const float4* in, const GridGeom* geom, const TreeView& t, hipStream_t s) {
+hipError_t launch_tree_leaves(const float4* in, const int* cell_start, const GridGeom* geom, const TreeView& t,
+                              hipStream_t s) {
     const int n = t.n;
     if (n <= 0) return hipSuccess;
-    morton_kernel<<<cdiv(n, 256), 256, 0, s>>>(in, n, geom, t.codes, t.vals);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipcub::DoubleBuffer<unsigned> kb(t.codes, t.codes + n), vb(t.vals, t.vals + n);
-    size_t bytes = t.sort_temp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(t.sort_temp, bytes, kb, vb, n, 0, 30, s)) != hipSuccess) return e;
-    // vals[0, n) = the input index of every tree point after the build (queries in global-id mode
-    // map a tree point to its grid slot with it: TArgs::src)
-    if (vb.Current() != t.vals &&
-        (e = hipMemcpyAsync(t.vals, vb.Current(), (size_t)n * sizeof(unsigned), hipMemcpyDeviceToDevice, s)) != hipSuccess)
-        return e;
-    gather_kernel<<<cdiv(n, 256), 256, 0, s>>>(in, t.vals, n, t.pts);
-    cut_kernel<<<cdiv(n, 256), 256, 0, s>>>(kb.Current(), n, t.flag);
-    bytes = t.sort_temp_bytes;
-    if ((e = hipcub::DeviceScan::InclusiveSum(t.sort_temp, bytes, t.flag, t.incl, n, s)) != hipSuccess) return e;
+    hipError_t e;
+    // Morton order of the cells (brick counts -> brick bases -> per-brick cell scan + copy)
+    const unsigned nreal = (unsigned)(t.nbricks[0] * t.nbricks[1] * t.nbricks[2]);
+    if ((e = hipMemsetAsync(t.bcount, 0, t.nbricks_pad * sizeof(unsigned), s)) != hipSuccess) return e;
+    brick_count_kernel<<<nreal, 64, 0, s>>>(cell_start, geom, t.nbricks[0], t.nbricks[1], t.bcount);
+    if ((e = tscan(t.bcount, (int)t.nbricks_pad, t.bcount, t.scan_sums, false, s)) != hipSuccess) return e;
+    brick_scatter_kernel<<<nreal, 256, 0, s>>>(in, cell_start, geom, t.nbricks[0], t.nbricks[1], t.bcount,
+                                               t.tmp_pts, t.tmp_vals, t.cell_code, t.cell_span);
+    subcell_rank_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.tmp_pts, t.tmp_vals, t.cell_code, t.cell_span, geom, n, t.pts,
+                                                     t.vals, t.codes);
+    // leaves: maximal prefix nodes of <= kTreeLeaf points, long equal-code runs chunked
+    cut_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.codes, n, t.flag);
+    if ((e = tscan(t.flag, n, t.incl, t.scan_sums, true, s)) != hipSuccess) return e;
     starts_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.flag, t.incl, n, t.seg_start, nullptr);
     leaf_flag_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.incl, t.seg_start, n, t.flag);
-    bytes = t.sort_temp_bytes;
-    if ((e = hipcub::DeviceScan::InclusiveSum(t.sort_temp, bytes, t.flag, t.incl, n, s)) != hipSuccess) return e;
+    if ((e = tscan(t.flag, n, t.incl, t.scan_sums, true, s)) != hipSuccess) return e;
     starts_kernel<<<cdiv(n, 256), 256, 0, s>>>(t.flag, t.incl, n, t.leaf_start, t.info);
     return hipGetLastError();
 }
 
 hipError_t launch_tree_nodes(const TreeView& t, hipStream_t s) {
     if (t.n <= 0) return hipSuccess;
-    if (!t.nlo || t.L < 1) return hipErrorInvalidValue;
-    leaf_box_kernel<<<cdiv(t.P, 4), 256, 0, s>>>(t.pts, t.leaf_start, t.L, t.P, t.nlo, t.nhi);
+    if (!t.nlo) return hipErrorInvalidValue;
+    const int logP = tree_log2(t.P);
+    leaf_box_kernel<<<std::max(1u, std::min(cdiv(t.n, 4 * 8), 4096u)), 256, 0, s>>>(t.pts, t.leaf_start, t.info, t.P,
+                                                                                     t.nlo, t.nhi);
     for (int m = t.P; m > 1; m /= std::min(m, 64))
-        node_box_kernel<<<m / std::min(m, 64), 64, 0, s>>>(t.nlo, t.nhi, m);
+        node_box_kernel<<<m / std::min(m, 64), 64, 0, s>>>(t.nlo, t.nhi, m, logP, t.info);
     return hipGetLastError();
 }
 
@@ -594,10 +802,11 @@ hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t 
     if (q.k <= 0 || q.k > 128) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s);
     if (e != hipSuccess || t.n == 0 || q.n_queries == 0) return e;
-    if (!t.nlo || t.L < 1) return hipErrorInvalidValue;
+    if (!t.nlo) return hipErrorInvalidValue;
     TArgs a{};
     a.pts = t.pts; a.leaf_start = t.leaf_start; a.nlo = t.nlo; a.nhi = t.nhi; a.list = t.list; a.thr = t.thr;
-    a.n = t.n; a.L = t.L; a.P = t.P; a.k = q.k; a.n_queries = q.n_queries; a.q_lo = 0; a.id_map = q.id_map;
+    a.Lp = t.info; a.n = t.n; a.P = t.P; a.logP = tree_log2(t.P);
+    a.k = q.k; a.n_queries = q.n_queries; a.q_lo = 0; a.id_map = q.id_map;
     a.row_of = q.row_of; a.src = t.vals; a.out_idx = q.out_idx; a.out_dist = q.out_dist; a.counters = q.counters;
     a.flags = q.flags;
     constexpr int M = 2;
@@ -618,6 +827,13 @@ hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t 
     const unsigned eg = all ? std::max(1u, std::min(cdiv(t.n, 4), 16384u)) : (unsigned)kExactGrid;
     knn_tree_exact_kernel<<<eg, 256, 0, s>>>(a, all ? 1 : 0);
     return hipGetLastError();
+}
+
+hipError_t tree_leaf_count(const TreeView& t, unsigned* L, hipStream_t s) {
+    *L = 0;
+    if (t.n <= 0) return hipSuccess;
+    hipError_t e = hipMemcpyAsync(L, t.info, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+    return e != hipSuccess ? e : hipStreamSynchronize(s);
 }
 
 KN_DEFINE_DEBUG_READER(debug_words_tree)

@@ -194,9 +194,11 @@ kn_status Engine::query_async(bool fused_step) {
     return check(launch_query(q, stream_), "query");
 }
 
-kn_status Engine::tree_query() {
+// Tree buffers for the current grid: workspace (sized by n and the grid dims) and the node
+// buffer (P = pow2 >= n leaf slots, any leaf count fits). Allocated outside any graph capture.
+kn_status Engine::ensure_tree() {
     kn_status st;
-    const size_t need = tree_workspace_bytes(n_);
+    const size_t need = tree_workspace_bytes(n_, ap_.dims);
     if (tree_ws_bytes_ < need) {
         if (tree_ws_) (void)hipFree(tree_ws_);
         tree_ws_ = nullptr;
@@ -204,15 +206,7 @@ kn_status Engine::tree_query() {
         if ((st = check(hipMalloc(&tree_ws_, need), "hipMalloc(tree)")) != KN_OK) return st;
         tree_ws_bytes_ = need;
     }
-    TreeView t = tree_view(tree_ws_, n_);
-    if ((st = check(launch_tree_leaves(sorted_, geom_, t, stream_), "tree leaves")) != KN_OK) return st;
-    unsigned L = 0;
-    if (n_ > 0) {
-        if ((st = check(hipMemcpyAsync(&L, t.info, sizeof(L), hipMemcpyDeviceToHost, stream_), "D2H leaves")) != KN_OK)
-            return st;
-        if ((st = check(hipStreamSynchronize(stream_), "tree sync")) != KN_OK) return st;
-    }
-    const size_t nb = tree_node_bytes((int)L);
+    const size_t nb = tree_node_bytes(n_);
     if (tree_nodes_bytes_ < nb) {
         if (tree_nodes_) (void)hipFree(tree_nodes_);
         tree_nodes_ = nullptr;
@@ -220,8 +214,16 @@ kn_status Engine::tree_query() {
         if ((st = check(hipMalloc(&tree_nodes_, nb), "hipMalloc(tree nodes)")) != KN_OK) return st;
         tree_nodes_bytes_ = nb;
     }
-    tree_leaves_ = (int)L;
-    tree_attach_nodes(t, tree_nodes_, (int)L);
+    return KN_OK;
+}
+
+// Stream-ordered, no host synchronisation (the leaf count stays on the device): capturable.
+kn_status Engine::tree_query() {
+    kn_status st;
+    if ((st = ensure_tree()) != KN_OK) return st;
+    TreeView t = tree_view(tree_ws_, n_, ap_.dims);
+    tree_attach_nodes(t, tree_nodes_);
+    if ((st = check(launch_tree_leaves(sorted_, cell_start_, geom_, t, stream_), "tree leaves")) != KN_OK) return st;
     if ((st = check(launch_tree_nodes(t, stream_), "tree nodes")) != KN_OK) return st;
     TreeQuery q{};
     q.k = cfg_.k;
@@ -230,6 +232,13 @@ kn_status Engine::tree_query() {
     q.out_dist = out_dist_;
     q.counters = counters_;
     return check(launch_tree_query(t, q, stream_), "tree query");
+}
+
+int Engine::tree_leaves() {
+    if (!use_tree_ || !tree_ws_ || !solved_) return 0;
+    TreeView t = tree_view(tree_ws_, n_, ap_.dims);
+    unsigned L = 0;
+    return tree_leaf_count(t, &L, stream_) == hipSuccess ? (int)L : -1;
 }
 
 kn_status Engine::occupancy(double* w) {
@@ -282,7 +291,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     // 1.27 vs 0.96 + 0.27; profiles/diag_r2_tree.jsonl): the tree path takes it.
     refined_ = refined;
     use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined));
-    if (use_tree_ && graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }  // grid or tree step of the new plan
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
     built_ = true;
     return KN_OK;
@@ -312,6 +321,7 @@ kn_status Engine::ensure_outputs() {
     if (cfg_.with_distances && !out_dist_ &&
         (st = check(hipMalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
         return st;
+    if (use_tree_ && (st = ensure_tree()) != KN_OK) return st;
     return KN_OK;
 }
 
@@ -389,16 +399,6 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     if (!built_) return fail(KN_ERR_STATE, "run_graph() before prepare()");
     kn_status st;
     if ((st = ensure_outputs()) != KN_OK) return st;  // not inside the capture
-    if (use_tree_) {  // eager steps (see launch_graph)
-        (void)hipEventRecord(ev_[0], stream_);
-        if ((st = launch_graph(iters)) != KN_OK) return st;
-        (void)hipEventRecord(ev_[1], stream_);
-        if ((st = check(hipEventSynchronize(ev_[1]), "graph sync")) != KN_OK) return st;
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, ev_[0], ev_[1]);
-        if (ms_per_iter) *ms_per_iter = iters > 0 ? ms / iters : 0.f;
-        return KN_OK;
-    }
     if (!graph_) {
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
@@ -429,16 +429,6 @@ kn_status Engine::launch_graph(int iters) {
     if (!built_) return fail(KN_ERR_STATE, "launch_graph() before prepare()");
     kn_status st;
     if ((st = ensure_outputs()) != KN_OK) return st;  // not inside the capture
-    if (use_tree_) {
-        // the tree build reads its leaf count back (sizes the node buffer): eager steps
-        for (int i = 0; i < iters; ++i) {
-            if ((st = build_async()) != KN_OK) return st;
-            if ((st = query_async()) != KN_OK) return st;
-        }
-        solved_ = true;
-        stored_valid_ = points3_valid_ = false;
-        return KN_OK;
-    }
     if (!graph_) {
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;

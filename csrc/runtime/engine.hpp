@@ -80,7 +80,7 @@ public:
     float ms_build() const { return ms_build_; }
     float ms_solve() const { return ms_solve_; }
     bool uses_tree() const { return use_tree_; }
-    int tree_leaves() const { return tree_leaves_; }
+    int tree_leaves();  // leaf count of the last tree step (diagnostics: one host sync)
 
     // raw device pointers (C API struct fields)
     float4* d_sorted() const { return sorted_; }
@@ -99,8 +99,9 @@ private:
     kn_status ensure_outputs();
     kn_status build_async(bool fused_step = false);
     kn_status query_async(bool fused_step = false);
-    // Morton-leaf tree over the built grid's points (one host sync: the leaf count) + its query
+    // Morton-leaf tree over the built grid's points + its query (stream-ordered, capturable)
     kn_status tree_query();
+    kn_status ensure_tree();
     QueryBuffers query_buffers() const;
     BuildBuffers build_buffers() const;
     void release();
@@ -143,7 +144,6 @@ private:
     size_t tree_ws_bytes_ = 0;
     void* tree_nodes_ = nullptr;
     size_t tree_nodes_bytes_ = 0;
-    int tree_leaves_ = 0;
     float ms_build_ = 0.f, ms_solve_ = 0.f;
 };
 

@@ -173,48 +173,58 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
 
 // Morton-leaf tree over a built grid's points (kn/tree.h): (workspace, node buffer, leaf count).
 // One host sync (the leaf count sizes the node buffer).
-std::tuple<torch::Tensor, torch::Tensor, int64_t> tree_build_impl(torch::Tensor sorted, torch::Tensor geom);
+std::tuple<torch::Tensor, torch::Tensor, int64_t> tree_build_impl(torch::Tensor sorted, torch::Tensor cell_start,
+                                                                  torch::Tensor geom, std::vector<int64_t> dims,
+                                                                  bool count_leaves);
 
-py::tuple tree_build(torch::Tensor sorted, torch::Tensor geom) {
-    auto r = tree_build_impl(sorted, geom);
+py::tuple tree_build(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom, std::vector<int64_t> dims,
+                     bool count_leaves) {
+    auto r = tree_build_impl(sorted, cell_start, geom, dims, count_leaves);
     return py::make_tuple(std::get<0>(r), std::get<1>(r), std::get<2>(r));
 }
 
-std::tuple<torch::Tensor, torch::Tensor, int64_t> tree_build_impl(torch::Tensor sorted, torch::Tensor geom) {
+// Stream-ordered tree build (no host sync); the leaf count is read back only on request
+// (count_leaves, diagnostics) -- the query kernels take it from the device.
+std::tuple<torch::Tensor, torch::Tensor, int64_t> tree_build_impl(torch::Tensor sorted, torch::Tensor cell_start,
+                                                                  torch::Tensor geom, std::vector<int64_t> dims,
+                                                                  bool count_leaves) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(geom.is_cuda() && geom.numel() == 16, "geom must be a 16-int GPU tensor");
+    TORCH_CHECK(dims.size() == 3 && dims[0] > 0 && dims[1] > 0 && dims[2] > 0, "dims = the grid's [X, Y, Z]");
+    TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32 &&
+                    cell_start.numel() == dims[0] * dims[1] * dims[2] + 1, "cell_start must match dims");
     const c10::DeviceGuard guard(sorted.device());
     const int n = (int)sorted.size(0);
+    const int d[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
     auto u8 = sorted.options().dtype(torch::kUInt8);
-    auto ws = torch::empty({(int64_t)kn::tree_workspace_bytes(n)}, u8);
-    kn::TreeView t = kn::tree_view(ws.data_ptr(), n);
+    auto ws = torch::empty({(int64_t)kn::tree_workspace_bytes(n, d)}, u8);
+    auto nodes = torch::empty({(int64_t)kn::tree_node_bytes(n)}, u8);
+    kn::TreeView t = kn::tree_view(ws.data_ptr(), n, d);
+    kn::tree_attach_nodes(t, nodes.data_ptr());
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_tree_leaves(reinterpret_cast<const float4*>(sorted.data_ptr<float>()),
+                                        cell_start.data_ptr<int>(),
                                         reinterpret_cast<const kn::GridGeom*>(geom.data_ptr<int>()), t, s));
-    unsigned L = 0;
-    if (n > 0) {
-        KN_CHECK_HIP(hipMemcpyAsync(&L, t.info, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-        KN_CHECK_HIP(hipStreamSynchronize(s));
-    }
-    auto nodes = torch::empty({(int64_t)kn::tree_node_bytes((int)L)}, u8);
-    kn::tree_attach_nodes(t, nodes.data_ptr(), (int)L);
     KN_CHECK_HIP(kn::launch_tree_nodes(t, s));
-    return {ws, nodes, (int64_t)L};
+    unsigned L = 0;
+    if (count_leaves) KN_CHECK_HIP(kn::tree_leaf_count(t, &L, s));
+    return {ws, nodes, count_leaves ? (int64_t)L : (int64_t)-1};
 }
 
-std::vector<torch::Tensor> tree_query(torch::Tensor ws, torch::Tensor nodes, int64_t leaves, int64_t n, int64_t k,
-                                      int64_t n_queries, c10::optional<torch::Tensor> id_map, bool with_dist,
+std::vector<torch::Tensor> tree_query(torch::Tensor ws, torch::Tensor nodes, std::vector<int64_t> dims, int64_t n,
+                                      int64_t k, int64_t n_queries, c10::optional<torch::Tensor> id_map, bool with_dist,
                                       int64_t flags, c10::optional<torch::Tensor> row_of = c10::nullopt) {
+    TORCH_CHECK(dims.size() == 3 && dims[0] > 0 && dims[1] > 0 && dims[2] > 0, "dims = the grid's [X, Y, Z]");
+    const int d[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
     TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kUInt8, "ws must be a tree_build workspace");
-    TORCH_CHECK(n >= 0 && (size_t)ws.numel() >= kn::tree_workspace_bytes((int)n), "workspace too small for n");
-    TORCH_CHECK(nodes.is_cuda() && (size_t)nodes.numel() >= kn::tree_node_bytes((int)leaves), "node buffer too small");
-    TORCH_CHECK(n == 0 || (leaves >= 1 && leaves <= n), "bad leaf count");
+    TORCH_CHECK(n >= 0 && (size_t)ws.numel() >= kn::tree_workspace_bytes((int)n, d), "workspace too small for n");
+    TORCH_CHECK(nodes.is_cuda() && (size_t)nodes.numel() >= kn::tree_node_bytes((int)n), "node buffer too small");
     TORCH_CHECK(k >= 1 && k <= 128, "k must be in [1, 128]");
     TORCH_CHECK(n_queries >= 0 && n_queries <= n, "n_queries out of range");
     const c10::DeviceGuard guard(ws.device());
-    kn::TreeView t = kn::tree_view(ws.data_ptr(), (int)n);
-    kn::tree_attach_nodes(t, nodes.data_ptr(), (int)leaves);
+    kn::TreeView t = kn::tree_view(ws.data_ptr(), (int)n, d);
+    kn::tree_attach_nodes(t, nodes.data_ptr());
     auto i32 = ws.options().dtype(torch::kInt32);
     auto out_idx = torch::empty({n_queries, k}, i32);
     torch::Tensor out_dist = torch::empty({with_dist ? n_queries : 0, with_dist ? k : 0}, ws.options().dtype(torch::kFloat32));
@@ -667,9 +677,8 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
         // Morton-leaf tree over the local grid's points in global-id mode (owned points are the
         // queries), then the complete-box certification the grid kernels do inline: uncertified
         // rows go to the forwarding round
-        auto tb = tree_build_impl(g[0], g[3]);
-        auto tq = tree_query(std::get<0>(tb), std::get<1>(tb), std::get<2>(tb), npts, k, n_owned, c10::nullopt, true,
-                             0, g[2]);
+        auto tb = tree_build_impl(g[0], g[1], g[3], dims, false);
+        auto tq = tree_query(std::get<0>(tb), std::get<1>(tb), dims, npts, k, n_owned, c10::nullopt, true, 0, g[2]);
         auto uncert = torch::empty({std::max<int64_t>(1, n_owned)}, pg[1].options());
         kn::CompleteBox cb;
         for (int a = 0; a < 3; ++a) { cb.lo[a] = (float)complete[a]; cb.hi[a] = (float)complete[3 + a]; }
@@ -1045,10 +1054,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         },
         "LDS bytes per workgroup of the tile query kernel for a plan");
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
-    m.def("tree_build", &tree_build, "Morton-leaf tree over a grid's sorted points: (workspace, nodes, leaves)",
-          py::arg("sorted"), py::arg("geom"));
+    m.def("tree_build", &tree_build,
+          "Morton-leaf tree over a grid's sorted points, stream-ordered: (workspace, nodes, leaves or -1)",
+          py::arg("sorted"), py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("count_leaves") = false);
     m.def("tree_query", &tree_query, "kNN through a tree_build result: (idx, d2, counters)", py::arg("ws"),
-          py::arg("nodes"), py::arg("leaves"), py::arg("n"), py::arg("k"), py::arg("n_queries"), py::arg("id_map") = py::none(),
+          py::arg("nodes"), py::arg("dims"), py::arg("n"), py::arg("k"), py::arg("n_queries"), py::arg("id_map") = py::none(),
           py::arg("with_dist") = true, py::arg("flags") = 0, py::arg("row_of") = py::none());
     m.def("cell_sort", &cell_sort, "in-cell order by original index (deterministic layout) of a built grid");
     m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");

@@ -103,13 +103,14 @@ def build_grid(points: torch.Tensor, k: int = 16, plan: Optional[Plan] = None,
     return Grid(s, cs, perm, geom, plan, n, {"algo": "tree" if refined else "grid"})
 
 
-def build_tree(grid: Grid) -> tuple:
+def build_tree(grid: Grid, count_leaves: bool = False) -> tuple:
     """Morton-leaf box tree over the grid's points (``kn/tree.h``), cached on the grid: the
     density-adaptive query structure for clouds one cell size cannot serve (clusters, scans).
-    Returns ``(workspace, nodes, leaves)``; one host sync (the leaf count)."""
+    Returns ``(workspace, nodes, leaves)``. Stream-ordered: the leaf count stays on the device
+    (``leaves`` is -1 unless ``count_leaves``, which costs one host sync)."""
     t = grid.extra.get("tree")
-    if t is None:
-        t = tuple(load().tree_build(grid.sorted, grid.geom))
+    if t is None or (count_leaves and t[2] < 0):
+        t = tuple(load().tree_build(grid.sorted, grid.cell_start, grid.geom, list(grid.plan.dims), count_leaves))
         grid.extra["tree"] = t
     return t
 
@@ -138,9 +139,9 @@ def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[
     if algo == "tree":
         if complete is not None:
             raise ValueError("the tree path serves complete (single-GPU) point sets only")
-        ws, nodes, leaves = build_tree(grid)
-        idx, d2, counters = load().tree_query(ws, nodes, leaves, grid.n, int(k), nq, id_map, bool(with_dist),
-                                              int(flags) & 1)
+        ws, nodes, _ = build_tree(grid)
+        idx, d2, counters = load().tree_query(ws, nodes, list(grid.plan.dims), grid.n, int(k), nq, id_map,
+                                              bool(with_dist), int(flags) & 1)
         if return_info:
             return idx, (d2 if with_dist else None), {"counters": counters,
                                                       "uncertified": counters.new_zeros(0),

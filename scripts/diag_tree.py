@@ -25,7 +25,8 @@ def timed(fn, reps=5):
     return e0.elapsed_time(e1) / reps, out
 
 
-tb, tr = timed(lambda: kn.ops.knn_ops.load().tree_build(g.sorted, g.geom))
+tb, _ = timed(lambda: kn.ops.knn_ops.load().tree_build(g.sorted, g.cell_start, g.geom, list(g.plan.dims), False))
+tr = kn.ops.knn_ops.load().tree_build(g.sorted, g.cell_start, g.geom, list(g.plan.dims), True)
 tg, (ig, dg, infog) = timed(lambda: kn.query(g, k, return_info=True))
 tt, (it, dt, infot) = timed(lambda: kn.query(g, k, algo="tree", return_info=True))
 same = bool(torch.equal(dg, dt))
