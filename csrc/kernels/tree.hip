@@ -30,6 +30,12 @@ constexpr int kSortPasses = 3;                // odd-even passes of the exact re
 // pruned only when the box distance exceeds the bound by more than that.
 constexpr float kShrink = 0.99999f;
 constexpr int kExactGrid = 512;
+// Round-3 A/Bs of the traversal that LOST (900K, identical rows): a breadth-first sweep with the
+// bounds frozen after the own leaves (profiles/ab_r3_tree_bfs.jsonl, 1.3-3.5x slower: a sparse
+// query near a cluster keeps a loose bound until the cluster's nearest leaves shrink it, which
+// only the depth-first order does); per-lane box distances stacked in LDS instead of re-loading a
+// popped node's box (profiles/ab_r3_tree_stackdist.jsonl, K=16 +16 %: the 10 KB per wave cost
+// more in resident waves than the loads it saved).
 
 struct TArgs {
     const float4* pts;
