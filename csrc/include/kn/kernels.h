@@ -145,6 +145,11 @@ hipError_t launch_certify_rows(const float* pts, int rows, int k, const float* o
 // query forwarding): row t of q.out_idx / q.out_dist; a point with the query's global id is
 // skipped (self). Uses q.sorted / cell_start / geom / dims / k / row_of / counters.
 hipError_t launch_query_external(const QueryBuffers& q, const float4* ext, int n_ext, hipStream_t stream);
+// Forwarding slots of a sync-free multi-GPU step (kn/route.h launch_fwd_pack): n_slots queries,
+// 2 float4 each ({x, y, z, bits(gid)}, {origin K-th d2, -, -, -}); gid 0xFFFFFFFF = empty. Rows
+// t of out_idx / out_dist (global ids, ascending (d2, id), <= K points within the seed) for every
+// filled slot; empty slots' rows are left untouched.
+hipError_t launch_query_external_slots(const QueryBuffers& q, const float4* slots, int n_slots, hipStream_t s);
 
 // out_sorted[i*k + j] = inv(out_orig[perm[i]*k + j]) : reference (stored-space) view.
 hipError_t launch_to_stored_space(const unsigned* out_orig, const unsigned* perm,

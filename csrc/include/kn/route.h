@@ -123,6 +123,22 @@ hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const do
 hipError_t launch_steady_flag(const double* local, const double* planned_meta, const int* totals,
                               const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                               hipStream_t s);
+// Query forwarding inside a sync-free multi-GPU step (fixed-capacity slots, no host sync):
+//   launch_fwd_pack    -> send: world x F slots of 2 float4 ({x, y, z, bits(gid)}, {K-th d2, ...}),
+//                         the uncertified queries (uncert[0 .. *ucount), local rows; their K-th
+//                         squared distance from d2 (rows x k)) to every other rank whose box is
+//                         within it; slot_row (world x F) / slot_of (umax x world, -1 = none);
+//                         overflow (> F per destination or > umax queries) counted in stat[1]
+//   (equal-split all-to-all of send; launch_query_external_slots answers the received slots;
+//    equal-split all-to-all of the answers back)
+//   launch_fwd_merge   -> each forwarded row merged with its answers: K smallest (d2, gid), no
+//                         duplicates (idx: global ids, -1 = empty)
+hipError_t launch_fwd_pack(const RouteParams* p, int world, int rank, int F, int k, const unsigned* uncert,
+                           const unsigned* ucount, int umax, const float* pts, const int* gids, const float* d2,
+                           float4* send, int* slot_row, int* slot_of, int* cnt, unsigned* stat, hipStream_t s);
+hipError_t launch_fwd_merge(int world, int F, int k, const unsigned* uncert, const unsigned* ucount, int umax,
+                            const int* slot_of, const int* back_idx, const float* back_d2, int* idx, float* d2,
+                            hipStream_t s);
 hipError_t debug_words_route(unsigned out[4], bool reset);
 
 }  // namespace kn

@@ -1358,6 +1358,10 @@ struct ExactArgs {
     unsigned* uncert_list;     // optional: original indices of uncertified queries
     const float4* ext;         // external queries {x, y, z, bits(global id)} (nullptr: stored points)
     int n_ext;
+    // 2: slot layout of the multi-GPU forwarding (launch_query_external_slots): query t is
+    // ext[2t] = {x, y, z, bits(gid)} and ext[2t + 1].x its origin's K-th squared distance (an
+    // upper bound: seeds the threshold); gid 0xFFFFFFFF = empty slot, skipped
+    int ext_stride;
 };
 
 // ---- wave-per-query exact kernel: threshold compaction + wave bitonic sort (any K <= 128) ----
@@ -1391,15 +1395,21 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
             (int)(a.list ? a.list[KN_IDX(t, a.n, 311)] : (unsigned)t));
         const bool seeded = !a.ext && a.list && (entry & kSeedBit) && a.out_dist;
         const unsigned sidx = a.ext ? ~0u : (entry & ~kSeedBit);
-        const float4 qp = a.ext ? a.ext[t] : a.sorted[KN_IDX(sidx, (unsigned)a.n, 312)];
+        const float4 qp = a.ext ? a.ext[(size_t)t * a.ext_stride] : a.sorted[KN_IDX(sidx, (unsigned)a.n, 312)];
         const unsigned qw = __float_as_uint(qp.w);
         if (!a.ext && !w_live(a, qw)) continue;
+        if (a.ext && a.ext_stride == 2 && qw == SENT) continue;  // empty forwarding slot
         const unsigned qorig = a.ext ? (unsigned)t : w_row(a, qw, sidx);
         const unsigned qid = a.ext ? w_id(a, qw) : ~0u;
         const float qx = qp.x, qy = qp.y, qz = qp.z;
         const int cx = cell_coord(g, 0, qx), cy = cell_coord(g, 1, qy), cz = cell_coord(g, 2, qz);
         int cnt = 0;            // keys in buf (uniform)
         float thr = INFINITY;   // current K-th distance bound (uniform)
+        if (a.ext && a.ext_stride == 2) {
+            // forwarded query: only points within the origin's K-th distance can improve its row
+            const float s0 = a.ext[(size_t)t * 2 + 1].x;
+            if (s0 >= 0.f && s0 < INFINITY) thr = s0;
+        }
         if (seeded) {
             // the tile kernel's K-th distance for this row (K real points within it): every true
             // neighbour passes d2 <= thr from the first shell on, rows are cut by the ball at once
@@ -1751,7 +1761,26 @@ hipError_t launch_query_external(const QueryBuffers& q, const float4* ext, int n
     b.uncert_list = nullptr;
     b.ext = ext;
     b.n_ext = n_ext;
+    b.ext_stride = 1;
     knn_exact_coop_kernel<<<std::max(1u, std::min(cdiv((size_t)n_ext, 4), 16384u)), 256, 0, s>>>(b);
+    return hipGetLastError();
+}
+
+hipError_t launch_query_external_slots(const QueryBuffers& q, const float4* slots, int n_slots, hipStream_t s) {
+    if (q.k <= 0 || q.k > 128 || n_slots < 0) return hipErrorInvalidValue;
+    if (n_slots == 0) return hipSuccess;
+    ExactArgs b{};
+    b.sorted = q.sorted; b.cell_start = q.cell_start; b.geom = q.geom; b.n = q.n;
+    b.X = q.dims[0]; b.Y = q.dims[1]; b.Z = q.dims[2]; b.k = q.k; b.n_queries = n_slots; b.q_lo = 0;
+    b.id_map = q.id_map; b.row_of = q.row_of;
+    for (int a = 0; a < 3; ++a) { b.complete.lo[a] = -INFINITY; b.complete.hi[a] = INFINITY; }
+    b.out_idx = q.out_idx; b.out_dist = q.out_dist;
+    b.counters = q.counters;
+    b.ext = slots;
+    b.n_ext = n_slots;
+    b.ext_stride = 2;
+    // fixed grid (the number of filled slots is only known on the device); empty slots are skipped
+    knn_exact_coop_kernel<<<std::max(1u, std::min(cdiv((size_t)n_slots, 4), 512u)), 256, 0, s>>>(b);
     return hipGetLastError();
 }
 

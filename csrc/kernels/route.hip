@@ -464,6 +464,103 @@ __global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsign
     if (lane == 0) flag[0] = (any ? 1 : 0) + (counters[1] != 0u ? 1 : 0);
 }
 
+// ---- query forwarding inside a sync-free step (fixed-capacity slots, no host round trip) -------
+// Every uncertified query of this rank (local row, K-th squared distance r2 of its local answer)
+// goes to each OTHER rank whose box lies within r2 (conservative slack), into that destination's
+// fixed slot block: slot = atomic counter, row pair {x, y, z, bits(gid)}, {r2, -, -, -}. A
+// destination block that would overflow F slots counts in stat[1] (the step's flag then fails it
+// and the caller re-solves the full way). slot_of[u * world + d] = the slot of query u at d (-1).
+__global__ __launch_bounds__(256) void fwd_pack_kernel(const RouteParams* __restrict__ pp, int rank, int F, int k,
+                                                       const unsigned* __restrict__ uncert,
+                                                       const unsigned* __restrict__ ucount, int umax,
+                                                       const float* __restrict__ pts, const int* __restrict__ gids,
+                                                       const float* __restrict__ d2, float4* __restrict__ send,
+                                                       int* __restrict__ slot_row, int* __restrict__ slot_of,
+                                                       int* __restrict__ cnt, unsigned* __restrict__ stat) {
+    const RouteParams& p = *pp;
+    const int world = p.world;
+    const int nu = (int)*ucount;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nu > umax) atomicAdd(stat + 1, (unsigned)(nu - umax));
+    for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < min(nu, umax); u += gridDim.x * blockDim.x) {
+        const int row = (int)uncert[u];
+        const float x = pts[3 * (size_t)row], y = pts[3 * (size_t)row + 1], z = pts[3 * (size_t)row + 2];
+        const float r2 = d2[(size_t)row * k + (k - 1)];
+        // the float box arithmetic may not miss a rank: same slack as the host-synchronised round
+        const float r2c = (r2 < INFINITY) ? r2 * (1.0f + 1e-5f) + 1e-6f : INFINITY;
+        for (int d = 0; d < world; ++d) {
+            int sl = -1;
+            if (d != rank) {
+                const float dx = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[d][0], x), 0.f), fmaxf(__fsub_rn(x, p.box_hi[d][0]), 0.f));
+                const float dy = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[d][1], y), 0.f), fmaxf(__fsub_rn(y, p.box_hi[d][1]), 0.f));
+                const float dz = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[d][2], z), 0.f), fmaxf(__fsub_rn(z, p.box_hi[d][2]), 0.f));
+                const float bd = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
+                if (bd <= r2c) {
+                    const int s = atomicAdd(&cnt[d], 1);
+                    if (s < F) {
+                        const size_t o = (size_t)d * F + s;
+                        send[2 * o] = make_float4(x, y, z, __int_as_float(gids[row]));
+                        send[2 * o + 1] = make_float4(r2, 0.f, 0.f, 0.f);
+                        slot_row[o] = row;
+                        sl = s;
+                    } else {
+                        atomicAdd(stat + 1, 1u);
+                    }
+                }
+            }
+            slot_of[(size_t)u * world + d] = sl;
+        }
+    }
+}
+
+// Merge of the answers: one thread per forwarded query. Its row (ascending (d2, id), K entries)
+// is merged with each destination's answer list (<= K, ascending) keeping the K smallest
+// (d2, gid), duplicates (a halo copy answered by its owner too) dropped.
+__global__ __launch_bounds__(256) void fwd_merge_kernel(int world, int F, int k, const unsigned* __restrict__ uncert,
+                                                        const unsigned* __restrict__ ucount, int umax,
+                                                        const int* __restrict__ slot_of, const int* __restrict__ back_idx,
+                                                        const float* __restrict__ back_d2, int* __restrict__ idx,
+                                                        float* __restrict__ d2) {
+    constexpr int kMaxK = 128;
+    const int nu = min((int)*ucount, umax);
+    for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += gridDim.x * blockDim.x) {
+        const int row = (int)uncert[u];
+        int* ri = idx + (size_t)row * k;
+        float* rd = d2 + (size_t)row * k;
+        for (int d = 0; d < world; ++d) {
+            const int sl = slot_of[(size_t)u * world + d];
+            if (sl < 0) continue;
+            const int* ai = back_idx + ((size_t)d * F + sl) * k;
+            const float* ad = back_d2 + ((size_t)d * F + sl) * k;
+            int oi[kMaxK];
+            float od[kMaxK];
+            int i = 0, j = 0, m = 0;
+            unsigned lastid = 0xFFFFFFFFu;
+            float lastd = -1.f;
+            while (m < k && (i < k || j < k)) {
+                const bool vi = i < k && ri[i] != -1, vj = j < k && ai[j] != -1;
+                if (!vi && !vj) break;
+                bool takei;
+                if (!vj) takei = true;
+                else if (!vi) takei = false;
+                else takei = rd[i] < ad[j] || (rd[i] == ad[j] && (unsigned)ri[i] <= (unsigned)ai[j]);
+                const int ci = takei ? ri[i] : ai[j];
+                const float cd = takei ? rd[i] : ad[j];
+                if (takei) ++i; else ++j;
+                if ((unsigned)ci == lastid && cd == lastd) continue;  // duplicate point
+                oi[m] = ci;
+                od[m] = cd;
+                lastid = (unsigned)ci;
+                lastd = cd;
+                ++m;
+            }
+            for (int t = 0; t < k; ++t) {
+                ri[t] = t < m ? oi[t] : -1;
+                rd[t] = t < m ? od[t] : INFINITY;
+            }
+        }
+    }
+}
+
 }  // namespace
 
 int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
@@ -535,6 +632,31 @@ hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const do
 
 hipError_t launch_global_w(float4* sorted, const unsigned* perm, const int* gids, int n, int n_owned, hipStream_t s) {
     if (n > 0) global_w_kernel<<<cdiv(n, kRT), kRT, 0, s>>>(sorted, perm, gids, n, n_owned);
+    return hipGetLastError();
+}
+
+hipError_t launch_fwd_pack(const RouteParams* p, int world, int rank, int F, int k, const unsigned* uncert,
+                           const unsigned* ucount, int umax, const float* pts, const int* gids, const float* d2,
+                           float4* send, int* slot_row, int* slot_of, int* cnt, unsigned* stat, hipStream_t s) {
+    if (world < 1 || world > kRouteMaxWorld || rank < 0 || rank >= world || F < 1 || k < 1 || umax < 0)
+        return hipErrorInvalidValue;
+    hipError_t e;
+    // empty slots: gid 0xFFFFFFFF (every float NaN); counters zeroed
+    if ((e = hipMemsetAsync(send, 0xFF, (size_t)world * F * 2 * sizeof(float4), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(cnt, 0, (size_t)world * sizeof(int), s)) != hipSuccess) return e;
+    if (umax > 0)
+        fwd_pack_kernel<<<std::max(1u, std::min(cdiv((size_t)umax, 256), 64u)), 256, 0, s>>>(
+            p, rank, F, k, uncert, ucount, umax, pts, gids, d2, send, slot_row, slot_of, cnt, stat);
+    return hipGetLastError();
+}
+
+hipError_t launch_fwd_merge(int world, int F, int k, const unsigned* uncert, const unsigned* ucount, int umax,
+                            const int* slot_of, const int* back_idx, const float* back_d2, int* idx, float* d2,
+                            hipStream_t s) {
+    if (world < 1 || F < 1 || k < 1 || k > 128 || umax < 0) return hipErrorInvalidValue;
+    if (umax > 0)
+        fwd_merge_kernel<<<std::max(1u, std::min(cdiv((size_t)umax, 256), 64u)), 256, 0, s>>>(
+            world, F, k, uncert, ucount, umax, slot_of, back_idx, back_d2, idx, d2);
     return hipGetLastError();
 }
 

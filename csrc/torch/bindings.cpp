@@ -728,6 +728,96 @@ std::vector<torch::Tensor> query_external(torch::Tensor sorted, torch::Tensor ce
     return {idx, d2};
 }
 
+// ---- query forwarding inside a sync-free step (kn/route.h launch_fwd_pack / launch_fwd_merge) ----
+// -> {send (world*F*2, 4) f32, slot_of (umax*world) i32, stat (2) i32: [1] = overflow}
+std::vector<torch::Tensor> fwd_pack(torch::Tensor plan, int64_t world, int64_t rank, int64_t F, int64_t k,
+                                    torch::Tensor uncert, torch::Tensor counters, int64_t umax, torch::Tensor pts,
+                                    torch::Tensor gids, torch::Tensor d2) {
+    TORCH_CHECK(plan.is_cuda() && plan.numel() == (int64_t)sizeof(kn::RouteParams), "plan must be a route plan");
+    TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld && rank >= 0 && rank < world, "bad world / rank");
+    TORCH_CHECK(F >= 1 && F <= (1 << 20) && umax >= 0 && umax <= (1 << 24), "bad slot capacity");
+    TORCH_CHECK(k >= 1 && k <= 128, "k must be in [1, 128]");
+    TORCH_CHECK(uncert.is_cuda() && uncert.scalar_type() == torch::kInt32, "uncert: int32 GPU list");
+    TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == torch::kInt32 && counters.numel() >= 2, "counters");
+    TORCH_CHECK(pts.is_cuda() && pts.scalar_type() == torch::kFloat32 && pts.dim() == 2 && pts.size(1) == 3 &&
+                    pts.is_contiguous(), "pts: (rows, 3) f32");
+    TORCH_CHECK(gids.is_cuda() && gids.scalar_type() == torch::kInt32 && gids.numel() >= pts.size(0), "gids");
+    TORCH_CHECK(d2.is_cuda() && d2.scalar_type() == torch::kFloat32 && d2.dim() == 2 && d2.size(1) == k &&
+                    d2.is_contiguous(), "d2: (owned, k) f32");
+    TORCH_CHECK(uncert.numel() >= std::min<int64_t>(umax, d2.size(0)) || d2.size(0) == 0, "uncert list too short");
+    const c10::DeviceGuard guard(pts.device());
+    auto f32 = pts.options();
+    auto i32 = pts.options().dtype(torch::kInt32);
+    auto send = torch::empty({world * F * 2, 4}, f32);
+    auto slot_row = torch::empty({world * F}, i32);
+    auto slot_of = torch::empty({std::max<int64_t>(1, umax * world)}, i32);
+    auto cnt = torch::empty({world}, i32);
+    auto stat = torch::zeros({2}, i32);
+    const int um = (int)std::min<int64_t>(umax, d2.size(0));
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_fwd_pack(reinterpret_cast<const kn::RouteParams*>(plan.data_ptr<uint8_t>()), (int)world,
+                                     (int)rank, (int)F, (int)k, reinterpret_cast<const unsigned*>(uncert.data_ptr<int>()),
+                                     reinterpret_cast<const unsigned*>(counters.data_ptr<int>() + 1), um,
+                                     pts.data_ptr<float>(), gids.data_ptr<int>(), d2.data_ptr<float>(),
+                                     reinterpret_cast<float4*>(send.data_ptr<float>()), slot_row.data_ptr<int>(),
+                                     slot_of.data_ptr<int>(), cnt.data_ptr<int>(),
+                                     reinterpret_cast<unsigned*>(stat.data_ptr<int>()), s));
+    return {send, slot_of, stat};
+}
+
+// Answers to received forwarding slots from the local grid (global-id mode): -> {idx (slots, k)
+// global ids, d2 (slots, k)}; rows of empty slots are undefined.
+std::vector<torch::Tensor> fwd_answer(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom,
+                                      std::vector<int64_t> dims, int64_t k, torch::Tensor slots, torch::Tensor row_of) {
+    TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4, "sorted must be (N,4) GPU");
+    TORCH_CHECK(slots.is_cuda() && slots.dim() == 2 && slots.size(1) == 4 && slots.size(0) % 2 == 0 &&
+                    slots.scalar_type() == torch::kFloat32 && slots.is_contiguous(), "slots: (2*S, 4) f32");
+    TORCH_CHECK(dims.size() == 3 && cell_start.numel() == dims[0] * dims[1] * dims[2] + 1, "bad dims");
+    TORCH_CHECK(k >= 1 && k <= 128, "k must be in [1, 128]");
+    TORCH_CHECK(row_of.is_cuda() && row_of.scalar_type() == torch::kInt32 && row_of.numel() >= sorted.size(0),
+                "row_of must be the grid's int32 perm");
+    const c10::DeviceGuard guard(sorted.device());
+    const int64_t m = slots.size(0) / 2;
+    auto idx = torch::empty({m, k}, sorted.options().dtype(torch::kInt32));
+    auto d2 = torch::empty({m, k}, sorted.options());
+    auto counters = torch::zeros({kn::kNumCounters}, sorted.options().dtype(torch::kInt32));
+    kn::QueryBuffers q{};
+    q.sorted = reinterpret_cast<const float4*>(sorted.data_ptr<float>());
+    q.cell_start = cell_start.data_ptr<int>();
+    q.geom = reinterpret_cast<const kn::GridGeom*>(geom.data_ptr<int>());
+    q.n = (int)sorted.size(0);
+    for (int a = 0; a < 3; ++a) q.dims[a] = (int)dims[a];
+    q.k = (int)k;
+    q.row_of = reinterpret_cast<const unsigned*>(row_of.data_ptr<int>());
+    q.out_idx = reinterpret_cast<unsigned*>(idx.data_ptr<int>());
+    q.out_dist = d2.data_ptr<float>();
+    q.counters = reinterpret_cast<unsigned*>(counters.data_ptr<int>());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_query_external_slots(q, reinterpret_cast<const float4*>(slots.data_ptr<float>()), (int)m, s));
+    return {idx, d2};
+}
+
+// Merges the answers (all-to-all'd back: (world*F, k) each) into the forwarded rows, in place.
+void fwd_merge(int64_t world, int64_t F, int64_t k, torch::Tensor uncert, torch::Tensor counters, int64_t umax,
+               torch::Tensor slot_of, torch::Tensor back_idx, torch::Tensor back_d2, torch::Tensor idx, torch::Tensor d2) {
+    TORCH_CHECK(back_idx.is_cuda() && back_idx.scalar_type() == torch::kInt32 && back_idx.numel() == world * F * k,
+                "back_idx: (world*F, k) i32");
+    TORCH_CHECK(back_d2.is_cuda() && back_d2.scalar_type() == torch::kFloat32 && back_d2.numel() == world * F * k,
+                "back_d2: (world*F, k) f32");
+    TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt32 && idx.dim() == 2 && idx.size(1) == k &&
+                    idx.is_contiguous(), "idx: (owned, k) i32");
+    TORCH_CHECK(d2.is_cuda() && d2.scalar_type() == torch::kFloat32 && d2.sizes() == idx.sizes() && d2.is_contiguous(),
+                "d2 like idx");
+    TORCH_CHECK(slot_of.is_cuda() && slot_of.numel() >= std::min<int64_t>(umax, idx.size(0)) * world, "slot_of");
+    const c10::DeviceGuard guard(idx.device());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_fwd_merge((int)world, (int)F, (int)k, reinterpret_cast<const unsigned*>(uncert.data_ptr<int>()),
+                                      reinterpret_cast<const unsigned*>(counters.data_ptr<int>() + 1),
+                                      (int)std::min<int64_t>(umax, idx.size(0)), slot_of.data_ptr<int>(),
+                                      back_idx.data_ptr<int>(), back_d2.data_ptr<float>(), idx.data_ptr<int>(),
+                                      d2.data_ptr<float>(), s));
+}
+
 // Sync-free distributed step check (one wave, on device): (1,) int32 = mismatch of this rank's
 // meta / send counts against the planned ones + (uncertified queries > 0)
 torch::Tensor steady_flag(torch::Tensor local, torch::Tensor metas, int64_t rank, torch::Tensor totals,
@@ -1081,6 +1171,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("query_external", &query_external,
           "multi-GPU query forwarding: exact K nearest of external points among a local grid");
     m.def("steady_flag", &steady_flag, "multi-GPU: on-device check of a sync-free steady-state step");
+    m.def("fwd_pack", &fwd_pack, "multi-GPU: uncertified queries into fixed forwarding slots (no host sync)");
+    m.def("fwd_answer", &fwd_answer, "multi-GPU: answers to received forwarding slots from the local grid");
+    m.def("fwd_merge", &fwd_merge, "multi-GPU: merge forwarded answers into the rows, in place");
     m.def("route_steady", &route_steady,
           "multi-GPU steady step: counts + scatter with a validated plan, share bbox partials on the way",
           py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("world"), py::arg("cap"), py::arg("rank"),

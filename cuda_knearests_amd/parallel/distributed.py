@@ -153,6 +153,14 @@ class DistributedKNearests:
         # uncertified queries: forward just those queries to the ranks within their K-th distance
         # (one targeted round) instead of re-routing everything with a doubled halo
         self.forward = True
+        # Steady steps forward on the device (fixed slots per rank pair, two equal-split
+        # all-to-alls, no host sync) once the validated step needed forwarding; with a halo wide
+        # enough that no query is uncertified (uniform clouds at the default factor) they skip the
+        # two extra collectives, and a rare uncertified query fails the step's flag instead.
+        # Slots per rank pair: twice the validated step's forwarded total (all ranks; a bound on
+        # every pair's count), a power of two in [256, fwd_slots_max]; more than that and the
+        # steady state is not entered. An overflowing steady step fails its flag.
+        self.fwd_slots_max = 65536
         # hipGraph replay of the steady step (torch.cuda.CUDAGraph), opt-in: KN_DIST_GRAPH=1 or
         # graph_steady = True. Replayed rows live in the graph's static buffers until the next
         # solve. At world 1 (RCCL) 200 back-to-back replays are valid and bit-identical to the
@@ -292,7 +300,9 @@ class DistributedKNearests:
         nh = 2 * HDR
         src_pts, src_ids = points, (ids.to(torch.int32).contiguous() if ids is not None else None)
         rounds = 0
+        growth = 0  # halo-doubling re-routes (the steady state needs a step without any)
         own_pts = own_ids = None
+        n_fwd = 0
         while True:
             rounds += 1
             while True:
@@ -385,6 +395,7 @@ class DistributedKNearests:
             if done:
                 break
             hf *= 2.0
+            growth += 1
             _log.info("rank %d: uncertified queries, growth round %d with halo factor %.3g", rank, rounds + 1, hf)
             src_pts, src_ids = own_pts, own_ids
         stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
@@ -392,9 +403,11 @@ class DistributedKNearests:
                  "local_dims": tuple(int(v) for v in local_grid[5].tolist()),
                  "local_tree": bool(local_grid[6].item())}
         _log.debug("rank %d: step %s", rank, stats)
-        if rounds == 1 and not full and self.steady:
+        if growth == 0 and not full and self.steady and 2 * n_fwd <= self.fwd_slots_max:
             # validated single-round step: the steady-state assumption for the next ones
             self._steady = {
+                "fwd": n_fwd > 0,  # device forwarding in the steady steps
+                "F": max(256, 1 << max(0, 2 * n_fwd - 1).bit_length()),  # slots per rank pair
                 "metas": metas, "grid": tuple(grid), "hdr": hv[:HDR], "cap": int(send.size(0)), "splits": splits,
                 "plan": plan,  # the validated route plan (steady steps do not re-plan)
                 "dims": [int(v) for v in local_grid[5].tolist()],  # the local grid (maybe refined)
@@ -513,11 +526,28 @@ class DistributedKNearests:
             recv = self._a2a(send[:x], st["cross_send"], st["cross_recv"])
         else:
             recv = send[:0]
-        pts, gids, idx, d2, counters, *_ = C.dist_local(recv, send[:0], st["recv_own"], st["recv_halo"],
-                                                        rank, list(st["grid"]), st["hdr"], self.k,
-                                                        self.points_per_cell, self.deterministic, st["exact_grid"],
-                                                        False, st["dims"], lpts, lgids, st["use_tree"])
-        flag = C.steady_flag_partials(partials, points.size(0), st["metas"], rank, totals, st["tot"], counters)
+        pts, gids, idx, d2, counters, *lg = C.dist_local(recv, send[:0], st["recv_own"], st["recv_halo"],
+                                                         rank, list(st["grid"]), st["hdr"], self.k,
+                                                         self.points_per_cell, self.deterministic, st["exact_grid"],
+                                                         False, st["dims"], lpts, lgids, st["use_tree"])
+        check = counters  # the flag's word [1]: uncertified queries (no forwarding) or slot overflow
+        if world > 1 and st.get("fwd"):
+            # uncertified queries answered inside the step: fixed-capacity forwarding slots and
+            # equal-split all-to-alls, so nothing waits for the host (kn/route.h launch_fwd_pack)
+            F = st["F"]
+            umax = world * F
+            sorted_, cell_start, geom, perm, uncert = lg[:5]
+            fsend, slot_of, check = C.fwd_pack(st["plan"], world, rank, F, self.k, uncert, counters, umax, pts,
+                                               gids, d2)
+            frecv = torch.empty_like(fsend)
+            self.comm.all_to_all_single(frecv, fsend)
+            aidx, ad2 = C.fwd_answer(sorted_, cell_start, geom, list(st["dims"]), self.k, frecv, perm)
+            ans = torch.cat([aidx.view(torch.float32), ad2], 1)  # one collective for both halves
+            back = torch.empty_like(ans)
+            self.comm.all_to_all_single(back, ans)
+            C.fwd_merge(world, F, self.k, uncert, counters, umax, slot_of,
+                        back[:, :self.k].contiguous().view(torch.int32), back[:, self.k:].contiguous(), idx, d2)
+        flag = C.steady_flag_partials(partials, points.size(0), st["metas"], rank, totals, st["tot"], check)
         if world > 1:
             self.comm.all_reduce_max(flag)
         return gids[:sum(st["recv_own"])], idx, d2, flag

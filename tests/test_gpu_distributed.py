@@ -450,3 +450,40 @@ def test_rccl_world1_graph_replay(cuda):
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "graph True valid True same rows as eager True" in r.stdout
+
+
+@pytest.mark.parametrize("world,gen,hf", [(4, "uniform", 0.6), (8, "clustered", 1.0)])
+def test_steady_forwarding_on_device(cuda, world, gen, hf):
+    """A halo too narrow for every query (uncertified queries each step): the validated step
+    forwards them on the host, and the following asynchronous steady steps forward them ON THE
+    DEVICE (fixed slots, equal-split all-to-alls): every steady step is valid and its rows equal
+    the kd-tree oracle's (route.hip launch_fwd_pack / launch_fwd_merge)."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+    from cuda_knearests_amd.utils import clustered_cloud
+
+    n, k = 30000, 16
+    cloud = uniform_cloud(n, seed=91) if gen == "uniform" else clustered_cloud(n, seed=92)
+    owner = torch.arange(n) % world
+
+    def body(t):
+        m = owner == t.rank
+        ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
+        pts = cloud[m].contiguous().to(cuda)
+        dk = DistributedKNearests(k=k, transport=t, halo_factor=hf)
+        r0 = dk.solve(pts, ids)
+        outs = []
+        for _ in range(3):
+            r = dk.solve(pts, ids, async_=True)
+            outs.append((r.valid(), bool(r.stats.get("steady")), r.ids.cpu(), r.neighbors.cpu(), r.d2.cpu()))
+        return r0.stats, outs
+
+    out = run_loopback(world, body)
+    _, od = kn.knn_cpu(cloud, k, "kdtree")
+    assert any(st["forwarded"] > 0 for st, _ in out), "the halo was wide enough: nothing was forwarded"
+    for st, outs in out:
+        for ok, steady, ids, nb, d2 in outs:
+            assert steady and ok, (st, steady, ok)
+            ids = ids.long()
+            assert torch.equal(d2, od[ids])
+            assert_knn_exact(cloud, ids, nb, d2, od[ids])
