@@ -52,6 +52,18 @@ hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hip
 //  [6] insertion networks executed        [7] query chunks (waves x chunk iterations)
 constexpr int kNumCounters = 8;
 
+// QueryBuffers::flags
+constexpr int kQueryFlagForceRescan = 1;  // exact re-scan for every query (tests)
+constexpr int kQueryFlagStream = 2;       // staging-free stream kernel
+constexpr int kQueryFlagTile = 4;         // LDS-staged tile kernel, row walk
+constexpr int kQueryFlagLane = 8;         // LDS-staged tile kernel, lane walk (default; env KN_QUERY_ALGO)
+// Second, wider exact re-rank window (query.hip kWin2): for point sets with many exactly equal
+// distances (lattice-like / symmetric samplings), whose truncated keys run longer than the
+// default window and would otherwise take the wave-serial cooperative sort. Costs ~3 % (900K
+// K=16) to 15 % (100K) where it is not needed, so callers set it from the previous solve's
+// counters[3] (cooperative finishes; kn::Engine: more than 1/64 of the queries).
+constexpr int kQueryFlagWide = 16;
+
 struct BuildBuffers {
     // inputs
     const float* points;      // N x 3 floats (AoS, 12-byte stride)
@@ -128,8 +140,7 @@ struct QueryBuffers {
     int halo;
     int lds_capacity;         // points staged per workgroup (power of two)
     int use_tiles;            // 0: exact ring walk for every query (debug / reference path)
-    int flags;                // 1: force the exact re-scan for every query (tests); 2: stream kernel;
-                              // 4: LDS-staged tile kernel (neither: env KN_QUERY_ALGO / default)
+    int flags;                // kQueryFlag* below
     int counters_zeroed;      // 1: the preceding build zeroed `counters` (no memset here)
     int exact_grid;           // workgroups of the fallback launch; 0 = default (sized for long
                               // lists). The engine passes a small grid when the previous solve's

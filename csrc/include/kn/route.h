@@ -139,6 +139,26 @@ hipError_t launch_fwd_pack(const RouteParams* p, int world, int rank, int F, int
 hipError_t launch_fwd_merge(int world, int F, int k, const unsigned* uncert, const unsigned* ucount, int umax,
                             const int* slot_of, const int* back_idx, const float* back_d2, int* idx, float* d2,
                             hipStream_t s);
+// Count-balanced kd splits (parallel/decomposition.py balanced_splits, the same bins and
+// slab / column assignment): the histogram stage of one rank's share. stage 0: x bins (1 row);
+// stage 1: y bins per x slab (px rows, slabs from xs); stage 2: z bins per (x, y) column
+// (px * py rows, columns from xs and ys). The caller sums the ranks' histograms and takes the
+// quantile edges (multi.cpp split_edges), then runs the next stage with them.
+constexpr int kSplitBins = 4096;
+struct SplitHistArgs {
+    float lo[3];
+    float ext[3];  // hi - lo in float32, clamped >= 1e-30
+    int grid[3];
+    int stage;
+    float xs[kRouteMaxWorld + 1];  // xs[0..px] (stages 1, 2)
+    float ys[2 * kRouteMaxWorld];  // ys[ix * (py + 1) + j] (stage 2)
+};
+inline int split_hist_rows(const int g[3], int stage) { return stage == 0 ? 1 : stage == 1 ? g[0] : g[0] * g[1]; }
+// scratch words launch_split_hist needs (per-block partial histograms)
+size_t split_hist_scratch_words(int n, const int grid[3], int stage);
+// hist: split_hist_rows x kSplitBins uint32, overwritten (stream-ordered, no host sync)
+hipError_t launch_split_hist(const float* pts, int n, const SplitHistArgs& a, unsigned* hist, unsigned* scratch,
+                             hipStream_t s);
 hipError_t debug_words_route(unsigned out[4], bool reset);
 
 }  // namespace kn

@@ -161,9 +161,31 @@ unsigned int *kn_get_neighbors_multi(kn_multi *m);  /* N x K original ids, row =
 float *kn_get_distances_multi(kn_multi *m);         /* N x K squared distances */
 kn_status kn_get_multi_info(kn_multi *m, int *ranks, int *rounds, int *halo_points, int *uses_rccl);
 void kn_free_multi(kn_multi **m);
+/* Options of the multi-GPU solve (kn_default_multi_options(); set before kn_solve_multi). */
+typedef struct {
+    double halo_factor; /* halo send width in expected K-th neighbour radii of the whole cloud (2.5) */
+    int balance;        /* 1: count-balanced kd rank boxes (default), 0: equal-volume boxes          */
+    int forward;        /* 1: uncertified queries answered by query forwarding (default),
+                           0: a halo-doubling round per uncertified step                           */
+    int max_rounds;     /* halo growth rounds at most (8)                                            */
+} kn_multi_options;
+kn_multi_options kn_default_multi_options(void);
+kn_status kn_set_multi_options(kn_multi *m, const kn_multi_options *o);
+/* New coordinates of the same N points (the next kn_solve_multi re-routes; buffers are kept). */
+kn_status kn_update_multi(kn_multi *m, const kn_float3 *points);
+typedef struct {
+    int ranks, rounds, halo_points;
+    int forwarded;          /* uncertified queries answered by query forwarding              */
+    int uses_rccl, balanced;
+    int min_owned, max_owned;  /* owned points per rank                                    */
+    int device_allocations; /* device allocations made by the last solve (0 once buffers fit) */
+    float ms_total;         /* host wall time of the last kn_solve_multi                      */
+} kn_multi_stats;
+kn_status kn_get_multi_stats(kn_multi *m, kn_multi_stats *out);
 
 /* ABI self-check for bindings (ctypes, other languages): sizeof of the public structs as
- * compiled into the library. which: 0 kn_config, 1 kn_problem, 2 kn_stats. */
+ * compiled into the library. which: 0 kn_config, 1 kn_problem, 2 kn_stats, 3 kn_multi_options,
+ * 4 kn_multi_stats. */
 size_t kn_struct_size(int which);
 
 #ifdef __cplusplus

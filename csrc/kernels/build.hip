@@ -20,6 +20,23 @@
 #include "kn/route.h"
 #include "kn/wave.h"
 
+// A/B knobs of round-3 build variants (scripts/ab_build.py, profiles/ab_r3_build.jsonl; eager
+// C.build, 900K K=16 / 12.5M):
+//  * KN_BUILD_BATCH: bucket count / scatter load 4 points per thread before their LDS atomics
+//    (3 float4 loads at a 48-B lane stride): 900K +2.1 us, 12.5M -1 % -> off
+//  * KN_SORT_REGS: the bucket sort keeps its points in registers between its two passes:
+//    900K -0.3 us, 12.5M -1.3 % -> on
+//  * KN_BBOX_THREADS 1024 (one float4 triple per thread): 900K +2.0 us -> 256
+#ifndef KN_BUILD_BATCH
+#define KN_BUILD_BATCH 0
+#endif
+#ifndef KN_SORT_REGS
+#define KN_SORT_REGS 1
+#endif
+#ifndef KN_BBOX_THREADS
+#define KN_BBOX_THREADS 256
+#endif
+
 namespace kn {
 
 namespace {
@@ -35,7 +52,7 @@ __device__ __forceinline__ float unord_float(unsigned u) {
 // Per-block partial bbox (see launch_bbox_partials). VEC: 4 points = 3 aligned float4 loads
 // per iteration (x0 y0 z0 x1 | y1 z1 x2 y2 | z2 x3 y3 z3); needs a 16-B aligned base.
 template <bool VEC>
-__global__ __launch_bounds__(256) void bbox_partials_kernel(const float* __restrict__ pts, int n,
+__global__ __launch_bounds__(KN_BBOX_THREADS) void bbox_partials_kernel(const float* __restrict__ pts, int n,
                                                             unsigned* __restrict__ partials) {
     float mn[3] = {INFINITY, INFINITY, INFINITY};
     float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -58,7 +75,7 @@ __global__ __launch_bounds__(256) void bbox_partials_kernel(const float* __restr
     for (int i = i0; i < n; i += nth) {
         acc(0, pts[3 * (size_t)i]); acc(1, pts[3 * (size_t)i + 1]); acc(2, pts[3 * (size_t)i + 2]);
     }
-    __shared__ unsigned red[6][4];
+    __shared__ unsigned red[6][16];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -322,20 +339,47 @@ inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 size_t scan_block_count(int num_cells) { return cdiv((size_t)num_cells, kScanItems); }
 
 int bbox_block_count(int n) {
-    return std::max(1, std::min((int)cdiv((size_t)std::max(n, 0), 256 * 8), kBBoxBlocks));
+    return std::max(1, std::min((int)cdiv((size_t)std::max(n, 0), KN_BBOX_THREADS == 1024 ? 1024 * 4 : 256 * 8),
+                                kBBoxBlocks));
 }
 
 hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int grid = bbox_block_count(n);
     if ((reinterpret_cast<uintptr_t>(pts) & 15u) == 0)
-        bbox_partials_kernel<true><<<grid, 256, 0, s>>>(pts, n, partials);
+        bbox_partials_kernel<true><<<grid, KN_BBOX_THREADS, 0, s>>>(pts, n, partials);
     else
-        bbox_partials_kernel<false><<<grid, 256, 0, s>>>(pts, n, partials);
+        bbox_partials_kernel<false><<<grid, KN_BBOX_THREADS, 0, s>>>(pts, n, partials);
     return hipGetLastError();
 }
 
 // ---- bucketed binning ---------------------------------------------------------------
+// A streaming block's points [i0, i1) (i0 a multiple of 4), 4 per thread and pass: thread t
+// takes points i0 + 4 (t + j blockDim) .. +3 -- 3 aligned float4 loads when the base is 16-B
+// aligned and the group is whole -- so every load of a pass is in flight before the first LDS
+// atomic (the compiler does not hoist global loads over LDS atomics by itself).
+struct Pts4 {
+    float p[4][3];
+    int i;  // first point index; points i..i+3 valid below `lim`
+};
+__device__ __forceinline__ void load_pts4(const float* __restrict__ pts, int i, int i1, bool vec, Pts4& q) {
+    q.i = i;
+    if (vec && i + 4 <= i1) {
+        const float4* p4 = reinterpret_cast<const float4*>(pts + 3 * (size_t)i);
+        const float4 a = p4[0], b = p4[1], c = p4[2];
+        q.p[0][0] = a.x; q.p[0][1] = a.y; q.p[0][2] = a.z;
+        q.p[1][0] = a.w; q.p[1][1] = b.x; q.p[1][2] = b.y;
+        q.p[2][0] = b.z; q.p[2][1] = b.w; q.p[2][2] = c.x;
+        q.p[3][0] = c.y; q.p[3][1] = c.z; q.p[3][2] = c.w;
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const size_t j = 3 * (size_t)min(i + u, i1 - 1);
+            q.p[u][0] = pts[j]; q.p[u][1] = pts[j + 1]; q.p[u][2] = pts[j + 2];
+        }
+    }
+}
+
 // A1: per-(bucket, block) counts with LDS atomics, table column = bucket (bucket-major, so the
 // exclusive scan of the table gives every block its write offset inside every bucket).
 __global__ __launch_bounds__(1024) void bucket_count_kernel(const float* __restrict__ pts, int n, GeomSrc src,
@@ -360,10 +404,21 @@ __global__ __launch_bounds__(1024) void bucket_count_kernel(const float* __restr
     __syncthreads();
     const GridGeom g = gs;
     const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
+#if KN_BUILD_BATCH
+    const bool vec = (reinterpret_cast<uintptr_t>(pts) & 15u) == 0;
+    for (int i = i0 + 4 * threadIdx.x; i < i1; i += 4 * blockDim.x) {
+        Pts4 q;
+        load_pts4(pts, i, i1, vec, q);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i + u < i1) atomicAdd(&hist[cell_of(g, q.p[u]) >> shift], 1);
+    }
+#else
     for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
         atomicAdd(&hist[cell_of(g, p) >> shift], 1);
     }
+#endif
     __syncthreads();
     for (int j = threadIdx.x; j < nbuckets; j += blockDim.x) table[(size_t)j * nblocks + blockIdx.x] = hist[j];
 }
@@ -393,11 +448,28 @@ __global__ __launch_bounds__(1024) void bucket_scatter_kernel(const float* __res
     __syncthreads();
     const GridGeom g = *gp;
     const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
+#if KN_BUILD_BATCH
+    const bool vec = (reinterpret_cast<uintptr_t>(pts) & 15u) == 0;
+    for (int i = i0 + 4 * threadIdx.x; i < i1; i += 4 * blockDim.x) {
+        Pts4 q;
+        load_pts4(pts, i, i1, vec, q);
+        int pos[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            pos[u] = (i + u < i1) ? atomicAdd(&cur[cell_of(g, q.p[u]) >> shift], 1) : -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (pos[u] >= 0)
+                tmp[KN_IDX(pos[u], n, 104)] =
+                    make_float4(q.p[u][0], q.p[u][1], q.p[u][2], __uint_as_float((unsigned)(i + u)));
+    }
+#else
     for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
         const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
         const int pos = atomicAdd(&cur[cell_of(g, p) >> shift], 1);
         tmp[KN_IDX(pos, n, 104)] = make_float4(p[0], p[1], p[2], __uint_as_float((unsigned)i));
     }
+#endif
 }
 
 // B: one workgroup per bucket: LDS histogram of its 2^shift cells, LDS exclusive scan ->
@@ -438,9 +510,26 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
     __syncthreads();
     const int bs = seg[0], be = seg[1];
     const GridGeom g = *gp;
-    for (int k = bs + threadIdx.x; k < be; k += 256) {
-        const float4 v = tmp[KN_IDX(k, n, 105)];
-        const float p[3] = {v.x, v.y, v.z};
+    // the bucket's first R x 256 points stay in registers between the two passes (a bucket holds
+    // ~2^shift x points-per-cell points: all of them at the usual densities); all R loads are
+    // issued before the first LDS atomic
+    constexpr int R = KN_SORT_REGS ? 4 : 0;
+    float4 v[R > 0 ? R : 1];
+    int cl[R > 0 ? R : 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int k = bs + threadIdx.x + r * 256;
+        v[r] = k < be ? tmp[KN_IDX(k, n, 105)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const float p[3] = {v[r].x, v[r].y, v[r].z};
+        cl[r] = bs + threadIdx.x + r * 256 < be ? KN_IDX(cell_of(g, p) - c0, cells, 106) : -1;
+        if (cl[r] >= 0) atomicAdd(&cur[cl[r]], 1);
+    }
+    for (int k = bs + threadIdx.x + R * 256; k < be; k += 256) {
+        const float4 w = tmp[KN_IDX(k, n, 105)];
+        const float p[3] = {w.x, w.y, w.z};
         atomicAdd(&cur[KN_IDX(cell_of(g, p) - c0, cells, 106)], 1);
     }
     __syncthreads();
@@ -463,12 +552,9 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
     }
     if (b == nbuckets - 1 && threadIdx.x == 0) cell_start[num_cells] = n;
     __syncthreads();
-    for (int k = bs + threadIdx.x; k < be; k += 256) {
-        const float4 v = tmp[KN_IDX(k, n, 105)];
-        const float p[3] = {v.x, v.y, v.z};
-        const int pos = atomicAdd(&cur[cell_of(g, p) - c0], 1);
-        const unsigned local = __float_as_uint(v.w);
-        float4 o = v;
+    auto place = [&](const float4& w, int pos) {
+        const unsigned local = __float_as_uint(w.w);
+        float4 o = w;
         if (gids) {  // global-id mode (see BuildBuffers::gids)
             // (A/B: carrying the ids through the bucket scatter instead -- a second scattered store
             // stream -- cost 4 us more at 900K than this gather)
@@ -477,6 +563,140 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
         }
         sorted[KN_IDX(pos, n, 107)] = o;
         perm[pos] = local;
+    };
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (cl[r] >= 0) place(v[r], atomicAdd(&cur[cl[r]], 1));
+    for (int k = bs + threadIdx.x + R * 256; k < be; k += 256) {
+        const float4 w = tmp[KN_IDX(k, n, 105)];
+        const float p[3] = {w.x, w.y, w.z};
+        place(w, atomicAdd(&cur[cell_of(g, p) - c0], 1));
+    }
+}
+
+// ---- small clouds: the whole build in ONE workgroup (no inter-kernel round trips) ----------------
+// For small clouds the multi-kernel build is latency-bound (pts20K: 5 kernels, ~30 us for ~1 us of
+// bandwidth). One 1024-thread workgroup instead: every thread loads its <= kSmallP points ONCE
+// (all loads in flight together) and keeps them in registers through the bbox (block
+// reduction, the same geometry function as the multi-block path), the LDS cell histogram and
+// scan (-> cell_start) and the LDS-cursor scatter of point indices into an LDS slot array; each
+// cell's slots are then ordered by original index in LDS (thread per cell) and the rows are
+// written with one gather. The layout is that of the deterministic multi-kernel build, so the
+// queries see identical input. LDS: C counts + n slots (small_build_fits).
+constexpr int kSmallP = 24;                  // points per thread (registers): n <= 24576
+constexpr int kSmallLdsWords = 150 * 256;    // 150 KB of the 160 KB LDS
+bool small_build_fits(int n, int C) {
+    return n > 0 && n <= 1024 * kSmallP && (size_t)C + (size_t)n <= (size_t)kSmallLdsWords;
+}
+__global__ __launch_bounds__(1024) void small_build_kernel(const float* __restrict__ pts, int n, int d0, int d1, int d2,
+                                                           int use_box, float bl0, float bl1, float bl2, float bh0,
+                                                           float bh1, float bh2, GridGeom* __restrict__ geom,
+                                                           int* __restrict__ cell_start, float4* __restrict__ sorted,
+                                                           unsigned* __restrict__ perm, unsigned* __restrict__ zero_words,
+                                                           int n_zero) {
+    extern __shared__ int sm[];
+    const int C = d0 * d1 * d2;
+    int* cnt = sm;      // C: counts, then cursors
+    int* slot = sm + C; // n: original index of every stored slot
+    __shared__ unsigned red[6][16];
+    __shared__ int wsum[16];
+    __shared__ GridGeom sg;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (t < n_zero) zero_words[t] = 0u;
+    float p[kSmallP][3];
+#pragma unroll
+    for (int j = 0; j < kSmallP; ++j) {
+        const int i = min(t + 1024 * j, n - 1);  // clamped: duplicates of the last point are harmless
+        p[j][0] = pts[3 * (size_t)i];
+        p[j][1] = pts[3 * (size_t)i + 1];
+        p[j][2] = pts[3 * (size_t)i + 2];
+    }
+    for (int c = t; c < C; c += 1024) cnt[c] = 0;
+    // 1. bbox -> geometry
+    if (!use_box) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < kSmallP; ++j) { mn = fminf(mn, p[j][a]); mx = fmaxf(mx, p[j][a]); }
+            const unsigned lo = wave_max_u32(~ord_float(mn)), hi = wave_max_u32(ord_float(mx));
+            if (lane == 0) { red[a][wid] = lo; red[3 + a][wid] = hi; }
+        }
+    }
+    __syncthreads();
+    if (t == 0) {
+        float lo[3], hi[3];
+        const int dims[3] = {d0, d1, d2};
+        if (use_box) {
+            lo[0] = bl0; lo[1] = bl1; lo[2] = bl2; hi[0] = bh0; hi[1] = bh1; hi[2] = bh2;
+        } else {
+            for (int a = 0; a < 3; ++a) {
+                unsigned wl = 0, wh = 0;
+                for (int w = 0; w < 16; ++w) { wl = max(wl, red[a][w]); wh = max(wh, red[3 + a][w]); }
+                lo[a] = unord_float(~wl);
+                hi[a] = unord_float(wh);
+            }
+        }
+        write_geom(&sg, lo, hi, dims);
+        *geom = sg;
+    }
+    __syncthreads();
+    const GridGeom g = sg;
+    // 2. histogram (cells stay in registers)
+    int cl[kSmallP];
+#pragma unroll
+    for (int j = 0; j < kSmallP; ++j) {
+        cl[j] = t + 1024 * j < n ? cell_of(g, p[j]) : -1;
+        if (cl[j] >= 0) atomicAdd(&cnt[cl[j]], 1);
+    }
+    __syncthreads();
+    // 3. exclusive scan (each thread a contiguous run of cells) -> cell_start, cursors
+    const int per = (C + 1023) / 1024, c0 = min(C, t * per), c1 = min(C, c0 + per);
+    int s = 0;
+    for (int c = c0; c < c1; ++c) s += cnt[c];
+    const int incl = wave_inclusive_scan_add(s);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int off = incl - s;
+    for (int w = 0; w < wid; ++w) off += wsum[w];
+    for (int c = c0; c < c1; ++c) {
+        const int v = cnt[c];
+        cell_start[c] = off;
+        cnt[c] = off;
+        off += v;
+    }
+    if (t == 1023) cell_start[C] = off;
+    __syncthreads();
+    // 4. scatter of indices (LDS cursors)
+#pragma unroll
+    for (int j = 0; j < kSmallP; ++j)
+        if (cl[j] >= 0) slot[atomicAdd(&cnt[cl[j]], 1)] = t + 1024 * j;
+    __syncthreads();
+    // 5. in-cell order by original index: cnt[c] is now the cell's end, its start the previous
+    //    cell's end (insertion sort in LDS; cells hold a few points)
+    for (int c = t; c < C; c += 1024) {
+        const int a = c ? cnt[c - 1] : 0, b = cnt[c];
+        for (int i = a + 1; i < b; ++i) {
+            const int key = slot[i];
+            int j = i - 1;
+            while (j >= a && slot[j] > key) {
+                slot[j + 1] = slot[j];
+                --j;
+            }
+            slot[j + 1] = key;
+        }
+    }
+    __syncthreads();
+    // 6. rows: one gather (all loads of a thread in flight together)
+#pragma unroll
+    for (int j = 0; j < kSmallP; ++j) {
+        const int pos = t + 1024 * j;
+        if (pos < n) {
+            const int i = slot[pos];
+            sorted[pos] = make_float4(pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2],
+                                      __uint_as_float((unsigned)i));
+            perm[pos] = (unsigned)i;
+        }
     }
 }
 
@@ -517,6 +737,24 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         const char* v = std::getenv("KN_BUILD_ALGO");
         return v && std::atoi(v) == 1;
     }();
+    const char* small_env = std::getenv("KN_SMALL_BUILD");  // read per launch: tests A/B both paths
+    const bool no_small = small_env && std::atoi(small_env) == 0;
+    if (!no_small && !force_atomic && small_build_fits(n, C) && !b.gids && b.n_zero_words <= 1024) {
+        // one workgroup, one launch (deterministic layout whatever b.deterministic says)
+        static const bool attr = [] {
+            // dynamic + static LDS may not pass 160 KB: the kernel's static words (~0.5 KB) come
+            // off the opt-in (asking for the whole 160 KB is rejected and leaves the 64 KB default)
+            (void)hipFuncSetAttribute((const void*)small_build_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      kSmallLdsWords * 4);
+            return true;
+        }();
+        (void)attr;
+        small_build_kernel<<<1, 1024, ((size_t)C + (size_t)n) * sizeof(int), s>>>(
+            b.points, n, b.dims[0], b.dims[1], b.dims[2], b.use_box, b.box_lo[0], b.box_lo[1], b.box_lo[2], b.box_hi[0],
+            b.box_hi[1], b.box_hi[2], b.geom, b.cell_start, b.sorted, b.perm, b.zero_words,
+            b.zero_words ? b.n_zero_words : 0);
+        return hipGetLastError();
+    }
     if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp)) {
         // geometry folded into bucket_count; scan top level folded into its consumers
         GeomSrc src{};

@@ -109,6 +109,19 @@ struct TileArgs {
 #define KN_WIN 1
 #endif
 constexpr int kWin = KN_WIN;  // exact re-rank window: same-bucket neighbours within +-kWin
+// Second, wider window for the lanes whose bucket runs overflow +-kWin but fit +-kWin2 (point
+// sets with many exactly equal distances -- symmetric / lattice-like samplings: pts20K has runs
+// of >= 3 equal buckets in 55 % of its K=8 queries, and sending them all to the wave-serial
+// cooperative sort made its query kernel 5x slower). The lanes run one of the two passes each
+// (divergent, but in parallel), only runs longer than kWin2 + 1 go cooperative. 0 = off.
+#ifndef KN_WIN2
+#define KN_WIN2 4
+#endif
+constexpr int kWin2 = KN_WIN2 > kWin ? KN_WIN2 : 0;
+template <int V>
+struct IntC {
+    static constexpr int value = V;
+};
 // Round-3 A/Bs of the lane walk that LOST against this kernel (900K uniform, interleaved in
 // process, identical rows; profiles/ab_r3_lane_variants.jsonl, profiles/ab_r3_collect.jsonl):
 //  * collect-then-select (d2-only scan + per-lane LDS queue of candidate slots, bulk med3
@@ -122,13 +135,16 @@ constexpr int kWin = KN_WIN;  // exact re-rank window: same-bucket neighbours wi
 //    tile density): K=16 +6 %, K=50 +8 %.
 
 constexpr int kCoopCap = 128;  // per-wave LDS buffer of the cooperative re-scan (u64 keys)
-constexpr int kQueryForceRescan = 1;
+constexpr int kQueryForceRescan = kQueryFlagForceRescan;
 // fallback-list entry flag: the query's output row holds K real candidates (their K-th squared
 // distance is an upper bound the exact kernel seeds its threshold with); stored indices < 2^31
 constexpr unsigned kSeedBit = 0x80000000u;
-constexpr int kQueryAlgoStream = 2;
-constexpr int kQueryAlgoTile = 4;
-constexpr int kQueryAlgoLane = 8;
+constexpr int kQueryAlgoStream = kQueryFlagStream;
+constexpr int kQueryAlgoTile = kQueryFlagTile;
+constexpr int kQueryAlgoLane = kQueryFlagLane;
+// lane walk with the second re-rank window (kQueryFlagWide; profiles/ab_r3_win2.jsonl: pts20K
+// K=8 query 0.19 -> 0.07 ms with it, 900K uniform K=16 +3 %, 100K +15 % without need)
+constexpr int kQueryWide = kQueryFlagWide;
 
 // Shared device helpers (key packing, med3 top-K insertion, id modes, wave sort): kn/knn_device.h
 
@@ -170,7 +186,7 @@ __device__ unsigned long long g_phase[kPhN];
 // block -- centre-out over the (2H+1)^2 row offsets around its cell, x-range cut by its own
 // bound -- as a divergent loop with per-lane LDS gathers. ~90 candidates per query instead of
 // the ~535 the union stream feeds every lane, at the price of divergent trip counts.
-template <int KT, int M, bool LANE>
+template <int KT, int M, bool LANE, bool WIDE = false>
 __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     // K + M margin slots + 1: the query itself is not filtered in the hot loop (that cost 3
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
@@ -660,23 +676,34 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         // duplication) take the wave-cooperative sort below.
         const unsigned qs = (unsigned)qslot;
         auto kvalid = [&](unsigned key) { return key != SENT && (key & MASK) != qs; };
-        bool ovf = (a.flags & kQueryForceRescan) != 0;
+        const bool force = (a.flags & kQueryForceRescan) != 0;
+        bool ovf = force;
+        // wider-window overflow (== ovf when the second window is off)
+        bool ovf2 = force;
         int nfound = 0;
 #pragma unroll
         for (int j = 0; j + kWin + 1 < KM; ++j)
             ovf |= keys[j + kWin + 1] != SENT && ((keys[j] ^ keys[j + kWin + 1]) & HIMASK) == 0u;
+        if constexpr (WIDE && kWin2 > 0) {
+#pragma unroll
+            for (int j = 0; j + kWin2 + 1 < KM; ++j)
+                ovf2 |= keys[j + kWin2 + 1] != SENT && ((keys[j] ^ keys[j + kWin2 + 1]) & HIMASK) == 0u;
+        } else {
+            ovf2 = ovf;
+        }
         const unsigned orow = act ? w_row(a, qorig, qsidx) : 0u;
         const size_t row = (size_t)orow * (size_t)k;
         float dK2 = INFINITY;
         // precision reference taken before the window pass consumes the keys
         const unsigned last = keys[KM - 1];
-        if (!ovf) {
+        auto window_pass = [&](auto wc) {
+            constexpr int W = decltype(wc)::value;
             // Rolled loop over the kept keys with constant register indices only: the key array
             // shifts down one slot per step (KM moves) and the window rotates, so no unrolled
             // straight-line code gives the scheduler room to pull every entry's LDS read and
             // compare forward (fully unrolled, K=50 needed 214 VGPRs; rolled it stays near the
             // scan loop's own pressure).
-            constexpr int NW = 2 * kWin + 1;
+            constexpr int NW = 2 * W + 1;
             float wd[NW];
             unsigned wi[NW], wk[NW];
             auto ld = [&](unsigned key, int t) {
@@ -688,39 +715,44 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 wi[t] = v ? w_id(a, __float_as_uint(p.w)) : SENT;
             };
 #pragma unroll
-            for (int t = 0; t < NW; ++t) ld((t >= kWin && t - kWin < KM) ? keys[t - kWin] : SENT, t);
+            for (int t = 0; t < NW; ++t) ld((t >= W && t - W < KM) ? keys[t - W] : SENT, t);
             int base = 0;
 #pragma unroll 1
             for (int j = 0; j < KM; ++j) {
-                const bool vj = wk[kWin] != SENT;
+                const bool vj = wk[W] != SENT;
                 int pos = base;
 #pragma unroll
                 for (int t = 0; t < NW; ++t) {
-                    if (t == kWin) continue;
+                    if (t == W) continue;
                     // branch-free: bitwise &/| (short-circuit forms compile to exec-mask branches)
-                    const int same = (int)(wk[t] != SENT) & (int)(((wk[t] ^ wk[kWin]) & HIMASK) == 0u);
-                    const float da = t > kWin ? wd[t] : wd[kWin], db = t > kWin ? wd[kWin] : wd[t];
-                    const unsigned ia = t > kWin ? wi[t] : wi[kWin], ib = t > kWin ? wi[kWin] : wi[t];
+                    const int same = (int)(wk[t] != SENT) & (int)(((wk[t] ^ wk[W]) & HIMASK) == 0u);
+                    const float da = t > W ? wd[t] : wd[W], db = t > W ? wd[W] : wd[t];
+                    const unsigned ia = t > W ? wi[t] : wi[W], ib = t > W ? wi[W] : wi[t];
                     const int lt = (int)(da < db) | ((int)(da == db) & (int)(ia < ib));
-                    pos += (t > kWin ? 1 : -1) * (same & lt);
+                    pos += (t > W ? 1 : -1) * (same & lt);
                 }
                 if (vj && act && pos < k) {
                     const size_t o = KN_IDX(row + pos, (size_t)a.n_queries * k, 209);
-                    a.out_idx[o] = out_id(a, wi[kWin]);
-                    if (a.out_dist) a.out_dist[o] = wd[kWin];
+                    a.out_idx[o] = out_id(a, wi[W]);
+                    if (a.out_dist) a.out_dist[o] = wd[W];
                 }
-                dK2 = (vj && pos == k - 1) ? wd[kWin] : dK2;
+                dK2 = (vj && pos == k - 1) ? wd[W] : dK2;
                 base += vj ? 1 : 0;
 #pragma unroll
                 for (int t = 0; t + 1 < NW; ++t) { wk[t] = wk[t + 1]; wd[t] = wd[t + 1]; wi[t] = wi[t + 1]; }
-                // entry j + kWin + 1 sits at keys[kWin + 1] after j + 1 shifts
-                ld(KM > kWin + 1 ? keys[kWin + 1 < KM ? kWin + 1 : KM - 1] : SENT, NW - 1);
+                // entry j + W + 1 sits at keys[W + 1] after j + 1 shifts
+                ld(KM > W + 1 ? keys[W + 1 < KM ? W + 1 : KM - 1] : SENT, NW - 1);
 #pragma unroll
                 for (int t = 0; t + 1 < KM; ++t) keys[t] = keys[t + 1];
                 keys[KM - 1] = SENT;
             }
             nfound = base;
+        };
+        if (!ovf) window_pass(IntC<kWin>{});
+        if constexpr (WIDE && kWin2 > 0) {
+            if (ovf && !ovf2) window_pass(IntC<kWin2>{});
         }
+        ovf = ovf2;  // what is left for the cooperative sort
         // Wave-cooperative finish of ONE lane's query at a time (rare paths): the wave holds
         // 64-bit (d2 bits, id) keys, E per lane, bitonic-sorts them across lanes and writes the
         // lane's row; the lane gets its exact K-th distance and found count back.
@@ -1681,12 +1713,16 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M, true>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M, true, true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             }
             attr_set = true;
         }
         if constexpr (KT <= 64) {
-            if (query_algo(q.flags, q.k) == kAlgoLane) knn_tile_kernel<KT, M, true><<<nt, kWG, lds, s>>>(a);
-            else knn_tile_kernel<KT, M, false><<<nt, kWG, lds, s>>>(a);
+            const bool wide = kWin2 > 0 && (q.flags & kQueryWide);
+            if (query_algo(q.flags, q.k) != kAlgoLane) knn_tile_kernel<KT, M, false><<<nt, kWG, lds, s>>>(a);
+            else if (wide) knn_tile_kernel<KT, M, true, true><<<nt, kWG, lds, s>>>(a);
+            else knn_tile_kernel<KT, M, true><<<nt, kWG, lds, s>>>(a);
         }
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -561,6 +561,60 @@ __global__ __launch_bounds__(256) void fwd_merge_kernel(int world, int F, int k,
     }
 }
 
+// ---- count-balanced split histograms (launch_split_hist) --------------------------------
+__device__ __forceinline__ int split_bin_row(const SplitHistArgs& a, float x, float y, float z, int* row) {
+    const int px = a.grid[0], py = a.grid[1];
+    int ix = 0, iy = 0;
+    if (a.stage >= 1)
+        for (int j = 1; j < px; ++j) ix += x >= a.xs[j] ? 1 : 0;
+    if (a.stage >= 2)
+        for (int j = 1; j < py; ++j) iy += y >= a.ys[ix * (py + 1) + j] ? 1 : 0;
+    *row = a.stage == 0 ? 0 : a.stage == 1 ? ix : ix + px * iy;
+    const int ax = a.stage;
+    const float v = ax == 0 ? x : ax == 1 ? y : z;
+    // (p - lo) / ext * B, float32 as balanced_splits
+    const float f = __fmul_rn(__fdiv_rn(__fsub_rn(v, a.lo[ax]), a.ext[ax]), (float)kSplitBins);
+    const int b = (int)floorf(f);
+    return b < 0 ? 0 : (b > kSplitBins - 1 ? kSplitBins - 1 : b);
+}
+
+constexpr int kSplitLdsBins = 16384;  // 64 KB of LDS: per-block partials up to 4 rows
+
+__global__ __launch_bounds__(1024) void split_hist_lds_kernel(const float* __restrict__ pts, int n, SplitHistArgs a,
+                                                              int bins, unsigned* __restrict__ part) {
+    __shared__ unsigned h[kSplitLdsBins];
+    for (int j = threadIdx.x; j < bins; j += 1024) h[j] = 0u;
+    __syncthreads();
+    const int per = (n + gridDim.x - 1) / gridDim.x, i0 = blockIdx.x * per, i1 = min(n, i0 + per);
+    for (int i = i0 + threadIdx.x; i < i1; i += 1024) {
+        int row;
+        const int b = split_bin_row(a, pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2], &row);
+        atomicAdd(&h[row * kSplitBins + b], 1u);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < bins; j += 1024) part[(size_t)blockIdx.x * bins + j] = h[j];
+}
+
+__global__ __launch_bounds__(256) void split_hist_sum_kernel(const unsigned* __restrict__ part, int nb, int bins,
+                                                             unsigned* __restrict__ hist) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= bins) return;
+    unsigned s = 0;
+    for (int b = 0; b < nb; ++b) s += part[(size_t)b * bins + j];
+    hist[j] = s;
+}
+
+__global__ __launch_bounds__(256) void split_hist_global_kernel(const float* __restrict__ pts, int n, SplitHistArgs a,
+                                                                unsigned* __restrict__ hist) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        int row;
+        const int b = split_bin_row(a, pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2], &row);
+        atomicAdd(&hist[(size_t)row * kSplitBins + b], 1u);
+    }
+}
+
+int split_hist_blocks(int n) { return std::max(1, std::min((int)cdiv((size_t)n, 8192), 128)); }
+
 }  // namespace
 
 int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
@@ -657,6 +711,30 @@ hipError_t launch_fwd_merge(int world, int F, int k, const unsigned* uncert, con
     if (umax > 0)
         fwd_merge_kernel<<<std::max(1u, std::min(cdiv((size_t)umax, 256), 64u)), 256, 0, s>>>(
             world, F, k, uncert, ucount, umax, slot_of, back_idx, back_d2, idx, d2);
+    return hipGetLastError();
+}
+
+size_t split_hist_scratch_words(int n, const int grid[3], int stage) {
+    const int bins = split_hist_rows(grid, stage) * kSplitBins;
+    return bins <= kSplitLdsBins ? (size_t)split_hist_blocks(n) * bins : 1;
+}
+
+hipError_t launch_split_hist(const float* pts, int n, const SplitHistArgs& a, unsigned* hist, unsigned* scratch,
+                             hipStream_t s) {
+    // px * py <= 64 keeps xs / ys (px * (py + 1) <= 128) and the rows in range
+    if (a.stage < 0 || a.stage > 2 || a.grid[0] < 1 || a.grid[1] < 1 || a.grid[0] * a.grid[1] > kRouteMaxWorld)
+        return hipErrorInvalidValue;
+    const int bins = split_hist_rows(a.grid, a.stage) * kSplitBins;
+    if (n <= 0) return hipMemsetAsync(hist, 0, (size_t)bins * sizeof(unsigned), s);
+    if (bins <= kSplitLdsBins) {
+        const int nb = split_hist_blocks(n);
+        split_hist_lds_kernel<<<nb, 1024, 0, s>>>(pts, n, a, bins, scratch);
+        split_hist_sum_kernel<<<(int)cdiv((size_t)bins, 256), 256, 0, s>>>(scratch, nb, bins, hist);
+    } else {
+        hipError_t e = hipMemsetAsync(hist, 0, (size_t)bins * sizeof(unsigned), s);
+        if (e != hipSuccess) return e;
+        split_hist_global_kernel<<<std::min((int)cdiv((size_t)n, 256), 2048), 256, 0, s>>>(pts, n, a, hist);
+    }
     return hipGetLastError();
 }
 

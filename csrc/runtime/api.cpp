@@ -255,6 +255,8 @@ size_t kn_struct_size(int which) {
         case 0: return sizeof(kn_config);
         case 1: return sizeof(kn_problem);
         case 2: return sizeof(kn_stats);
+        case 3: return sizeof(kn_multi_options);
+        case 4: return sizeof(kn_multi_stats);
         default: return 0;
     }
 }

@@ -174,6 +174,8 @@ QueryBuffers Engine::query_buffers() const {
     q.use_tiles = cfg_.use_tiles;
     // fallback grid from the last observed fallback count: 256 workgroups when it was short
     q.exact_grid = last_fallback_ < 4096u ? 256 : 0;
+    // many cooperative re-rank finishes last time (exactly equal distances): the wide window
+    if ((unsigned long long)last_coop_ * 64 > (unsigned long long)n_) q.flags |= kQueryFlagWide;
     return q;
 }
 
@@ -355,9 +357,12 @@ kn_status Engine::solve() {
     (void)hipEventRecord(ev_[3], stream_);
     if ((st = check(hipEventSynchronize(ev_[3]), "solve sync")) != KN_OK) return st;
     (void)hipEventElapsedTime(&ms_solve_, ev_[2], ev_[3]);
-    // the stream is idle: one word tells the next launches how long the fallback list runs
-    if (hipMemcpy(&last_fallback_, counters_, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess)
-        last_fallback_ = ~0u;
+    // the stream is idle: the counters tell the next launches how long the fallback list runs
+    // and how many queries needed the cooperative re-rank
+    unsigned cw[4] = {~0u, 0, 0, 0};
+    if (hipMemcpy(cw, counters_, sizeof(cw), hipMemcpyDeviceToHost) != hipSuccess) cw[0] = ~0u;
+    last_fallback_ = cw[0];
+    if (!use_tree_) last_coop_ = cw[3];
     if (cfg_.verbose) {
         unsigned c[kNumCounters] = {0};
         (void)hipMemcpy(c, counters_, sizeof(c), hipMemcpyDeviceToHost);

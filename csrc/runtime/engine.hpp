@@ -138,6 +138,7 @@ private:
     bool points3_valid_ = false;
     bool built_ = false, solved_ = false, stored_valid_ = false;
     unsigned last_fallback_ = ~0u;  // fallback-list length of the last eager solve (~0: unknown)
+    unsigned last_coop_ = 0;        // cooperative re-rank finishes of the last eager solve
     bool use_tree_ = false;         // chosen at prepare (EngineConfig::algo)
     bool refined_ = false;          // the occupancy-adaptive grid was refined (saved with the grid)
     void* tree_ws_ = nullptr;

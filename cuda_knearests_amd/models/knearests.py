@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from ..ops import knn_ops as ops
+from ..ops.knn_ops import QUERY_FLAG_WIDE
 from .._ext import load
 from ..utils import get_logger
 
@@ -55,6 +56,7 @@ class KNearests:
         # verbose=True logs the reference's timing lines at WARNING (always shown); otherwise
         # they are INFO records of the "knearests" logger (env KN_LOG=INFO shows them)
         self.verbose = verbose
+        self._qflags = 0  # query flags learned from the last eager solve (wide re-rank window)
         self._lvl = logging.WARNING if verbose else logging.INFO
         self.grid: Optional[ops.Grid] = None
         self.points: Optional[torch.Tensor] = None
@@ -113,11 +115,15 @@ class KNearests:
         t1 = torch.cuda.Event(enable_timing=True)
         t0.record()
         idx, d2, info = ops.query(self.grid, self.k, use_tiles=self.use_tiles,
-                                  with_dist=self.with_distances, return_info=True, algo=self.algo)
+                                  with_dist=self.with_distances, return_info=True, algo=self.algo,
+                                  flags=self._qflags)
         t1.record()
         t1.synchronize()
         self.timings["ms_solve"] = t0.elapsed_time(t1)
         c = info["counters"].cpu()
+        # many cooperative re-rank finishes (exactly equal distances: lattice-like clouds): the
+        # next solves take the wide re-rank window (kn/kernels.h kQueryFlagWide), as kn::Engine
+        self._qflags = QUERY_FLAG_WIDE if int(c[3]) * 64 > self.grid.n else 0
         algo = self.grid.extra.get("algo", "grid") if self.algo == "auto" else self.algo
         self.info = {"exact_path": int(c[0]), "uncertified": int(c[1]), "dense_tiles": int(c[2]), "algo": algo}
         self.neighbors, self.distances = idx, d2
@@ -170,7 +176,8 @@ class KNearests:
         if not capture:
             g = ops.build_grid(pts, self.k, plan=self.plan(pts.size(0)), deterministic=self.deterministic)
             self.neighbors, self.distances = ops.query(g, self.k, use_tiles=self.use_tiles,
-                                                       with_dist=self.with_distances, algo=self.algo)
+                                                       with_dist=self.with_distances, algo=self.algo,
+                                                       flags=self._qflags)
             self.grid = g
             return self
         if self._graph is None or self._graph_n != pts.size(0):
@@ -179,6 +186,7 @@ class KNearests:
                                         True, {"auto": 0, "grid": 1, "tree": 2}[self.algo])
             self._graph_n = pts.size(0)
             self._graph.prepare(pts)  # eager first build: decides the (occupancy-adaptive) grid
+            self._graph.solve()  # eager first solve: its counters pick the captured query variant
         # the engine keeps its own copy of the input, so every step re-uploads (D2D) + replays
         self._graph.prepare_async(pts)
         self._graph.launch_graph(1)

@@ -23,6 +23,9 @@ import torch
 from .._ext import load
 
 INF = float("inf")
+# query flags (kn/kernels.h kQueryFlag*): the wide exact re-rank window, for clouds with many
+# exactly equal distances (KNearests sets it from the previous solve's cooperative re-ranks)
+QUERY_FLAG_WIDE = 16
 
 
 @dataclass

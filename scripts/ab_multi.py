@@ -6,7 +6,7 @@ from cuda_knearests_amd.ops import knn_ops as ops
 from cuda_knearests_amd import utils
 
 var = sys.argv[1]
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 900000
+n0 = int(sys.argv[2]) if len(sys.argv) > 2 else 900000
 ks = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "16,50").split(",")]
 gens = (sys.argv[4] if len(sys.argv) > 4 else "uniform").split(",")
 rounds = int(sys.argv[5]) if len(sys.argv) > 5 else 10
@@ -15,7 +15,12 @@ B = importlib.import_module(f"cuda_knearests_amd._C_{var}")
 dev = torch.device("cuda", 0)
 inf = float("inf")
 for gen in gens:
-    pts = getattr(utils, f"{gen}_cloud")(n, seed=0, device=dev)
+    if gen.startswith("xyz:"):  # a reference-format point file (normalised), e.g. xyz:data/pts20K.xyz
+        from cuda_knearests_amd import read_xyz
+        pts = read_xyz(gen[4:], normalize=True).float().to(dev)
+    else:
+        pts = getattr(utils, f"{gen}_cloud")(n0, seed=0, device=dev)
+    n = pts.size(0)
     for k in ks:
         plan = ops.Plan.auto(n, k)
         s, cs, perm, geom = A.build(pts, plan.dims, True, None)

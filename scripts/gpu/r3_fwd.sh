@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 3: sync-free device forwarding in steady steps + the distributed GPU tests.
+set -o pipefail
+export PYTHONPATH=$PWD
+O=gpurun_out/fwd
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v --timeout 120 --timeout-method thread -k "forwarding" > $O/pytest_fwd.log 2>&1 || { echo FWD_FAIL; tail -40 $O/pytest_fwd.log; exit 1; }
+tail -3 $O/pytest_fwd.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_distributed.py tests/test_capi.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo TESTS_FAIL; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo GPU_FAIL; tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+for v in 1 0; do KN_SMALL_BUILD=$v timeout -k 10 200 python -u bench.py --xyz data/pts20K.xyz --k 8 --steps 200 --warmup 20 > $O/small_$v.json 2>$O/small_$v.err || exit 1; cat $O/small_$v.json; done
+timeout -k 10 200 python -u bench.py --steps 50 --warmup 10 > $O/bench_k16.json 2>$O/bench_k16.err && cat $O/bench_k16.json || exit 1
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run -- python3 $R/bench.py --steps 40 --warmup 5 > $R/$O/prof.log 2>&1 || { echo PROF_FAIL; tail $R/$O/prof.log; exit 1; }
+cd $R
+python scripts/kernel_stats.py $(find $O/prof -name '*.db' | head -1) > $O/kstats.txt 2>&1; head -12 $O/kstats.txt

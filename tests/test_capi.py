@@ -31,6 +31,16 @@ class KnStats(C.Structure):
                 ("ms_solve", C.c_float)]
 
 
+class KnMultiOptions(C.Structure):
+    _fields_ = [("halo_factor", C.c_double), ("balance", C.c_int), ("forward", C.c_int), ("max_rounds", C.c_int)]
+
+
+class KnMultiStats(C.Structure):
+    _fields_ = [("ranks", C.c_int), ("rounds", C.c_int), ("halo_points", C.c_int), ("forwarded", C.c_int),
+                ("uses_rccl", C.c_int), ("balanced", C.c_int), ("min_owned", C.c_int), ("max_owned", C.c_int),
+                ("device_allocations", C.c_int), ("ms_total", C.c_float)]
+
+
 def _lib():
     lib = load_capi()
     lib.kn_default_config.restype = KnConfig
@@ -62,7 +72,7 @@ def test_struct_layout_matches_library():
     """ctypes mirrors == the structs compiled into libknearests.so (drift fails loudly: a short
     KnConfig once let kn_default_config write past the ctypes buffer)."""
     lib = _lib()
-    for which, cls in enumerate((KnConfig, KnProblem, KnStats)):
+    for which, cls in enumerate((KnConfig, KnProblem, KnStats, KnMultiOptions, KnMultiStats)):
         assert lib.kn_struct_size(which) == C.sizeof(cls), cls.__name__
 
 
@@ -184,7 +194,21 @@ def _multi_lib():
     lib.kn_get_distances_multi.argtypes = [C.c_void_p]
     lib.kn_get_multi_info.argtypes = [C.c_void_p] + [C.POINTER(C.c_int)] * 4
     lib.kn_free_multi.argtypes = [C.POINTER(C.c_void_p)]
+    lib.kn_default_multi_options.restype = KnMultiOptions
+    lib.kn_set_multi_options.argtypes = [C.c_void_p, C.POINTER(KnMultiOptions)]
+    lib.kn_update_multi.argtypes = [C.c_void_p, C.c_void_p]
+    lib.kn_get_multi_stats.argtypes = [C.c_void_p, C.POINTER(KnMultiStats)]
     return lib
+
+
+def _multi_rows(lib, m, n, k):
+    libc = C.CDLL(None)
+    gi, gd = lib.kn_get_neighbors_multi(m), lib.kn_get_distances_multi(m)
+    idx = np.ctypeslib.as_array(gi, shape=(n * k,)).reshape(n, k).astype(np.int64).copy()
+    d2 = np.ctypeslib.as_array(gd, shape=(n * k,)).reshape(n, k).copy()
+    libc.free(gi)
+    libc.free(gd)
+    return idx, d2
 
 
 @pytest.mark.gpu
@@ -226,3 +250,74 @@ def test_capi_multi_device(devices):
     _, od = kn.knn_cpu(cloud, k, "kdtree")
     assert torch.equal(torch.from_numpy(d2), od)
     assert_knn_exact(cloud, torch.arange(n), torch.from_numpy(idx), torch.from_numpy(d2), od)
+
+
+@pytest.mark.gpu
+def test_capi_multi_balanced_forwarding_persistent():
+    """The C++ multi-GPU runtime (multi.cpp) end to end on 4 virtual ranks: count-balanced boxes
+    on a clustered cloud (owned counts within 2x, equal-volume boxes far worse), query forwarding
+    of the uncertified queries of a narrow halo (exact rows, one round), halo growth rounds when
+    forwarding is off, no device allocation on a repeated solve, kn_update_multi coordinates."""
+    import torch
+
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.utils import clustered_cloud
+    from cuda_knearests_amd.utils.check import assert_knn_exact
+
+    lib = _multi_lib()
+    n, k, W = 60000, 16, 4
+    cloud = clustered_cloud(n, seed=7)
+    pts = cloud.numpy().astype(np.float32).copy()
+    cfg = lib.kn_default_config()
+    cfg.k = k
+    devs = (C.c_int * W)(*([0] * W))
+    m = lib.kn_prepare_multi(pts.ctypes.data, n, devs, W, C.byref(cfg))
+    assert m, lib.kn_last_error()
+    _, od = kn.knn_cpu(cloud, k, "kdtree")
+    st = KnMultiStats()
+
+    def check(c, o):
+        idx, d2 = _multi_rows(lib, m, n, k)
+        assert torch.equal(torch.from_numpy(d2), o)
+        assert_knn_exact(c, torch.arange(n), torch.from_numpy(idx), torch.from_numpy(d2), o)
+
+    opt = lib.kn_default_multi_options()
+    assert opt.balance == 1 and opt.forward == 1
+    # equal-volume boxes first: the clustered cloud's counts are far apart
+    opt.balance = 0
+    assert lib.kn_set_multi_options(m, C.byref(opt)) == 0
+    assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
+    lib.kn_get_multi_stats(m, C.byref(st))
+    vol_ratio = st.max_owned / max(1, st.min_owned)
+    check(cloud, od)
+    # count-balanced + a narrow halo: forwarding answers the uncertified queries in one round
+    opt.balance, opt.halo_factor = 1, 0.5
+    assert lib.kn_set_multi_options(m, C.byref(opt)) == 0
+    assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
+    lib.kn_get_multi_stats(m, C.byref(st))
+    assert st.balanced == 1 and st.rounds == 1 and st.forwarded > 0
+    assert st.max_owned <= 2 * st.min_owned < 2 * vol_ratio * st.min_owned
+    check(cloud, od)
+    # the same solve again: every buffer fits
+    assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
+    lib.kn_get_multi_stats(m, C.byref(st))
+    assert st.device_allocations == 0, st.device_allocations
+    check(cloud, od)
+    # forwarding off: halo growth rounds instead, same rows
+    opt.forward = 0
+    assert lib.kn_set_multi_options(m, C.byref(opt)) == 0
+    assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
+    lib.kn_get_multi_stats(m, C.byref(st))
+    assert st.rounds > 1 and st.forwarded == 0
+    check(cloud, od)
+    # new coordinates of the same points
+    moved = cloud + 0.01 * torch.randn(n, 3, generator=torch.Generator().manual_seed(3))
+    mp = moved.numpy().astype(np.float32).copy()
+    assert lib.kn_update_multi(m, mp.ctypes.data) == 0, lib.kn_last_error()
+    opt.forward = 1
+    assert lib.kn_set_multi_options(m, C.byref(opt)) == 0
+    assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
+    _, od2 = kn.knn_cpu(moved, k, "kdtree")
+    check(moved, od2)
+    h = C.c_void_p(m)
+    lib.kn_free_multi(C.byref(h))

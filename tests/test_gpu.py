@@ -13,7 +13,7 @@ import pytest
 import torch
 
 import cuda_knearests_amd as kn
-from cuda_knearests_amd.utils import REPO, blue_cloud, clustered_cloud, dataset, uniform_cloud
+from cuda_knearests_amd.utils import REPO, blue_cloud, clustered_cloud, dataset, surface_cloud, uniform_cloud
 from cuda_knearests_amd.utils.check import assert_knn_exact
 
 pytestmark = pytest.mark.gpu
@@ -178,6 +178,23 @@ def test_deterministic_reruns(cuda):
     a = kn.knn(p, 16)
     b = kn.knn(p, 16)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("n,gen", [(1, "uniform"), (777, "uniform"), (20000, "uniform"),
+                                   (60000, "clustered"), (65536, "surface")])
+def test_small_build_matches_multikernel(cuda, n, gen, monkeypatch):
+    # the one-workgroup build of small clouds (build.hip small_build_kernel) lays out exactly
+    # what the deterministic multi-kernel build does
+    p = {"uniform": uniform_cloud, "clustered": clustered_cloud, "surface": surface_cloud}[gen](n, seed=21, device=cuda)
+    a = kn.build_grid(p, 8)
+    monkeypatch.setenv("KN_SMALL_BUILD", "0")
+    b = kn.build_grid(p, 8)
+    monkeypatch.delenv("KN_SMALL_BUILD")
+    assert torch.equal(a.geom[:14], b.geom[:14])  # kn::GridGeom is 14 words of the 16
+    for f in ("cell_start", "perm", "sorted"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+    i, d = kn.query(a, 8)
+    _assert_matches_oracle(p, i, d, 8)
 
 
 def test_set_k_and_save_load(cuda, tmp_path):
