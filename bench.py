@@ -213,8 +213,9 @@ def run_dist(args) -> dict:
 
     # failure detection: a dead or hung peer fails this rank's collective after 120 s
     # (CollectiveError -> non-zero exit) instead of blocking the job
+    hf = {"halo_factor": args.halo_factor} if args.halo_factor else {}
     dk = DistributedKNearests(k=args.k, deterministic=args.deterministic, timeout_s=120.0,
-                              transport=HostStagedTransport() if staged else None)
+                              transport=HostStagedTransport() if staged else None, **hf)
     res = None
     part = args.layout == "partitioned"
     for _ in range(args.warmup):
@@ -314,7 +315,8 @@ def run_loopback_bench(args) -> dict:
     times = []
 
     def body(t):
-        dk = DistributedKNearests(k=args.k, transport=t)
+        hf = {"halo_factor": args.halo_factor} if args.halo_factor else {}
+        dk = DistributedKNearests(k=args.k, transport=t, **hf)
         res, steps = None, []
         for i in range(args.warmup + args.steps):
             if i == args.warmup and t.rank == 0:
@@ -344,6 +346,8 @@ def run_loopback_bench(args) -> dict:
     halo = [r.stats["n_halo"] for r in out]
     return {"t": dt, "n_total": sum(s.size(0) for s in shares), "check": chk,
             "stats": {**{k: st[k] for k in ("n_halo", "halo_width", "rounds", "grid")},
+                      "forwarded": sum(int(r.stats.get("forwarded", 0)) for r in out),
+                      "steady": all(bool(r.stats.get("steady")) for r in out),
                       "owned_max_over_mean": max(owned) / (sum(owned) / len(owned)),
                       "halo_frac_max": max(h / max(1, o) for h, o in zip(halo, owned))}}
 
@@ -392,6 +396,8 @@ def main() -> int:
     ap.add_argument("--algo", choices=["auto", "grid", "tree"], default="auto",
                     help="1 GPU native: query structure (auto: the Morton-leaf tree when the adaptive grid "
                          "had to be refined, i.e. clustered / surface clouds)")
+    ap.add_argument("--halo-factor", type=float, default=0.0,
+                    help="multi-GPU halo width in expected K-th neighbour radii (0: the engine default)")
     ap.add_argument("--loopback", type=int, default=0,
                     help="W virtual ranks on one GPU (multi-rank algorithm at W x n points)")
     ap.add_argument("--cpu-oracle", action="store_true", help="time the CPU kd-tree path (BASELINE config 1)")

@@ -133,6 +133,11 @@ struct IntC {
 //    costs more than the window pass saves (K=16 +4 %, K=50 2.2x).
 //  * software-pipelined lane gathers: +0-3 %. R-capped lane bound (Poisson-quantile ball at the
 //    tile density): K=16 +6 %, K=50 +8 %.
+//  * query groups (G = 2 or 4 adjacent lanes per query, slots interleaved, group-min bound, DPP
+//    merge of the lists): never faster -- u20000 K=8 0.039 (G=1) / 0.039 / 0.044 ms, u100000
+//    K=8 0.051 / 0.075 / 0.122, 900K K=16 0.29 / 0.46 / 0.79 (profiles/ab_r3_qgroup.jsonl).
+//    Small clouds are bound by the per-workgroup fixed costs (cell bounds, prefix scans,
+//    staging round trips), not by the per-lane candidate chain.
 
 constexpr int kCoopCap = 128;  // per-wave LDS buffer of the cooperative re-scan (u64 keys)
 constexpr int kQueryForceRescan = kQueryFlagForceRescan;

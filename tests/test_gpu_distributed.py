@@ -471,6 +471,7 @@ def test_steady_forwarding_on_device(cuda, world, gen, hf):
         ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
         pts = cloud[m].contiguous().to(cuda)
         dk = DistributedKNearests(k=k, transport=t, halo_factor=hf)
+        dk.halo_boost_max = 1.0  # no adaptive halo: the steady steps forward on the device
         r0 = dk.solve(pts, ids)
         outs = []
         for _ in range(3):
@@ -487,3 +488,36 @@ def test_steady_forwarding_on_device(cuda, world, gen, hf):
             ids = ids.long()
             assert torch.equal(d2, od[ids])
             assert_knn_exact(cloud, ids, nb, d2, od[ids])
+
+
+def test_adaptive_halo_boost(cuda):
+    """A validated step that needed forwarding widens the halo (x1.6 per full step, kept across
+    steps) instead of entering the steady state with device forwarding; once a step needs none,
+    the asynchronous steady steps follow, every row exact (distributed.py halo_boost)."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+
+    world, n, k = 4, 30000, 16
+    cloud = uniform_cloud(n, seed=93)
+    owner = torch.arange(n) % world
+
+    def body(t):
+        m = owner == t.rank
+        ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
+        pts = cloud[m].contiguous().to(cuda)
+        dk = DistributedKNearests(k=k, transport=t, halo_factor=0.6)
+        hist = []
+        for _ in range(6):
+            r = dk.solve(pts, ids, async_=True)
+            hist.append((bool(r.stats.get("steady")), r.valid(), int(r.stats["forwarded"]), dk.halo_boost,
+                         r.ids.cpu(), r.d2.cpu()))
+        return hist
+
+    out = run_loopback(world, body)
+    _, od = kn.knn_cpu(cloud, k, "kdtree")
+    for hist in out:
+        assert hist[0][2] > 0 and hist[-1][3] > 1.0, [h[:4] for h in hist]  # forwarded, then widened
+        assert hist[-1][0], [h[:4] for h in hist]  # steady by the last step
+        for steady, ok, _, _, ids, d2 in hist:
+            assert ok
+            assert torch.equal(d2, od[ids.long()])
