@@ -137,7 +137,8 @@ struct QueryBuffers {
     unsigned* counters;       // kNumCounters words, see below
     unsigned* uncert_list;    // optional n_queries: original indices of uncertified queries
     int tile[3];
-    int halo;
+    int halo;                 // halo rings of cells in y and z
+    int xsub = 1;             // x sub-cells per y/z cell width (AutoParams::xsub): x halo = halo * xsub
     int lds_capacity;         // points staged per workgroup (power of two)
     int use_tiles;            // 0: exact ring walk for every query (debug / reference path)
     int flags;                // kQueryFlag* below
@@ -179,21 +180,28 @@ hipError_t launch_sorted_xyz(const float4* sorted, int n, float* xyz, hipStream_
 hipError_t launch_cell_occupancy(const int* cell_start, int num_cells, unsigned long long* out,
                                  hipStream_t stream);
 // Finer dims for an over-occupied grid (w = sum count^2 / N), or false if the grid is fine.
-bool refine_dims(const int dims[3], double w, int k, float points_per_cell, int n, int out[3]);
+bool refine_dims(const int dims[3], double w, int k, float points_per_cell, int n, int out[3], int xsub = 1);
 float default_points_per_cell(int k);
 hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int hist_len,
                              hipStream_t stream);
 
 // Heuristics shared by the engine, the torch binding and the CLI.
+// xsub: the grid's cells are xsub times finer along x (the axis of the contiguous cell rows) than
+// along y and z; dims[0] and tile[0] count x sub-cells, halo counts y/z cells (x halo = halo *
+// xsub sub-cells). A lane's row x-range is then cut at sub-cell granularity for the same row
+// count (query.hip, lane walk).
 struct AutoParams {
     int dims[3];
     int tile[3];
     int halo;
     int lds_capacity;
     size_t lds_bytes;
+    int xsub = 1;
 };
 AutoParams auto_params(int n, int k, float points_per_cell, const int* tile_hint, int halo_hint,
-                       const float* extent /* nullable: cubic grid */);
+                       const float* extent /* nullable: cubic grid */, int xsub_hint = 0 /* 0 = auto */);
+// points staged per query workgroup of the plan at `ppc` points per (y/z-sized) cell
+double staged_points(const AutoParams& p, double ppc);
 // Checked builds only (KN_CHECKED): first out-of-bounds report of each kernel file
 // {site code, index, limit, index high word}; all 0xFFFFFFFF in release builds.
 hipError_t debug_words_build(unsigned out[4], bool reset);
@@ -203,7 +211,7 @@ hipError_t debug_words_query(unsigned out[4], bool reset);
 // Other builds: hipErrorNotSupported.
 hipError_t debug_phase_cycles(unsigned long long out[8], bool reset);
 
-size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity);
+size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity, int xsub = 1);
 int lds_capacity_for(double staged_points);
 
 }  // namespace kn

@@ -71,13 +71,19 @@ struct TileArgs {
     unsigned* fallback_list;
     unsigned* counters;
     int TX, TY, TZ, H;
+    int Hx;         // x halo in x sub-cells (H * xsub)
     int cap;        // LDS point capacity (multiple of 64)
     int slot_bits;  // log2(cap)
     int ntx, nty, ntz;
     int cb_stride;  // max staged cells per row + 1
     int max_rows;
     int flags;      // kQueryForceRescan: every query takes the exact re-scan (tests)
+    // lane walk row order (KN_ROW_ORDER): the (2H+1)^2 row offsets (oy, oz), one byte each
+    // ((oy + 8) | (oz + 8) << 4), sorted by their expected squared distance with +1 on the near
+    // side of the query's cell; each lane mirrors it to its own position (row_order_table)
+    unsigned row_order[32];
 };
+constexpr int kRowOrderMax = 128;
 
 #ifndef KN_STAGE_ROWS
 #define KN_STAGE_ROWS 0
@@ -98,6 +104,18 @@ struct TileArgs {
 // code; profiles/ab_r1_lane_full.jsonl), 2 always.
 #ifndef KN_LANE_FULL
 #define KN_LANE_FULL 1
+#endif
+// Lane walk row order: 0 = z-slab then y centre-out (0, +1, -1, +2, -2) for every lane; 1 = the
+// host-built distance-sorted table of TileArgs::row_order, mirrored per lane so the near side of
+// the query's own cell comes first. Rows closer to the query tighten its bound sooner, so later
+// rows are cut shorter (numpy replay of the walk at 3.4 points/cell, K=16: 115 -> 103
+// candidates per query, 152 -> 135 per 64-lane wave).
+#ifndef KN_ROW_ORDER
+#define KN_ROW_ORDER 0
+#endif
+// Default AutoParams::xsub of the tile path (K <= 64)
+#ifndef KN_DEFAULT_XSUB
+#define KN_DEFAULT_XSUB 1
 #endif
 // Re-rank of the kept keys: 1 = streaming window (O(kWin) live registers), 0 = odd-even
 // transposition over (d2, id) arrays of KM entries each plus the in-wave exact re-scan of
@@ -200,9 +218,15 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     KN_PH_DECL
     float4* pts = reinterpret_cast<float4*>(smem);
-    int* cb = reinterpret_cast<int*>(smem + (size_t)a.cap * sizeof(float4));
-    int* rowbase = cb + a.max_rows * a.cb_stride;
-    int* qpref = rowbase + a.max_rows + 1;  // TY*TZ + 1 entries
+    // cell boundaries of the staged rows, RELATIVE to the row's first point (u16: half the LDS of
+    // int offsets, which buys the x sub-cells); rows of >= 65536 points only occur in tiles far
+    // beyond the LDS capacity (the dense path below reads cell_start directly)
+    unsigned short* cbr = reinterpret_cast<unsigned short*>(smem + (size_t)a.cap * sizeof(float4));
+    int* rowbase = reinterpret_cast<int*>(smem + (size_t)a.cap * sizeof(float4) +
+                                          (((size_t)a.max_rows * a.cb_stride * 2 + 3) & ~(size_t)3));
+    int* rowst = rowbase + a.max_rows + 1;  // global sorted index of each row's first point
+    int* rowend = rowst + a.max_rows;       // ... and one past its last
+    int* qpref = rowend + a.max_rows;       // TY*TZ + 1 entries
     int* misc = qpref + a.TY * a.TZ + 1;
 
     const GridGeom g = *a.geom;
@@ -218,12 +242,12 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     // cells inward instead of H and certify on the tile path instead of the exact kernel.
     int sx0, sx1, sy0, sy1, sz0, sz1;
     if constexpr (kFull) {
-        const int wx = a.TX + 2 * a.H, wy = a.TY + 2 * a.H, wz = a.TZ + 2 * a.H;
-        sx0 = max(0, min(tx0 - a.H, a.X - wx)); sx1 = min(a.X, sx0 + wx);
+        const int wx = a.TX + 2 * a.Hx, wy = a.TY + 2 * a.H, wz = a.TZ + 2 * a.H;
+        sx0 = max(0, min(tx0 - a.Hx, a.X - wx)); sx1 = min(a.X, sx0 + wx);
         sy0 = max(0, min(ty0 - a.H, a.Y - wy)); sy1 = min(a.Y, sy0 + wy);
         sz0 = max(0, min(tz0 - a.H, a.Z - wz)); sz1 = min(a.Z, sz0 + wz);
     } else {
-        sx0 = max(0, tx0 - a.H); sx1 = min(a.X, tx1 + a.H);
+        sx0 = max(0, tx0 - a.Hx); sx1 = min(a.X, tx1 + a.Hx);
         sy0 = max(0, ty0 - a.H); sy1 = min(a.Y, ty1 + a.H);
         sz0 = max(0, tz0 - a.H); sz1 = min(a.Z, tz1 + a.H);
     }
@@ -235,18 +259,25 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 
     // ---- 1. cell boundaries of every staged row ----------------------------------------
+    auto row_cell = [&](int r) { return ((sz0 + r / nys) * a.Y + sy0 + r % nys) * a.X + sx0; };
     for (int t = threadIdx.x; t < nrows * cbs; t += kWG) {
         const int r = t / cbs, i = t - r * cbs;
-        const int y = sy0 + r % nys, z = sz0 + r / nys;
-        cb[r * cbs + i] = a.cell_start[KN_IDX((z * a.Y + y) * a.X + sx0 + i, a.X * a.Y * a.Z + 1, 201)];
+        const int c0 = row_cell(r);
+        const int v = a.cell_start[KN_IDX(c0 + i, a.X * a.Y * a.Z + 1, 201)];
+        const int v0 = a.cell_start[KN_IDX(c0, a.X * a.Y * a.Z + 1, 201)];
+        cbr[r * cbs + i] = (unsigned short)(v - v0);
+        if (i == 0) rowst[r] = v;
+        if (i == nxs) rowend[r] = v;
     }
     __syncthreads();
     // ---- 2. row prefix (LDS offsets) and tile-row query prefix (wave 0) ----------------
     if (wid == 0) {
         int carry = 0;
+        bool big = false;  // a row too long for u16 offsets: the tile takes the dense path
         for (int base = 0; base < nrows; base += 64) {
             const int r = base + lane;
-            const int len = (r < nrows) ? cb[r * cbs + nxs] - cb[r * cbs] : 0;
+            const int len = (r < nrows) ? rowend[r] - rowst[r] : 0;
+            big = big || __builtin_amdgcn_ballot_w64(len > 65535) != 0;
             const int incl = wave_inclusive_scan_add(len);
             if (r < nrows) rowbase[r] = carry + incl - len;
             carry += __shfl(incl, 63, 64);
@@ -258,7 +289,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             int len = 0;
             if (t < ntr) {
                 const int r = (ty0 - sy0 + t % ntry) + nys * (tz0 - sz0 + t / ntry);
-                len = cb[r * cbs + hx + (tx1 - tx0)] - cb[r * cbs + hx];
+                len = big ? a.cell_start[row_cell(r) + hx + (tx1 - tx0)] - a.cell_start[row_cell(r) + hx]
+                          : (int)cbr[r * cbs + hx + (tx1 - tx0)] - (int)cbr[r * cbs + hx];
             }
             const int incl = wave_inclusive_scan_add(len);
             if (t < ntr) qpref[t] = qc + incl - len;
@@ -276,7 +308,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             int lo = 0, hi = ntr - 1;
             while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (qpref[mid] <= t) lo = mid; else hi = mid - 1; }
             const int r = (ty0 - sy0 + lo % ntry) + nys * (tz0 - sz0 + lo / ntry);
-            const unsigned sidx = (unsigned)(cb[r * cbs + hx] + (t - qpref[lo]));
+            const unsigned sidx = (unsigned)(a.cell_start[row_cell(r) + hx] + (t - qpref[lo]));
             const unsigned orig = __float_as_uint(a.sorted[KN_IDX(sidx, (unsigned)a.n, 204)].w);
             if (w_live(a, orig)) {
                 const unsigned pos = atomicAdd(a.counters + 0, 1u);
@@ -297,7 +329,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             const int r = r0 + u * kWaves;
             const int len = r < nrows ? rowbase[r + 1] - rowbase[r] : 0;
             dst[u] = lane < len ? rowbase[r] + lane : -1;
-            if (dst[u] >= 0) v[u] = a.sorted[KN_IDX(cb[r * cbs] + lane, a.n, 202)];
+            if (dst[u] >= 0) v[u] = a.sorted[KN_IDX(rowst[r] + lane, a.n, 202)];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -307,7 +339,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             const int r = r0 + u * kWaves;
             const int len = r < nrows ? rowbase[r + 1] - rowbase[r] : 0;
             for (int i = lane + 64; i < len; i += 64)
-                pts[KN_IDX(rowbase[r] + i, a.cap, 203)] = a.sorted[KN_IDX(cb[r * cbs] + i, a.n, 202)];
+                pts[KN_IDX(rowbase[r] + i, a.cap, 203)] = a.sorted[KN_IDX(rowst[r] + i, a.n, 202)];
         }
     }
 #else
@@ -315,7 +347,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     for (int s = threadIdx.x; s < S; s += kWG) {
         int lo = 0, hi = nrows - 1;
         while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rowbase[mid] <= s) lo = mid; else hi = mid - 1; }
-        pts[KN_IDX(s, a.cap, 203)] = a.sorted[KN_IDX(cb[lo * cbs] + (s - rowbase[lo]), a.n, 202)];
+        pts[KN_IDX(s, a.cap, 203)] = a.sorted[KN_IDX(rowst[lo] + (s - rowbase[lo]), a.n, 202)];
     }
 #endif
     __syncthreads();
@@ -336,9 +368,9 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         int lo = 0, hi = ntr - 1;
         while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (qpref[mid] <= qi) lo = mid; else hi = mid - 1; }
         const int qrow = (ty0 - sy0 + lo % ntry) + nys * (tz0 - sz0 + lo / ntry);
-        const int qoff = cb[qrow * cbs + hx] - cb[qrow * cbs] + (qi - qpref[lo]);
+        const int qoff = (int)cbr[qrow * cbs + hx] + (qi - qpref[lo]);
         const int qslot = rowbase[qrow] + qoff;
-        const unsigned qsidx = (unsigned)(cb[qrow * cbs] + qoff);
+        const unsigned qsidx = (unsigned)(rowst[qrow] + qoff);
         const float4 qp = pts[KN_IDX(qslot, S, 206)];
         const unsigned qorig = __float_as_uint(qp.w);
         const bool live = w_live(a, qorig);  // halo points of a multi-GPU rank are not queries
@@ -353,7 +385,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         int hx0 = 0, hx1 = -1, hy0 = 0, hy1 = -1, hz0 = 0, hz1 = -1;
         if constexpr (LANE) {
             if (!__builtin_amdgcn_ballot_w64(live)) continue;  // no live query in this chunk
-            hx0 = max(0, cx - a.H); hx1 = min(nxs - 1, cx + a.H);
+            hx0 = max(0, cx - a.Hx); hx1 = min(nxs - 1, cx + a.Hx);
             hy0 = max(0, cy - a.H); hy1 = min(nys - 1, cy + a.H);
             hz0 = max(0, cz - a.H); hz1 = min(nzs - 1, cz + a.H);
             if constexpr (kFull) {
@@ -369,7 +401,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             if (bx.x > bx.y) continue;  // no live query in this chunk (uniform)
             const int2 by = wave_minmax_i32(live ? cy : INT_MAX, live ? cy : INT_MIN);
             const int2 bz = wave_minmax_i32(live ? cz : INT_MAX, live ? cz : INT_MIN);
-            rx0 = max(0, bx.x - a.H); rx1 = min(nxs - 1, bx.y + a.H);
+            rx0 = max(0, bx.x - a.Hx); rx1 = min(nxs - 1, bx.y + a.Hx);
             ry0 = max(0, by.x - a.H); ry1 = min(nys - 1, by.y + a.H);
             rz0 = max(0, bz.x - a.H); rz1 = min(nzs - 1, bz.y + a.H);
             zc = (bz.x + bz.y) >> 1; yc = (by.x + by.y) >> 1;
@@ -389,13 +421,51 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 int2 sp = make_int2(0, 0);
                 if (x0 <= x1) {
                     const int r = y + nys * z;
-                    const int rb = rowbase[r] - cb[r * cbs];
-                    sp.x = rb + cb[r * cbs + x0];
-                    sp.y = KN_IDX(rb + cb[r * cbs + x1 + 1], S + 1, 212);
+                    const int rb = rowbase[r];
+                    sp.x = rb + (int)cbr[r * cbs + x0];
+                    sp.y = KN_IDX(rb + (int)cbr[r * cbs + x1 + 1], S + 1, 212);
                 }
                 return sp;
             };
             auto body = [&](int2 sp) { body2(sp.x, sp.y); };
+#if KN_ROW_ORDER
+            {
+            const int nent = side * side;
+            // mirror the table so that offset +1 is the near neighbour row of the query's cell
+            const float fy = (qy - g.origin[1]) * g.inv_cell[1] - (float)(sy0 + cy);
+            const float fz = (qz - g.origin[2]) * g.inv_cell[2] - (float)(sz0 + cz);
+            const int sgy = fy < 0.5f ? -1 : 1, sgz = fz < 0.5f ? -1 : 1;
+            for (int t = 0; t < nent; ++t) {
+                int oy, oz;
+                if (nent <= kRowOrderMax) {
+                    const unsigned e = (a.row_order[t >> 2] >> ((t & 3) * 8)) & 255u;
+                    oy = (int)(e & 15u) - 8;
+                    oz = (int)(e >> 4) - 8;
+                } else {
+                    const int iz = t / side, iy = t - iz * side;
+                    oz = (iz & 1) ? ((iz + 1) >> 1) : -(iz >> 1);
+                    oy = (iy & 1) ? ((iy + 1) >> 1) : -(iy >> 1);
+                }
+                const int z = cz + sgz * oz, y = cy + sgy * oy;
+                const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
+                const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
+                const float dyz2 = fmaf(dyb, dyb, dzb * dzb);
+                const float tau = lane_tau();
+                int lx0 = 0, lx1 = -1;
+                if (live && z >= hz0 && z <= hz1 && y >= hy0 && y <= hy1 && dyz2 <= tau) {
+                    if (tau == INFINITY) {
+                        lx0 = hx0; lx1 = hx1;
+                    } else {
+                        const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                        lx0 = max(hx0, cell_coord(g, 0, qx - rr) - sx0);
+                        lx1 = min(hx1, cell_coord(g, 0, qx + rr) - sx0);
+                    }
+                }
+                if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
+                body(lane_span(y, z, lx0, lx1));
+            }
+            }
+#else
             for (int tz_ = 0; tz_ < side; ++tz_) {
                 const int z = cz + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
                 const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
@@ -421,6 +491,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     body(lane_span(y, z, lx0, lx1));
                 }
             }
+#endif
             if constexpr (kFull) {
             // Phase 2: the rest of the staged block, only for lanes whose bound still reaches
             // a cell outside their own +-H box (the slabs just outside it are the nearest such
@@ -539,10 +610,10 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const int2 X = wave_minmax_i32(lx0, lx1);
                     if (X.x > X.y) continue;
                     const int r = y + nys * z;
-                    const int rb = rowbase[r] - cb[r * cbs];
+                    const int rb = rowbase[r];
                     // uniform bounds -> scalar loop control
-                    const int s0 = __builtin_amdgcn_readfirstlane(rb + cb[r * cbs + X.x]);
-                    const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + cb[r * cbs + X.y + 1], S + 1, 207));
+                    const int s0 = __builtin_amdgcn_readfirstlane(rb + (int)cbr[r * cbs + X.x]);
+                    const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + (int)cbr[r * cbs + X.y + 1], S + 1, 207));
                     body2(s0, s1);
                 }
             }
@@ -848,9 +919,9 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const int lx1 = min(x1, cell_coord(g, 0, qxL + rr) - sx0);
                     if (lx0 > lx1) continue;
                     const int r = y + nys * z;
-                    const int rb = rowbase[r] - cb[r * cbs];
-                    const int s0 = __builtin_amdgcn_readfirstlane(rb + cb[r * cbs + lx0]);
-                    const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + cb[r * cbs + lx1 + 1], S + 1, 215));
+                    const int rb = rowbase[r];
+                    const int s0 = __builtin_amdgcn_readfirstlane(rb + (int)cbr[r * cbs + lx0]);
+                    const int s1 = __builtin_amdgcn_readfirstlane(KN_IDX(rb + (int)cbr[r * cbs + lx1 + 1], S + 1, 215));
                     for (int sb = s0; sb < s1; sb += 64) {
                         const int sl = sb + lane;
                         bool pass = false;
@@ -1063,7 +1134,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
     const int tx = tile % a.ntx, ty = (tile / a.ntx) % a.nty, tz = tile / (a.ntx * a.nty);
     const int tx0 = tx * a.TX, ty0 = ty * a.TY, tz0 = tz * a.TZ;
     const int tx1 = min(a.X, tx0 + a.TX), ty1 = min(a.Y, ty0 + a.TY), tz1 = min(a.Z, tz0 + a.TZ);
-    const int sx0 = max(0, tx0 - a.H), sx1 = min(a.X, tx1 + a.H);
+    const int sx0 = max(0, tx0 - a.Hx), sx1 = min(a.X, tx1 + a.Hx);
     const int sy0 = max(0, ty0 - a.H), sy1 = min(a.Y, ty1 + a.H);
     const int sz0 = max(0, tz0 - a.H), sz1 = min(a.Z, tz1 + a.H);
     const int nxs = sx1 - sx0, nys = sy1 - sy0, nzs = sz1 - sz0;
@@ -1122,7 +1193,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
         if (bx.x > bx.y) continue;  // no live query in this chunk (uniform)
         const int2 by = wave_minmax_i32(live ? cy : INT_MAX, live ? cy : INT_MIN);
         const int2 bz = wave_minmax_i32(live ? cz : INT_MAX, live ? cz : INT_MIN);
-        const int rx0 = max(0, bx.x - a.H), rx1 = min(nxs - 1, bx.y + a.H);
+        const int rx0 = max(0, bx.x - a.Hx), rx1 = min(nxs - 1, bx.y + a.Hx);
         const int ry0 = max(0, by.x - a.H), ry1 = min(nys - 1, by.y + a.H);
         const int rz0 = max(0, bz.x - a.H), rz1 = min(nzs - 1, bz.y + a.H);
         const int zc = (bz.x + bz.y) >> 1, yc = (by.x + by.y) >> 1;
@@ -1667,6 +1738,29 @@ inline int query_algo(int flags, int k) {
     return def ? def : default_algo(k);
 }
 
+// Lane walk row order for halo H: the (2H+1)^2 offsets (oy, oz) sorted by expected squared
+// distance from a query in the near half of its cell (offset m > 0 is the near side: expected
+// gap m - 0.75 cells; m < 0: |m| - 0.25), ties by |oz|, |oy|, then value. Empty when > 128.
+void row_order_table(int H, unsigned out[32]) {
+    for (int i = 0; i < 32; ++i) out[i] = 0;
+    const int side = 2 * H + 1;
+    if (side * side > kRowOrderMax) return;
+    struct E { double key; int oy, oz; };
+    E e[kRowOrderMax];
+    int n = 0;
+    auto gap = [](int m) { return m > 0 ? m - 0.75 : (m < 0 ? -m - 0.25 : 0.0); };
+    for (int oz = -H; oz <= H; ++oz)
+        for (int oy = -H; oy <= H; ++oy) e[n++] = {gap(oy) * gap(oy) + gap(oz) * gap(oz), oy, oz};
+    std::stable_sort(e, e + n, [](const E& u, const E& v) {
+        if (u.key != v.key) return u.key < v.key;
+        if (std::abs(u.oz) != std::abs(v.oz)) return std::abs(u.oz) < std::abs(v.oz);
+        if (std::abs(u.oy) != std::abs(v.oy)) return std::abs(u.oy) < std::abs(v.oy);
+        return u.oz != v.oz ? u.oz > v.oz : u.oy > v.oy;
+    });
+    for (int t = 0; t < n; ++t)
+        out[t >> 2] |= (unsigned)((e[t].oy + 8) | ((e[t].oz + 8) << 4)) << ((t & 3) * 8);
+}
+
 template <int KT>
 hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     // margin slots beyond K: a query is lost to the exact path only if the K-th and (K+M)-th
@@ -1690,13 +1784,15 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.complete = q.complete; a.out_idx = q.out_idx; a.out_dist = q.out_dist;
         a.fallback_list = q.fallback_list; a.counters = q.counters;
         a.TX = q.tile[0]; a.TY = q.tile[1]; a.TZ = q.tile[2]; a.H = q.halo;
+        a.Hx = q.halo * std::max(1, q.xsub);
         a.cap = q.lds_capacity;
         a.flags = q.flags;
+        row_order_table(a.H, a.row_order);
         int sb = 0;
         while ((1 << sb) < q.lds_capacity) ++sb;
         a.slot_bits = sb;
         a.ntx = (X + a.TX - 1) / a.TX; a.nty = (Y + a.TY - 1) / a.TY; a.ntz = (Z + a.TZ - 1) / a.TZ;
-        a.cb_stride = std::min(X, a.TX + 2 * a.H) + 1;
+        a.cb_stride = std::min(X, a.TX + 2 * a.Hx) + 1;
         a.max_rows = std::min(Y, a.TY + 2 * a.H) * std::min(Z, a.TZ + 2 * a.H);
         const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
         if (query_algo(q.flags, q.k) == kAlgoStream) {
@@ -1710,7 +1806,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             const char* v = std::getenv("KN_LDS_EXTRA");
             return v ? (size_t)std::max(0, std::atoi(v)) : (size_t)0;
         }();
-        const size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity) + lds_extra;
+        const size_t lds = query_lds_bytes(q.tile, q.halo, q.lds_capacity, q.xsub) + lds_extra;
         static bool attr_set = false;
         if (!attr_set) {
             if constexpr (KT <= 64) {
@@ -1752,12 +1848,13 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
 
 }  // namespace
 
-size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity) {
+size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity, int xsub) {
     const int rows = (tile[1] + 2 * halo) * (tile[2] + 2 * halo);
-    const int cbs = tile[0] + 2 * halo + 1;
+    const int cbs = tile[0] + 2 * halo * std::max(1, xsub) + 1;
     size_t b = (size_t)lds_capacity * 16;
-    b += (size_t)rows * cbs * 4;
-    b += (size_t)(rows + 1) * 4;
+    b += ((size_t)rows * cbs * 2 + 3) & ~(size_t)3;  // u16 row-relative cell boundaries
+    b += (size_t)(rows + 1) * 4;                      // rowbase
+    b += (size_t)rows * 2 * 4;                        // rowst, rowend
     b += (size_t)(tile[1] * tile[2] + 1) * 4;
     b += 16;
     b = (b + 15) & ~(size_t)15;  // (cooperative re-scan buffers: the staged area's unused tail)
@@ -1888,9 +1985,9 @@ int lds_capacity_for(double staged) {
 // (6.94 -> 8.01), so it is not the default. K > 64 (exact kernel only): 2.9.
 float default_points_per_cell(int k) { return k <= 64 ? 3.4f : 2.9f; }
 
-bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3]) {
+bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3], int xsub) {
     if (!(ppc > 0.f)) ppc = default_points_per_cell(k);
-    const double wt = 1.0 + ppc;  // a Poisson grid at the target density
+    const double wt = 1.0 + ppc / std::max(1, xsub);  // a Poisson grid at the target density
     if (!(w > 2.0 * wt) || n <= 0) return false;
     double f = std::cbrt(w / wt);
     const double c0 = (double)dims[0] * dims[1] * dims[2];
@@ -1901,9 +1998,25 @@ bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3
     return true;
 }
 
+// Default x subdivision of the tile-path grid (AutoParams::xsub); KN_XSUB overrides.
+int default_xsub(int k) {
+    static const int env = [] {
+        const char* v = std::getenv("KN_XSUB");
+        return v ? std::max(1, std::min(4, std::atoi(v))) : 0;
+    }();
+    if (env) return env;
+    return k <= 64 ? KN_DEFAULT_XSUB : 1;
+}
+
+double staged_points(const AutoParams& p, double ppc_cell) {
+    const int xs = std::max(1, p.xsub);
+    return (double)(p.tile[0] + 2 * p.halo * xs) * (p.tile[1] + 2 * p.halo) * (p.tile[2] + 2 * p.halo) * ppc_cell;
+}
+
 AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_hint,
-                       const float* extent) {
+                       const float* extent, int xsub_hint) {
     AutoParams p;
+    p.xsub = xsub_hint > 0 ? std::min(4, xsub_hint) : default_xsub(k);
     if (!(ppc > 0.f)) ppc = default_points_per_cell(k);
     const double cells = std::max(1.0, (double)n / ppc);
     for (int a = 0; a < 3; ++a) p.tile[a] = (tile_hint && tile_hint[a] > 0) ? tile_hint[a] : 4;
@@ -1929,10 +2042,13 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
         if (x[a] >= 4.0 * p.tile[a]) p.dims[a] = std::max(p.tile[a], (int)std::lround(x[a] / p.tile[a]) * p.tile[a]);
     }
     // guard against int overflow of the cell count
-    while ((double)p.dims[0] * p.dims[1] * p.dims[2] > 4.0e8)
+    while ((double)p.dims[0] * p.dims[1] * p.dims[2] * p.xsub > 4.0e8)
         for (int a = 0; a < 3; ++a) p.dims[a] = std::max(1, p.dims[a] * 4 / 5);
     if (n > 0)  // the halo (K-th radius in cells) and the LDS plan follow the ACTUAL density
         ppc = (float)((double)n / ((double)p.dims[0] * p.dims[1] * p.dims[2]));
+    // x sub-cells: same rows, xsub x the cell boundaries per row
+    p.dims[0] *= p.xsub;
+    p.tile[0] *= p.xsub;
     if (halo_hint > 0) {
         p.halo = halo_hint;
     } else {
@@ -1945,10 +2061,8 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
         // 900K uniform: K=50 1.31 -> 0.95 ms, K=64 1.68 -> 1.33 ms (profiles/ab_r2_exact.log)
         if (k > 40 && k <= 64) p.halo = std::min(p.halo, 2);
     }
-    const double staged = (double)(p.tile[0] + 2 * p.halo) * (p.tile[1] + 2 * p.halo) *
-                          (p.tile[2] + 2 * p.halo) * ppc;
-    p.lds_capacity = lds_capacity_for(staged);
-    p.lds_bytes = query_lds_bytes(p.tile, p.halo, p.lds_capacity);
+    p.lds_capacity = lds_capacity_for(staged_points(p, ppc / p.xsub));
+    p.lds_bytes = query_lds_bytes(p.tile, p.halo, p.lds_capacity, p.xsub);
     return p;
 }
 

@@ -56,7 +56,7 @@ kn_status Engine::check(hipError_t e, const char* what) {
                 std::string(what) + ": " + hipGetErrorString(e));
 }
 
-kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
+kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xsub_override) {
     if (n < 0) return fail(KN_ERR_INVALID_ARGUMENT, "negative point count");
     if (cfg_.k < 1 || cfg_.k > KN_MAX_K) return fail(KN_ERR_INVALID_ARGUMENT, "k out of range [1,128]");
     kn_status st;
@@ -72,12 +72,14 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined) {
         // about the target density)
         for (int a = 0; a < 3; ++a) ap_.dims[a] = std::max(1, dims_override[a]);
     } else if (dims_override) {
+        // a given grid (kn_load): its x subdivision comes with it (default: none)
+        const int xs = std::max(1, xsub_override);
+        ap_.tile[0] = std::max(1, ap_.tile[0] / std::max(1, ap_.xsub)) * xs;
+        ap_.xsub = xs;
         for (int a = 0; a < 3; ++a) ap_.dims[a] = std::max(1, dims_override[a]);
         const double ppc = (double)std::max(1, n) / ((double)ap_.dims[0] * ap_.dims[1] * ap_.dims[2]);
-        const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
-                              (ap_.tile[2] + 2 * ap_.halo) * ppc;
-        ap_.lds_capacity = lds_capacity_for(staged);
-        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity);
+        ap_.lds_capacity = lds_capacity_for(staged_points(ap_, ppc));
+        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity, ap_.xsub);
     }
     const int C = ap_.dims[0] * ap_.dims[1] * ap_.dims[2];
     const size_t nb = scan_block_count(C) + 1;
@@ -170,6 +172,7 @@ QueryBuffers Engine::query_buffers() const {
     q.counters = counters_;
     for (int a = 0; a < 3; ++a) q.tile[a] = ap_.tile[a];
     q.halo = ap_.halo;
+    q.xsub = ap_.xsub;
     q.lds_capacity = ap_.lds_capacity;
     q.use_tiles = cfg_.use_tiles;
     // fallback grid from the last observed fallback count: 256 workgroups when it was short
@@ -277,7 +280,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
         double w = 0.0;
         int nd[3];
         if (round < 3 && (st = occupancy(&w)) != KN_OK) return st;
-        if (round == 3 || !refine_dims(ap_.dims, w, cfg_.k, cfg_.points_per_cell, n, nd)) {
+        if (round == 3 || !refine_dims(ap_.dims, w, cfg_.k, cfg_.points_per_cell, n, nd, ap_.xsub)) {
             if (cfg_.deterministic &&
                 (st = check(launch_cell_sort(cell_start_, geom_, n, sorted_, perm_, bin_tmp_, stream_), "cell sort")) != KN_OK)
                 return st;
@@ -380,18 +383,17 @@ kn_status Engine::set_k(int k) {
     if (k == cfg_.k) return KN_OK;
     cfg_.k = k;
     // grid density stays; the halo/LDS plan follows K
-    const AutoParams np = auto_params(n_, k, cfg_.points_per_cell, cfg_.tile, cfg_.halo, nullptr);
+    // (the grid's x subdivision stays with the grid)
+    const AutoParams np = auto_params(n_, k, cfg_.points_per_cell, cfg_.tile, cfg_.halo, nullptr, ap_.xsub);
     ap_.tile[0] = np.tile[0]; ap_.tile[1] = np.tile[1]; ap_.tile[2] = np.tile[2];
     ap_.halo = np.halo;
     {
         // occupied cells hold about the target density (refined grids have many empty cells)
         const double ppc = std::max((double)n_ / std::max(1, C_),
                                     (double)(cfg_.points_per_cell > 0.f ? cfg_.points_per_cell
-                                                                        : default_points_per_cell(k)));
-        const double staged = (double)(ap_.tile[0] + 2 * ap_.halo) * (ap_.tile[1] + 2 * ap_.halo) *
-                              (ap_.tile[2] + 2 * ap_.halo) * ppc;
-        ap_.lds_capacity = lds_capacity_for(staged);
-        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity);
+                                                                        : default_points_per_cell(k)) / ap_.xsub);
+        ap_.lds_capacity = lds_capacity_for(staged_points(ap_, ppc));
+        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity, ap_.xsub);
     }
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_})
         if (*q) { (void)hipFree(*q); *q = nullptr; }
@@ -592,7 +594,7 @@ constexpr unsigned kMagicV1 = 0x4b4e4731;  // "KNG1": {magic, n, dims[3], k}
 constexpr unsigned kMagic = 0x4b4e4732;    // "KNG2": + {tile[3], halo, lds_capacity, flags}
 // KNG2 flags word: bit 0 = the plan words are valid, bit 1 = the grid was refined (the cloud's
 // density varies: algo auto serves it with the tree path)
-constexpr int kPlanValid = 1, kPlanRefined = 2;
+constexpr int kPlanValid = 1, kPlanRefined = 2, kPlanXsubShift = 8;  // flags: bits 8-11 = xsub
 constexpr size_t kMaxLdsBytes = 160 * 1024;  // gfx950 LDS per workgroup
 }  // namespace
 
@@ -611,7 +613,7 @@ kn_status Engine::save(const char* path) {
     // the plan of the target density, which allocate() cannot re-derive from n / C
     const int hdr[12] = {(int)kMagic, n_, ap_.dims[0], ap_.dims[1], ap_.dims[2], cfg_.k,
                          ap_.tile[0], ap_.tile[1], ap_.tile[2], ap_.halo, ap_.lds_capacity,
-                         kPlanValid | (refined_ ? kPlanRefined : 0)};
+                         kPlanValid | (refined_ ? kPlanRefined : 0) | (ap_.xsub << kPlanXsubShift)};
     f.write((const char*)hdr, sizeof(hdr));
     f.write((const char*)&g, sizeof(g));
     f.write((const char*)s.data(), s.size() * sizeof(float4));
@@ -656,7 +658,8 @@ Engine* Engine::load(const char* path, const EngineConfig& cfg, std::string* err
     if (c.k <= 0) c.k = hdr[5];
     Engine* e = new Engine(c);
     const int dims[3] = {hdr[2], hdr[3], hdr[4]};
-    if (e->allocate(n, dims) != KN_OK) { if (err) *err = e->error(); delete e; return nullptr; }
+    const int xs = v2 ? std::max(1, std::min(4, (hdr[11] >> kPlanXsubShift) & 15)) : 1;
+    if (e->allocate(n, dims, false, xs) != KN_OK) { if (err) *err = e->error(); delete e; return nullptr; }
     if (v2 && (hdr[11] & kPlanValid) && c.k == hdr[5]) {
         // same K: restore the saved plan (refined grids keep the target density's LDS plan);
         // a plan the device cannot launch (corrupt / hostile file) is rejected here, not at the
@@ -665,7 +668,7 @@ Engine* Engine::load(const char* path, const EngineConfig& cfg, std::string* err
         for (int a = 0; a < 3; ++a) tile[a] = hdr[6 + a];
         const bool sane = tile[0] >= 1 && tile[1] >= 1 && tile[2] >= 1 && tile[0] <= 64 && tile[1] <= 64 &&
                           tile[2] <= 64 && hdr[9] >= 1 && hdr[9] <= 16 && hdr[10] >= 64 && hdr[10] <= 8192;
-        if (!sane || query_lds_bytes(tile, hdr[9], hdr[10]) > kMaxLdsBytes) {
+        if (!sane || query_lds_bytes(tile, hdr[9], hdr[10], xs) > kMaxLdsBytes) {
             if (err) *err = "corrupt file: query plan exceeds the device's LDS";
             delete e;
             return nullptr;
@@ -673,7 +676,7 @@ Engine* Engine::load(const char* path, const EngineConfig& cfg, std::string* err
         for (int a = 0; a < 3; ++a) e->ap_.tile[a] = tile[a];
         e->ap_.halo = hdr[9];
         e->ap_.lds_capacity = hdr[10];
-        e->ap_.lds_bytes = query_lds_bytes(e->ap_.tile, e->ap_.halo, e->ap_.lds_capacity);
+        e->ap_.lds_bytes = query_lds_bytes(e->ap_.tile, e->ap_.halo, e->ap_.lds_capacity, xs);
     }
     // the refined state travels with the grid: algo auto serves a refined grid with the tree
     e->refined_ = v2 && (hdr[11] & kPlanRefined);

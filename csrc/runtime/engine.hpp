@@ -93,7 +93,7 @@ public:
 private:
     kn_status fail(kn_status s, const std::string& msg);
     kn_status check(hipError_t e, const char* what);
-    kn_status allocate(int n, const int* dims_override = nullptr, bool refined = false);
+    kn_status allocate(int n, const int* dims_override = nullptr, bool refined = false, int xsub_override = 0);
     kn_status prepare_from(const float* src, int n, hipMemcpyKind kind);
     kn_status occupancy(double* w);
     kn_status ensure_outputs();

@@ -452,6 +452,7 @@ kn_status solve_round(kn_multi* m, double hf, const int grid[3], bool balanced, 
         q.uncert_list = R.uncert.as<unsigned>();
         for (int a = 0; a < 3; ++a) q.tile[a] = ap.tile[a];
         q.halo = ap.halo;
+        q.xsub = ap.xsub;
         q.lds_capacity = ap.lds_capacity;
         q.use_tiles = m->cfg.exact_only ? 0 : 1;
         KN_M(kn::launch_query(q, R.s));

@@ -105,7 +105,8 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                                  std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
                                  bool use_tiles, bool with_dist, int64_t flags,
                                  c10::optional<torch::Tensor> row_of, int64_t exact_grid = 0,
-                                 c10::optional<torch::Tensor> zeroed_counters = c10::nullopt, int64_t q_lo = 0) {
+                                 c10::optional<torch::Tensor> zeroed_counters = c10::nullopt, int64_t q_lo = 0,
+                                 int64_t xsub = 1) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
@@ -157,6 +158,8 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     q.uncert_list = reinterpret_cast<unsigned*>(uncert.data_ptr<int>());
     for (int a = 0; a < 3; ++a) q.tile[a] = (int)tile[a];
     q.halo = (int)halo;
+    TORCH_CHECK(xsub >= 1 && xsub <= 4, "xsub must be in [1, 4]");
+    q.xsub = (int)xsub;
     q.lds_capacity = (int)lds_capacity;
     q.use_tiles = use_tiles ? 1 : 0;
     q.flags = (int)flags;
@@ -164,7 +167,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     q.counters_zeroed = zeroed_counters.has_value() ? 1 : 0;
     TORCH_CHECK(lds_capacity >= 64 && lds_capacity % 64 == 0 && lds_capacity <= 8192,
                 "lds_capacity must be a multiple of 64 in [64, 8192]");
-    TORCH_CHECK(kn::query_lds_bytes(q.tile, q.halo, q.lds_capacity) <= 160 * 1024, "tile plan exceeds 160 KiB LDS");
+    TORCH_CHECK(kn::query_lds_bytes(q.tile, q.halo, q.lds_capacity, q.xsub) <= 160 * 1024, "tile plan exceeds 160 KiB LDS");
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_query(q, s));
     if (!with_dist) out_dist = torch::empty({0}, sorted.options());
@@ -252,7 +255,7 @@ std::vector<torch::Tensor> tree_query(torch::Tensor ws, torch::Tensor nodes, std
 }
 
 py::dict auto_params(int64_t n, int64_t k, double ppc, std::vector<int64_t> tile, int64_t halo,
-                     c10::optional<std::vector<double>> extent) {
+                     c10::optional<std::vector<double>> extent, int64_t xsub) {
     int th[3] = {0, 0, 0};
     for (size_t a = 0; a < tile.size() && a < 3; ++a) th[a] = (int)tile[a];
     float ext[3];
@@ -261,8 +264,9 @@ py::dict auto_params(int64_t n, int64_t k, double ppc, std::vector<int64_t> tile
         for (int a = 0; a < 3; ++a) ext[a] = (float)(*extent)[a];
         pe = ext;
     }
-    const kn::AutoParams p = kn::auto_params((int)n, (int)k, (float)ppc, th, (int)halo, pe);
+    const kn::AutoParams p = kn::auto_params((int)n, (int)k, (float)ppc, th, (int)halo, pe, (int)xsub);
     py::dict d;
+    d["xsub"] = p.xsub;
     d["dims"] = std::vector<int>{p.dims[0], p.dims[1], p.dims[2]};
     d["tile"] = std::vector<int>{p.tile[0], p.tile[1], p.tile[2]};
     d["halo"] = p.halo;
@@ -661,7 +665,7 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
             const double w = (double)occ.cpu().item<int64_t>() / (double)npts;
             const int cur[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
             int nd[3];
-            if (!kn::refine_dims(cur, w, (int)k, (float)ppc, (int)npts, nd)) break;
+            if (!kn::refine_dims(cur, w, (int)k, (float)ppc, (int)npts, nd, ap.xsub)) break;
             dims = {nd[0], nd[1], nd[2]};
             g = build_impl(pg[0], dims, deterministic, box, pg[1].data_ptr<int>(), (int)n_owned,
                            reinterpret_cast<unsigned*>(counters.data_ptr<int>()), kn::kNumCounters);
@@ -690,7 +694,7 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
         return {pg[0], pg[1], tq[0], tq[1], tq[2], g[0], g[1], g[3], g[2], uncert, dims_t, tree_t};
     }
     auto q = query(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
-                   ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid, counters);
+                   ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid, counters, 0, ap.xsub);
     // + the local grid (global-id mode) and the uncertified list, for query forwarding
     return {pg[0], pg[1], q[0], q[1], q[2], g[0], g[1], g[3], g[2], q[3], dims_t, tree_t};
 }
@@ -938,11 +942,11 @@ torch::Tensor occupancy(torch::Tensor cell_start) {
     return out;
 }
 
-py::object refine_dims(std::vector<int64_t> dims, double w, int64_t k, double ppc, int64_t n) {
+py::object refine_dims(std::vector<int64_t> dims, double w, int64_t k, double ppc, int64_t n, int64_t xsub) {
     TORCH_CHECK(dims.size() == 3, "dims must have 3 entries");
     const int d[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
     int out[3];
-    if (!kn::refine_dims(d, w, (int)k, (float)ppc, (int)n, out)) return py::none();
+    if (!kn::refine_dims(d, w, (int)k, (float)ppc, (int)n, out, (int)xsub)) return py::none();
     return py::cast(std::vector<int64_t>{out[0], out[1], out[2]});
 }
 
@@ -1133,16 +1137,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("k"), py::arg("n_queries"),
           py::arg("id_map"), py::arg("complete"), py::arg("tile"), py::arg("halo"), py::arg("lds_capacity"),
           py::arg("use_tiles"), py::arg("with_dist"), py::arg("flags") = 0, py::arg("row_of") = py::none(),
-          py::arg("exact_grid") = 0, py::arg("zeroed_counters") = py::none(), py::arg("q_lo") = 0);
-    m.def("auto_params", &auto_params, "grid / tile plan");
+          py::arg("exact_grid") = 0, py::arg("zeroed_counters") = py::none(), py::arg("q_lo") = 0,
+          py::arg("xsub") = 1);
+    m.def("auto_params", &auto_params, "grid / tile plan", py::arg("n"), py::arg("k"), py::arg("ppc"),
+          py::arg("tile"), py::arg("halo"), py::arg("extent") = py::none(), py::arg("xsub") = 0);
     m.def(
         "query_lds_bytes",
-        [](std::vector<int64_t> tile, int64_t halo, int64_t cap) {
+        [](std::vector<int64_t> tile, int64_t halo, int64_t cap, int64_t xsub) {
             TORCH_CHECK(tile.size() == 3, "tile must have 3 entries");
             const int t[3] = {(int)tile[0], (int)tile[1], (int)tile[2]};
-            return (int64_t)kn::query_lds_bytes(t, (int)halo, (int)cap);
+            return (int64_t)kn::query_lds_bytes(t, (int)halo, (int)cap, (int)xsub);
         },
-        "LDS bytes per workgroup of the tile query kernel for a plan");
+        "LDS bytes per workgroup of the tile query kernel for a plan", py::arg("tile"), py::arg("halo"),
+        py::arg("cap"), py::arg("xsub") = 1);
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
     m.def("tree_build", &tree_build,
           "Morton-leaf tree over a grid's sorted points, stream-ordered: (workspace, nodes, leaves or -1)",
@@ -1152,7 +1159,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("with_dist") = true, py::arg("flags") = 0, py::arg("row_of") = py::none());
     m.def("cell_sort", &cell_sort, "in-cell order by original index (deterministic layout) of a built grid");
     m.def("occupancy", &occupancy, "sum over cells of count^2 (occupancy-adaptive grid)");
-    m.def("refine_dims", &refine_dims, "finer grid dims for an over-occupied grid, or None");
+    m.def("refine_dims", &refine_dims, "finer grid dims for an over-occupied grid, or None", py::arg("dims"),
+          py::arg("w"), py::arg("k"), py::arg("ppc"), py::arg("n"), py::arg("xsub") = 1);
     m.def("local_meta", &local_meta, "multi-GPU: {lo[3], hi[3], n, 0} of the local points (float64, on device)");
     m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts",
           py::arg("points"), py::arg("lo"), py::arg("hi"), py::arg("grid"), py::arg("boxes"), py::arg("h"),

@@ -77,8 +77,8 @@ class KNearests:
             raise ValueError("points must be (N, 3)")
         return t.to(self.device).contiguous()
 
-    def plan(self, n: int) -> ops.Plan:
-        return ops.Plan.auto(n, self.k, self.points_per_cell, self.tile, self.halo)
+    def plan(self, n: int, xsub: int = 0) -> ops.Plan:
+        return ops.Plan.auto(n, self.k, self.points_per_cell, self.tile, self.halo, xsub=xsub)
 
     def prepare(self, points) -> "KNearests":
         """Upload (if needed) and bin the points (reference kn_prepare, knearests.cu:235-344)."""
@@ -152,7 +152,7 @@ class KNearests:
             raise ValueError("k must be in [1, 128]")
         self.k = int(k)
         if self.grid is not None:
-            p = self.plan(self.grid.n)
+            p = self.plan(self.grid.n, xsub=self.grid.plan.xsub)  # the x subdivision stays with the grid
             self.grid.plan.halo, self.grid.plan.tile = p.halo, p.tile
             self.grid.plan.lds_capacity = p.lds_capacity
         self.neighbors = self.distances = None
@@ -246,14 +246,14 @@ class KNearests:
         g = self.grid
         torch.save({"k": self.k, "sorted": g.sorted.cpu(), "cell_start": g.cell_start.cpu(),
                     "perm": g.perm.cpu(), "geom": g.geom.cpu(), "dims": list(g.plan.dims),
-                    "points": self.points.cpu()}, path)
+                    "xsub": int(g.plan.xsub), "points": self.points.cpu()}, path)
 
     @classmethod
     def load(cls, path: str, device="cuda", **kw) -> "KNearests":
         d = torch.load(path, map_location="cpu", weights_only=True)
         kn = cls(k=kw.pop("k", d["k"]), device=device, **kw)
         kn.points = d["points"].to(kn.device)
-        plan = kn.plan(d["sorted"].size(0))
+        plan = kn.plan(d["sorted"].size(0), xsub=int(d.get("xsub", 1)))
         plan.dims = list(d["dims"])
         kn.grid = ops.Grid(d["sorted"].to(kn.device), d["cell_start"].to(kn.device), d["perm"].to(kn.device),
                            d["geom"].to(kn.device), plan, d["sorted"].size(0))

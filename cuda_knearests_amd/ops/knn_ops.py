@@ -37,14 +37,16 @@ class Plan:
     halo: int
     lds_capacity: int
     lds_bytes: int = 0
+    # x sub-cells per y/z cell width: dims[0] and tile[0] count sub-cells, the x halo is halo * xsub
+    xsub: int = 1
 
     @staticmethod
     def auto(n: int, k: int, points_per_cell: float = 0.0, tile: Sequence[int] = (),
-             halo: int = 0, extent: Optional[Sequence[float]] = None) -> "Plan":
+             halo: int = 0, extent: Optional[Sequence[float]] = None, xsub: int = 0) -> "Plan":
         d = load().auto_params(int(n), int(k), float(points_per_cell), list(tile), int(halo),
-                               list(extent) if extent is not None else None)
+                               list(extent) if extent is not None else None, int(xsub))
         return Plan(list(d["dims"]), list(d["tile"]), int(d["halo"]), int(d["lds_capacity"]),
-                    int(d["lds_bytes"]))
+                    int(d["lds_bytes"]), int(d["xsub"]))
 
 
 @dataclass
@@ -93,10 +95,10 @@ def build_grid(points: torch.Tensor, k: int = 16, plan: Optional[Plan] = None,
     refined = False
     for _ in range(3 if probe else 0):
         w = int(C.occupancy(cs).item()) / n
-        dims = C.refine_dims(list(plan.dims), w, int(k), float(points_per_cell), n)
+        dims = C.refine_dims(list(plan.dims), w, int(k), float(points_per_cell), n, plan.xsub)
         if dims is None:
             break
-        plan = Plan(list(dims), list(plan.tile), plan.halo, plan.lds_capacity, plan.lds_bytes)
+        plan = Plan(list(dims), list(plan.tile), plan.halo, plan.lds_capacity, plan.lds_bytes, plan.xsub)
         s, cs, perm, geom = C.build(points, list(plan.dims), False, bx)
         refined = True
     if probe and deterministic:
@@ -157,7 +159,8 @@ def query(grid: Grid, k: int, n_queries: Optional[int] = None, id_map: Optional[
     halo, cap = p.halo, p.lds_capacity
     idx, d2, counters, uncert, fallback = load().query(grid.sorted, grid.cell_start, grid.geom, list(p.dims), int(k), nq,
                                              id_map, comp, list(p.tile), int(halo), int(cap), bool(use_tiles),
-                                             bool(with_dist), int(flags), None, 0, None, int(first))
+                                             bool(with_dist), int(flags), None, 0, None, int(first),
+                                             int(p.xsub))
     if return_info:
         return idx, (d2 if with_dist else None), {"counters": counters, "uncertified": uncert,
                                                   "exact_path": fallback}
