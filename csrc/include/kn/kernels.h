@@ -180,6 +180,7 @@ hipError_t launch_sorted_xyz(const float4* sorted, int n, float* xyz, hipStream_
 hipError_t launch_cell_occupancy(const int* cell_start, int num_cells, unsigned long long* out,
                                  hipStream_t stream);
 // Finer dims for an over-occupied grid (w = sum count^2 / N), or false if the grid is fine.
+// The refined dims are isotropic (their grid has xsub 1).
 bool refine_dims(const int dims[3], double w, int k, float points_per_cell, int n, int out[3], int xsub = 1);
 float default_points_per_cell(int k);
 hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int hist_len,

@@ -82,6 +82,7 @@ struct TileArgs {
     // ((oy + 8) | (oz + 8) << 4), sorted by their expected squared distance with +1 on the near
     // side of the query's cell; each lane mirrors it to its own position (row_order_table)
     unsigned row_order[32];
+    int row_mirror;  // 1: each lane mirrors the table to its own cell position (distance order)
 };
 constexpr int kRowOrderMax = 128;
 
@@ -105,17 +106,31 @@ constexpr int kRowOrderMax = 128;
 #ifndef KN_LANE_FULL
 #define KN_LANE_FULL 1
 #endif
-// Lane walk row order: 0 = z-slab then y centre-out (0, +1, -1, +2, -2) for every lane; 1 = the
+// Lane walk row order: z-slab then y centre-out (0, +1, -1, +2, -2) for every lane, or the
 // host-built distance-sorted table of TileArgs::row_order, mirrored per lane so the near side of
-// the query's own cell comes first. Rows closer to the query tighten its bound sooner, so later
-// rows are cut shorter (numpy replay of the walk at 3.4 points/cell, K=16: 115 -> 103
-// candidates per query, 152 -> 135 per 64-lane wave).
+// the query's own cell comes first (rows closer to the query tighten its bound sooner; numpy
+// replay at 3.4 points/cell, K=16: 115 -> 103 candidates per query). KN_ROW_ORDER 0 = never,
+// 1 = always, 2 = the whole-block walk only (K > 40). Interleaved in-process A/B, 900K uniform,
+// identical rows (profiles/ab_r3_row_order.jsonl): K=50 query 0.943 -> 0.794 ms, but K=8 +4 %,
+// K=16 -1 %, K=32 +13 % (the row-synchronous wave pays the longest lane span of every row, and
+// the per-lane mirror makes the spans of one row iteration more uneven).
 #ifndef KN_ROW_ORDER
-#define KN_ROW_ORDER 0
+#define KN_ROW_ORDER 2
 #endif
-// Default AutoParams::xsub of the tile path (K <= 64)
+// KN_ROW_RING=1: the other lane walks (K <= 40) take a table too, in ring order without the
+// per-lane mirror: the 3x3 rows around the query's own row first, the outer ring after (every
+// lane of a wave visits the same relative row, so the spans of one row iteration stay alike).
+#ifndef KN_ROW_RING
+#define KN_ROW_RING 0
+#endif
+// Default AutoParams::xsub of the tile path for K <= KN_XSUB_MAX_K. Interleaved A/B at 900K
+// uniform (profiles/ab_r3_xsub.jsonl): xsub 2 query K=8 0.207 -> 0.198, K=16 0.305 -> 0.292 ms
+// (build +3 us), K=32 +2 %, K=50 +4 %; xsub 4 at K=16 0.318 -> 0.301 but build +11 us.
 #ifndef KN_DEFAULT_XSUB
-#define KN_DEFAULT_XSUB 1
+#define KN_DEFAULT_XSUB 2
+#endif
+#ifndef KN_XSUB_MAX_K
+#define KN_XSUB_MAX_K 16
 #endif
 // Re-rank of the kept keys: 1 = streaming window (O(kWin) live registers), 0 = odd-even
 // transposition over (d2, id) arrays of KM entries each plus the in-wave exact re-scan of
@@ -215,6 +230,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
     constexpr int KM = KT + M + 1;
     constexpr bool kFull = LANE && (KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40));
+    constexpr bool kRowOrder = LANE && (KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && kFull) || KN_ROW_RING);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     KN_PH_DECL
     float4* pts = reinterpret_cast<float4*>(smem);
@@ -428,13 +444,12 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 return sp;
             };
             auto body = [&](int2 sp) { body2(sp.x, sp.y); };
-#if KN_ROW_ORDER
-            {
+            if constexpr (kRowOrder) {
             const int nent = side * side;
             // mirror the table so that offset +1 is the near neighbour row of the query's cell
             const float fy = (qy - g.origin[1]) * g.inv_cell[1] - (float)(sy0 + cy);
             const float fz = (qz - g.origin[2]) * g.inv_cell[2] - (float)(sz0 + cz);
-            const int sgy = fy < 0.5f ? -1 : 1, sgz = fz < 0.5f ? -1 : 1;
+            const int sgy = (a.row_mirror && fy < 0.5f) ? -1 : 1, sgz = (a.row_mirror && fz < 0.5f) ? -1 : 1;
             for (int t = 0; t < nent; ++t) {
                 int oy, oz;
                 if (nent <= kRowOrderMax) {
@@ -464,8 +479,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
                 body(lane_span(y, z, lx0, lx1));
             }
-            }
-#else
+            } else {
             for (int tz_ = 0; tz_ < side; ++tz_) {
                 const int z = cz + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
                 const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
@@ -491,7 +505,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     body(lane_span(y, z, lx0, lx1));
                 }
             }
-#endif
+            }
             if constexpr (kFull) {
             // Phase 2: the rest of the staged block, only for lanes whose bound still reaches
             // a cell outside their own +-H box (the slabs just outside it are the nearest such
@@ -1741,7 +1755,8 @@ inline int query_algo(int flags, int k) {
 // Lane walk row order for halo H: the (2H+1)^2 offsets (oy, oz) sorted by expected squared
 // distance from a query in the near half of its cell (offset m > 0 is the near side: expected
 // gap m - 0.75 cells; m < 0: |m| - 0.25), ties by |oz|, |oy|, then value. Empty when > 128.
-void row_order_table(int H, unsigned out[32]) {
+// ring = true: by Chebyshev ring max(|oy|, |oz|), then the centre-out z-slab / y order.
+void row_order_table(int H, unsigned out[32], bool ring) {
     for (int i = 0; i < 32; ++i) out[i] = 0;
     const int side = 2 * H + 1;
     if (side * side > kRowOrderMax) return;
@@ -1749,8 +1764,11 @@ void row_order_table(int H, unsigned out[32]) {
     E e[kRowOrderMax];
     int n = 0;
     auto gap = [](int m) { return m > 0 ? m - 0.75 : (m < 0 ? -m - 0.25 : 0.0); };
+    auto co = [](int m) { return m > 0 ? 2 * m - 1 : -2 * m; };  // centre-out rank 0, +1, -1, +2, ...
     for (int oz = -H; oz <= H; ++oz)
-        for (int oy = -H; oy <= H; ++oy) e[n++] = {gap(oy) * gap(oy) + gap(oz) * gap(oz), oy, oz};
+        for (int oy = -H; oy <= H; ++oy)
+            e[n++] = {ring ? 1e4 * std::max(std::abs(oy), std::abs(oz)) + 100.0 * co(oz) + co(oy)
+                           : gap(oy) * gap(oy) + gap(oz) * gap(oz), oy, oz};
     std::stable_sort(e, e + n, [](const E& u, const E& v) {
         if (u.key != v.key) return u.key < v.key;
         if (std::abs(u.oz) != std::abs(v.oz)) return std::abs(u.oz) < std::abs(v.oz);
@@ -1787,7 +1805,14 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.Hx = q.halo * std::max(1, q.xsub);
         a.cap = q.lds_capacity;
         a.flags = q.flags;
-        row_order_table(a.H, a.row_order);
+        {
+            // the distance-sorted, mirrored table for the whole-block walk (K > 40), ring order
+            // for the others (KN_ROW_RING)
+            constexpr bool full = KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40);
+            const bool ring = KN_ROW_RING && !(KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && full));
+            row_order_table(a.H, a.row_order, ring);
+            a.row_mirror = ring ? 0 : 1;
+        }
         int sb = 0;
         while ((1 << sb) < q.lds_capacity) ++sb;
         a.slot_bits = sb;
@@ -1990,11 +2015,14 @@ bool refine_dims(const int dims[3], double w, int k, float ppc, int n, int out[3
     const double wt = 1.0 + ppc / std::max(1, xsub);  // a Poisson grid at the target density
     if (!(w > 2.0 * wt) || n <= 0) return false;
     double f = std::cbrt(w / wt);
-    const double c0 = (double)dims[0] * dims[1] * dims[2];
+    // refined grids are isotropic (xsub 1): the x sub-cells serve the uniform tile path only
+    const int xs = std::max(1, xsub);
+    const int base[3] = {std::max(1, dims[0] / xs), dims[1], dims[2]};
+    const double c0 = (double)base[0] * base[1] * base[2];
     const double cmax = std::min(4.0e8, std::max(16.0 * n, 1048576.0));  // cell_start <= 64 B/point
     if (c0 * f * f * f > cmax) f = std::cbrt(cmax / c0);
     if (f < 1.2) return false;
-    for (int a = 0; a < 3; ++a) out[a] = std::max(4, (int)std::ceil(dims[a] * f / 4.0) * 4);  // whole 4-cell tiles
+    for (int a = 0; a < 3; ++a) out[a] = std::max(4, (int)std::ceil(base[a] * f / 4.0) * 4);  // whole 4-cell tiles
     return true;
 }
 
@@ -2005,7 +2033,7 @@ int default_xsub(int k) {
         return v ? std::max(1, std::min(4, std::atoi(v))) : 0;
     }();
     if (env) return env;
-    return k <= 64 ? KN_DEFAULT_XSUB : 1;
+    return k <= KN_XSUB_MAX_K ? KN_DEFAULT_XSUB : 1;
 }
 
 double staged_points(const AutoParams& p, double ppc_cell) {

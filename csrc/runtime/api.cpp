@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "hostio.hpp"
 #include "../host/host.hpp"
 #include "knearests.h"
 
@@ -249,6 +250,8 @@ kn_problem* kn_load(const char* path, const kn_config* cfg) {
     sync_fields(kn);
     return kn;
 }
+
+void kn_release_cached_memory(void) { kn::arena_release_all(); }
 
 size_t kn_struct_size(int which) {
     switch (which) {

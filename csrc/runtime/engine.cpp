@@ -4,12 +4,16 @@
 // atomic `reserve` bump allocator, hipGraph replay of the whole build+solve step.
 #include "engine.hpp"
 
+#include <chrono>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+
+#include "hostio.hpp"
 
 namespace kn {
 
@@ -32,7 +36,9 @@ Engine::~Engine() { release(); }
 
 void Engine::release() {
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
-    if (arena_) { (void)hipFree(arena_); arena_ = nullptr; }
+    // the arena goes back to the process-wide cache (hostio.hpp): the next kn_prepare of a similar
+    // size skips hipMalloc
+    if (arena_) { arena_release(cfg_.device, arena_, arena_bytes_); arena_ = nullptr; arena_bytes_ = 0; }
     if (out_idx_) { (void)hipFree(out_idx_); out_idx_ = nullptr; }
     if (out_dist_) { (void)hipFree(out_dist_); out_dist_ = nullptr; }
     if (inv_perm_) { (void)hipFree(inv_perm_); inv_perm_ = nullptr; }
@@ -68,9 +74,12 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     }
     ap_ = auto_params(n, cfg_.k, cfg_.points_per_cell, cfg_.tile, cfg_.halo, nullptr);
     if (dims_override && refined) {
-        // occupancy refinement: finer cells, same tile / halo / LDS plan (occupied cells keep
-        // about the target density)
+        // occupancy refinement: finer isotropic cells (xsub 1), same tile / halo / LDS capacity
+        // (occupied cells keep about the target density)
         for (int a = 0; a < 3; ++a) ap_.dims[a] = std::max(1, dims_override[a]);
+        ap_.tile[0] = std::max(1, ap_.tile[0] / std::max(1, ap_.xsub));
+        ap_.xsub = 1;
+        ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity, 1);
     } else if (dims_override) {
         // a given grid (kn_load): its x subdivision comes with it (default: none)
         const int xs = std::max(1, xsub_override);
@@ -96,10 +105,17 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     bytes += align_up(sizeof(unsigned long long));
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (bytes > arena_bytes_) {
-        if (arena_) (void)hipFree(arena_);
+        if (arena_) arena_release(cfg_.device, arena_, arena_bytes_);
         arena_ = nullptr;
-        if ((st = check(hipMalloc(&arena_, bytes), "hipMalloc(arena)")) != KN_OK) return st;
-        arena_bytes_ = bytes;
+        arena_bytes_ = 0;
+        size_t got = 0;
+        if (void* c = arena_acquire(cfg_.device, bytes, &got)) {
+            arena_ = static_cast<char*>(c);
+            arena_bytes_ = got;
+        } else {
+            if ((st = check(hipMalloc(&arena_, bytes), "hipMalloc(arena)")) != KN_OK) return st;
+            arena_bytes_ = bytes;
+        }
     }
     char* p = arena_;
     points_ = carve<float>(p, (size_t)n * 3);
@@ -262,11 +278,17 @@ kn_status Engine::occupancy(double* w) {
 kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     kn_status st;
     if (!src && n > 0) return fail(KN_ERR_INVALID_ARGUMENT, "null points");
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     if ((st = allocate(n)) != KN_OK) return st;
+    const auto t1 = clk::now();
     bool refined = false;
     for (int round = 0;; ++round) {
-        if (n > 0 && (st = check(hipMemcpyAsync(points_, src, (size_t)n * 12, kind, stream_), "copy points")) != KN_OK)
-            return st;
+        // host points: through the pinned staging ring (hostio.hpp), device points: D2D
+        const hipError_t ce = kind == hipMemcpyHostToDevice
+                                  ? copy_h2d_staged(points_, src, (size_t)n * 12, stream_)
+                                  : hipMemcpyAsync(points_, src, (size_t)n * 12, kind, stream_);
+        if (n > 0 && (st = check(ce, "copy points")) != KN_OK) return st;
         (void)hipEventRecord(ev_[0], stream_);
         points3_valid_ = false;
         // adaptive: probe grids are binned without the in-cell order (see launch_cell_sort)
@@ -298,6 +320,12 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined));
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }  // grid or tree step of the new plan
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
+    if (cfg_.verbose > 1) {
+        const auto t2 = clk::now();
+        auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+        fprintf(stderr, "kn_prepare host phases: allocate %.3f ms, upload + build + plan %.3f ms\n", ms(t1 - t0),
+                ms(t2 - t1));
+    }
     built_ = true;
     return KN_OK;
 }
@@ -507,12 +535,13 @@ float* Engine::d_points3() {
     return points3_;
 }
 
+// malloc'd host copy (the reference getters' contract: the caller free()s it), through the
+// pinned staging ring
 template <class T>
 static T* d2h(const T* d, size_t count, hipStream_t s) {
     T* h = (T*)malloc(std::max<size_t>(1, count) * sizeof(T));
     if (!h) return nullptr;
-    if (count && (hipMemcpyAsync(h, d, count * sizeof(T), hipMemcpyDeviceToHost, s) != hipSuccess ||
-                  hipStreamSynchronize(s) != hipSuccess)) {
+    if (count && copy_d2h_staged(h, d, count * sizeof(T), s) != hipSuccess) {
         free(h);
         return nullptr;
     }
@@ -521,12 +550,9 @@ static T* d2h(const T* d, size_t count, hipStream_t s) {
 
 float* Engine::get_points_sorted() {
     if (!built_) { fail(KN_ERR_STATE, "not prepared"); return nullptr; }
-    float4* tmp = d2h(sorted_, (size_t)n_, stream_);
-    if (!tmp) return nullptr;
-    float* out = (float*)malloc(std::max<size_t>(1, (size_t)n_ * 3) * sizeof(float));
-    for (size_t i = 0; i < (size_t)n_; ++i) { out[3 * i] = tmp[i].x; out[3 * i + 1] = tmp[i].y; out[3 * i + 2] = tmp[i].z; }
-    free(tmp);
-    return out;
+    const float* d = d_points3();  // float3 view of the stored points (one device pass)
+    if (!d) return nullptr;
+    return d2h(d, (size_t)n_ * 3, stream_);
 }
 unsigned* Engine::get_permutation() {
     if (!built_) { fail(KN_ERR_STATE, "not prepared"); return nullptr; }

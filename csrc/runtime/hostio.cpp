@@ -1,0 +1,197 @@
+// hostio.cpp -- staged pageable copies and the device arena cache (see hostio.hpp).
+#include "hostio.hpp"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace kn {
+
+namespace {
+
+constexpr size_t kChunk = 4u << 20;       // bytes per staging slot
+constexpr size_t kDirectBelow = 1u << 20;  // smaller copies skip the ring
+
+bool env_on(const char* name, bool dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) != 0 : dflt;
+}
+
+// Parallel host memcpy in 256 KiB blocks (page-fault and bandwidth bound on freshly malloc'd
+// destinations: one thread reaches ~6-10 GB/s).
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kBlk = 256u << 10;
+    const long nb = (long)((bytes + kBlk - 1) / kBlk);
+    const int nt = std::max(1, std::min(16, omp_get_max_threads()));
+    if (nb <= 1 || nt == 1) { std::memcpy(dst, src, bytes); return; }
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (long b = 0; b < nb; ++b) {
+        const size_t off = (size_t)b * kBlk;
+        std::memcpy((char*)dst + off, (const char*)src + off, std::min(kBlk, bytes - off));
+    }
+}
+
+struct Ring {
+    std::mutex mu;
+    void* slot[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool pending[2] = {false, false};
+    int dev = -1;
+
+    hipError_t ready() {
+        hipError_t e = hipSuccess;
+        if (!slot[0]) {
+            for (auto& p : slot)
+                if ((e = hipHostMalloc(&p, kChunk, hipHostMallocDefault)) != hipSuccess) return e;
+        }
+        int d = 0;
+        if ((e = hipGetDevice(&d)) != hipSuccess) return e;
+        if (d != dev) {
+            for (int i = 0; i < 2; ++i) {
+                if (ev[i]) {
+                    if (pending[i]) (void)hipEventSynchronize(ev[i]);
+                    (void)hipEventDestroy(ev[i]);
+                    ev[i] = nullptr;
+                }
+                pending[i] = false;
+                if ((e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming)) != hipSuccess) return e;
+            }
+            dev = d;
+        }
+        return e;
+    }
+    hipError_t wait(int i) {
+        if (!pending[i]) return hipSuccess;
+        pending[i] = false;
+        return hipEventSynchronize(ev[i]);
+    }
+};
+
+Ring& ring() {
+    static Ring* r = new Ring();  // never destroyed: pinned memory is released at process exit
+    return *r;
+}
+
+struct Cached {
+    int dev;
+    void* p;
+    size_t bytes;
+};
+std::mutex g_pool_mu;
+std::vector<Cached> g_pool;
+constexpr size_t kPoolMaxBytes = 4ull << 30;
+constexpr int kPoolPerDevice = 2;
+
+}  // namespace
+
+hipError_t copy_h2d_staged(void* d, const void* h, size_t bytes, hipStream_t s) {
+    if (bytes < kDirectBelow || !env_on("KN_HOST_STAGE", true))
+        return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+    Ring& r = ring();
+    std::lock_guard<std::mutex> lock(r.mu);
+    hipError_t e = r.ready();
+    if (e != hipSuccess) return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+    int i = 0;
+    for (size_t off = 0; off < bytes; off += kChunk, i ^= 1) {
+        const size_t len = std::min(kChunk, bytes - off);
+        if ((e = r.wait(i)) != hipSuccess) return e;  // the slot's previous DMA has drained
+        par_memcpy(r.slot[i], (const char*)h + off, len);
+        if ((e = hipMemcpyAsync((char*)d + off, r.slot[i], len, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+        if ((e = hipEventRecord(r.ev[i], s)) != hipSuccess) return e;
+        r.pending[i] = true;
+    }
+    return hipSuccess;
+}
+
+hipError_t copy_d2h_staged(void* h, const void* d, size_t bytes, hipStream_t s) {
+    if (bytes < kDirectBelow || !env_on("KN_HOST_STAGE", true)) {
+        hipError_t e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
+        return e != hipSuccess ? e : hipStreamSynchronize(s);
+    }
+    Ring& r = ring();
+    std::lock_guard<std::mutex> lock(r.mu);
+    hipError_t e = r.ready();
+    if (e != hipSuccess) {
+        if ((e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        return hipStreamSynchronize(s);
+    }
+    for (int i = 0; i < 2; ++i)
+        if ((e = r.wait(i)) != hipSuccess) return e;
+    const size_t nchunks = (bytes + kChunk - 1) / kChunk;
+    auto issue = [&](size_t c) -> hipError_t {
+        const int i = (int)(c & 1);
+        const size_t off = c * kChunk, len = std::min(kChunk, bytes - off);
+        hipError_t x = hipMemcpyAsync(r.slot[i], (const char*)d + off, len, hipMemcpyDeviceToHost, s);
+        if (x != hipSuccess) return x;
+        if ((x = hipEventRecord(r.ev[i], s)) != hipSuccess) return x;
+        r.pending[i] = true;
+        return hipSuccess;
+    };
+    if ((e = issue(0)) != hipSuccess) return e;
+    for (size_t c = 0; c < nchunks; ++c) {
+        // chunk c + 1 streams into the other slot while the host drains chunk c
+        if (c + 1 < nchunks && (e = issue(c + 1)) != hipSuccess) return e;
+        const int i = (int)(c & 1);
+        if ((e = r.wait(i)) != hipSuccess) return e;
+        const size_t off = c * kChunk, len = std::min(kChunk, bytes - off);
+        par_memcpy((char*)h + off, r.slot[i], len);
+    }
+    return hipSuccess;
+}
+
+void* arena_acquire(int device, size_t bytes, size_t* got) {
+    if (!env_on("KN_ARENA_CACHE", true)) return nullptr;
+    std::lock_guard<std::mutex> lock(g_pool_mu);
+    int best = -1;
+    for (int i = 0; i < (int)g_pool.size(); ++i) {
+        const Cached& c = g_pool[i];
+        if (c.dev == device && c.bytes >= bytes && c.bytes <= 2 * bytes + (64u << 20) &&
+            (best < 0 || c.bytes < g_pool[best].bytes))
+            best = i;
+    }
+    if (best < 0) return nullptr;
+    void* p = g_pool[best].p;
+    *got = g_pool[best].bytes;
+    g_pool.erase(g_pool.begin() + best);
+    return p;
+}
+
+void arena_release(int device, void* p, size_t bytes) {
+    if (!p) return;
+    if (env_on("KN_ARENA_CACHE", true)) {
+        std::lock_guard<std::mutex> lock(g_pool_mu);
+        size_t total = bytes;
+        int same = 0;
+        for (const Cached& c : g_pool) {
+            total += c.bytes;
+            same += c.dev == device ? 1 : 0;
+        }
+        if (total <= kPoolMaxBytes && same < kPoolPerDevice) {
+            g_pool.push_back({device, p, bytes});
+            return;
+        }
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    (void)hipFree(p);
+    (void)hipSetDevice(cur);
+}
+
+void arena_release_all() {
+    std::lock_guard<std::mutex> lock(g_pool_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (const Cached& c : g_pool) {
+        (void)hipSetDevice(c.dev);
+        (void)hipFree(c.p);
+    }
+    g_pool.clear();
+    (void)hipSetDevice(cur);
+}
+
+}  // namespace kn

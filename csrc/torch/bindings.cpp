@@ -638,7 +638,7 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     const int64_t npts = pg[0].size(0);
     float fext[3] = {(float)ext[0], (float)ext[1], (float)ext[2]};
     const int th[3] = {0, 0, 0};
-    const kn::AutoParams ap = kn::auto_params((int)npts, (int)k, (float)ppc, th, 0, fext);
+    kn::AutoParams ap = kn::auto_params((int)npts, (int)k, (float)ppc, th, 0, fext);
     std::vector<int64_t> dims = {ap.dims[0], ap.dims[1], ap.dims[2]};
     if (dims_hint.has_value()) {
         TORCH_CHECK(dims_hint->size() == 3 && (*dims_hint)[0] > 0 && (*dims_hint)[1] > 0 && (*dims_hint)[2] > 0,
@@ -692,6 +692,11 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
                                              reinterpret_cast<unsigned*>(uncert.data_ptr<int>()),
                                              c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
         return {pg[0], pg[1], tq[0], tq[1], tq[2], g[0], g[1], g[3], g[2], uncert, dims_t, tree_t};
+    }
+    if (dims[0] != ap.dims[0] || dims[1] != ap.dims[1] || dims[2] != ap.dims[2]) {
+        // a refined grid (this step's or the validated step's hint): isotropic, xsub 1
+        ap.tile[0] = std::max(1, ap.tile[0] / std::max(1, ap.xsub));
+        ap.xsub = 1;
     }
     auto q = query(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
                    ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid, counters, 0, ap.xsub);

@@ -98,7 +98,10 @@ def build_grid(points: torch.Tensor, k: int = 16, plan: Optional[Plan] = None,
         dims = C.refine_dims(list(plan.dims), w, int(k), float(points_per_cell), n, plan.xsub)
         if dims is None:
             break
-        plan = Plan(list(dims), list(plan.tile), plan.halo, plan.lds_capacity, plan.lds_bytes, plan.xsub)
+        # refined grids are isotropic (xsub 1)
+        tile = [max(1, plan.tile[0] // plan.xsub), plan.tile[1], plan.tile[2]]
+        plan = Plan(list(dims), tile, plan.halo, plan.lds_capacity,
+                    int(C.query_lds_bytes(tile, plan.halo, plan.lds_capacity, 1)), 1)
         s, cs, perm, geom = C.build(points, list(plan.dims), False, bx)
         refined = True
     if probe and deterministic:

@@ -321,3 +321,47 @@ def test_capi_multi_balanced_forwarding_persistent():
     check(moved, od2)
     h = C.c_void_p(m)
     lib.kn_free_multi(C.byref(h))
+
+
+@pytest.mark.gpu
+def test_capi_staged_host_copies_and_arena_cache(monkeypatch):
+    """kn_prepare from host points and the malloc'd getters go through the pinned staging ring
+    (csrc/runtime/hostio.cpp) for copies >= 1 MiB; kn_free parks the device arena for the next
+    kn_prepare. Results equal those of the direct (unstaged, uncached) path byte for byte."""
+    lib = _lib()
+    lib.kn_release_cached_memory.restype = None
+    libc = C.CDLL(None)
+    libc.free.argtypes = [C.c_void_p]
+    n, k = 300_000, 16  # 3.6 MB of points, 19 MB of rows: several 4 MiB chunks each way
+    pts = (np.random.default_rng(7).random((n, 3), dtype=np.float32) * 1000.0).astype(np.float32)
+
+    def run():
+        cfg = lib.kn_default_config()
+        cfg.k = k
+        cfg.verbose = 0
+        kp = lib.kn_prepare_ex(pts.ctypes.data, n, C.byref(cfg))
+        assert kp, lib.kn_last_error()
+        assert lib.kn_solve_ex(kp) == 0, lib.kn_last_error()
+        out = []
+        for getter, cnt, ty in (("kn_get_knearests", n * k, np.uint32), ("kn_get_permutation", n, np.uint32),
+                                ("kn_get_points", n * 3, np.float32)):
+            ptr = getattr(lib, getter)(kp)
+            assert ptr, getter
+            out.append(np.ctypeslib.as_array(ptr, shape=(cnt,)).astype(ty).copy())
+            libc.free(C.cast(ptr, C.c_void_p))
+        pp = C.pointer(kp)
+        lib.kn_free(pp)
+        return out
+
+    monkeypatch.setenv("KN_HOST_STAGE", "0")
+    monkeypatch.setenv("KN_ARENA_CACHE", "0")
+    ref = run()
+    monkeypatch.setenv("KN_HOST_STAGE", "1")
+    monkeypatch.setenv("KN_ARENA_CACHE", "1")
+    for _ in range(3):  # the second and third prepares take the cached arena
+        got = run()
+        for a, b in zip(ref, got):
+            assert np.array_equal(a, b)
+    # stored points are a permutation of the input
+    assert np.array_equal(np.sort(got[2].reshape(-1, 3), axis=0), np.sort(pts, axis=0))
+    lib.kn_release_cached_memory()

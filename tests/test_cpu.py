@@ -100,12 +100,15 @@ def test_normalize_matches_reference_rule():
 def test_plan_auto_reference_density():
     p = kn.Plan.auto(900_000, 16)
     # ~3.4 points per cell (reference knearests.cu:249 uses 3.1), rounded to whole 4-cell tiles:
-    # (900000/3.4)^(1/3) = 64.2 -> 64
-    assert p.dims == [64, 64, 64]
+    # (900000/3.4)^(1/3) = 64.2 -> 64; K <= 16 grids split x into 2 sub-cells (AutoParams::xsub)
+    assert p.xsub == 2 and p.dims == [128, 64, 64] and p.tile == [8, 4, 4]
+    assert kn.Plan.auto(900_000, 16, xsub=1).dims == [64, 64, 64]
     q = kn.Plan.auto(10_000_000, 32)
-    assert q.tile == [4, 4, 4] and all(d % t == 0 for d, t in zip(q.dims, q.tile))
+    assert q.xsub == 1 and q.tile == [4, 4, 4] and all(d % t == 0 for d, t in zip(q.dims, q.tile))
     assert kn.Plan.auto(900_000, 50).halo == 2
-    assert kn.Plan.auto(1000, 8).dims == [7, 7, 7]  # small grids are not rounded
+    assert kn.Plan.auto(1000, 8).dims == [14, 7, 7]  # small grids are not rounded
+    # x sub-cells keep the LDS plan within 4 workgroups per CU
+    assert p.lds_bytes <= 40 * 1024
     assert p.halo >= 1 and p.lds_capacity >= 1024 and p.lds_bytes <= 160 * 1024
 
 
