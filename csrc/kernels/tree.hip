@@ -35,7 +35,12 @@ constexpr int kExactGrid = 512;
 // query near a cluster keeps a loose bound until the cluster's nearest leaves shrink it, which
 // only the depth-first order does); per-lane box distances stacked in LDS instead of re-loading a
 // popped node's box (profiles/ab_r3_tree_stackdist.jsonl, K=16 +16 %: the 10 KB per wave cost
-// more in resident waves than the loads it saved).
+// more in resident waves than the loads it saved). Session 2: a leaf-filtered variant (the traversal
+// only lists the leaves it enters; every 32 listed leaves each lane box-tests them against its own
+// bound and scans just the ones it needs with per-lane 4-wide global gathers) lost everywhere
+// (profiles/ab_r3_tree_filter.jsonl, K=16: clustered 1.59 -> 2.29 ms, surface 0.96 -> 1.34,
+// uniform 1.36 -> 1.88; K=50 +10-40 %): the divergent global-memory gathers and the bounds frozen
+// between chunks (+20 % listed leaves) cost more than the broadcast union stream of staged leaves.
 
 struct TArgs {
     const float4* pts;

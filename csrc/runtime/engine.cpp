@@ -32,7 +32,13 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     if (cfg_.k <= 0) cfg_.k = KN_DEFAULT_K;
 }
 
-Engine::~Engine() { release(); }
+Engine::~Engine() {
+    const auto t0 = std::chrono::steady_clock::now();
+    release();
+    if (std::getenv("KN_PREP_TIMING"))
+        fprintf(stderr, "kn_free: release %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+}
 
 void Engine::release() {
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
@@ -67,6 +73,7 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     if (cfg_.k < 1 || cfg_.k > KN_MAX_K) return fail(KN_ERR_INVALID_ARGUMENT, "k out of range [1,128]");
     kn_status st;
     if ((st = check(hipSetDevice(cfg_.device), "hipSetDevice")) != KN_OK) return st;
+    const auto ta0 = std::chrono::steady_clock::now();
     if (!stream_) {
         if ((st = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate")) != KN_OK) return st;
         for (auto& e : ev_)
@@ -117,6 +124,9 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
             arena_bytes_ = bytes;
         }
     }
+    if (std::getenv("KN_PREP_TIMING"))
+        fprintf(stderr, "allocate: stream/events + arena %.3f ms (arena %zu B)\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta0).count(), arena_bytes_);
     char* p = arena_;
     points_ = carve<float>(p, (size_t)n * 3);
     bbox_ = carve<unsigned>(p, kBBoxWords);
@@ -289,6 +299,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
                                   ? copy_h2d_staged(points_, src, (size_t)n * 12, stream_)
                                   : hipMemcpyAsync(points_, src, (size_t)n * 12, kind, stream_);
         if (n > 0 && (st = check(ce, "copy points")) != KN_OK) return st;
+        const auto tc = clk::now();
         (void)hipEventRecord(ev_[0], stream_);
         points3_valid_ = false;
         // adaptive: probe grids are binned without the in-cell order (see launch_cell_sort)
@@ -298,6 +309,11 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
         (void)hipEventRecord(ev_[1], stream_);
         if ((st = check(hipEventSynchronize(ev_[1]), "build sync")) != KN_OK) return st;
         (void)hipEventElapsedTime(&ms_build_, ev_[0], ev_[1]);
+        if (std::getenv("KN_PREP_TIMING")) {
+            auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
+            fprintf(stderr, "prepare round %d: copy enqueue %.3f ms, build + sync %.3f ms (device build %.3f ms)\n", round,
+                    ms(tc - t1), ms(clk::now() - tc), ms_build_);
+        }
         if (!cfg_.adaptive || n == 0) break;
         double w = 0.0;
         int nd[3];
@@ -320,7 +336,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined));
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }  // grid or tree step of the new plan
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
-    if (cfg_.verbose > 1) {
+    if (cfg_.verbose > 1 || std::getenv("KN_PREP_TIMING")) {
         const auto t2 = clk::now();
         auto ms = [](clk::duration d) { return std::chrono::duration<double, std::milli>(d).count(); };
         fprintf(stderr, "kn_prepare host phases: allocate %.3f ms, upload + build + plan %.3f ms\n", ms(t1 - t0),

@@ -25,7 +25,7 @@ for gen in gens:
         plan = ops.Plan.auto(n, k)
         s, cs, perm, geom = A.build(pts, plan.dims, True, None)
         args = lambda: (s, cs, geom, plan.dims, k, n, None, [-inf, -inf, -inf, inf, inf, inf], plan.tile, plan.halo,
-                        plan.lds_capacity, True, True, 0)
+                        plan.lds_capacity, True, True, 0, None, 0, None, 0, plan.xsub)
         ra = A.query(*args())
         rb = B.query(*args())
         torch.cuda.synchronize()

@@ -26,3 +26,5 @@ for st in 0 1; do
 done
 KN_LOG=DEBUG timeout -k 10 100 ./bin/knn_cli --uniform 900000 --k 16 --api-bench 2 > /dev/null 2> $O/api_phases.log || true
 grep "host phases" $O/api_phases.log | tail -3
+timeout -k 10 400 python scripts/ab_tree.py tfilt 900000 16,50 clustered,surface,uniform 6 > $O/ab_tfilt.jsonl 2>> $O/err.log || { echo ABT_FAIL; tail -20 $O/err.log; cat $O/ab_tfilt.jsonl; exit 1; }
+cat $O/ab_tfilt.jsonl
