@@ -44,16 +44,49 @@ void Engine::release() {
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     // the arena goes back to the process-wide cache (hostio.hpp): the next kn_prepare of a similar
     // size skips hipMalloc
+    if (stream_) (void)hipStreamSynchronize(stream_);
     if (arena_) { arena_release(cfg_.device, arena_, arena_bytes_); arena_ = nullptr; arena_bytes_ = 0; }
-    if (out_idx_) { (void)hipFree(out_idx_); out_idx_ = nullptr; }
-    if (out_dist_) { (void)hipFree(out_dist_); out_dist_ = nullptr; }
-    if (inv_perm_) { (void)hipFree(inv_perm_); inv_perm_ = nullptr; }
-    if (knn_stored_) { (void)hipFree(knn_stored_); knn_stored_ = nullptr; }
-    if (points3_) { (void)hipFree(points3_); points3_ = nullptr; }
-    if (tree_ws_) { (void)hipFree(tree_ws_); tree_ws_ = nullptr; }
-    if (tree_nodes_) { (void)hipFree(tree_nodes_); tree_nodes_ = nullptr; }
-    for (auto& e : ev_) if (e) { (void)hipEventDestroy(e); e = nullptr; }  // reference leaks these (D6)
-    if (stream_) { (void)hipStreamDestroy(stream_); stream_ = nullptr; }
+    if (out_idx_) { dfree(out_idx_); out_idx_ = nullptr; }
+    if (out_dist_) { dfree(out_dist_); out_dist_ = nullptr; }
+    if (inv_perm_) { dfree(inv_perm_); inv_perm_ = nullptr; }
+    if (knn_stored_) { dfree(knn_stored_); knn_stored_ = nullptr; }
+    if (points3_) { dfree(points3_); points3_ = nullptr; }
+    if (tree_ws_) { dfree(tree_ws_); tree_ws_ = nullptr; }
+    if (tree_nodes_) { dfree(tree_nodes_); tree_nodes_ = nullptr; }
+    // the (idle) stream and its events go back to the pool; the reference leaks its events (D6)
+    if (stream_) {
+        (void)hipStreamSynchronize(stream_);
+        StreamSet ss;
+        ss.stream = stream_;
+        for (int i = 0; i < 4; ++i) ss.ev[i] = ev_[i];
+        streamset_release(cfg_.device, ss);
+    }
+    stream_ = nullptr;
+    for (auto& e : ev_) e = nullptr;
+}
+
+hipError_t Engine::dmalloc(void** p, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 1);
+    size_t got = 0;
+    if (void* c = arena_acquire(cfg_.device, bytes, &got)) {
+        *p = c;
+        dsize_[c] = got;
+        return hipSuccess;
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) dsize_[*p] = bytes;
+    return e;
+}
+
+void Engine::dfree(void* p) {
+    if (!p) return;
+    // a parked block may go to another engine (another stream) at once: this engine's pending
+    // work on it must have drained
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    auto it = dsize_.find(p);
+    if (it == dsize_.end()) { (void)hipFree(p); return; }
+    arena_release(cfg_.device, p, it->second);
+    dsize_.erase(it);
 }
 
 kn_status Engine::fail(kn_status s, const std::string& msg) {
@@ -75,9 +108,11 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     if ((st = check(hipSetDevice(cfg_.device), "hipSetDevice")) != KN_OK) return st;
     const auto ta0 = std::chrono::steady_clock::now();
     if (!stream_) {
-        if ((st = check(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate")) != KN_OK) return st;
-        for (auto& e : ev_)
-            if ((st = check(hipEventCreate(&e), "hipEventCreate")) != KN_OK) return st;
+        // from the process-wide pool (hostio.hpp): stream + event creation cost 2-8 ms per engine
+        StreamSet ss;
+        if ((st = check(streamset_acquire(cfg_.device, &ss), "hipStreamCreate")) != KN_OK) return st;
+        stream_ = ss.stream;
+        for (int i = 0; i < 4; ++i) ev_[i] = ss.ev[i];
     }
     ap_ = auto_params(n, cfg_.k, cfg_.points_per_cell, cfg_.tile, cfg_.halo, nullptr);
     if (dims_override && refined) {
@@ -112,7 +147,10 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     bytes += align_up(sizeof(unsigned long long));
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (bytes > arena_bytes_) {
-        if (arena_) arena_release(cfg_.device, arena_, arena_bytes_);
+        if (arena_) {
+            if (stream_) (void)hipStreamSynchronize(stream_);
+            arena_release(cfg_.device, arena_, arena_bytes_);
+        }
         arena_ = nullptr;
         arena_bytes_ = 0;
         size_t got = 0;
@@ -145,7 +183,7 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     // outputs
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
                      (void**)&points3_})
-        if (*q) { (void)hipFree(*q); *q = nullptr; }
+        if (*q) { dfree(*q); *q = nullptr; }
     // the N x K outputs are allocated on the first whole solve (ensure_outputs): a caller that
     // only solves query ranges (solve_range, kn_solve_range) never holds them
     const size_t nk = std::max<size_t>(1, (size_t)n * cfg_.k);
@@ -231,18 +269,18 @@ kn_status Engine::ensure_tree() {
     kn_status st;
     const size_t need = tree_workspace_bytes(n_, ap_.dims);
     if (tree_ws_bytes_ < need) {
-        if (tree_ws_) (void)hipFree(tree_ws_);
+        if (tree_ws_) dfree(tree_ws_);
         tree_ws_ = nullptr;
         tree_ws_bytes_ = 0;
-        if ((st = check(hipMalloc(&tree_ws_, need), "hipMalloc(tree)")) != KN_OK) return st;
+        if ((st = check(dmalloc(&tree_ws_, need), "hipMalloc(tree)")) != KN_OK) return st;
         tree_ws_bytes_ = need;
     }
     const size_t nb = tree_node_bytes(n_);
     if (tree_nodes_bytes_ < nb) {
-        if (tree_nodes_) (void)hipFree(tree_nodes_);
+        if (tree_nodes_) dfree(tree_nodes_);
         tree_nodes_ = nullptr;
         tree_nodes_bytes_ = 0;
-        if ((st = check(hipMalloc(&tree_nodes_, nb), "hipMalloc(tree nodes)")) != KN_OK) return st;
+        if ((st = check(dmalloc(&tree_nodes_, nb), "hipMalloc(tree nodes)")) != KN_OK) return st;
         tree_nodes_bytes_ = nb;
     }
     return KN_OK;
@@ -366,9 +404,9 @@ kn_status Engine::upload_device(const float* d_pts, int n) {
 kn_status Engine::ensure_outputs() {
     const size_t nk = std::max<size_t>(1, (size_t)n_ * cfg_.k);
     kn_status st;
-    if (!out_idx_ && (st = check(hipMalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
+    if (!out_idx_ && (st = check(dmalloc(&out_idx_, nk * sizeof(unsigned)), "hipMalloc(knn)")) != KN_OK) return st;
     if (cfg_.with_distances && !out_dist_ &&
-        (st = check(hipMalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
+        (st = check(dmalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
         return st;
     if (use_tree_ && (st = ensure_tree()) != KN_OK) return st;
     return KN_OK;
@@ -440,7 +478,7 @@ kn_status Engine::set_k(int k) {
         ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity, ap_.xsub);
     }
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_})
-        if (*q) { (void)hipFree(*q); *q = nullptr; }
+        if (*q) { dfree(*q); *q = nullptr; }
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     solved_ = stored_valid_ = false;
     return KN_OK;
@@ -526,9 +564,9 @@ unsigned* Engine::d_knn_stored() {
     // ids only: the reference exposes no distances (knearests.h:3-16), so the stored-space
     // distance copy is made on demand by get_distances_stored()
     const size_t nk = std::max<size_t>(1, (size_t)n_ * cfg_.k);
-    if (!inv_perm_ && check(hipMalloc(&inv_perm_, std::max<size_t>(1, n_) * sizeof(unsigned)), "hipMalloc(inv)") != KN_OK)
+    if (!inv_perm_ && check(dmalloc(&inv_perm_, std::max<size_t>(1, n_) * sizeof(unsigned)), "hipMalloc(inv)") != KN_OK)
         return nullptr;
-    if (!knn_stored_ && check(hipMalloc(&knn_stored_, nk * sizeof(unsigned)), "hipMalloc(knn_stored)") != KN_OK)
+    if (!knn_stored_ && check(dmalloc(&knn_stored_, nk * sizeof(unsigned)), "hipMalloc(knn_stored)") != KN_OK)
         return nullptr;
     if (check(launch_invert_perm(perm_, n_, inv_perm_, stream_), "invert perm") != KN_OK) return nullptr;
     if (check(launch_to_stored_space(out_idx_, perm_, inv_perm_, n_, cfg_.k, knn_stored_, nullptr, nullptr, stream_),
@@ -542,7 +580,7 @@ unsigned* Engine::d_knn_stored() {
 float* Engine::d_points3() {
     if (!built_) return nullptr;
     if (points3_valid_) return points3_;
-    if (!points3_ && check(hipMalloc(&points3_, std::max<size_t>(1, (size_t)n_ * 3) * sizeof(float)),
+    if (!points3_ && check(dmalloc(&points3_, std::max<size_t>(1, (size_t)n_ * 3) * sizeof(float)),
                            "hipMalloc(points3)") != KN_OK)
         return nullptr;
     if (check(launch_sorted_xyz(sorted_, n_, points3_, stream_), "sorted xyz") != KN_OK) return nullptr;
@@ -585,13 +623,13 @@ float* Engine::get_distances_stored() {
     // stored-space distances: a temporary device buffer, freed before returning
     const size_t nk = (size_t)n_ * cfg_.k;
     float* tmp = nullptr;
-    if (check(hipMalloc(&tmp, std::max<size_t>(1, nk) * sizeof(float)), "hipMalloc(dist_stored)") != KN_OK) return nullptr;
+    if (check(dmalloc(&tmp, std::max<size_t>(1, nk) * sizeof(float)), "hipMalloc(dist_stored)") != KN_OK) return nullptr;
     float* out = nullptr;
     // the id half rewrites knn_stored_ with the values it already holds
     if (check(launch_to_stored_space(out_idx_, perm_, inv_perm_, n_, cfg_.k, knn_stored_, out_dist_, tmp, stream_),
               "to stored space") == KN_OK)
         out = d2h(tmp, nk, stream_);
-    (void)hipFree(tmp);
+    dfree(tmp);
     return out;
 }
 unsigned* Engine::get_neighbors_original() {

@@ -7,6 +7,8 @@
 // * Errors are returned as kn_status + message, never exit() (reference defect D7).
 #pragma once
 
+#include <unordered_map>
+
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -114,6 +116,12 @@ private:
     hipGraphExec_t graph_ = nullptr;
     int n_ = 0, C_ = 0;
     size_t arena_bytes_ = 0;
+    // result / tree buffers through the process-wide device block cache (hostio.hpp)
+    std::unordered_map<void*, size_t> dsize_;
+    hipError_t dmalloc(void** p, size_t bytes);
+    template <class T>
+    hipError_t dmalloc(T** p, size_t bytes) { return dmalloc(reinterpret_cast<void**>(p), bytes); }
+    void dfree(void* p);
     char* arena_ = nullptr;
     float* points_ = nullptr;
     unsigned* bbox_ = nullptr;

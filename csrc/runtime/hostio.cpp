@@ -84,7 +84,7 @@ struct Cached {
 std::mutex g_pool_mu;
 std::vector<Cached> g_pool;
 constexpr size_t kPoolMaxBytes = 4ull << 30;
-constexpr int kPoolPerDevice = 2;
+constexpr int kPoolPerDevice = 8;  // an engine's arena + its result / tree buffers
 
 }  // namespace
 
@@ -180,6 +180,46 @@ void arena_release(int device, void* p, size_t bytes) {
     (void)hipSetDevice(device);
     (void)hipFree(p);
     (void)hipSetDevice(cur);
+}
+
+namespace {
+std::mutex g_ss_mu;
+std::vector<std::pair<int, StreamSet>> g_ss;
+}  // namespace
+
+hipError_t streamset_acquire(int device, StreamSet* out) {
+    {
+        std::lock_guard<std::mutex> lock(g_ss_mu);
+        for (size_t i = 0; i < g_ss.size(); ++i)
+            if (g_ss[i].first == device) {
+                *out = g_ss[i].second;
+                g_ss.erase(g_ss.begin() + (long)i);
+                return hipSuccess;
+            }
+    }
+    StreamSet s;
+    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    for (auto& ev : s.ev)
+        if (e == hipSuccess) e = hipEventCreate(&ev);
+    if (e != hipSuccess) {
+        for (auto& ev : s.ev) if (ev) (void)hipEventDestroy(ev);
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        return e;
+    }
+    *out = s;
+    return hipSuccess;
+}
+
+void streamset_release(int device, const StreamSet& s) {
+    if (!s.stream) return;
+    {
+        std::lock_guard<std::mutex> lock(g_ss_mu);
+        int same = 0;
+        for (const auto& p : g_ss) same += p.first == device ? 1 : 0;
+        if (same < 8) { g_ss.emplace_back(device, s); return; }
+    }
+    for (auto ev : s.ev) if (ev) (void)hipEventDestroy(ev);
+    (void)hipStreamDestroy(s.stream);
 }
 
 void arena_release_all() {

@@ -5,10 +5,12 @@
 // * Staged copies: a process-wide pinned ring (2 slots x 4 MiB, allocated once). Host memcpy of
 //   chunk i into a slot (OpenMP threads) overlaps the DMA of chunk i-1; the runtime's own pageable
 //   path copies through its staging buffer with one thread. Copies below 1 MiB go direct.
-// * Arena cache: kn_free / Engine teardown parks the engine's device arena (at most 2 per device,
-//   <= 4 GiB in total) and the next Engine of a size it fits (within 2x) takes it instead of
-//   hipMalloc + hipFree per kn_prepare. KN_ARENA_CACHE=0 disables it, kn_release_cached_memory()
-//   frees it.
+// * Device block cache: kn_free / Engine teardown parks the engine's device arena and result /
+//   tree buffers (at most 8 blocks per device, <= 4 GiB in total) and the next Engine takes a block
+//   of a size it fits (within 2x + 64 MiB) instead of hipMalloc; a kn_prepare / kn_solve / kn_free
+//   cycle then allocates and frees nothing on the device (hipFree of the 3 N x K result buffers
+//   alone took ~7 ms per kn_free at 900K, K=16). KN_ARENA_CACHE=0 disables it,
+//   kn_release_cached_memory() frees it.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -23,10 +25,20 @@ hipError_t copy_h2d_staged(void* d, const void* h, size_t bytes, hipStream_t s);
 // returns when the host buffer holds the data.
 hipError_t copy_d2h_staged(void* h, const void* d, size_t bytes, hipStream_t s);
 
-// Device arena cache (see above). acquire: a cached block of >= bytes (and <= 2 x bytes) on
-// `device`, or nullptr; *got = its size. release: park or free.
+// Device block cache (see above). acquire: a cached block of >= bytes (and <= 2 x bytes + 64 MiB)
+// on `device`, or nullptr; *got = its size. release: park or free.
 void* arena_acquire(int device, size_t bytes, size_t* got);
 void arena_release(int device, void* p, size_t bytes);
 void arena_release_all();
+
+// Stream + 4 timing events of an engine from a per-device pool (creating a HIP stream and its
+// events cost 2-8 ms per kn_prepare on MI355X, measured with KN_PREP_TIMING): acquire creates when
+// the pool is empty; release parks up to 8 sets per device (the stream must be idle).
+struct StreamSet {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+hipError_t streamset_acquire(int device, StreamSet* out);
+void streamset_release(int device, const StreamSet& s);
 
 }  // namespace kn
