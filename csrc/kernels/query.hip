@@ -83,6 +83,7 @@ struct TileArgs {
     // side of the query's cell; each lane mirrors it to its own position (row_order_table)
     unsigned row_order[32];
     int row_mirror;  // 1: each lane mirrors the table to its own cell position (distance order)
+    int n_outer;     // KN_OUTER_PACK: row_order holds the n_outer rows of Chebyshev ring >= 2
 };
 constexpr int kRowOrderMax = 128;
 
@@ -122,6 +123,16 @@ constexpr int kRowOrderMax = 128;
 // lane of a wave visits the same relative row, so the spans of one row iteration stay alike).
 #ifndef KN_ROW_RING
 #define KN_ROW_RING 0
+#endif
+// KN_OUTER_PACK=1 (lane walk, K <= 40, the fixed order): the 3x3 rows around the query's row stay
+// row-synchronous, the outer rows (Chebyshev ring >= 2 of the (2H+1)^2 block) are PACKED: each
+// lane marks the outer rows its bound still reaches (a 64-bit mask, distances from 8 per-lane
+// slab gaps selected by the uniform table entry), then iteration i visits every lane's i-th marked
+// row. The row-synchronous loop paid, for each of up to 16 outer rows, the longest span of the
+// few lanes whose bound was still wide (numpy replay: outer rows 56 candidate steps over 9.2 row
+// iterations per wave at K=16 -> 26 over 3.8).
+#ifndef KN_OUTER_PACK
+#define KN_OUTER_PACK 0
 #endif
 // Default AutoParams::xsub of the tile path for K <= KN_XSUB_MAX_K. Interleaved A/B at 900K
 // uniform (profiles/ab_r3_xsub.jsonl): xsub 2 query K=8 0.207 -> 0.198, K=16 0.305 -> 0.292 ms
@@ -480,13 +491,15 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 body(lane_span(y, z, lx0, lx1));
             }
             } else {
-            for (int tz_ = 0; tz_ < side; ++tz_) {
+            const bool pack = KN_OUTER_PACK && a.n_outer > 0;
+            const int sidein = pack ? 3 : side;  // rows visited row-synchronously
+            for (int tz_ = 0; tz_ < sidein; ++tz_) {
                 const int z = cz + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
                 const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
                 const float dz2 = dzb * dzb;
                 const bool zin = live && z >= hz0 && z <= hz1;
                 if (!__builtin_amdgcn_ballot_w64(zin && dz2 <= lane_tau())) continue;
-                for (int ty_ = 0; ty_ < side; ++ty_) {
+                for (int ty_ = 0; ty_ < sidein; ++ty_) {
                     const int y = cy + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
                     const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
                     const float dyz2 = fmaf(dyb, dyb, dz2);
@@ -496,6 +509,56 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                         if (tau == INFINITY) {
                             lx0 = hx0; lx1 = hx1;
                         } else {
+                            const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                            lx0 = max(hx0, cell_coord(g, 0, qx - rr) - sx0);
+                            lx1 = min(hx1, cell_coord(g, 0, qx + rr) - sx0);
+                        }
+                    }
+                    if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
+                    body(lane_span(y, z, lx0, lx1));
+                }
+            }
+            if (KN_OUTER_PACK && pack) {
+                // per-lane slab gaps of offsets +-1, +-2 on y and z (the table holds ring >= 2 rows
+                // with |offset| <= H; offsets beyond +-2 use the exact slab distance)
+                const float fy = (qy - g.origin[1]) * g.inv_cell[1] - (float)(sy0 + cy);
+                const float fz = (qz - g.origin[2]) * g.inv_cell[2] - (float)(sz0 + cz);
+                const int sgy = fy < 0.5f ? -1 : 1, sgz = fz < 0.5f ? -1 : 1;
+                auto gap = [&](int axis, int o) {
+                    const int c = axis == 1 ? cy + sgy * o : cz + sgz * o;
+                    const int s0c = axis == 1 ? sy0 : sz0;
+                    const float qv = axis == 1 ? qy : qz;
+                    const int lo = axis == 1 ? hy0 : hz0, hi = axis == 1 ? hy1 : hz1;
+                    return (c >= lo && c <= hi) ? slab_dist(g, axis, qv, s0c + c, s0c + c) : INFINITY;
+                };
+                const float y1p = gap(1, 1), y1m = gap(1, -1), y2p = gap(1, 2), y2m = gap(1, -2);
+                const float z1p = gap(2, 1), z1m = gap(2, -1), z2p = gap(2, 2), z2m = gap(2, -2);
+                const float y0 = gap(1, 0), z0 = gap(2, 0);
+                auto sel = [](int o, float m2, float m1, float c0, float p1, float p2, float far) {
+                    return o == 0 ? c0 : o == 1 ? p1 : o == -1 ? m1 : o == 2 ? p2 : o == -2 ? m2 : far;
+                };
+                const float tau0 = lane_tau();
+                unsigned long long mask = 0;
+                for (int t = 0; t < a.n_outer; ++t) {
+                    const unsigned e = (a.row_order[t >> 2] >> ((t & 3) * 8)) & 255u;  // uniform
+                    const int oy = (int)(e & 15u) - 8, oz = (int)(e >> 4) - 8;
+                    const float gy = sel(oy, y2m, y1m, y0, y1p, y2p, gap(1, oy));
+                    const float gz = sel(oz, z2m, z1m, z0, z1p, z2p, gap(2, oz));
+                    mask |= (live && fmaf(gy, gy, gz * gz) <= tau0) ? (1ull << t) : 0ull;
+                }
+                while (__builtin_amdgcn_ballot_w64(mask != 0ull)) {
+                    int y = cy, z = cz, lx0 = 0, lx1 = -1;
+                    if (mask) {
+                        const int t = __builtin_ctzll(mask);
+                        mask &= mask - 1;
+                        const unsigned e = (a.row_order[t >> 2] >> ((t & 3) * 8)) & 255u;
+                        y = cy + sgy * ((int)(e & 15u) - 8);
+                        z = cz + sgz * ((int)(e >> 4) - 8);
+                        const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
+                        const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
+                        const float dyz2 = fmaf(dyb, dyb, dzb * dzb);
+                        const float tau = lane_tau();
+                        if (dyz2 <= tau) {
                             const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
                             lx0 = max(hx0, cell_coord(g, 0, qx - rr) - sx0);
                             lx1 = min(hx1, cell_coord(g, 0, qx + rr) - sx0);
@@ -1812,6 +1875,22 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             const bool ring = KN_ROW_RING && !(KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && full));
             row_order_table(a.H, a.row_order, ring);
             a.row_mirror = ring ? 0 : 1;
+            a.n_outer = 0;
+            if (KN_OUTER_PACK && !full && !ring && !(KN_ROW_ORDER == 1) && a.H >= 2 &&
+                (2 * a.H + 1) * (2 * a.H + 1) - 9 <= 64) {
+                // the distance-sorted table minus the 3x3 rows around the query's own row
+                unsigned all[32];
+                row_order_table(a.H, all, false);
+                for (int i = 0; i < 32; ++i) a.row_order[i] = 0;
+                const int nent = (2 * a.H + 1) * (2 * a.H + 1);
+                for (int t = 0; t < nent; ++t) {
+                    const unsigned e = (all[t >> 2] >> ((t & 3) * 8)) & 255u;
+                    const int oy = (int)(e & 15u) - 8, oz = (int)(e >> 4) - 8;
+                    if (std::max(std::abs(oy), std::abs(oz)) < 2) continue;
+                    a.row_order[a.n_outer >> 2] |= e << ((a.n_outer & 3) * 8);
+                    ++a.n_outer;
+                }
+            }
         }
         int sb = 0;
         while ((1 << sb) < q.lds_capacity) ++sb;

@@ -89,7 +89,7 @@ constexpr int kPoolPerDevice = 8;  // an engine's arena + its result / tree buff
 }  // namespace
 
 hipError_t copy_h2d_staged(void* d, const void* h, size_t bytes, hipStream_t s) {
-    if (bytes < kDirectBelow || !env_on("KN_HOST_STAGE", true))
+    if (bytes < kDirectBelow || !env_on("KN_HOST_STAGE", false))
         return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
     Ring& r = ring();
     std::lock_guard<std::mutex> lock(r.mu);
@@ -108,7 +108,7 @@ hipError_t copy_h2d_staged(void* d, const void* h, size_t bytes, hipStream_t s) 
 }
 
 hipError_t copy_d2h_staged(void* h, const void* d, size_t bytes, hipStream_t s) {
-    if (bytes < kDirectBelow || !env_on("KN_HOST_STAGE", true)) {
+    if (bytes < kDirectBelow || !env_on("KN_HOST_STAGE", false)) {
         hipError_t e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
         return e != hipSuccess ? e : hipStreamSynchronize(s);
     }

@@ -2,9 +2,11 @@
 // reference-API path (kn_prepare from host points, the malloc'd getters; reference
 // knearests.cu:205-231 gpuMalloc* helpers and :410-438 getters).
 //
-// * Staged copies: a process-wide pinned ring (2 slots x 4 MiB, allocated once). Host memcpy of
-//   chunk i into a slot (OpenMP threads) overlaps the DMA of chunk i-1; the runtime's own pageable
-//   path copies through its staging buffer with one thread. Copies below 1 MiB go direct.
+// * Staged copies (opt-in, KN_HOST_STAGE=1): a process-wide pinned ring (2 slots x 4 MiB,
+//   allocated once); host memcpy of chunk i into a slot (OpenMP threads) overlaps the DMA of chunk
+//   i-1. Measured on MI355X (profiles/api_r3_host_staging.jsonl): kn_get_knearests 3.34 -> 2.82 ms
+//   at K=16 but 7.9 -> 14.3 ms at K=50, and the whole prepare/solve/get/free cycle slower (the
+//   runtime's own pageable path already streams at 17-23 GB/s): off by default.
 // * Device block cache: kn_free / Engine teardown parks the engine's device arena and result /
 //   tree buffers (at most 8 blocks per device, <= 4 GiB in total) and the next Engine takes a block
 //   of a size it fits (within 2x + 64 MiB) instead of hipMalloc; a kn_prepare / kn_solve / kn_free
