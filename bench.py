@@ -109,11 +109,15 @@ def run_native(args) -> dict:
     info0 = e.info()
     cnt = e.counters()
     log(f"eager done: {info0} counters {cnt}")
-    e.launch_graph(args.warmup)
+    # --pipeline: software-pipelined steps (kn::Engine::launch_pipelined): step i+1's binning runs
+    # on a second stream while step i queries (two grid sets); every step still bins and queries
+    # the whole cloud
+    launch = e.launch_pipelined if args.pipeline else e.launch_graph
+    launch(args.warmup)
     e.sync()
     log("warmup done")
     t0 = time.perf_counter()
-    e.launch_graph(args.steps)
+    launch(args.steps)
     e.sync()
     dt = time.perf_counter() - t0
     log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
@@ -379,6 +383,8 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--layout", choices=["scattered", "partitioned"], default="partitioned")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="native 1-GPU path: overlap step i+1's binning with step i's queries (two grid sets)")
     ap.add_argument("--path", choices=["native", "torch"], default="native",
                     help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
     ap.add_argument("--no-check", action="store_true")
@@ -446,7 +452,8 @@ def main() -> int:
         n_gpus = 1
         extra = {"ms_build": round(r["ms_build"], 4), "ms_solve": round(r["ms_solve"], 4),
                  "grid": r.get("dims"), "query_algo": r.get("algo", "grid"),
-                 "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph, "path": args.path}
+                 "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph, "path": args.path,
+                 "pipelined": bool(args.pipeline)}
     ms = r["t"] / args.steps * 1e3
     qps = r["n_total"] * args.steps / r["t"]
     line = {

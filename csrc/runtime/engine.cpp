@@ -42,6 +42,7 @@ Engine::~Engine() {
 
 void Engine::release() {
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    drop_pipeline();
     // the arena goes back to the process-wide cache (hostio.hpp): the next kn_prepare of a similar
     // size skips hipMalloc
     if (stream_) (void)hipStreamSynchronize(stream_);
@@ -146,6 +147,7 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     bytes += align_up(kNumCounters * sizeof(unsigned));
     bytes += align_up(sizeof(unsigned long long));
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    drop_pipeline();
     if (bytes > arena_bytes_) {
         if (arena_) {
             if (stream_) (void)hipStreamSynchronize(stream_);
@@ -372,7 +374,8 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     // 1.27 vs 0.96 + 0.27; profiles/diag_r2_tree.jsonl): the tree path takes it.
     refined_ = refined;
     use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined));
-    if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }  // grid or tree step of the new plan
+    if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    drop_pipeline();  // grid or tree step of the new plan
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
     if (cfg_.verbose > 1 || std::getenv("KN_PREP_TIMING")) {
         const auto t2 = clk::now();
@@ -480,6 +483,7 @@ kn_status Engine::set_k(int k) {
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_})
         if (*q) { dfree(*q); *q = nullptr; }
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    drop_pipeline();
     solved_ = stored_valid_ = false;
     return KN_OK;
 }
@@ -511,6 +515,123 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     if (ms_per_iter) *ms_per_iter = iters > 0 ? ms / iters : 0.f;
     solved_ = true;
     stored_valid_ = points3_valid_ = false;  // the graph rebuilt the grid
+    return KN_OK;
+}
+
+void Engine::drop_pipeline() {
+    for (auto& g : pgraph_)
+        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    if (bstream_) {
+        (void)hipStreamSynchronize(bstream_);
+        StreamSet ss;
+        ss.stream = bstream_;
+        for (int i = 0; i < 4; ++i) ss.ev[i] = pev_[i];
+        streamset_release(cfg_.device, ss);
+        bstream_ = nullptr;
+        for (auto& e : pev_) e = nullptr;
+    }
+    if (arena2_) { dfree(arena2_); arena2_ = nullptr; }
+    alt_ = GridSet{};
+    pipe_i_ = 0;
+}
+
+void Engine::swap_grid_set() {
+    std::swap(bbox_, alt_.bbox); std::swap(geom_, alt_.geom); std::swap(cell_count_, alt_.cell_count);
+    std::swap(cell_scan_, alt_.cell_scan); std::swap(block_sums_, alt_.block_sums);
+    std::swap(cell_start_, alt_.cell_start); std::swap(cell_rank_, alt_.cell_rank); std::swap(bin_tmp_, alt_.bin_tmp);
+    std::swap(sorted_, alt_.sorted); std::swap(perm_, alt_.perm); std::swap(fallback_, alt_.fallback);
+    std::swap(counters_, alt_.counters); std::swap(occ_, alt_.occ);
+}
+
+// Software-pipelined steps over two grid sets (s = step parity): build(i) on bstream_ after the
+// query of step i-2 released set s; query(i) on stream_ after build(i). The query kernel fills the
+// chip, and the build's five latency-bound kernels (~50 us at 900K, ~15 % of a step) run in its
+// shadow. Each of the 4 stage graphs is captured once.
+kn_status Engine::launch_pipelined(int iters) {
+    if (use_tree_ || cfg_.algo != 0) return launch_graph(iters);  // tree buffers are single
+    if (!built_) return fail(KN_ERR_STATE, "launch_pipelined() before prepare()");
+    kn_status st;
+    if ((st = ensure_outputs()) != KN_OK) return st;
+    if (!pgraph_[0]) {
+        if (!arena2_) {
+            if ((st = check(dmalloc(&arena2_, arena_bytes_), "hipMalloc(grid set 2)")) != KN_OK) return st;
+            // the same carve as allocate(); points_ stays shared (read-only input of every build)
+            const int C = C_, n = n_;
+            const size_t nb = scan_block_count(C) + 1;
+            char* p = arena2_;
+            (void)carve<float>(p, (size_t)n * 3);
+            alt_.bbox = carve<unsigned>(p, kBBoxWords);
+            alt_.geom = carve<GridGeom>(p, 1);
+            alt_.cell_count = carve<int>(p, C + 1);
+            alt_.cell_scan = carve<int>(p, C + 1);
+            alt_.cell_start = carve<int>(p, C + 1);
+            alt_.block_sums = carve<int>(p, nb);
+            alt_.bin_tmp = carve<float4>(p, n);
+            alt_.cell_rank = reinterpret_cast<int2*>(alt_.bin_tmp);
+            alt_.sorted = carve<float4>(p, n);
+            alt_.perm = carve<unsigned>(p, n);
+            alt_.fallback = carve<unsigned>(p, n);
+            alt_.counters = carve<unsigned>(p, kNumCounters);
+            alt_.occ = carve<unsigned long long>(p, 1);
+        }
+        if (!bstream_) {
+            StreamSet ss;
+            if ((st = check(streamset_acquire(cfg_.device, &ss), "hipStreamCreate")) != KN_OK) return st;
+            bstream_ = ss.stream;
+            for (int i = 0; i < 4; ++i) pev_[i] = ss.ev[i];
+        }
+        // capture the 4 stage graphs on stream_ (a graph can be launched on any stream)
+        for (int set = 0; set < 2; ++set) {
+            if (set == 1) swap_grid_set();
+            for (int stage = 0; stage < 2; ++stage) {
+                hipGraph_t g;
+                kn_status s1 = KN_OK;
+                if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) {
+                    if (set == 1) swap_grid_set();
+                    return st;
+                }
+                s1 = stage == 0 ? build_async(true) : query_async(true);
+                hipError_t e = hipStreamEndCapture(stream_, &g);
+                if (s1 == KN_OK && e == hipSuccess) {
+                    e = hipGraphInstantiate(&pgraph_[stage * 2 + set], g, nullptr, nullptr, 0);
+                    (void)hipGraphDestroy(g);
+                }
+                if (s1 != KN_OK || e != hipSuccess) {
+                    if (set == 1) swap_grid_set();
+                    drop_pipeline();
+                    return s1 != KN_OK ? s1 : check(e, "pipeline capture");
+                }
+            }
+            if (set == 1) swap_grid_set();
+        }
+        // both sets start free
+        for (int s = 0; s < 2; ++s)
+            if ((st = check(hipEventRecord(pev_[2 + s], stream_), "event")) != KN_OK) return st;
+        pipe_i_ = 0;
+    }
+    for (int i = 0; i < iters; ++i, ++pipe_i_) {
+        const int s = (int)(pipe_i_ & 1);
+        if ((st = check(hipStreamWaitEvent(bstream_, pev_[2 + s], 0), "wait query")) != KN_OK) return st;
+        if ((st = check(hipGraphLaunch(pgraph_[s], bstream_), "build launch")) != KN_OK) return st;
+        if ((st = check(hipEventRecord(pev_[s], bstream_), "event")) != KN_OK) return st;
+        if ((st = check(hipStreamWaitEvent(stream_, pev_[s], 0), "wait build")) != KN_OK) return st;
+        if ((st = check(hipGraphLaunch(pgraph_[2 + s], stream_), "query launch")) != KN_OK) return st;
+        if ((st = check(hipEventRecord(pev_[2 + s], stream_), "event")) != KN_OK) return st;
+    }
+    // the last step's grid is the engine's current grid (getters, stats, stored-space views)
+    if ((pipe_i_ & 1) == 0 && iters > 0) {
+        // the last step used set 1: relabel it set 0 (host bookkeeping only: the queued graphs hold
+        // their own pointers, and later getters are stream-ordered after the last query), and
+        // keep the parity so the next step builds into the other set
+        swap_grid_set();
+        std::swap(pgraph_[0], pgraph_[1]);
+        std::swap(pgraph_[2], pgraph_[3]);
+        std::swap(pev_[0], pev_[1]);
+        std::swap(pev_[2], pev_[3]);
+        ++pipe_i_;
+    }
+    solved_ = true;
+    stored_valid_ = points3_valid_ = false;
     return KN_OK;
 }
 

@@ -57,6 +57,10 @@ public:
     kn_status run_graph(int iters, float* ms_per_iter);
     // Enqueue `iters` graph replays without waiting (capturing on first use); sync() waits.
     kn_status launch_graph(int iters);
+    // Enqueue `iters` PIPELINED steps (grid path; otherwise launch_graph): two grid sets, the
+    // build of step i+1 runs on a second stream while step i queries (a stream of clouds: each
+    // step still bins and queries the whole cloud). sync() waits; results are the last step's.
+    kn_status launch_pipelined(int iters);
     kn_status sync();
     // Device-to-device copy of the original-space results into caller buffers.
     kn_status copy_results(unsigned* d_idx, float* d_dist);
@@ -107,6 +111,20 @@ private:
     QueryBuffers query_buffers() const;
     BuildBuffers build_buffers() const;
     void release();
+    // pipelined steps: the second grid set (same carve as the arena, own block) and its stream
+    struct GridSet {
+        unsigned* bbox; GridGeom* geom; int* cell_count; int* cell_scan; int* block_sums; int* cell_start;
+        int2* cell_rank; float4* bin_tmp; float4* sorted; unsigned* perm; unsigned* fallback; unsigned* counters;
+        unsigned long long* occ;
+    };
+    void swap_grid_set();  // exchange the grid-set members with alt_
+    void drop_pipeline();
+    GridSet alt_{};
+    char* arena2_ = nullptr;
+    hipStream_t bstream_ = nullptr;
+    hipEvent_t pev_[4] = {nullptr, nullptr, nullptr, nullptr};  // built s0, s1; queried s0, s1
+    hipGraphExec_t pgraph_[4] = {nullptr, nullptr, nullptr, nullptr};  // build s0, s1; query s0, s1
+    unsigned long long pipe_i_ = 0;
 
     EngineConfig cfg_;
     AutoParams ap_{};

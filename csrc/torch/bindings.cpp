@@ -1000,6 +1000,16 @@ public:
     }
     void solve() { TORCH_CHECK(e_->solve() == KN_OK, e_->error()); }
     void launch_graph(int64_t iters) { TORCH_CHECK(e_->launch_graph((int)iters) == KN_OK, e_->error()); }
+    void launch_pipelined(int64_t iters) { TORCH_CHECK(e_->launch_pipelined((int)iters) == KN_OK, e_->error()); }
+    // stored -> original permutation of the engine's current grid (host int32)
+    torch::Tensor permutation() {
+        unsigned* p = e_->get_permutation();
+        TORCH_CHECK(p, e_->error());
+        auto t = torch::empty({(int64_t)e_->n()}, torch::kInt32);
+        std::memcpy(t.data_ptr<int>(), p, (size_t)e_->n() * sizeof(unsigned));
+        free(p);
+        return t;
+    }
     void sync() { TORCH_CHECK(e_->sync() == KN_OK, e_->error()); }
     std::vector<torch::Tensor> results(torch::Device dev) {
         const int64_t n = e_->n(), k = e_->k();
@@ -1215,6 +1225,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("prepare_async", &PyEngine::prepare_async)
         .def("solve", &PyEngine::solve)
         .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
+        .def("launch_pipelined", &PyEngine::launch_pipelined, py::arg("iters") = 1)
+        .def("get_permutation", &PyEngine::permutation)
         .def("sync", &PyEngine::sync)
         .def("results", &PyEngine::results)
         .def("solve_range", &PyEngine::solve_range, py::arg("first"), py::arg("count"), py::arg("device"))

@@ -125,3 +125,31 @@ def test_knearests_model_tree(cuda):
     _check(p, m.neighbors, m.distances, 16)
     m.step(p, capture=True)
     _check(p, m.neighbors, m.distances, 16)
+
+
+@pytest.mark.parametrize("k,gen", [(16, "uniform"), (50, "uniform"), (16, "clustered")])
+def test_engine_pipelined_steps(cuda, k, gen):
+    """kn::Engine::launch_pipelined: step i+1's binning on a second stream over the other grid set
+    while step i queries. Results of any step count equal the graph replay's bit for bit, the
+    engine's grid afterwards is the last step's (stored-space getters stay consistent), and the
+    tree path falls back to launch_graph."""
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    p = (clustered_cloud if gen == "clustered" else uniform_cloud)(60000, seed=53).to(cuda)
+    e = C.Engine(k)
+    e.prepare(p)
+    e.solve()
+    idx, d2 = e.results(cuda)
+    _check(p, idx, d2, k)
+    perm0 = e.get_permutation()
+    for steps in (1, 2, 3, 4, 7):
+        e.launch_pipelined(steps)
+        e.sync()
+        i2, e2 = e.results(cuda)
+        assert torch.equal(i2, idx) and torch.equal(e2, d2), steps
+        assert torch.equal(e.get_permutation(), perm0), steps
+    e.launch_graph(2)
+    e.sync()
+    i3, e3 = e.results(cuda)
+    assert torch.equal(i3, idx) and torch.equal(e3, d2)
