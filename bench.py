@@ -7,7 +7,9 @@
 One *step* = the reference's kn_prepare + kn_solve on device-resident points (knearests.cu
 :235-392): bounding box, binning (count/scan/scatter), LDS-tiled kNN of EVERY point,
 exact-path fallback, results in original order with squared distances. On 1 GPU the step
-is replayed from a HIP graph. On N GPUs (weak scaling: N x 900K points, a globally uniform
+is replayed from HIP graphs, software-pipelined by default (kn::Engine::launch_pipelined: two
+grid sets, step i+1's binning runs on a second stream while step i queries, as for a stream of
+clouds; every step still bins and queries the whole cloud; ``--no-pipeline`` = serial steps). On N GPUs (weak scaling: N x 900K points, a globally uniform
 cloud of the [0,1000]^3 cube) the BASELINE config is "spatial split + RCCL halo all-to-all":
 with ``--layout partitioned`` (default) rank r holds the uniform points of its own box of the
 decomposition; every step re-derives the global domain (all-gather), classifies EVERY point
@@ -109,9 +111,9 @@ def run_native(args) -> dict:
     info0 = e.info()
     cnt = e.counters()
     log(f"eager done: {info0} counters {cnt}")
-    # --pipeline: software-pipelined steps (kn::Engine::launch_pipelined): step i+1's binning runs
-    # on a second stream while step i queries (two grid sets); every step still bins and queries
-    # the whole cloud
+    # pipelined steps (default; kn::Engine::launch_pipelined): step i+1's binning runs on a second
+    # stream while step i queries (two grid sets); every step still bins and queries the whole
+    # cloud. --no-pipeline: serial graph replays
     launch = e.launch_pipelined if args.pipeline else e.launch_graph
     launch(args.warmup)
     e.sync()
@@ -383,8 +385,10 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--layout", choices=["scattered", "partitioned"], default="partitioned")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="native 1-GPU path: overlap step i+1's binning with step i's queries (two grid sets)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="native 1-GPU path: serial steps (default: step i+1's binning overlaps step i's "
+                         "queries on a second stream, two grid sets; every step bins and queries the whole "
+                         "cloud)")
     ap.add_argument("--path", choices=["native", "torch"], default="native",
                     help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
     ap.add_argument("--no-check", action="store_true")

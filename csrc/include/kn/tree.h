@@ -37,7 +37,10 @@
 
 namespace kn {
 
-constexpr int kTreeLeaf = 32;  // points per leaf (at most)
+#ifndef KN_TREE_LEAF_BITS
+#define KN_TREE_LEAF_BITS 5
+#endif
+constexpr int kTreeLeaf = 1 << KN_TREE_LEAF_BITS;  // points per leaf (at most)
 
 // A tree: one workspace (carved by tree_view) plus a node buffer sized from n.
 struct TreeView {

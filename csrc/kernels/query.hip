@@ -131,9 +131,12 @@ constexpr int kRowOrderMax = 128;
 // row. The row-synchronous loop paid, for each of up to 16 outer rows, the longest span of the
 // few lanes whose bound was still wide (numpy replay: outer rows 56 candidate steps over 9.2 row
 // iterations per wave at K=16 -> 26 over 3.8).
+// 0 = off, 1 = every K <= 40 bucket, 2 = the K buckets 12..40 (A/B: K=8 +9 %).
 #ifndef KN_OUTER_PACK
 #define KN_OUTER_PACK 0
 #endif
+template <int KT>
+constexpr bool outer_pack_k() { return KN_OUTER_PACK == 1 ? KT <= 40 : (KN_OUTER_PACK == 2 && KT >= 12 && KT <= 40); }
 // Default AutoParams::xsub of the tile path for K <= KN_XSUB_MAX_K. Interleaved A/B at 900K
 // uniform (profiles/ab_r3_xsub.jsonl): xsub 2 query K=8 0.207 -> 0.198, K=16 0.305 -> 0.292 ms
 // (build +3 us), K=32 +2 %, K=50 +4 %; xsub 4 at K=16 0.318 -> 0.301 but build +11 us.
@@ -491,7 +494,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 body(lane_span(y, z, lx0, lx1));
             }
             } else {
-            const bool pack = KN_OUTER_PACK && a.n_outer > 0;
+            const bool pack = outer_pack_k<KT>() && a.n_outer > 0;
             const int sidein = pack ? 3 : side;  // rows visited row-synchronously
             for (int tz_ = 0; tz_ < sidein; ++tz_) {
                 const int z = cz + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
@@ -518,7 +521,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     body(lane_span(y, z, lx0, lx1));
                 }
             }
-            if (KN_OUTER_PACK && pack) {
+            if (outer_pack_k<KT>() && pack) {
                 // per-lane slab gaps of offsets +-1, +-2 on y and z (the table holds ring >= 2 rows
                 // with |offset| <= H; offsets beyond +-2 use the exact slab distance)
                 const float fy = (qy - g.origin[1]) * g.inv_cell[1] - (float)(sy0 + cy);
@@ -544,7 +547,10 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const int oy = (int)(e & 15u) - 8, oz = (int)(e >> 4) - 8;
                     const float gy = sel(oy, y2m, y1m, y0, y1p, y2p, gap(1, oy));
                     const float gz = sel(oz, z2m, z1m, z0, z1p, z2p, gap(2, oz));
-                    mask |= (live && fmaf(gy, gy, gz * gz) <= tau0) ? (1ull << t) : 0ull;
+                    // out-of-box rows have an infinite gap: excluded explicitly (a lane whose bound is
+                    // still infinite would otherwise take them, INF <= INF)
+                    const bool in = gy < INFINITY && gz < INFINITY;
+                    mask |= (live && in && fmaf(gy, gy, gz * gz) <= tau0) ? (1ull << t) : 0ull;
                 }
                 while (__builtin_amdgcn_ballot_w64(mask != 0ull)) {
                     int y = cy, z = cz, lx0 = 0, lx1 = -1;
@@ -1876,7 +1882,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             row_order_table(a.H, a.row_order, ring);
             a.row_mirror = ring ? 0 : 1;
             a.n_outer = 0;
-            if (KN_OUTER_PACK && !full && !ring && !(KN_ROW_ORDER == 1) && a.H >= 2 &&
+            if (outer_pack_k<KT>() && !full && !ring && !(KN_ROW_ORDER == 1) && a.H >= 2 &&
                 (2 * a.H + 1) * (2 * a.H + 1) - 9 <= 64) {
                 // the distance-sorted table minus the 3x3 rows around the query's own row
                 unsigned all[32];

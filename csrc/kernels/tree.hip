@@ -18,8 +18,8 @@ namespace kn {
 namespace {
 
 constexpr unsigned SENT = 0xFFFFFFFFu;
-constexpr int kLeafBits = 5;                  // kTreeLeaf = 32 points per leaf
-constexpr int kVisitBits = 8;                 // key slot = visit index (8 bits) | point in leaf (5 bits)
+constexpr int kLeafBits = KN_TREE_LEAF_BITS;  // kTreeLeaf = 32 points per leaf (default)
+constexpr int kVisitBits = 13 - kLeafBits;    // key slot = visit index | point in leaf: 13 bits
 constexpr int kMaxVisit = 1 << kVisitBits;    // leaves a wave may visit before its queries go exact
 constexpr unsigned kMask = (1u << (kVisitBits + kLeafBits)) - 1u;
 static_assert((1 << kLeafBits) == kTreeLeaf, "leaf size");
@@ -41,6 +41,8 @@ constexpr int kExactGrid = 512;
 // (profiles/ab_r3_tree_filter.jsonl, K=16: clustered 1.59 -> 2.29 ms, surface 0.96 -> 1.34,
 // uniform 1.36 -> 1.88; K=50 +10-40 %): the divergent global-memory gathers and the bounds frozen
 // between chunks (+20 % listed leaves) cost more than the broadcast union stream of staged leaves.
+// Leaves of 16 instead of 32 points (KN_TREE_LEAF_BITS=4: tighter boxes, twice the visits) lost too
+// (profiles/ab_r3_tree_leaf16.jsonl: clustered K=16 1.61 -> 2.03 ms, surface 0.97 -> 1.46).
 
 struct TArgs {
     const float4* pts;

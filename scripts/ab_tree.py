@@ -17,8 +17,10 @@ for gen in gens:
     for k in ks:
         g = kn.build_grid(pts, k, adaptive=True)
         dims = list(g.plan.dims)
-        ws, nodes, L = A.tree_build(g.sorted, g.cell_start, g.geom, dims, True)
-        run = lambda M: M.tree_query(ws, nodes, dims, g.n, k, g.n, None, True, 0)
+        # each module builds its own tree (variants may change the leaves)
+        trees = {id(M): M.tree_build(g.sorted, g.cell_start, g.geom, dims, True) for M in (A, B)}
+        L = trees[id(A)][2]
+        run = lambda M: M.tree_query(trees[id(M)][0], trees[id(M)][1], dims, g.n, k, g.n, None, True, 0)
         ra, rb = run(A), run(B)
         torch.cuda.synchronize()
         same = torch.equal(ra[0], rb[0]) and torch.equal(ra[1], rb[1])
