@@ -124,16 +124,19 @@ constexpr int kRowOrderMax = 128;
 #ifndef KN_ROW_RING
 #define KN_ROW_RING 0
 #endif
-// KN_OUTER_PACK=1 (lane walk, K <= 40, the fixed order): the 3x3 rows around the query's row stay
+// KN_OUTER_PACK (lane walk, K <= 40, the fixed order): the 3x3 rows around the query's row stay
 // row-synchronous, the outer rows (Chebyshev ring >= 2 of the (2H+1)^2 block) are PACKED: each
 // lane marks the outer rows its bound still reaches (a 64-bit mask, distances from 8 per-lane
 // slab gaps selected by the uniform table entry), then iteration i visits every lane's i-th marked
 // row. The row-synchronous loop paid, for each of up to 16 outer rows, the longest span of the
 // few lanes whose bound was still wide (numpy replay: outer rows 56 candidate steps over 9.2 row
-// iterations per wave at K=16 -> 26 over 3.8).
-// 0 = off, 1 = every K <= 40 bucket, 2 = the K buckets 12..40 (A/B: K=8 +9 %).
+// iterations per wave at K=16 -> 26 over 3.8). Interleaved A/B, 900K uniform, identical rows
+// (profiles/ab_r3_outer_pack.jsonl): query K=12 -5 %, K=16 -2 %, K=24 -17 %, K=32 -3 %, K=40 -6 %,
+// blue noise K=16 -5 %, 300K K=16 -12 %; K=8 +9 % (its outer rows are almost never needed, the
+// mask costs more): 0 = off, 1 = every K <= 40 bucket, 2 = the K buckets 12..40 (default).
+// Oracle check on clustered clouds (profiles/diag_r3_outer_pack_oracle.txt).
 #ifndef KN_OUTER_PACK
-#define KN_OUTER_PACK 0
+#define KN_OUTER_PACK 2
 #endif
 template <int KT>
 constexpr bool outer_pack_k() { return KN_OUTER_PACK == 1 ? KT <= 40 : (KN_OUTER_PACK == 2 && KT >= 12 && KT <= 40); }
