@@ -737,8 +737,12 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         const char* v = std::getenv("KN_BUILD_ALGO");
         return v && std::atoi(v) == 1;
     }();
-    const char* small_env = std::getenv("KN_SMALL_BUILD");  // read per launch: tests A/B both paths
-    const bool no_small = small_env && std::atoi(small_env) == 0;
+    // KN_SMALL_BUILD=1: the one-workgroup build below for small clouds (read per launch: tests A/B
+    // both paths). Off by default: measured on MI355X it takes 42 us for pts20K where the
+    // multi-kernel build takes 25-27 us (step 0.107 vs 0.089 ms serial, equal when pipelined;
+    // profiles/ab_r3_small_cloud.jsonl)
+    const char* small_env = std::getenv("KN_SMALL_BUILD");
+    const bool no_small = !(small_env && std::atoi(small_env) == 1);
     if (!no_small && !force_atomic && small_build_fits(n, C) && !b.gids && b.n_zero_words <= 1024) {
         // one workgroup, one launch (deterministic layout whatever b.deterministic says)
         static const bool attr = [] {

@@ -291,11 +291,22 @@ kn_status Engine::ensure_tree() {
 // Stream-ordered, no host synchronisation (the leaf count stays on the device): capturable.
 kn_status Engine::tree_query() {
     kn_status st;
+    if ((st = tree_build_async()) != KN_OK) return st;
+    return tree_query_async();
+}
+
+kn_status Engine::tree_build_async() {
+    kn_status st;
     if ((st = ensure_tree()) != KN_OK) return st;
     TreeView t = tree_view(tree_ws_, n_, ap_.dims);
     tree_attach_nodes(t, tree_nodes_);
     if ((st = check(launch_tree_leaves(sorted_, cell_start_, geom_, t, stream_), "tree leaves")) != KN_OK) return st;
-    if ((st = check(launch_tree_nodes(t, stream_), "tree nodes")) != KN_OK) return st;
+    return check(launch_tree_nodes(t, stream_), "tree nodes");
+}
+
+kn_status Engine::tree_query_async() {
+    TreeView t = tree_view(tree_ws_, n_, ap_.dims);
+    tree_attach_nodes(t, tree_nodes_);
     TreeQuery q{};
     q.k = cfg_.k;
     q.n_queries = n_;
@@ -531,6 +542,8 @@ void Engine::drop_pipeline() {
         for (auto& e : pev_) e = nullptr;
     }
     if (arena2_) { dfree(arena2_); arena2_ = nullptr; }
+    if (alt_.tree_ws) dfree(alt_.tree_ws);
+    if (alt_.tree_nodes) dfree(alt_.tree_nodes);
     alt_ = GridSet{};
     pipe_i_ = 0;
 }
@@ -541,6 +554,7 @@ void Engine::swap_grid_set() {
     std::swap(cell_start_, alt_.cell_start); std::swap(cell_rank_, alt_.cell_rank); std::swap(bin_tmp_, alt_.bin_tmp);
     std::swap(sorted_, alt_.sorted); std::swap(perm_, alt_.perm); std::swap(fallback_, alt_.fallback);
     std::swap(counters_, alt_.counters); std::swap(occ_, alt_.occ);
+    std::swap(tree_ws_, alt_.tree_ws); std::swap(tree_nodes_, alt_.tree_nodes);
 }
 
 // Software-pipelined steps over two grid sets (s = step parity): build(i) on bstream_ after the
@@ -548,7 +562,6 @@ void Engine::swap_grid_set() {
 // chip, and the build's five latency-bound kernels (~50 us at 900K, ~15 % of a step) run in its
 // shadow. Each of the 4 stage graphs is captured once.
 kn_status Engine::launch_pipelined(int iters) {
-    if (use_tree_ || cfg_.algo != 0) return launch_graph(iters);  // tree buffers are single
     if (!built_) return fail(KN_ERR_STATE, "launch_pipelined() before prepare()");
     kn_status st;
     if ((st = ensure_outputs()) != KN_OK) return st;
@@ -573,6 +586,14 @@ kn_status Engine::launch_pipelined(int iters) {
             alt_.fallback = carve<unsigned>(p, n);
             alt_.counters = carve<unsigned>(p, kNumCounters);
             alt_.occ = carve<unsigned long long>(p, 1);
+            if (use_tree_) {
+                // the second set's tree workspace and node buffer (the first set's come from ensure_tree)
+                if ((st = check(dmalloc(&alt_.tree_ws, tree_workspace_bytes(n_, ap_.dims)), "hipMalloc(tree 2)")) != KN_OK ||
+                    (st = check(dmalloc(&alt_.tree_nodes, tree_node_bytes(n_)), "hipMalloc(tree nodes 2)")) != KN_OK) {
+                    drop_pipeline();
+                    return st;
+                }
+            }
         }
         if (!bstream_) {
             StreamSet ss;
@@ -590,7 +611,13 @@ kn_status Engine::launch_pipelined(int iters) {
                     if (set == 1) swap_grid_set();
                     return st;
                 }
-                s1 = stage == 0 ? build_async(true) : query_async(true);
+                // tree path: the build stage also builds the set's tree, the query stage queries it
+                if (stage == 0) {
+                    s1 = build_async(true);
+                    if (s1 == KN_OK && use_tree_) s1 = tree_build_async();
+                } else {
+                    s1 = use_tree_ ? tree_query_async() : query_async(true);
+                }
                 hipError_t e = hipStreamEndCapture(stream_, &g);
                 if (s1 == KN_OK && e == hipSuccess) {
                     e = hipGraphInstantiate(&pgraph_[stage * 2 + set], g, nullptr, nullptr, 0);

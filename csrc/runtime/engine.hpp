@@ -57,7 +57,7 @@ public:
     kn_status run_graph(int iters, float* ms_per_iter);
     // Enqueue `iters` graph replays without waiting (capturing on first use); sync() waits.
     kn_status launch_graph(int iters);
-    // Enqueue `iters` PIPELINED steps (grid path; otherwise launch_graph): two grid sets, the
+    // Enqueue `iters` PIPELINED steps: two grid sets (and tree buffers on the tree path), the
     // build of step i+1 runs on a second stream while step i queries (a stream of clouds: each
     // step still bins and queries the whole cloud). sync() waits; results are the last step's.
     kn_status launch_pipelined(int iters);
@@ -107,6 +107,8 @@ private:
     kn_status query_async(bool fused_step = false);
     // Morton-leaf tree over the built grid's points + its query (stream-ordered, capturable)
     kn_status tree_query();
+    kn_status tree_build_async();  // leaves + node boxes of the current grid (stream-ordered)
+    kn_status tree_query_async();  // the tree query over them
     kn_status ensure_tree();
     QueryBuffers query_buffers() const;
     BuildBuffers build_buffers() const;
@@ -116,6 +118,8 @@ private:
         unsigned* bbox; GridGeom* geom; int* cell_count; int* cell_scan; int* block_sums; int* cell_start;
         int2* cell_rank; float4* bin_tmp; float4* sorted; unsigned* perm; unsigned* fallback; unsigned* counters;
         unsigned long long* occ;
+        void* tree_ws;
+        void* tree_nodes;
     };
     void swap_grid_set();  // exchange the grid-set members with alt_
     void drop_pipeline();

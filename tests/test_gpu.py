@@ -186,6 +186,7 @@ def test_small_build_matches_multikernel(cuda, n, gen, monkeypatch):
     # the one-workgroup build of small clouds (build.hip small_build_kernel) lays out exactly
     # what the deterministic multi-kernel build does
     p = {"uniform": uniform_cloud, "clustered": clustered_cloud, "surface": surface_cloud}[gen](n, seed=21, device=cuda)
+    monkeypatch.setenv("KN_SMALL_BUILD", "1")  # opt-in (slower than the multi-kernel build)
     a = kn.build_grid(p, 8)
     monkeypatch.setenv("KN_SMALL_BUILD", "0")
     b = kn.build_grid(p, 8)
@@ -418,3 +419,14 @@ def test_python_cli_gpu_batches(cuda, tmp_path):
                        capture_output=True, text=True, timeout=300, cwd=str(REPO))
     assert r.returncode == 0, r.stderr[-2000:]
     assert '"ok": true' in r.stdout
+
+
+@pytest.mark.parametrize("k", [16, 24])
+def test_grid_path_clustered_vs_oracle(cuda, k):
+    """The grid kernels on a clustered cloud (no refinement: dense tiles go exact, sparse lanes
+    keep an infinite bound after their 3x3 rows): exact against the kd-tree oracle. Caught the
+    first packed-outer-row version, which took out-of-box rows for such lanes."""
+    p = clustered_cloud(100000, seed=0).to(cuda)
+    g = kn.build_grid(p, k)
+    idx, d2 = kn.query(g, k, algo="grid")
+    _assert_matches_oracle(p, idx, d2, k)
