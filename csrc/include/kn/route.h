@@ -7,6 +7,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "kn/kernels.h"
+
 namespace kn {
 
 constexpr int kRouteMaxWorld = 64;
@@ -41,6 +43,18 @@ constexpr int kPlanHdr = 24;
 // [0..2] global lo  [3..5] global hi  [6] h (certification halo)  [7] h_send  [8] n_total
 // [9] id offset of this rank  [10] 1 if the halo covers the whole domain  [11] domain diagonal
 // [12..14] this rank's box lo  [15..17] its box hi
+
+// The local geometry of `rank` from its plan header -- ONE definition for every distributed
+// runtime (the torch binding's dist_local and the C-API kn_solve_multi): the complete box (own box
+// grown by the certification halo h, unbounded on domain faces or when the halo covers the
+// domain), the local grid box (own box grown by the send halo, clipped to the domain) and its
+// extent (the grid plan's aspect).
+struct RankLocal {
+    CompleteBox complete;
+    double box[6];  // lo[3], hi[3]
+    float ext[3];
+};
+RankLocal rank_local(const double* hdr, int rank, const int grid[3]);
 
 // Receive-side table: source s's segment starts at seg[s], holds own[s] owned rows then its
 // halo rows; owned rows of all sources go first (own_pref), then halo rows (halo_pref).

@@ -714,6 +714,23 @@ hipError_t launch_fwd_merge(int world, int F, int k, const unsigned* uncert, con
     return hipGetLastError();
 }
 
+RankLocal rank_local(const double* hd, int rank, const int grid[3]) {
+    RankLocal r{};
+    const double h = hd[6], hs = hd[7];
+    const bool full = hd[10] != 0.0;
+    const int c[3] = {rank % grid[0], (rank / grid[0]) % grid[1], rank / (grid[0] * grid[1])};
+    for (int a = 0; a < 3; ++a) {
+        const double lo = hd[a], hi = hd[3 + a];
+        const double blo = hd[12 + a], bhi = hd[15 + a];  // equal-volume or count-balanced box
+        r.complete.lo[a] = full || c[a] == 0 ? -INFINITY : (float)(blo - h);
+        r.complete.hi[a] = full || c[a] == grid[a] - 1 ? INFINITY : (float)(bhi + h);
+        r.box[a] = std::max(lo, blo - hs);
+        r.box[3 + a] = std::min(hi, bhi + hs);
+        r.ext[a] = (float)(r.box[3 + a] - r.box[a]);
+    }
+    return r;
+}
+
 size_t split_hist_scratch_words(int n, const int grid[3], int stage) {
     const int bins = split_hist_rows(grid, stage) * kSplitBins;
     return bins <= kSplitLdsBins ? (size_t)split_hist_blocks(n) * bins : 1;

@@ -43,6 +43,11 @@ constexpr int kExactGrid = 512;
 // between chunks (+20 % listed leaves) cost more than the broadcast union stream of staged leaves.
 // Leaves of 16 instead of 32 points (KN_TREE_LEAF_BITS=4: tighter boxes, twice the visits) lost too
 // (profiles/ab_r3_tree_leaf16.jsonl: clustered K=16 1.61 -> 2.03 ms, surface 0.97 -> 1.46).
+// Grouped traversal (G = 2 / 4 groups of 32 / 16 queries per wave, each with its own near-first
+// traversal, stack, visit list and leaf buffer; rounds alternate node steps and leaf streams) lost
+// 1.5-4x (profiles/ab_r3_tree_groups{2,4}.jsonl): a group's union is far more than 1/G of the
+// wave's (clustered K=16: 709K leaf visits per solve -> 1.06M / 1.62M summed over groups), and
+// each round waits for the slowest group.
 
 struct TArgs {
     const float4* pts;
@@ -408,30 +413,19 @@ __global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, 
 }
 
 // ---- query: one wave per 64 consecutive points of the Morton order (lanes = queries) -------------
-// G > 1 (KN_TREE_GROUPS): the wave's lanes form G groups of 64/G consecutive queries, each with its
-// own near-first traversal (stack, visit list, leaf buffer): a group streams the union of ITS
-// queries' leaves only. Rounds alternate between advancing every group's traversal to its next
-// leaf (group-uniform node steps, group ballots) and streaming the groups' current leaves (each
-// group reads its own LDS buffer). G = 1 is the wave-wide traversal.
-#ifndef KN_TREE_GROUPS
-#define KN_TREE_GROUPS 1
-#endif
-template <int KT, int M, int G = 1>
+template <int KT, int M>
 __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     constexpr int KM = KT + M + 1;  // + 1: the query itself enters its own list at d2 = 0
-    constexpr int GL = 64 / G;      // lanes per group
-    __shared__ float4 s_pts[4][G][kTreeLeaf];
-    __shared__ int s_visit[4][G][kMaxVisit];  // first point of each visited leaf
-    __shared__ int s_stack[4][G][kStack];
+    __shared__ float4 s_pts[4][kTreeLeaf];
+    __shared__ int s_visit[4][kMaxVisit];  // first point of each visited leaf
+    __shared__ int s_stack[4][kStack];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int w = xcd_remap(blockIdx.x, gridDim.x) * 4 + wid;
     const int base = w * 64;
     if (base >= a.n) return;
-    const int grp = G == 1 ? 0 : lane / GL, gl = grp * GL;  // group, its first lane
-    const unsigned long long gm = G == 1 ? ~0ull : (((1ull << (GL & 63)) - 1ull) << gl);
-    float4* buf = s_pts[wid][grp];
-    int* vis = s_visit[wid][grp];
-    int* stk = s_stack[wid][grp];
+    float4* buf = s_pts[wid];
+    int* vis = s_visit[wid];
+    int* stk = s_stack[wid];
     const int qcnt = min(64, a.n - base);
     // lanes past the last point duplicate it (same candidate stream, never written back)
     const unsigned qpos = (unsigned)(base + min(lane, qcnt - 1));
@@ -464,97 +458,10 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         ++nv;
         __builtin_amdgcn_wave_barrier();
     };
-    const int L = (int)*a.Lp;
-    if constexpr (G > 1) {
-    // ---- grouped traversal ----------------------------------------------------------------------
-    // stage leaf lf (group-uniform; -1 = this group has none this round) in the group's buffer and
-    // stream it to the group's lanes; the wave loops to the longest leaf of the round
-    auto visit_g = [&](int lf) __attribute__((always_inline)) {
-        const bool has = lf >= 0;
-        int b = 0, cnt = 0;
-        if (has) {
-            b = (int)a.leaf_start[lf];
-            cnt = (int)a.leaf_start[lf + 1] - b;
-        }
-        for (int r = lane - gl; r < cnt; r += GL) buf[r] = a.pts[KN_IDX(b + r, a.n, 402)];
-        if (has && lane == gl) vis[nv] = b;
-        __builtin_amdgcn_wave_barrier();
-        const int sb = nv << kLeafBits;
-        for (int j = 0; __builtin_amdgcn_ballot_w64(j < cnt); ++j) {
-            const float4 c = buf[min(j, max(cnt - 1, 0))];
-            const unsigned kk = cand_key(c, qx, qy, qz, ~kMask, sb + j, 0);
-            nnet += topk_push(keys, j < cnt ? kk : SENT);
-        }
-        if (has) ++nv;
-        __builtin_amdgcn_wave_barrier();
-    };
-    // the leaves holding the group's own queries first (the group's starting bound)
-    const int gq0 = base + gl, gq1 = base + min(gl + GL, qcnt);  // [gq0, gq1)
-    const bool glive = (__builtin_amdgcn_ballot_w64(live) & gm) != 0;
-    int l0 = 0, l1 = L - 1;
-    while (l0 < l1) {  // last leaf starting at or before gq0
-        const int mid = (l0 + l1 + 1) >> 1;
-        if ((int)a.leaf_start[mid] <= gq0) l0 = mid; else l1 = mid - 1;
-    }
-    l1 = l0;
-    while (l1 + 1 < L && (int)a.leaf_start[l1 + 1] < gq1) ++l1;
-    if (!glive) l1 = l0 - 1;  // an empty group visits nothing
-    for (int t = 0;; ++t) {
-        const bool has = l0 + t <= l1 && nv < kMaxVisit;
-        if (!__builtin_amdgcn_ballot_w64(has)) break;
-        visit_g(has ? l0 + t : -1);
-    }
-    int sp = 0;
-    if (glive) {
-        sp = 1;
-        if (lane == gl) stk[0] = 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    while (true) {
-        // advance every searching group to its next leaf (or the end of its traversal)
-        int lf_sel = -1;
-        while (__builtin_amdgcn_ballot_w64(lf_sel < 0 && sp > 0)) {
-            if (lf_sel < 0 && sp > 0) {
-                --sp;
-                const int node = stk[sp];
-                const unsigned last = keys[KM - 1];
-                const float ub = last == SENT ? INFINITY : __uint_as_float(last | kMask);
-                const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
-                if ((__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub) & gm) != 0) {
-                    if (node >= a.P) {
-                        const int lf = node - a.P;
-                        if (!(lf >= l0 && lf <= l1)) {  // own leaves were visited first
-                            if (nv == kMaxVisit) { over = true; sp = 0; }
-                            else lf_sel = lf;
-                        }
-                    } else {
-                        const int c0 = 2 * node;
-                        const float b0 = box_d2(qx, qy, qz, a.nlo[c0], a.nhi[c0]);
-                        const float b1 = first_leaf(c0 + 1, a.logP) < L ? box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1])
-                                                                        : INFINITY;
-                        const bool need0 = (__builtin_amdgcn_ballot_w64(live && b0 < INFINITY && b0 * kShrink <= ub) & gm) != 0;
-                        const bool need1 = (__builtin_amdgcn_ballot_w64(live && b1 < INFINITY && b1 * kShrink <= ub) & gm) != 0;
-                        const int votes = __builtin_popcountll(__builtin_amdgcn_ballot_w64(live && b0 <= b1) & gm);
-                        const bool first0 = 2 * votes >= __builtin_popcountll(__builtin_amdgcn_ballot_w64(live) & gm);
-                        const int nearc = first0 ? c0 : c0 + 1, farc = first0 ? c0 + 1 : c0;
-                        const bool nn = first0 ? need0 : need1, nf = first0 ? need1 : need0;
-                        if (lane == gl) {
-                            if (nf) stk[sp] = farc;
-                            if (nn) stk[sp + (nf ? 1 : 0)] = nearc;
-                        }
-                        sp += (nf ? 1 : 0) + (nn ? 1 : 0);
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (!__builtin_amdgcn_ballot_w64(lf_sel >= 0)) break;
-        visit_g(lf_sel);
-    }
-    } else {
     // the leaves holding the wave's own 64 points first: every lane starts the traversal with a
     // bound from ~64 nearby candidates (small leaves alone leave the early bounds loose, and a
     // loose bound of any lane opens nodes for the whole wave)
+    const int L = (int)*a.Lp;
     int l0 = 0, l1 = L - 1;
     while (l0 < l1) {  // last leaf starting at or before base
         const int mid = (l0 + l1 + 1) >> 1;
@@ -600,7 +507,6 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         }
         sp += (nf ? 1 : 0) + (nn ? 1 : 0);
         __builtin_amdgcn_wave_barrier();
-    }
     }
 
     // exact re-rank of the kept slots by (d2, id). The query itself gets the smallest key (it sits
@@ -670,11 +576,11 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             a.thr[KN_IDX(pos, (unsigned)a.n, 405)] = kb == SENT ? INFINITY : __uint_as_float(kb | kMask);
         }
     }
-    if (lane == gl) {  // per group (G = 1: the wave)
+    if (lane == 0) {
         if (over) atomicAdd(a.counters + 2, 1u);
         atomicAdd(a.counters + 5, (unsigned)nv);  // leaves visited
+        atomicAdd(a.counters + 7, 1u);            // waves
     }
-    if (lane == 0) atomicAdd(a.counters + 7, 1u);  // waves
     if (unc) {  // causes (diagnostics): [3] re-rank left unsorted, [4] K-th not below the floor
         const unsigned nu = (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live && !over && !sorted));
         const unsigned nf = (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live && !over && sorted && !cert));
@@ -925,15 +831,15 @@ hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t 
     const unsigned grid = cdiv(cdiv(t.n, 64), 4);
     const int k = q.k;
     bool all = false;
-    if (k <= 4) knn_tree_kernel<4, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 8) knn_tree_kernel<8, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 12) knn_tree_kernel<12, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 16) knn_tree_kernel<16, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 24) knn_tree_kernel<24, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 32) knn_tree_kernel<32, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 40) knn_tree_kernel<40, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 50) knn_tree_kernel<50, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
-    else if (k <= 64) knn_tree_kernel<64, M, KN_TREE_GROUPS><<<grid, 256, 0, s>>>(a);
+    if (k <= 4) knn_tree_kernel<4, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 8) knn_tree_kernel<8, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 12) knn_tree_kernel<12, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 16) knn_tree_kernel<16, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 24) knn_tree_kernel<24, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 32) knn_tree_kernel<32, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 40) knn_tree_kernel<40, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 50) knn_tree_kernel<50, M><<<grid, 256, 0, s>>>(a);
+    else if (k <= 64) knn_tree_kernel<64, M><<<grid, 256, 0, s>>>(a);
     else all = true;  // K > 64: the exact traversal serves every query
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const unsigned eg = all ? std::max(1u, std::min(cdiv(t.n, 4), 16384u)) : (unsigned)kExactGrid;

@@ -529,6 +529,11 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     return KN_OK;
 }
 
+static int pipe_prio() {
+    const char* v = std::getenv("KN_PIPE_PRIO");
+    return v && std::atoi(v) == 1 ? 1 : 0;
+}
+
 void Engine::drop_pipeline() {
     for (auto& g : pgraph_)
         if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
@@ -537,7 +542,7 @@ void Engine::drop_pipeline() {
         StreamSet ss;
         ss.stream = bstream_;
         for (int i = 0; i < 4; ++i) ss.ev[i] = pev_[i];
-        streamset_release(cfg_.device, ss);
+        streamset_release(cfg_.device, ss, pipe_prio());
         bstream_ = nullptr;
         for (auto& e : pev_) e = nullptr;
     }
@@ -596,8 +601,10 @@ kn_status Engine::launch_pipelined(int iters) {
             }
         }
         if (!bstream_) {
+            // KN_PIPE_PRIO=1: the build stream at the device's highest priority (its latency-bound
+            // kernels then take CU slots as soon as the query's workgroups free them)
             StreamSet ss;
-            if ((st = check(streamset_acquire(cfg_.device, &ss), "hipStreamCreate")) != KN_OK) return st;
+            if ((st = check(streamset_acquire(cfg_.device, &ss, pipe_prio()), "hipStreamCreate")) != KN_OK) return st;
             bstream_ = ss.stream;
             for (int i = 0; i < 4; ++i) pev_[i] = ss.ev[i];
         }

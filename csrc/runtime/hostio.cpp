@@ -184,21 +184,29 @@ void arena_release(int device, void* p, size_t bytes) {
 
 namespace {
 std::mutex g_ss_mu;
-std::vector<std::pair<int, StreamSet>> g_ss;
+std::vector<std::pair<int, StreamSet>> g_ss;  // key: device * 2 + priority
 }  // namespace
 
-hipError_t streamset_acquire(int device, StreamSet* out) {
+hipError_t streamset_acquire(int device, StreamSet* out, int priority) {
+    const int key = device * 2 + (priority ? 1 : 0);
     {
         std::lock_guard<std::mutex> lock(g_ss_mu);
         for (size_t i = 0; i < g_ss.size(); ++i)
-            if (g_ss[i].first == device) {
+            if (g_ss[i].first == key) {
                 *out = g_ss[i].second;
                 g_ss.erase(g_ss.begin() + (long)i);
                 return hipSuccess;
             }
     }
     StreamSet s;
-    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    hipError_t e;
+    if (priority) {
+        int least = 0, greatest = 0;
+        e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking, greatest);
+    } else {
+        e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    }
     for (auto& ev : s.ev)
         if (e == hipSuccess) e = hipEventCreate(&ev);
     if (e != hipSuccess) {
@@ -210,13 +218,14 @@ hipError_t streamset_acquire(int device, StreamSet* out) {
     return hipSuccess;
 }
 
-void streamset_release(int device, const StreamSet& s) {
+void streamset_release(int device, const StreamSet& s, int priority) {
     if (!s.stream) return;
+    const int key = device * 2 + (priority ? 1 : 0);
     {
         std::lock_guard<std::mutex> lock(g_ss_mu);
         int same = 0;
-        for (const auto& p : g_ss) same += p.first == device ? 1 : 0;
-        if (same < 8) { g_ss.emplace_back(device, s); return; }
+        for (const auto& p : g_ss) same += p.first == key ? 1 : 0;
+        if (same < 8) { g_ss.emplace_back(key, s); return; }
     }
     for (auto ev : s.ev) if (ev) (void)hipEventDestroy(ev);
     (void)hipStreamDestroy(s.stream);

@@ -40,7 +40,8 @@ struct StreamSet {
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
-hipError_t streamset_acquire(int device, StreamSet* out);
-void streamset_release(int device, const StreamSet& s);
+// priority: 0 = default, 1 = the device's highest stream priority (pooled separately)
+hipError_t streamset_acquire(int device, StreamSet* out, int priority = 0);
+void streamset_release(int device, const StreamSet& s, int priority = 0);
 
 }  // namespace kn

@@ -382,23 +382,12 @@ kn_status solve_round(kn_multi* m, double hf, const int grid[3], bool balanced, 
         KN_M(ensure_n<float>(m, R.lpts, (size_t)nl * 3));
         KN_M(ensure_n<int>(m, R.lgids, nl));
         KN_M(kn::launch_route_unpack(R.recv.as<float4>(), nullptr, nl, t, R.lpts.as<float>(), R.lgids.as<int>(), R.s));
-        // rank box (equal-volume or count-balanced, as the plan kernel computed it) / complete box /
-        // local grid box from the plan header -- the arithmetic of bindings.cpp dist_local
-        const auto& hd = R.hdr_host;
-        const double h = hd[6], hs = hd[7];
-        const int c[3] = {i % grid[0], (i / grid[0]) % grid[1], i / (grid[0] * grid[1])};
-        double box[6];
-        kn::CompleteBox comp;
-        float fext[3];
-        for (int a = 0; a < 3; ++a) {
-            const double l = hd[a], u = hd[3 + a];
-            const double blo = hd[12 + a], bhi = hd[15 + a];
-            comp.lo[a] = *full || c[a] == 0 ? -INFINITY : (float)(blo - h);
-            comp.hi[a] = *full || c[a] == grid[a] - 1 ? INFINITY : (float)(bhi + h);
-            box[a] = std::max(l, blo - hs);
-            box[3 + a] = std::min(u, bhi + hs);
-            fext[a] = (float)(box[3 + a] - box[a]);
-        }
+        // rank box / complete box / local grid box from the plan header (kn::rank_local, shared
+        // with the torch binding's dist_local)
+        const kn::RankLocal rl = kn::rank_local(R.hdr_host.data(), i, grid);
+        const double* box = rl.box;
+        const kn::CompleteBox comp = rl.complete;
+        const float* fext = rl.ext;
         const int th[3] = {m->cfg.tile[0], m->cfg.tile[1], m->cfg.tile[2]};
         const kn::AutoParams ap = kn::auto_params(nl, k, m->cfg.points_per_cell, th, m->cfg.halo, fext);
         for (int a = 0; a < 3; ++a) R.dims[a] = ap.dims[a];

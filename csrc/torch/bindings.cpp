@@ -619,24 +619,17 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     }
     int64_t n_owned = 0;
     for (auto v : recv_own) n_owned += v;
-    const double h = hdr[6], hs = hdr[7];
-    const bool full = hdr[10] != 0.0;
-    const int64_t c[3] = {rank % grid[0], (rank / grid[0]) % grid[1], rank / (grid[0] * grid[1])};
-    std::vector<double> complete(6), box(6);
-    std::vector<double> ext(3);
+    // the rank's box / complete box / local grid box from the plan header (kn::rank_local, shared
+    // with the C-API multi-GPU runtime)
+    const int gi[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
+    const kn::RankLocal rl = kn::rank_local(hdr.data(), (int)rank, gi);
+    std::vector<double> complete(6), box(rl.box, rl.box + 6);
     for (int a = 0; a < 3; ++a) {
-        // the rank's box (equal-volume or count-balanced) as the plan kernel computed it
-        const double lo = hdr[a], hi = hdr[3 + a];
-        const double blo = hdr[12 + a], bhi = hdr[15 + a];
-        const double inf = std::numeric_limits<double>::infinity();
-        complete[a] = full ? -inf : (c[a] == 0 ? -inf : blo - h);
-        complete[3 + a] = full ? inf : (c[a] == grid[a] - 1 ? inf : bhi + h);
-        box[a] = std::max(lo, blo - hs);
-        box[3 + a] = std::min(hi, bhi + hs);
-        ext[a] = box[3 + a] - box[a];
+        complete[a] = (double)rl.complete.lo[a];
+        complete[3 + a] = (double)rl.complete.hi[a];
     }
     const int64_t npts = pg[0].size(0);
-    float fext[3] = {(float)ext[0], (float)ext[1], (float)ext[2]};
+    float fext[3] = {rl.ext[0], rl.ext[1], rl.ext[2]};
     const int th[3] = {0, 0, 0};
     kn::AutoParams ap = kn::auto_params((int)npts, (int)k, (float)ppc, th, 0, fext);
     std::vector<int64_t> dims = {ap.dims[0], ap.dims[1], ap.dims[2]};
