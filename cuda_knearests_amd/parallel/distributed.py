@@ -169,13 +169,13 @@ class DistributedKNearests:
         # boost is collective (n_fwd is all-reduced), kept across steps.
         self.halo_boost = 1.0
         self.halo_boost_max = 4.0
-        # hipGraph replay of the steady step (torch.cuda.CUDAGraph), opt-in: KN_DIST_GRAPH=1 or
-        # graph_steady = True. Replayed rows live in the graph's static buffers until the next
-        # solve. At world 1 (RCCL) 200 back-to-back replays are valid and bit-identical to the
-        # eager steady step on the release and the bounds-checked builds, host enqueue 0.14 ->
-        # 0.06 ms per step (profiles/ab_r2_dist_graph.txt; an early round-2 version faulted once
-        # in this mode). Not the default because capturing RCCL collectives (world > 1) cannot
-        # be exercised on a one-GPU box.
+        # hipGraph replay of the steady step (torch.cuda.CUDAGraph): the default at world 1 (round
+        # 3; no collective inside the captured step), opt-in above (KN_DIST_GRAPH=1 or
+        # graph_steady = True: capturing RCCL collectives cannot be exercised on a one-GPU box);
+        # KN_DIST_GRAPH=0 / graph_steady = False turn it off. Replayed rows live in the graph's
+        # static buffers until the next solve. At world 1 200 back-to-back replays are valid and
+        # bit-identical to the eager steady step on the release and the bounds-checked builds, host
+        # enqueue 0.14 -> 0.06 ms per step (profiles/ab_r2_dist_graph.txt).
         self.graph_steady = None
         self._graph = None
         # asynchronous steady results not yet checked by the solver. Before the next steady step
@@ -572,7 +572,11 @@ class DistributedKNearests:
             return bool(self.graph_steady)
         import os
 
-        return os.environ.get("KN_DIST_GRAPH") == "1" and isinstance(self.comm, TorchDistTransport)
+        # default at world 1 (no collective inside the captured step); KN_DIST_GRAPH=1 also for
+        # world > 1 (RCCL capture), =0 never
+        env = os.environ.get("KN_DIST_GRAPH")
+        on = env == "1" or (env != "0" and self.world == 1)
+        return on and isinstance(self.comm, TorchDistTransport)
 
     def _solve_steady(self, points: torch.Tensor, ids: Optional[torch.Tensor]) -> DistResult:
         """One step with no host synchronisation (see ``self.steady``), replayed from a hipGraph
