@@ -134,6 +134,11 @@ hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* o
 hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const double* planned_meta, const int* totals,
                                        const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                                        hipStream_t stream);
+// World-1 steady step check (no routing pass): one bbox pass over the share + the same flag
+// kernel. sticky / host_flag (both or neither): also max-accumulate the flag into the device word
+// `sticky` and store it to `host_flag`, a device-visible pointer to pinned host memory.
+hipError_t launch_steady_flag_local(const float* pts, int n, unsigned* words, const double* planned_meta,
+                                    const unsigned* counters, int* flag, int* sticky, int* host_flag, hipStream_t s);
 hipError_t launch_steady_flag(const double* local, const double* planned_meta, const int* totals,
                               const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                               hipStream_t s);

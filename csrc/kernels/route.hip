@@ -420,10 +420,15 @@ __global__ void steady_flag_kernel(const double* __restrict__ local, const doubl
 // Steady-state check from the routing pass's bbox partials (route_count_kernel): this share's
 // {lo, hi, n} against the planned meta (the same double conversion as meta_finalize_kernel), the
 // send counts against the planned ones, and no uncertified query.
-__global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsigned* __restrict__ partials, int nb, int n,
+// partials[a * stride + b] for the nb blocks b < nb. sticky / host_flag (optional, graph-replayed
+// world-1 steps): the flag is also max-accumulated into sticky and stored to host_flag (a device
+// pointer to pinned host memory), so no copy node follows the step.
+__global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsigned* __restrict__ partials, int nb,
+                                            int stride, int n,
                                             const double* __restrict__ planned, const int* __restrict__ totals,
                                             const int* __restrict__ ptotals, int nt,
-                                            const unsigned* __restrict__ counters, int* __restrict__ flag) {
+                                            const unsigned* __restrict__ counters, int* __restrict__ flag,
+                                            int* __restrict__ sticky, int* __restrict__ host_flag) {
     // block-wide reduction of the nb x 6 partials (1024 threads: one pass at ~900K points)
     __shared__ unsigned red[6][16];
     __shared__ unsigned words_s[6];
@@ -432,7 +437,7 @@ __global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsign
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         unsigned v = 0u;
-        for (int b = threadIdx.x; b < nbr; b += blockDim.x) v = max(v, partials[(size_t)a * nb + b]);
+        for (int b = threadIdx.x; b < nbr; b += blockDim.x) v = max(v, partials[(size_t)a * stride + b]);
         v = wave_max_u32(v);
         if (lane == 0) red[a][wid] = v;
     }
@@ -461,7 +466,15 @@ __global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsign
     }
     for (int i = lane; i < nt; i += 64) diff |= totals[i] != ptotals[i];
     const bool any = __builtin_amdgcn_ballot_w64(diff) != 0ull;
-    if (lane == 0) flag[0] = (any ? 1 : 0) + (counters[1] != 0u ? 1 : 0);
+    if (lane == 0) {
+        int f = (any ? 1 : 0) + (counters[1] != 0u ? 1 : 0);
+        if (sticky) {
+            f = max(f, sticky[0]);
+            sticky[0] = f;
+            host_flag[0] = f;
+        }
+        flag[0] = f;
+    }
 }
 
 // ---- query forwarding inside a sync-free step (fixed-capacity slots, no host round trip) -------
@@ -679,8 +692,19 @@ hipError_t launch_steady_flag(const double* local, const double* planned_meta, c
 hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const double* planned_meta, const int* totals,
                                        const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                                        hipStream_t s) {
-    steady_flag_partials_kernel<<<1, 1024, 0, s>>>(partials, route_block_count(n), n, planned_meta, totals,
-                                                 planned_totals, n_totals, counters, flag);
+    const int nb = route_block_count(n);
+    steady_flag_partials_kernel<<<1, 1024, 0, s>>>(partials, nb, nb, n, planned_meta, totals, planned_totals, n_totals,
+                                                 counters, flag, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_steady_flag_local(const float* pts, int n, unsigned* words, const double* planned_meta,
+                                    const unsigned* counters, int* flag, int* sticky, int* host_flag, hipStream_t s) {
+    if ((sticky == nullptr) != (host_flag == nullptr)) return hipErrorInvalidValue;
+    hipError_t e;
+    if ((e = launch_bbox_partials(pts, n, words, s)) != hipSuccess) return e;
+    steady_flag_partials_kernel<<<1, 1024, 0, s>>>(words, n > 0 ? bbox_block_count(n) : 0, kBBoxBlocks, n,
+                                                 planned_meta, nullptr, nullptr, 0, counters, flag, sticky, host_flag);
     return hipGetLastError();
 }
 

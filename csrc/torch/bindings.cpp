@@ -841,6 +841,39 @@ torch::Tensor steady_flag(torch::Tensor local, torch::Tensor metas, int64_t rank
     return flag;
 }
 
+// World-1 steady step check from one bbox pass over the share (no routing pass): (1,) int32 flag.
+// sticky ((1,) int32 GPU) + host ((1,) int32 pinned CPU), optional: the flag is max-accumulated
+// into sticky and stored to host by the kernel (graph replays need no copy node after the step).
+torch::Tensor steady_flag_local(torch::Tensor points, torch::Tensor metas, int64_t rank, torch::Tensor counters,
+                                c10::optional<torch::Tensor> sticky, c10::optional<torch::Tensor> host) {
+    check_points(points, true);
+    TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.numel() >= 8 * (rank + 1) &&
+                    metas.is_contiguous(), "metas: (world*8,) f64 GPU");
+    TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == torch::kInt32 && counters.numel() >= 2, "counters");
+    TORCH_CHECK(sticky.has_value() == host.has_value(), "sticky and host go together");
+    const c10::DeviceGuard guard(points.device());
+    int* sp = nullptr;
+    int* hp = nullptr;
+    if (sticky.has_value()) {
+        TORCH_CHECK(sticky->is_cuda() && sticky->scalar_type() == torch::kInt32 && sticky->numel() == 1, "sticky");
+        TORCH_CHECK(!host->is_cuda() && host->is_pinned() && host->scalar_type() == torch::kInt32 && host->numel() == 1,
+                    "host: (1,) int32 pinned CPU tensor");
+        void* d = nullptr;
+        KN_CHECK_HIP(hipHostGetDevicePointer(&d, host->data_ptr(), 0));
+        sp = sticky->data_ptr<int>();
+        hp = static_cast<int*>(d);
+    }
+    auto words = torch::empty({kn::kBBoxWords}, points.options().dtype(torch::kInt32));
+    auto flag = torch::empty({1}, counters.options());
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_steady_flag_local(points.data_ptr<float>(), (int)points.size(0),
+                                              reinterpret_cast<unsigned*>(words.data_ptr<int>()),
+                                              metas.data_ptr<double>() + 8 * rank,
+                                              reinterpret_cast<const unsigned*>(counters.data_ptr<int>()),
+                                              flag.data_ptr<int>(), sp, hp, s));
+    return flag;
+}
+
 // Pre-collective half of a steady-state step: counts + scatter with the validated step's plan
 // (no re-planning; the plan kernel is a serial one-thread pass) and this share's bbox partials
 // taken by the counting pass. -> (totals (2*world,) int32, send (cap, 4), partials)
@@ -1194,6 +1227,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "multi-GPU steady step: counts + scatter with a validated plan, share bbox partials on the way",
           py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("world"), py::arg("cap"), py::arg("rank"),
           py::arg("place") = py::none());
+    m.def("steady_flag_local", &steady_flag_local,
+          "multi-GPU world 1: steady check from one bbox pass (+ optional sticky / pinned host flag)",
+          py::arg("points"), py::arg("metas"), py::arg("rank"), py::arg("counters"), py::arg("sticky") = py::none(),
+          py::arg("host") = py::none());
     m.def("steady_flag_partials", &steady_flag_partials,
           "multi-GPU: steady-step check with the share bbox from route_steady's partials");
     m.def("dist_local", &dist_local,

@@ -175,7 +175,10 @@ class DistributedKNearests:
         # KN_DIST_GRAPH=0 / graph_steady = False turn it off. Replayed rows live in the graph's
         # static buffers until the next solve. At world 1 200 back-to-back replays are valid and
         # bit-identical to the eager steady step on the release and the bounds-checked builds, host
-        # enqueue 0.14 -> 0.06 ms per step (profiles/ab_r2_dist_graph.txt).
+        # enqueue 0.14 -> 0.06 ms per step (profiles/ab_r2_dist_graph.txt). The world-1 steady
+        # step skips the routing passes (the share is the local set), reads the caller's input in
+        # place and copies its flag out inside the graph (one graph launch per step, no stream op
+        # between replays; profiles/bench_r3_dist_world1.txt).
         self.graph_steady = None
         self._graph = None
         # asynchronous steady results not yet checked by the solver. Before the next steady step
@@ -436,6 +439,8 @@ class DistributedKNearests:
                 # fallback launch sized from the validated step's list (short list: 256 WGs)
                 "exact_grid": 256 if int(counters[0].item()) < 4096 else 0,
             }
+            if world == 1:  # ids of the world-1 steady step (no routing) when the caller gives none
+                self._steady["gids1"] = torch.arange(points.size(0), dtype=torch.int32, device=points.device)
         else:
             self._steady = None
         return DistResult(own_ids, idx, d2, stats)
@@ -522,13 +527,30 @@ class DistributedKNearests:
             return int(sum(int(x.item()) for x in parts))
         return n_unc
 
-    def _steady_body(self, points: torch.Tensor, ids: Optional[torch.Tensor]):
+    def _steady_body(self, points: torch.Tensor, ids: Optional[torch.Tensor], sink=None):
         """Device work of one steady step (no host synchronisation): -> (owned gids, idx, d2,
-        flag); the flag is already all-reduced."""
+        flag); the flag is already all-reduced. sink (world 1, graph capture): (sticky (1,) int32
+        GPU, host (1,) int32 pinned) that the flag kernel max-accumulates / stores into."""
         st = self._steady
         C = ops.load()
         world, rank = self.world, self.rank
         src_ids = ids.to(torch.int32).contiguous() if ids is not None else None
+        if world == 1:
+            # a world of one routes every point to itself, in order, with no halo: the share IS the
+            # local point set (ids: the caller's or 0..n-1). Skip the routing passes; the flag
+            # checks this share's {lo, hi, n} against the validated step's meta (one bbox pass)
+            # and the uncertified count, as steady_flag_partials does. Rows are bit-identical.
+            gin = src_ids if src_ids is not None else st["gids1"]
+            if gin.numel() != points.size(0):  # a share of another size: the flag fails below
+                gin = torch.zeros(points.size(0), dtype=torch.int32, device=points.device)
+            n = points.size(0)
+            pts, gids, idx, d2, counters, *lg = C.dist_local(
+                points.new_empty((0, 4)), points.new_empty((0, 4)), [n], [0], 0, [1, 1, 1], st["hdr"], self.k,
+                self.points_per_cell, self.deterministic, st["exact_grid"], False, st["dims"], points, gin,
+                st["use_tree"])
+            sticky, host = sink if sink is not None else (None, None)
+            flag = C.steady_flag_local(points, st["metas"], 0, counters, sticky, host)
+            return gids, idx, d2, flag
         # counts + scatter with the validated plan; the share's bbox comes from the counting pass,
         # and the rank's own segment goes straight to its local rows (no send-buffer copy, no
         # unpack of it): only rows received from other ranks are unpacked
@@ -584,27 +606,51 @@ class DistributedKNearests:
         st = self._steady
         if self._use_graph(points):
             g = self._graph
-            if g is None or g["st"] is not st or g["n"] != points.size(0) or g["ids"] != (ids is not None):
-                sp = points.clone()
-                si = ids.to(torch.int32).contiguous().clone() if ids is not None else None
+            ids32 = ids.to(torch.int32).contiguous() if ids is not None else None
+            # Direct input: the graph reads the caller's tensors in place while every call passes
+            # the same storage (a training / serving loop refilling one buffer); it keeps them
+            # alive, so an equal address is that storage. The first call with other tensors
+            # recaptures once on graph-owned input buffers filled by a copy per step.
+            same = (g is not None and g["direct"] and points.data_ptr() == g["pts"].data_ptr()
+                    and (ids32 is None or ids32.data_ptr() == g["idsb"].data_ptr()))
+            if (g is None or g["st"] is not st or g["n"] != points.size(0) or g["ids"] != (ids is not None)
+                    or (g["direct"] and not same)):
+                direct = g is None or g["st"] is not st
+                sp = points if direct else points.clone()
+                si = (ids32 if direct else ids32.clone()) if ids32 is not None else None
                 side = torch.cuda.Stream()
                 side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side):
                     for _ in range(2):  # warm-up: allocator pools, kernel attributes
                         self._steady_body(sp, si)
                 torch.cuda.current_stream().wait_stream(side)
+                # the step's flag leaves the device inside the graph (no stream op between
+                # replays): a sticky max over the replays of this graph into one pinned word, so a
+                # step reads its own flag or a later one's -- never valid after an invalid step (an
+                # invalid step drops the graph). World 1: the flag kernel itself stores it.
+                sticky = torch.zeros(1, dtype=torch.int32, device=points.device)
+                host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
-                    out = self._steady_body(sp, si)
+                    out = self._steady_body(sp, si, sink=(sticky, host) if self.world == 1 else None)
+                    if self.world > 1:
+                        torch.maximum(sticky, out[3], out=sticky)
+                        host.copy_(sticky, non_blocking=True)
                 g = self._graph = {"graph": graph, "pts": sp, "ids": si is not None, "idsb": si, "out": out,
-                                   "st": st, "n": points.size(0)}
-            g["pts"].copy_(points)
-            if ids is not None:
-                g["idsb"].copy_(ids.to(torch.int32))
+                                   "st": st, "n": points.size(0), "direct": direct, "host": host}
+            if not g["direct"]:
+                g["pts"].copy_(points)
+                if ids32 is not None:
+                    g["idsb"].copy_(ids32)
             g["graph"].replay()
-            gid, idx, d2, flag = g["out"]
-        else:
-            gid, idx, d2, flag = self._steady_body(points, ids)
+            gid, idx, d2, _ = g["out"]
+            ev = torch.cuda.Event()
+            ev.record()
+            stats = dict(st["stats"])
+            stats["steady"] = True
+            stats["graph"] = True
+            return DistResult(gid, idx, d2, stats, flag=g["host"], event=ev)
+        gid, idx, d2, flag = self._steady_body(points, ids)
         host = torch.empty(1, dtype=torch.int32, pin_memory=points.is_cuda)
         host.copy_(flag, non_blocking=True)
         ev = torch.cuda.Event() if points.is_cuda else None
@@ -612,7 +658,7 @@ class DistributedKNearests:
             ev.record()
         stats = dict(st["stats"])
         stats["steady"] = True
-        stats["graph"] = self._graph is not None and self._use_graph(points)
+        stats["graph"] = False
         return DistResult(gid, idx, d2, stats, flag=host, event=ev)
 
     def _drop_steady(self) -> None:

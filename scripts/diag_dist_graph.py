@@ -24,9 +24,11 @@ C = load()
 print("module", C.__name__, flush=True)
 pts = uniform_cloud(n, seed=3, device=dev)
 ref = DistributedKNearests(k=16, deterministic=False)
-ref.solve(pts)
+ref.graph_steady = False
+r_full = ref.solve(pts)  # the validated full (routed) step
 r_eager = ref.solve(pts)  # steady, eager
-assert r_eager.valid()
+assert r_eager.valid() and r_eager.stats.get("steady")
+assert torch.equal(r_full.neighbors, r_eager.neighbors) and torch.equal(r_full.d2, r_eager.d2)
 dk = DistributedKNearests(k=16, deterministic=False)
 dk.graph_steady = True
 dk.solve(pts)  # validating step
@@ -37,6 +39,20 @@ last = res[-1]
 same = torch.equal(last.neighbors, r_eager.neighbors) and torch.equal(last.d2, r_eager.d2) and \
     torch.equal(last.ids, r_eager.ids)
 print("graph", bool(last.stats.get("graph")), "valid", ok, "same rows as eager", same, flush=True)
+# other input storage (same values): one recapture on graph-owned input buffers, same rows
+res2 = [dk.solve(pts.clone(), async_=True) for _ in range(4)]
+torch.cuda.synchronize()
+ok2 = all(r.valid() for r in res2) and not dk._graph["direct"]
+same2 = torch.equal(res2[-1].neighbors, r_eager.neighbors) and torch.equal(res2[-1].d2, r_eager.d2)
+# a moved share (bbox changed): the steady step must report invalid, the synchronous call recovers
+moved = pts * 0.5
+bad = dk.solve(moved, async_=True)
+inval = not bad.valid()
+r_moved = dk.solve(moved)
+ref_moved = DistributedKNearests(k=16, deterministic=False).solve(moved)
+same3 = torch.equal(r_moved.neighbors, ref_moved.neighbors) and torch.equal(r_moved.d2, ref_moved.d2)
+print("staged", ok2, same2, "moved share invalid", inval, "recovered", same3, flush=True)
+same = same and ok2 and same2 and inval and same3
 if "checked" in C.__name__:
     w = C.debug_words(False)
     print("debug words (build, query, route, tree):", w, flush=True)

@@ -432,9 +432,11 @@ def test_adaptive_local_grid_clustered(cuda):
 
 
 def test_rccl_world1_graph_replay(cuda):
-    """Steady distributed steps replayed from a hipGraph (torch.cuda.CUDAGraph, opt-in
-    graph_steady / KN_DIST_GRAPH=1): back-to-back replays without host synchronisation are all
-    valid and give the eager steady step's rows bit for bit."""
+    """Steady distributed steps replayed from a hipGraph (torch.cuda.CUDAGraph, the default at
+    world 1): back-to-back replays without host synchronisation are all valid and give the eager
+    steady step's rows (and the routed full step's) bit for bit; a call with other input storage
+    recaptures on graph-owned buffers with the same rows; a moved share reports invalid through
+    the in-graph flag and the synchronous call recovers the full step's rows."""
     import subprocess
     import sys
 
@@ -450,6 +452,7 @@ def test_rccl_world1_graph_replay(cuda):
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "graph True valid True same rows as eager True" in r.stdout
+    assert "staged True True moved share invalid True recovered True" in r.stdout
 
 
 @pytest.mark.parametrize("world,gen,hf", [(4, "uniform", 0.6), (8, "clustered", 1.0)])
