@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Headline benchmark (BASELINE.json): queries/s (whole node) + ms/build, 900K points, k=16.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 900000] [--k 16]
+  python bench.py [--gpus N] [--steps K=200] [--warmup W=50] [--n 900000] [--k 16]
   torchrun --nproc-per-node N bench.py --gpus N ...          (driver launch for N > 1)
 
 One *step* = the reference's kn_prepare + kn_solve on device-resident points (knearests.cu
@@ -377,8 +377,11 @@ def run_cpu_oracle(args) -> dict:
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults time the steady state: a step of the default 900K run takes ~0.33 ms for its first
+    # ~30 steps after idle and settles at ~0.30 ms (clock ramp; profiles/bench_r3_steps.txt:
+    # 20/5 -> 0.333-0.335 ms, 200/20 -> 0.303-0.305); 250 steps still take < 0.1 s
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--n", "--points", dest="n", type=int, default=900_000,
                     help="points per GPU (use --points under torchrun: it claims --n* prefixes)")
     ap.add_argument("--k", type=int, default=16)
