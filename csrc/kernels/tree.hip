@@ -30,6 +30,7 @@ constexpr int kSortPasses = 3;                // odd-even passes of the exact re
 // pruned only when the box distance exceeds the bound by more than that.
 constexpr float kShrink = 0.99999f;
 constexpr int kExactGrid = 512;
+constexpr int kFrontier = 256;  // exact kernel: breadth-first frontier / leaf list per wave
 // Round-3 A/Bs of the traversal that LOST (900K, identical rows): a breadth-first sweep with the
 // bounds frozen after the own leaves (profiles/ab_r3_tree_bfs.jsonl, 1.3-3.5x slower: a sparse
 // query near a cluster keeps a loose bound until the cluster's nearest leaves shrink it, which
@@ -613,9 +614,13 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
 __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
     __shared__ unsigned long long s_buf[4][kTCap];
     __shared__ int s_stack[4][kStack];
+    __shared__ float s_sbd[4][kStack];  // box distance of each stacked node (computed by its parent)
+    __shared__ int s_fr[4][2][kFrontier];
+    __shared__ int s_lf[4][kFrontier];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long* buf = s_buf[wid];
     int* stk = s_stack[wid];
+    float* sbd = s_sbd[wid];
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int total = all ? a.n : (int)a.counters[0];
     const int k = a.k;
@@ -648,13 +653,89 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
             }
             __builtin_amdgcn_wave_barrier();
         };
-        int sp = 1;
-        if (lane == 0) stk[0] = 1;
+        // A finite bound (listed queries: the (K+1)-th truncated key, rounded up) is already tight:
+        // sweep the tree breadth-first, 64 nodes per step (one dependent global round per level
+        // instead of per node), collect the leaves within the bound, then scan them two per step
+        // (a half-wave per leaf). The kept set is order-independent (the bound only ever tightens to
+        // a K-th distance found, ties break by id), so rows equal the depth-first walk's. A
+        // frontier or leaf list past kFrontier falls back to that walk.
+        bool dfs = !(thr < INFINITY);
+        if (!dfs) {
+            int* cur = s_fr[wid][0];
+            int* nxt = s_fr[wid][1];
+            int* lfl = s_lf[wid];
+            if (lane == 0) cur[0] = 1;
+            int ncur = 1, nleaf = 0;
+            __builtin_amdgcn_wave_barrier();
+            while (ncur > 0 && !dfs) {
+                int nn = 0;
+                for (int i0 = 0; i0 < ncur; i0 += 64) {
+                    const int i = i0 + lane;
+                    const int node = i < ncur ? cur[i] : 0;
+                    bool isleaf = false, p0 = false, p1 = false;
+                    if (i < ncur) {
+                        if (node >= a.P) {
+                            isleaf = true;
+                        } else {
+                            const int c0 = 2 * node;
+                            const float b0 = box_d2(qx, qy, qz, a.nlo[c0], a.nhi[c0]);
+                            const float b1 = first_leaf(c0 + 1, a.logP) < L
+                                                 ? box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]) : INFINITY;
+                            p0 = b0 < INFINITY && b0 * kShrink <= thr;
+                            p1 = b1 < INFINITY && b1 * kShrink <= thr;
+                        }
+                    }
+                    const unsigned long long bl = __builtin_amdgcn_ballot_w64(isleaf);
+                    const unsigned long long q0 = __builtin_amdgcn_ballot_w64(p0);
+                    const unsigned long long q1 = __builtin_amdgcn_ballot_w64(p1);
+                    const int nl = __builtin_popcountll(bl), nc = __builtin_popcountll(q0) + __builtin_popcountll(q1);
+                    if (nleaf + nl > kFrontier || nn + nc > kFrontier) { dfs = true; break; }
+                    if (isleaf) lfl[nleaf + __builtin_popcountll(bl & lt)] = node - a.P;
+                    const int off = nn + __builtin_popcountll(q0 & lt) + __builtin_popcountll(q1 & lt);
+                    if (p0) nxt[off] = 2 * node;
+                    if (p1) nxt[off + (p0 ? 1 : 0)] = 2 * node + 1;
+                    nleaf += nl;
+                    nn += nc;
+                }
+                __builtin_amdgcn_wave_barrier();
+                int* t = cur; cur = nxt; nxt = t;
+                ncur = nn;
+            }
+            if (!dfs) {
+                const int half = lane >> 5, sub = lane & 31;
+                for (int j = 0; j < nleaf; j += 2) {
+                    if (cnt + 64 > kTCap) compact();
+                    bool pass = false;
+                    unsigned long long key = 0;
+                    if (j + half < nleaf) {
+                        const int lf = lfl[j + half];
+                        const int p = (int)a.leaf_start[lf] + sub;
+                        if (sub < kTreeLeaf && p < (int)a.leaf_start[lf + 1] && (unsigned)p != qpos) {
+                            const float4 c = a.pts[KN_IDX(p, a.n, 416)];
+                            const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
+                            const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+                            pass = d2 <= thr;
+                            key = pack_key64(d2, w_id(a, __float_as_uint(c.w)));
+                        }
+                    }
+                    const unsigned long long bal = __builtin_amdgcn_ballot_w64(pass);
+                    if (pass) buf[cnt + __builtin_popcountll(bal & lt)] = key;
+                    cnt += __builtin_popcountll(bal);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        // one query per wave: box distances are wave-uniform, so a node's distance is stacked with
+        // it by its parent and the pop re-tests it against the (possibly tighter) bound without
+        // re-loading the node's box -- one dependent global round per node instead of two for a
+        // lone, latency-bound wave. The root holds the query: distance 0.
+        int sp = dfs ? 1 : 0;
+        if (lane == 0) { stk[0] = 1; sbd[0] = 0.f; }
         __builtin_amdgcn_wave_barrier();
         while (sp > 0) {
             --sp;
             const int node = __builtin_amdgcn_readfirstlane(stk[sp]);
-            const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
+            const float bd = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sbd[sp])));
             if (!(bd < INFINITY && bd * kShrink <= thr)) continue;
             if (node >= a.P) {
                 if (cnt + 64 > kTCap) compact();
@@ -681,10 +762,11 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
             const bool need1 = b1 < INFINITY && b1 * kShrink <= thr;
             const bool first0 = b0 <= b1;
             const int nearc = first0 ? c0 : c0 + 1, farc = first0 ? c0 + 1 : c0;
+            const float nearb = first0 ? b0 : b1, farb = first0 ? b1 : b0;
             const bool nn = first0 ? need0 : need1, nf = first0 ? need1 : need0;
             if (lane == 0) {
-                if (nf) stk[sp] = farc;
-                if (nn) stk[sp + (nf ? 1 : 0)] = nearc;
+                if (nf) { stk[sp] = farc; sbd[sp] = farb; }
+                if (nn) { stk[sp + (nf ? 1 : 0)] = nearc; sbd[sp + (nf ? 1 : 0)] = nearb; }
             }
             sp += (nf ? 1 : 0) + (nn ? 1 : 0);
             __builtin_amdgcn_wave_barrier();
