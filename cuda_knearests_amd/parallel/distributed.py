@@ -173,7 +173,9 @@ class DistributedKNearests:
         # 3; no collective inside the captured step), opt-in above (KN_DIST_GRAPH=1 or
         # graph_steady = True: capturing RCCL collectives cannot be exercised on a one-GPU box);
         # KN_DIST_GRAPH=0 / graph_steady = False turn it off. Replayed rows live in the graph's
-        # static buffers until the next solve. At world 1 200 back-to-back replays are valid and
+        # static buffers until the next solve (read-only: at world 1 `ids` of an async replayed
+        # step is the caller's id tensor or the cached 0..n-1 table; synchronous calls return
+        # copies). At world 1 200 back-to-back replays are valid and
         # bit-identical to the eager steady step on the release and the bounds-checked builds, host
         # enqueue 0.14 -> 0.06 ms per step (profiles/ab_r2_dist_graph.txt). The world-1 steady
         # step skips the routing passes (the share is the local set), reads the caller's input in
@@ -651,6 +653,8 @@ class DistributedKNearests:
             stats["graph"] = True
             return DistResult(gid, idx, d2, stats, flag=g["host"], event=ev)
         gid, idx, d2, flag = self._steady_body(points, ids)
+        if st.get("gids1") is not None and gid.data_ptr() == st["gids1"].data_ptr():
+            gid = gid.clone()  # world 1: never hand out the cached id table itself
         host = torch.empty(1, dtype=torch.int32, pin_memory=points.is_cuda)
         host.copy_(flag, non_blocking=True)
         ev = torch.cuda.Event() if points.is_cuda else None

@@ -3,7 +3,7 @@
 # kernel stats of the default (pipelined) bench, the distributed path at world 1 for comparison.
 set -o pipefail
 export PYTHONPATH=$PWD
-O=gpurun_out/end3
+O=gpurun_out/${END_DIR:-end3}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo TESTS_FAIL; tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
