@@ -1,8 +1,8 @@
 """Bounds-checked run (KN_CHECKED=1 loads _C_checked) of the tree path after the round-3 exact
 kernel change (breadth-first sweep of bounded listed queries, stacked node distances on the
 depth-first walk, K > 64 every query): clustered and surface clouds through algo="tree",
-squared distances against the kd-tree oracle, then the violation words (all 0xFFFFFFFF = no
-out-of-range index)."""
+squared distances against the kd-tree oracle, then the violation words (all 0 = no out-of-range
+index)."""
 import os
 
 os.environ["KN_CHECKED"] = "1"
