@@ -1,5 +1,7 @@
 #!/bin/bash
 # Every BASELINE.json configuration on one MI355X (run through gpurun from the repo root).
+# Step counts time the steady state (the first ~30 steps after idle run ~10 % slow,
+# profiles/bench_r3_steps.txt).
 # One JSON line per configuration -> gpurun_out/bench_suite.jsonl (copy to profiles/).
 #   1. pts20K.xyz, k=8, CPU kd-tree path            (+ the same file on the GPU)
 #   2. 300K uniform, k=16, 1 GPU                     (pts300K.xyz is missing from the reference)
@@ -30,14 +32,14 @@ PY
   echo "ok $label"
 }
 run 200 "cfg1 pts20K k8 cpu-kdtree" --cpu-oracle --k 8 --steps 5
-run 200 "cfg1b pts20K k8 gpu" --xyz data/pts20K.xyz --k 8 --steps 50 --warmup 10
-run 200 "cfg2 300K uniform k16 gpu" --n 300000 --k 16 --steps 50 --warmup 10
-run 200 "cfg3 900K blue k16 gpu" --gen blue --n 900000 --k 16 --steps 50 --warmup 10
-run 200 "headline 900K uniform k16 gpu" --n 900000 --k 16 --steps 50 --warmup 10
-run 200 "900K uniform k50 gpu (reference K)" --n 900000 --k 50 --steps 20 --warmup 5
-run 300 "cfg4 10M uniform k32 gpu" --n 10000000 --k 32 --steps 10 --warmup 3
-run 200 "900K points on surfaces k16 gpu (occupancy-adaptive grid)" --gen surface --n 900000 --k 16 --steps 10 --warmup 2
-run 300 "900K clustered k16 gpu (occupancy-adaptive grid)" --gen clustered --n 900000 --k 16 --steps 5 --warmup 1
-run 300 "cfg5a 12.5M/rank k16 rccl world1 (100M/8 share)" --dist --n 12500000 --k 16 --steps 5 --warmup 2
-run 600 "cfg5b 100M k16 loopback 8 ranks on 1 gpu" --loopback 8 --n 12500000 --k 16 --steps 3 --warmup 1
+run 200 "cfg1b pts20K k8 gpu" --xyz data/pts20K.xyz --k 8 --steps 200 --warmup 50
+run 200 "cfg2 300K uniform k16 gpu" --n 300000 --k 16 --steps 200 --warmup 50
+run 200 "cfg3 900K blue k16 gpu" --gen blue --n 900000 --k 16 --steps 200 --warmup 50
+run 200 "headline 900K uniform k16 gpu" --n 900000 --k 16 --steps 200 --warmup 50
+run 200 "900K uniform k50 gpu (reference K)" --n 900000 --k 50 --steps 100 --warmup 30
+run 300 "cfg4 10M uniform k32 gpu" --n 10000000 --k 32 --steps 20 --warmup 5
+run 200 "900K points on surfaces k16 gpu (occupancy-adaptive grid)" --gen surface --n 900000 --k 16 --steps 100 --warmup 20
+run 300 "900K clustered k16 gpu (occupancy-adaptive grid)" --gen clustered --n 900000 --k 16 --steps 100 --warmup 20
+run 300 "cfg5a 12.5M/rank k16 rccl world1 (100M/8 share)" --dist --n 12500000 --k 16 --steps 20 --warmup 5
+run 600 "cfg5b 100M k16 loopback 8 ranks on 1 gpu" --loopback 8 --n 12500000 --k 16 --steps 5 --warmup 2
 cat $OUT
