@@ -188,8 +188,10 @@ kn_status kn_get_multi_stats(kn_multi *m, kn_multi_stats *out);
  * 4 kn_multi_stats. */
 size_t kn_struct_size(int which);
 
-/* Extension: free the device arenas that kn_free parks for reuse by the next kn_prepare (a
-   process-wide cache of at most 2 arenas per device; KN_ARENA_CACHE=0 disables it). */
+/* Extension: free the device blocks that kn_free parks for reuse by the next kn_prepare (a
+   process-wide cache of at most 8 blocks per device and 4 GiB in all: arenas, result and tree
+   buffers; KN_ARENA_CACHE=0 disables it). An allocation that fails for lack of device memory
+   frees the cache and retries once by itself. */
 void kn_release_cached_memory(void);
 
 #ifdef __cplusplus

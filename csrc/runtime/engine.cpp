@@ -74,7 +74,7 @@ hipError_t Engine::dmalloc(void** p, size_t bytes) {
         dsize_[c] = got;
         return hipSuccess;
     }
-    hipError_t e = hipMalloc(p, bytes);
+    hipError_t e = device_malloc(p, bytes);
     if (e == hipSuccess) dsize_[*p] = bytes;
     return e;
 }
@@ -160,10 +160,11 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
             arena_ = static_cast<char*>(c);
             arena_bytes_ = got;
         } else {
-            if ((st = check(hipMalloc(&arena_, bytes), "hipMalloc(arena)")) != KN_OK) return st;
+            if ((st = check(device_malloc(reinterpret_cast<void**>(&arena_), bytes), "hipMalloc(arena)")) != KN_OK) return st;
             arena_bytes_ = bytes;
         }
     }
+    arena_used_ = bytes;
     if (std::getenv("KN_PREP_TIMING"))
         fprintf(stderr, "allocate: stream/events + arena %.3f ms (arena %zu B)\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta0).count(), arena_bytes_);
@@ -494,7 +495,7 @@ kn_status Engine::set_k(int k) {
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_})
         if (*q) { dfree(*q); *q = nullptr; }
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
-    drop_pipeline();
+    drop_pipeline(true);  // the grid stays: the next solve() queries it with the new K
     solved_ = stored_valid_ = false;
     return KN_OK;
 }
@@ -534,7 +535,7 @@ static int pipe_prio() {
     return v && std::atoi(v) == 1 ? 1 : 0;
 }
 
-void Engine::drop_pipeline() {
+void Engine::drop_pipeline(bool keep_grid) {
     for (auto& g : pgraph_)
         if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
     if (bstream_) {
@@ -546,7 +547,18 @@ void Engine::drop_pipeline() {
         bstream_ = nullptr;
         for (auto& e : pev_) e = nullptr;
     }
-    if (arena2_) { dfree(arena2_); arena2_ = nullptr; }
+    if (live_alt_) {
+        // the live grid sits in arena2_, which is about to go back to the block cache: move the
+        // members back to arena_ (copying the grid over when it is still needed) and drop the
+        // graph captured against the arena2_ set
+        if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+        const size_t pts = align_up((size_t)n_ * 3 * sizeof(float));
+        if (keep_grid && arena2_ && arena_used_ > pts)
+            (void)hipMemcpyAsync(arena_ + pts, arena2_ + pts, arena_used_ - pts, hipMemcpyDeviceToDevice, stream_);
+        swap_grid_set();
+        live_alt_ = false;
+    }
+    if (arena2_) { dfree(arena2_); arena2_ = nullptr; }  // dfree waits for stream_ (the copy)
     if (alt_.tree_ws) dfree(alt_.tree_ws);
     if (alt_.tree_nodes) dfree(alt_.tree_nodes);
     alt_ = GridSet{};
@@ -663,6 +675,9 @@ kn_status Engine::launch_pipelined(int iters) {
         std::swap(pev_[0], pev_[1]);
         std::swap(pev_[2], pev_[3]);
         ++pipe_i_;
+        live_alt_ = !live_alt_;
+        // a serial-step graph captured before holds the other set's pointers
+        if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     }
     solved_ = true;
     stored_valid_ = points3_valid_ = false;

@@ -122,13 +122,16 @@ private:
         void* tree_nodes;
     };
     void swap_grid_set();  // exchange the grid-set members with alt_
-    void drop_pipeline();
+    // keep_grid: the live grid (maybe in arena2_) must survive into arena_ (set_k keeps solving it)
+    void drop_pipeline(bool keep_grid = false);
     GridSet alt_{};
     char* arena2_ = nullptr;
     hipStream_t bstream_ = nullptr;
     hipEvent_t pev_[4] = {nullptr, nullptr, nullptr, nullptr};  // built s0, s1; queried s0, s1
     hipGraphExec_t pgraph_[4] = {nullptr, nullptr, nullptr, nullptr};  // build s0, s1; query s0, s1
     unsigned long long pipe_i_ = 0;
+    bool live_alt_ = false;  // the grid-set members point into arena2_ (an odd number of relabels)
+    size_t arena_used_ = 0;  // bytes of arena_ carved by allocate() (arena2_ has the same carve)
 
     EngineConfig cfg_;
     AutoParams ap_{};

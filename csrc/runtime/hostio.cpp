@@ -231,6 +231,16 @@ void streamset_release(int device, const StreamSet& s, int priority) {
     (void)hipStreamDestroy(s.stream);
 }
 
+hipError_t device_malloc(void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipErrorOutOfMemory) return e;
+    // blocks parked in the cache (up to kPoolPerDevice per device, kPoolMaxBytes in all) may be
+    // what the device is missing: give them back and retry once
+    (void)hipGetLastError();
+    arena_release_all();
+    return hipMalloc(p, bytes);
+}
+
 void arena_release_all() {
     std::lock_guard<std::mutex> lock(g_pool_mu);
     int cur = 0;

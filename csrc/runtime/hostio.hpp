@@ -32,6 +32,9 @@ hipError_t copy_d2h_staged(void* h, const void* d, size_t bytes, hipStream_t s);
 void* arena_acquire(int device, size_t bytes, size_t* got);
 void arena_release(int device, void* p, size_t bytes);
 void arena_release_all();
+// hipMalloc that, on hipErrorOutOfMemory, frees every parked cache block and retries once (the
+// cache must never be why an allocation fails)
+hipError_t device_malloc(void** p, size_t bytes);
 
 // Stream + 4 timing events of an engine from a per-device pool (creating a HIP stream and its
 // events cost 2-8 ms per kn_prepare on MI355X, measured with KN_PREP_TIMING): acquire creates when

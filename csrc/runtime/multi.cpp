@@ -28,6 +28,8 @@
 // synchronises at the meta, split-histogram, count, certification and result copies.
 #include <hip/hip_runtime.h>
 
+#include "hostio.hpp"
+
 #include <algorithm>
 #include <array>
 #include <chrono>
@@ -171,7 +173,7 @@ hipError_t ensure(kn_multi* m, DBuf& b, size_t bytes) {
     b.p = nullptr;
     b.cap = 0;
     const size_t want = bytes + bytes / 8;
-    hipError_t e = hipMalloc(&b.p, want);
+    hipError_t e = kn::device_malloc(&b.p, want);
     if (e != hipSuccess) return e;
     b.cap = want;
     ++m->allocations;

@@ -1025,6 +1025,7 @@ public:
         TORCH_CHECK(e_->upload_device(points.data_ptr<float>(), (int)points.size(0)) == KN_OK, e_->error());
     }
     void solve() { TORCH_CHECK(e_->solve() == KN_OK, e_->error()); }
+    void set_k(int64_t k) { TORCH_CHECK(e_->set_k((int)k) == KN_OK, e_->error()); }
     void launch_graph(int64_t iters) { TORCH_CHECK(e_->launch_graph((int)iters) == KN_OK, e_->error()); }
     void launch_pipelined(int64_t iters) { TORCH_CHECK(e_->launch_pipelined((int)iters) == KN_OK, e_->error()); }
     // stored -> original permutation of the engine's current grid (host int32)
@@ -1254,6 +1255,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("prepare", &PyEngine::prepare)
         .def("prepare_async", &PyEngine::prepare_async)
         .def("solve", &PyEngine::solve)
+        .def("set_k", &PyEngine::set_k)
         .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
         .def("launch_pipelined", &PyEngine::launch_pipelined, py::arg("iters") = 1)
         .def("get_permutation", &PyEngine::permutation)

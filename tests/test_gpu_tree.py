@@ -153,3 +153,41 @@ def test_engine_pipelined_steps(cuda, k, gen):
     e.sync()
     i3, e3 = e.results(cuda)
     assert torch.equal(i3, idx) and torch.equal(e3, d2)
+
+
+@pytest.mark.parametrize("k", [16])
+def test_engine_pipeline_relabel_then_new_points(cuda, k):
+    """A serial graph captured before an even number of pipelined steps must not survive the
+    grid-set relabel: launch_graph -> launch_pipelined(2) -> new points -> launch_graph
+    rebuilds into the LIVE set, so the permutation and the rows match a fresh engine on the new
+    points; set_k after an even pipelined run keeps the live grid (no use of freed memory)."""
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    p = uniform_cloud(50000, seed=71).to(cuda)
+    q = (p + 0.37).contiguous()  # moved cloud, same size
+    e = C.Engine(k)
+    e.prepare(p)
+    e.launch_graph(1)
+    e.launch_pipelined(2)
+    e.sync()
+    e.prepare_async(q)
+    e.launch_graph(1)
+    e.sync()
+    ref = C.Engine(k)
+    ref.prepare(q)
+    ref.solve()
+    i1, d1 = e.results(cuda)
+    i0, d0 = ref.results(cuda)
+    assert torch.equal(i1, i0) and torch.equal(d1, d0)
+    assert torch.equal(e.get_permutation(), ref.get_permutation())
+    # even pipelined run, then a K change: the grid stays valid for the next solve
+    e.launch_pipelined(2)
+    e.sync()
+    e.set_k(8)
+    e.solve()
+    ref.set_k(8)
+    ref.solve()
+    i1, d1 = e.results(cuda)
+    i0, d0 = ref.results(cuda)
+    assert torch.equal(i1, i0) and torch.equal(d1, d0)
