@@ -114,7 +114,23 @@ def run_native(args) -> dict:
     # pipelined steps (default; kn::Engine::launch_pipelined): step i+1's binning runs on a second
     # stream while step i queries (two grid sets); every step still bins and queries the whole
     # cloud. --no-pipeline: serial graph replays
-    launch = e.launch_pipelined if args.pipeline else e.launch_graph
+    if args.stream_clouds:
+        # a stream of distinct clouds (kn::Engine::stream_step): every step copies ITS cloud into
+        # the free grid set, bins and queries it; the next cloud is binned while this one queries
+        clouds = [pts] + [make_cloud(args, dev, 104729 * j) for j in range(1, args.stream_clouds)]
+        M = len(clouds)
+        state = {"i": 0}
+
+        def launch(n):
+            for _ in range(n):
+                i = state["i"]
+                e.stream_step(clouds[i % M], clouds[(i + 1) % M])
+                state["i"] = i + 1
+    elif args.pipeline:
+        def launch(n):
+            e.launch_pipelined(n, args.unroll)
+    else:
+        launch = e.launch_graph
     launch(args.warmup)
     e.sync()
     log("warmup done")
@@ -124,7 +140,8 @@ def run_native(args) -> dict:
     dt = time.perf_counter() - t0
     log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
     idx, d2 = e.results(dev)
-    chk = brute_check(pts, torch.arange(pts.size(0), device=dev), idx, d2, args.k) if not args.no_check else {}
+    last = clouds[(state["i"] - 1) % M] if args.stream_clouds else pts
+    chk = brute_check(last, torch.arange(last.size(0), device=dev), idx, d2, args.k) if not args.no_check else {}
     log(f"check {chk}")
     bts, sts = [], []
     for _ in range(5):
@@ -392,6 +409,12 @@ def main() -> int:
                     help="native 1-GPU path: serial steps (default: step i+1's binning overlaps step i's "
                          "queries on a second stream, two grid sets; every step bins and queries the whole "
                          "cloud)")
+    ap.add_argument("--unroll", type=int, default=-1,
+                    help="native pipelined steps per graph launch (even; 0: one graph per stage; -1: KN_PIPE_UNROLL "
+                         "or the engine default)")
+    ap.add_argument("--stream-clouds", type=int, default=0,
+                    help="native 1-GPU path: cycle M distinct clouds (a new cloud every step, copied into the free "
+                         "grid set, binned and queried) instead of re-solving one resident cloud")
     ap.add_argument("--path", choices=["native", "torch"], default="native",
                     help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
     ap.add_argument("--no-check", action="store_true")
@@ -460,7 +483,8 @@ def main() -> int:
         extra = {"ms_build": round(r["ms_build"], 4), "ms_solve": round(r["ms_solve"], 4),
                  "grid": r.get("dims"), "query_algo": r.get("algo", "grid"),
                  "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph, "path": args.path,
-                 "pipelined": bool(args.pipeline)}
+                 "pipelined": bool(args.pipeline), "unroll": args.unroll,
+                 **({"stream_clouds": args.stream_clouds} if args.stream_clouds else {})}
     ms = r["t"] / args.steps * 1e3
     qps = r["n_total"] * args.steps / r["t"]
     line = {

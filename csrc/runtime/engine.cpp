@@ -183,6 +183,9 @@ kn_status Engine::allocate(int n, const int* dims_override, bool refined, int xs
     fallback_ = carve<unsigned>(p, n);
     counters_ = carve<unsigned>(p, kNumCounters);
     occ_ = carve<unsigned long long>(p, 1);
+    live_ = 0;
+    graph_set_ = -1;
+    set_[0] = members();
     // outputs
     for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&inv_perm_, (void**)&knn_stored_,
                      (void**)&points3_})
@@ -286,6 +289,8 @@ kn_status Engine::ensure_tree() {
         if ((st = check(dmalloc(&tree_nodes_, nb), "hipMalloc(tree nodes)")) != KN_OK) return st;
         tree_nodes_bytes_ = nb;
     }
+    set_[live_].tree_ws = tree_ws_;
+    set_[live_].tree_nodes = tree_nodes_;
     return KN_OK;
 }
 
@@ -408,6 +413,10 @@ kn_status Engine::upload_device(const float* d_pts, int n) {
     if (!arena_ || n != n_) {
         if ((st = allocate(n)) != KN_OK) return st;
     }
+    // the primed pipelined build (if any) reads the other set's input: let it finish, it is stale
+    if ((st = check(pipe_.unprime(), "pipeline")) != KN_OK) return st;
+    other_stale_ = true;
+    stream_mode_ = false;
     if (n > 0 && (st = check(hipMemcpyAsync(points_, d_pts, (size_t)n * 12, hipMemcpyDeviceToDevice, stream_),
                              "D2D points")) != KN_OK)
         return st;
@@ -504,7 +513,9 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     if (!built_) return fail(KN_ERR_STATE, "run_graph() before prepare()");
     kn_status st;
     if ((st = ensure_outputs()) != KN_OK) return st;  // not inside the capture
+    if (graph_ && graph_set_ != live_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (!graph_) {
+        graph_set_ = live_;
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
         kn_status s1 = build_async(true);
@@ -535,11 +546,23 @@ static int pipe_prio() {
     return v && std::atoi(v) == 1 ? 1 : 0;
 }
 
+Engine::GridSet Engine::members() const {
+    return GridSet{points_, bbox_, geom_, cell_count_, cell_scan_, block_sums_, cell_start_, cell_rank_, bin_tmp_,
+                   sorted_, perm_, fallback_, counters_, occ_, tree_ws_, tree_nodes_};
+}
+
+void Engine::view_set(int s) {
+    const GridSet& g = set_[s];
+    points_ = g.points; bbox_ = g.bbox; geom_ = g.geom; cell_count_ = g.cell_count; cell_scan_ = g.cell_scan;
+    block_sums_ = g.block_sums; cell_start_ = g.cell_start; cell_rank_ = g.cell_rank; bin_tmp_ = g.bin_tmp;
+    sorted_ = g.sorted; perm_ = g.perm; fallback_ = g.fallback; counters_ = g.counters; occ_ = g.occ;
+    tree_ws_ = g.tree_ws; tree_nodes_ = g.tree_nodes;
+    live_ = s;
+}
+
 void Engine::drop_pipeline(bool keep_grid) {
-    for (auto& g : pgraph_)
-        if (g) { (void)hipGraphExecDestroy(g); g = nullptr; }
+    pipe_.reset();  // waits for both streams, destroys the stage graphs
     if (bstream_) {
-        (void)hipStreamSynchronize(bstream_);
         StreamSet ss;
         ss.stream = bstream_;
         for (int i = 0; i < 4; ++i) ss.ev[i] = pev_[i];
@@ -547,138 +570,168 @@ void Engine::drop_pipeline(bool keep_grid) {
         bstream_ = nullptr;
         for (auto& e : pev_) e = nullptr;
     }
-    if (live_alt_) {
-        // the live grid sits in arena2_, which is about to go back to the block cache: move the
-        // members back to arena_ (copying the grid over when it is still needed) and drop the
-        // graph captured against the arena2_ set
+    if (live_ == 1) {
+        // the live grid sits in arena2_, which is about to go back to the block cache: copy it (with
+        // its input points) to arena_ when it is still needed, view set 0 again and drop the graph
+        // captured against set 1
         if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
-        const size_t pts = align_up((size_t)n_ * 3 * sizeof(float));
-        if (keep_grid && arena2_ && arena_used_ > pts)
-            (void)hipMemcpyAsync(arena_ + pts, arena2_ + pts, arena_used_ - pts, hipMemcpyDeviceToDevice, stream_);
-        swap_grid_set();
-        live_alt_ = false;
+        if (keep_grid && arena2_ && arena_used_)
+            (void)hipMemcpyAsync(arena_, arena2_, arena_used_, hipMemcpyDeviceToDevice, stream_);
+        // the live tree buffers (same sizes in both sets) stay with the live view
+        std::swap(set_[0].tree_ws, set_[1].tree_ws);
+        std::swap(set_[0].tree_nodes, set_[1].tree_nodes);
+        view_set(0);
     }
     if (arena2_) { dfree(arena2_); arena2_ = nullptr; }  // dfree waits for stream_ (the copy)
-    if (alt_.tree_ws) dfree(alt_.tree_ws);
-    if (alt_.tree_nodes) dfree(alt_.tree_nodes);
-    alt_ = GridSet{};
-    pipe_i_ = 0;
+    if (set_[1].tree_ws) dfree(set_[1].tree_ws);
+    if (set_[1].tree_nodes) dfree(set_[1].tree_nodes);
+    set_[1] = GridSet{};
+    set_[0] = members();
+    other_stale_ = true;
 }
 
-void Engine::swap_grid_set() {
-    std::swap(bbox_, alt_.bbox); std::swap(geom_, alt_.geom); std::swap(cell_count_, alt_.cell_count);
-    std::swap(cell_scan_, alt_.cell_scan); std::swap(block_sums_, alt_.block_sums);
-    std::swap(cell_start_, alt_.cell_start); std::swap(cell_rank_, alt_.cell_rank); std::swap(bin_tmp_, alt_.bin_tmp);
-    std::swap(sorted_, alt_.sorted); std::swap(perm_, alt_.perm); std::swap(fallback_, alt_.fallback);
-    std::swap(counters_, alt_.counters); std::swap(occ_, alt_.occ);
-    std::swap(tree_ws_, alt_.tree_ws); std::swap(tree_nodes_, alt_.tree_nodes);
+// Stage bodies of the pipeline (captured once per set): the members view set s while the stage
+// enqueues, then the live view comes back.
+kn_status Engine::stage_build(int s, hipStream_t st) {
+    const int keep = live_;
+    hipStream_t ks = stream_;
+    view_set(s);
+    stream_ = st;
+    kn_status r = build_async(true);
+    if (r == KN_OK && use_tree_) r = tree_build_async();
+    stream_ = ks;
+    view_set(keep);
+    return r;
 }
 
-// Software-pipelined steps over two grid sets (s = step parity): build(i) on bstream_ after the
-// query of step i-2 released set s; query(i) on stream_ after build(i). The query kernel fills the
-// chip, and the build's five latency-bound kernels (~50 us at 900K, ~15 % of a step) run in its
-// shadow. Each of the 4 stage graphs is captured once.
-kn_status Engine::launch_pipelined(int iters) {
-    if (!built_) return fail(KN_ERR_STATE, "launch_pipelined() before prepare()");
+kn_status Engine::stage_query(int s, hipStream_t st) {
+    const int keep = live_;
+    hipStream_t ks = stream_;
+    view_set(s);
+    stream_ = st;
+    kn_status r = use_tree_ ? tree_query_async() : query_async(true);
+    stream_ = ks;
+    view_set(keep);
+    return r;
+}
+
+// The second grid set (same carve as allocate(), its own input points) + the build stream +
+// the pipeline's stage graphs.
+kn_status Engine::ensure_pipeline() {
     kn_status st;
     if ((st = ensure_outputs()) != KN_OK) return st;
-    if (!pgraph_[0]) {
-        if (!arena2_) {
-            if ((st = check(dmalloc(&arena2_, arena_bytes_), "hipMalloc(grid set 2)")) != KN_OK) return st;
-            // the same carve as allocate(); points_ stays shared (read-only input of every build)
-            const int C = C_, n = n_;
-            const size_t nb = scan_block_count(C) + 1;
-            char* p = arena2_;
-            (void)carve<float>(p, (size_t)n * 3);
-            alt_.bbox = carve<unsigned>(p, kBBoxWords);
-            alt_.geom = carve<GridGeom>(p, 1);
-            alt_.cell_count = carve<int>(p, C + 1);
-            alt_.cell_scan = carve<int>(p, C + 1);
-            alt_.cell_start = carve<int>(p, C + 1);
-            alt_.block_sums = carve<int>(p, nb);
-            alt_.bin_tmp = carve<float4>(p, n);
-            alt_.cell_rank = reinterpret_cast<int2*>(alt_.bin_tmp);
-            alt_.sorted = carve<float4>(p, n);
-            alt_.perm = carve<unsigned>(p, n);
-            alt_.fallback = carve<unsigned>(p, n);
-            alt_.counters = carve<unsigned>(p, kNumCounters);
-            alt_.occ = carve<unsigned long long>(p, 1);
-            if (use_tree_) {
-                // the second set's tree workspace and node buffer (the first set's come from ensure_tree)
-                if ((st = check(dmalloc(&alt_.tree_ws, tree_workspace_bytes(n_, ap_.dims)), "hipMalloc(tree 2)")) != KN_OK ||
-                    (st = check(dmalloc(&alt_.tree_nodes, tree_node_bytes(n_)), "hipMalloc(tree nodes 2)")) != KN_OK) {
-                    drop_pipeline();
-                    return st;
-                }
+    set_[live_] = members();  // tree buffers allocated since the last carve
+    if (!arena2_) {
+        if ((st = check(dmalloc(&arena2_, arena_bytes_), "hipMalloc(grid set 2)")) != KN_OK) return st;
+        const int C = C_, n = n_;
+        const size_t nb = scan_block_count(C) + 1;
+        char* p = arena2_;
+        GridSet& g = set_[live_ ^ 1];
+        g.points = carve<float>(p, (size_t)n * 3);
+        g.bbox = carve<unsigned>(p, kBBoxWords);
+        g.geom = carve<GridGeom>(p, 1);
+        g.cell_count = carve<int>(p, C + 1);
+        g.cell_scan = carve<int>(p, C + 1);
+        g.cell_start = carve<int>(p, C + 1);
+        g.block_sums = carve<int>(p, nb);
+        g.bin_tmp = carve<float4>(p, n);
+        g.cell_rank = reinterpret_cast<int2*>(g.bin_tmp);
+        g.sorted = carve<float4>(p, n);
+        g.perm = carve<unsigned>(p, n);
+        g.fallback = carve<unsigned>(p, n);
+        g.counters = carve<unsigned>(p, kNumCounters);
+        g.occ = carve<unsigned long long>(p, 1);
+        g.tree_ws = g.tree_nodes = nullptr;
+        if (use_tree_) {
+            if ((st = check(dmalloc(&g.tree_ws, tree_workspace_bytes(n_, ap_.dims)), "hipMalloc(tree 2)")) != KN_OK ||
+                (st = check(dmalloc(&g.tree_nodes, tree_node_bytes(n_)), "hipMalloc(tree nodes 2)")) != KN_OK) {
+                drop_pipeline();
+                return st;
             }
         }
-        if (!bstream_) {
-            // KN_PIPE_PRIO=1: the build stream at the device's highest priority (its latency-bound
-            // kernels then take CU slots as soon as the query's workgroups free them)
-            StreamSet ss;
-            if ((st = check(streamset_acquire(cfg_.device, &ss, pipe_prio()), "hipStreamCreate")) != KN_OK) return st;
-            bstream_ = ss.stream;
-            for (int i = 0; i < 4; ++i) pev_[i] = ss.ev[i];
-        }
-        // capture the 4 stage graphs on stream_ (a graph can be launched on any stream)
-        for (int set = 0; set < 2; ++set) {
-            if (set == 1) swap_grid_set();
-            for (int stage = 0; stage < 2; ++stage) {
-                hipGraph_t g;
-                kn_status s1 = KN_OK;
-                if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) {
-                    if (set == 1) swap_grid_set();
-                    return st;
-                }
-                // tree path: the build stage also builds the set's tree, the query stage queries it
-                if (stage == 0) {
-                    s1 = build_async(true);
-                    if (s1 == KN_OK && use_tree_) s1 = tree_build_async();
-                } else {
-                    s1 = use_tree_ ? tree_query_async() : query_async(true);
-                }
-                hipError_t e = hipStreamEndCapture(stream_, &g);
-                if (s1 == KN_OK && e == hipSuccess) {
-                    e = hipGraphInstantiate(&pgraph_[stage * 2 + set], g, nullptr, nullptr, 0);
-                    (void)hipGraphDestroy(g);
-                }
-                if (s1 != KN_OK || e != hipSuccess) {
-                    if (set == 1) swap_grid_set();
-                    drop_pipeline();
-                    return s1 != KN_OK ? s1 : check(e, "pipeline capture");
-                }
-            }
-            if (set == 1) swap_grid_set();
-        }
-        // both sets start free
-        for (int s = 0; s < 2; ++s)
-            if ((st = check(hipEventRecord(pev_[2 + s], stream_), "event")) != KN_OK) return st;
-        pipe_i_ = 0;
+        other_stale_ = true;
     }
-    for (int i = 0; i < iters; ++i, ++pipe_i_) {
-        const int s = (int)(pipe_i_ & 1);
-        if ((st = check(hipStreamWaitEvent(bstream_, pev_[2 + s], 0), "wait query")) != KN_OK) return st;
-        if ((st = check(hipGraphLaunch(pgraph_[s], bstream_), "build launch")) != KN_OK) return st;
-        if ((st = check(hipEventRecord(pev_[s], bstream_), "event")) != KN_OK) return st;
-        if ((st = check(hipStreamWaitEvent(stream_, pev_[s], 0), "wait build")) != KN_OK) return st;
-        if ((st = check(hipGraphLaunch(pgraph_[2 + s], stream_), "query launch")) != KN_OK) return st;
-        if ((st = check(hipEventRecord(pev_[2 + s], stream_), "event")) != KN_OK) return st;
+    if (!bstream_) {
+        // KN_PIPE_PRIO=1: the build stream at the device's highest priority (its latency-bound
+        // kernels then take CU slots as soon as the query's workgroups free them)
+        StreamSet ss;
+        if ((st = check(streamset_acquire(cfg_.device, &ss, pipe_prio()), "hipStreamCreate")) != KN_OK) return st;
+        bstream_ = ss.stream;
+        for (int i = 0; i < 4; ++i) pev_[i] = ss.ev[i];
     }
-    // the last step's grid is the engine's current grid (getters, stats, stored-space views)
-    if ((pipe_i_ & 1) == 0 && iters > 0) {
-        // the last step used set 1: relabel it set 0 (host bookkeeping only: the queued graphs hold
-        // their own pointers, and later getters are stream-ordered after the last query), and
-        // keep the parity so the next step builds into the other set
-        swap_grid_set();
-        std::swap(pgraph_[0], pgraph_[1]);
-        std::swap(pgraph_[2], pgraph_[3]);
-        std::swap(pev_[0], pev_[1]);
-        std::swap(pev_[2], pev_[3]);
-        ++pipe_i_;
-        live_alt_ = !live_alt_;
-        // a serial-step graph captured before holds the other set's pointers
-        if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
+    if (!pipe_.ready()) {
+        auto b = [this](int s, hipStream_t st2) { return stage_build(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
+        auto q = [this](int s, hipStream_t st2) { return stage_query(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
+        if ((st = check(pipe_.init(stream_, bstream_, b, q), "pipeline init")) != KN_OK) return st;
     }
+    return KN_OK;
+}
+
+static int pipe_unroll_default() {
+    const char* v = std::getenv("KN_PIPE_UNROLL");
+    return v ? std::atoi(v) : 0;
+}
+
+// Software-pipelined steps over two grid sets (pipeline.hpp): build(i+1) on bstream_ while
+// query(i) runs on stream_. The query kernel fills the chip and the build's five latency-bound
+// kernels (~50 us at 900K, ~15 % of a step) run in its shadow. Resident mode: every step bins
+// and queries the engine's current cloud (both sets hold it as input).
+kn_status Engine::launch_pipelined(int iters, int unroll) {
+    if (!built_) return fail(KN_ERR_STATE, "launch_pipelined() before prepare()");
+    kn_status st;
+    if ((st = ensure_pipeline()) != KN_OK) return st;
+    if (other_stale_) {
+        // the other set's input takes the live cloud (resident mode: both sets bin it); the
+        // primed build of a previous stream read other points
+        if ((st = check(pipe_.unprime(), "pipeline")) != KN_OK) return st;
+        if (n_ > 0 && (st = check(hipMemcpyAsync(set_[live_ ^ 1].points, points_, (size_t)n_ * 12,
+                                                 hipMemcpyDeviceToDevice, stream_), "D2D points")) != KN_OK)
+            return st;
+        if ((st = check(hipStreamSynchronize(stream_), "sync")) != KN_OK) return st;
+        other_stale_ = false;
+    }
+    stream_mode_ = false;
+    if (iters <= 0) return KN_OK;
+    if (unroll < 0) unroll = pipe_unroll_default();
+    hipError_t e = pipe_.launch(iters, unroll);
+    if (e != hipSuccess) {
+        drop_pipeline();
+        return check(e == hipErrorUnknown ? hipErrorLaunchFailure : e, "pipelined launch");
+    }
+    // the last step's grid is the engine's current grid (getters, stats, stored-space views);
+    // later getters are stream-ordered after its query (stream_), and the primed build writes the
+    // other set
+    view_set(pipe_.last_set());
+    solved_ = true;
+    stored_valid_ = points3_valid_ = false;
+    return KN_OK;
+}
+
+kn_status Engine::stream_step(const float* d_pts, const float* d_next) {
+    if (!built_) return fail(KN_ERR_STATE, "stream_step() before prepare()");
+    if (!d_pts && n_ > 0) return fail(KN_ERR_INVALID_ARGUMENT, "null points");
+    kn_status st;
+    if ((st = ensure_pipeline()) != KN_OK) return st;
+    const size_t bytes = (size_t)n_ * 12;
+    auto copy_in = [this, bytes](const float* src) {
+        return [this, bytes, src](int s, hipStream_t sd) {
+            return bytes ? hipMemcpyAsync(set_[s].points, src, bytes, hipMemcpyDeviceToDevice, sd) : hipSuccess;
+        };
+    };
+    if (!stream_mode_) {
+        // a resident-mode prime read the resident cloud: this stream's first step bins its own
+        if ((st = check(pipe_.unprime(), "pipeline")) != KN_OK) return st;
+        stream_mode_ = true;
+    }
+    Pipeline::Stage pre = copy_in(d_pts);
+    Pipeline::Stage nxt = copy_in(d_next);
+    hipError_t e = pipe_.step_with(pre, d_next ? &nxt : nullptr);
+    if (e != hipSuccess) {
+        drop_pipeline();
+        return check(e == hipErrorUnknown ? hipErrorLaunchFailure : e, "stream step");
+    }
+    view_set(pipe_.last_set());
+    other_stale_ = true;
     solved_ = true;
     stored_valid_ = points3_valid_ = false;
     return KN_OK;
@@ -688,7 +741,9 @@ kn_status Engine::launch_graph(int iters) {
     if (!built_) return fail(KN_ERR_STATE, "launch_graph() before prepare()");
     kn_status st;
     if ((st = ensure_outputs()) != KN_OK) return st;  // not inside the capture
+    if (graph_ && graph_set_ != live_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     if (!graph_) {
+        graph_set_ = live_;
         hipGraph_t g;
         if ((st = check(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal), "capture")) != KN_OK) return st;
         kn_status s1 = build_async(true);
@@ -708,7 +763,11 @@ kn_status Engine::launch_graph(int iters) {
     return KN_OK;
 }
 
-kn_status Engine::sync() { return check(hipStreamSynchronize(stream_), "stream sync"); }
+kn_status Engine::sync() {
+    kn_status st;
+    if ((st = check(pipe_.sync(), "pipeline sync")) != KN_OK) return st;
+    return check(hipStreamSynchronize(stream_), "stream sync");
+}
 
 kn_status Engine::copy_results(unsigned* d_idx, float* d_dist) {
     if (!solved_) return fail(KN_ERR_STATE, "not solved");

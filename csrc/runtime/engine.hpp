@@ -17,6 +17,7 @@
 #include "knearests.h"
 #include "kn/kernels.h"
 #include "kn/tree.h"
+#include "pipeline.hpp"
 
 namespace kn {
 
@@ -60,8 +61,15 @@ public:
     // Enqueue `iters` PIPELINED steps: two grid sets (and tree buffers on the tree path), the
     // build of step i+1 runs on a second stream while step i queries (a stream of clouds: each
     // step still bins and queries the whole cloud). sync() waits; results are the last step's.
-    kn_status launch_pipelined(int iters);
-    kn_status sync();
+    // unroll >= 2 (even): groups of `unroll` steps per graph (pipeline.hpp); < 0: KN_PIPE_UNROLL.
+    // The pipeline stays primed between calls (the next step's build is already enqueued).
+    kn_status launch_pipelined(int iters, int unroll = -1);
+    // A stream of distinct clouds (n points each, device pointers): the step's cloud is copied
+    // into the free grid set's input on the build stream, then binned and queried; `d_next`
+    // (may be null) is the next step's cloud, binned now, while this step queries. The results
+    // (original space) and the grid are this step's until the next call; sync() waits.
+    kn_status stream_step(const float* d_pts, const float* d_next);
+    kn_status sync();  // both streams
     // Device-to-device copy of the original-space results into caller buffers.
     kn_status copy_results(unsigned* d_idx, float* d_dist);
     kn_status counters(unsigned out[kNumCounters]);
@@ -113,24 +121,32 @@ private:
     QueryBuffers query_buffers() const;
     BuildBuffers build_buffers() const;
     void release();
-    // pipelined steps: the second grid set (same carve as the arena, own block) and its stream
+    // pipelined steps (pipeline.hpp): two grid sets, set 0 carved from arena_, set 1 from arena2_
+    // (same carve, input points included); the members above always view the LIVE set (the one
+    // the last step queried), so getters, stats and serial steps see the last step's grid
     struct GridSet {
-        unsigned* bbox; GridGeom* geom; int* cell_count; int* cell_scan; int* block_sums; int* cell_start;
-        int2* cell_rank; float4* bin_tmp; float4* sorted; unsigned* perm; unsigned* fallback; unsigned* counters;
-        unsigned long long* occ;
+        float* points; unsigned* bbox; GridGeom* geom; int* cell_count; int* cell_scan; int* block_sums;
+        int* cell_start; int2* cell_rank; float4* bin_tmp; float4* sorted; unsigned* perm; unsigned* fallback;
+        unsigned* counters; unsigned long long* occ;
         void* tree_ws;
         void* tree_nodes;
     };
-    void swap_grid_set();  // exchange the grid-set members with alt_
+    GridSet members() const;
+    void view_set(int s);  // members <- set_[s]
+    kn_status ensure_pipeline();
+    kn_status stage_build(int s, hipStream_t st);
+    kn_status stage_query(int s, hipStream_t st);
     // keep_grid: the live grid (maybe in arena2_) must survive into arena_ (set_k keeps solving it)
     void drop_pipeline(bool keep_grid = false);
-    GridSet alt_{};
+    GridSet set_[2]{};
+    int live_ = 0;             // set the members view
+    int graph_set_ = -1;       // set graph_ was captured against
+    bool other_stale_ = true;  // set live_^1's input differs from the live input
+    bool stream_mode_ = false; // the last pipelined steps were stream_step()s (distinct clouds)
     char* arena2_ = nullptr;
     hipStream_t bstream_ = nullptr;
-    hipEvent_t pev_[4] = {nullptr, nullptr, nullptr, nullptr};  // built s0, s1; queried s0, s1
-    hipGraphExec_t pgraph_[4] = {nullptr, nullptr, nullptr, nullptr};  // build s0, s1; query s0, s1
-    unsigned long long pipe_i_ = 0;
-    bool live_alt_ = false;  // the grid-set members point into arena2_ (an odd number of relabels)
+    hipEvent_t pev_[4] = {nullptr, nullptr, nullptr, nullptr};  // the side stream's pooled events
+    Pipeline pipe_;
     size_t arena_used_ = 0;  // bytes of arena_ carved by allocate() (arena2_ has the same carve)
 
     EngineConfig cfg_;

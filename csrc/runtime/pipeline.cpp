@@ -1,0 +1,249 @@
+// pipeline.cpp -- see pipeline.hpp.
+#include "pipeline.hpp"
+
+namespace kn {
+
+namespace {
+#define KN_TRY(expr)                          \
+    do {                                      \
+        hipError_t e_ = (expr);               \
+        if (e_ != hipSuccess) return e_;      \
+    } while (0)
+
+void destroy(hipGraphExec_t& g) {
+    if (g) (void)hipGraphExecDestroy(g);
+    g = nullptr;
+}
+void destroy(hipEvent_t& e) {
+    if (e) (void)hipEventDestroy(e);
+    e = nullptr;
+}
+}  // namespace
+
+hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r) {
+    reset();
+    main_ = main;
+    side_ = side;
+    b_ = std::move(b);
+    q_ = std::move(q);
+    r_ = std::move(r);
+    for (int s = 0; s < 2; ++s) {
+        for (hipEvent_t* e : {&evB_[s], &evQ_[s], &evF_[s]})
+            KN_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        // both sets start free
+        KN_TRY(hipEventRecord(evF_[s], main_));
+    }
+    KN_TRY(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming));
+    KN_TRY(hipEventRecord(last_done_, main_));
+    return hipSuccess;
+}
+
+void Pipeline::reset() {
+    if (main_) (void)hipStreamSynchronize(main_);
+    if (side_) (void)hipStreamSynchronize(side_);
+    for (int s = 0; s < 2; ++s) {
+        destroy(gB_[s]);
+        destroy(gQ_[s]);
+        destroy(gR_[s]);
+        destroy(gU_[s]);
+        gU_len_[s] = 0;
+        destroy(evB_[s]);
+        destroy(evQ_[s]);
+        destroy(evF_[s]);
+    }
+    destroy(last_done_);
+    for (auto& e : cap_ev_) destroy(e);
+    cap_ev_.clear();
+    main_ = side_ = nullptr;
+    next_ = 0;
+    primed_ = r_pending_ = false;
+    last_set_ = -1;
+}
+
+hipError_t Pipeline::capture(const Stage& st, int set, hipGraphExec_t* out) {
+    hipGraph_t g = nullptr;
+    KN_TRY(hipStreamBeginCapture(main_, hipStreamCaptureModeThreadLocal));
+    const hipError_t e1 = st(set, main_);
+    const hipError_t e2 = hipStreamEndCapture(main_, &g);
+    if (e1 != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        return e1;
+    }
+    KN_TRY(e2);
+    const hipError_t e3 = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    return e3;
+}
+
+hipError_t Pipeline::graphs() {
+    for (int s = 0; s < 2; ++s) {
+        if (!gB_[s]) KN_TRY(capture(b_, s, &gB_[s]));
+        if (!gQ_[s]) KN_TRY(capture(q_, s, &gQ_[s]));
+        if (r_ && !gR_[s]) KN_TRY(capture(r_, s, &gR_[s]));
+    }
+    return hipSuccess;
+}
+
+// U steps starting at set s0, both streams in one graph. Step j: Q(j) on the main branch after
+// B(j) (j = 0: built before the graph) and Q(j-1); on the side branch R(j-1) after Q(j-1), then
+// B(j+1) into the set Q(j-1) released. Ends after Q(U-1) and B(U) (R(U-1) is flushed after it).
+hipError_t Pipeline::unrolled(int s0, int U) {
+    if (gU_[s0] && gU_len_[s0] == U) return hipSuccess;
+    destroy(gU_[s0]);
+    gU_len_[s0] = 0;
+    const size_t need = 2 * (size_t)U + 2;
+    while (cap_ev_.size() < need) {
+        hipEvent_t e = nullptr;
+        KN_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        cap_ev_.push_back(e);
+    }
+    hipEvent_t fork = cap_ev_[0], join = cap_ev_[1];
+    hipEvent_t* eq = cap_ev_.data() + 2;      // after Q(j)
+    hipEvent_t* eb = cap_ev_.data() + 2 + U;  // after B(j+1)
+    hipGraph_t g = nullptr;
+    KN_TRY(hipStreamBeginCapture(main_, hipStreamCaptureModeThreadLocal));
+    hipError_t e = hipEventRecord(fork, main_);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side_, fork, 0);
+    for (int j = 0; j < U && e == hipSuccess; ++j) {
+        const int s = (s0 + j) & 1;
+        e = q_(s, main_);
+        if (e == hipSuccess) e = hipEventRecord(eq[j], main_);
+        if (e == hipSuccess && j >= 1) {
+            e = hipStreamWaitEvent(side_, eq[j - 1], 0);
+            if (e == hipSuccess && r_) e = r_(s ^ 1, side_);
+        }
+        if (e == hipSuccess) e = b_(s ^ 1, side_);
+        if (e == hipSuccess) e = hipEventRecord(eb[j], side_);
+        if (e == hipSuccess && j + 1 < U) e = hipStreamWaitEvent(main_, eb[j], 0);
+    }
+    if (e == hipSuccess) e = hipEventRecord(join, side_);
+    if (e == hipSuccess) e = hipStreamWaitEvent(main_, join, 0);
+    const hipError_t ee = hipStreamEndCapture(main_, &g);
+    if (e != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        return e;
+    }
+    KN_TRY(ee);
+    e = hipGraphInstantiate(&gU_[s0], g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e == hipSuccess) gU_len_[s0] = U;
+    return e;
+}
+
+hipError_t Pipeline::enqueue_build(int s) {
+    KN_TRY(hipStreamWaitEvent(side_, evF_[s], 0));
+    KN_TRY(hipGraphLaunch(gB_[s], side_));
+    return hipEventRecord(evB_[s], side_);
+}
+
+hipError_t Pipeline::enqueue_query(int s) {
+    KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
+    KN_TRY(hipGraphLaunch(gQ_[s], main_));
+    KN_TRY(hipEventRecord(evQ_[s], main_));
+    if (!r_) {
+        KN_TRY(hipEventRecord(evF_[s], main_));
+        KN_TRY(hipEventRecord(last_done_, main_));
+    }
+    return hipSuccess;
+}
+
+hipError_t Pipeline::enqueue_epilogue(int s) {
+    KN_TRY(hipStreamWaitEvent(side_, evQ_[s], 0));
+    KN_TRY(hipGraphLaunch(gR_[s], side_));
+    KN_TRY(hipEventRecord(evF_[s], side_));
+    return hipEventRecord(last_done_, side_);
+}
+
+hipError_t Pipeline::flush() {
+    if (!r_pending_) return hipSuccess;
+    r_pending_ = false;
+    return enqueue_epilogue(last_set_);
+}
+
+hipError_t Pipeline::launch(int iters, int unroll) {
+    if (!main_) return hipErrorNotInitialized;
+    KN_TRY(graphs());
+    if (unroll < 2 || (unroll & 1)) unroll = 0;
+    if (unroll && iters >= unroll) {
+        // both start parities up front: a capture never lands inside a later (timed) call
+        KN_TRY(unrolled(0, unroll));
+        KN_TRY(unrolled(1, unroll));
+    }
+    int done = 0;
+    while (done < iters) {
+        const int s = (int)(next_ & 1);
+        if (unroll && iters - done >= unroll) {
+            KN_TRY(unrolled(s, unroll));
+            if (!primed_) KN_TRY(enqueue_build(s));
+            KN_TRY(flush());
+            // the graph's first query reads set s (built on the side stream); its first build
+            // writes set s^1, released by the last query (main, stream order) and R (side)
+            KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
+            KN_TRY(hipStreamWaitEvent(main_, evF_[s ^ 1], 0));
+            KN_TRY(hipGraphLaunch(gU_[s], main_));
+            // U is even: the last query used set s^1, the primed build (B(next)) wrote set s
+            last_set_ = s ^ 1;
+            KN_TRY(hipEventRecord(evQ_[s ^ 1], main_));
+            KN_TRY(hipEventRecord(evB_[s], main_));
+            if (!r_) {
+                KN_TRY(hipEventRecord(evF_[s ^ 1], main_));
+                KN_TRY(hipEventRecord(last_done_, main_));
+            }
+            primed_ = true;
+            r_pending_ = (bool)r_;
+            next_ += unroll;
+            done += unroll;
+            continue;
+        }
+        if (!primed_) KN_TRY(enqueue_build(s));
+        KN_TRY(enqueue_query(s));
+        KN_TRY(flush());  // R(i-1) (last_set_ is still step i-1's set)
+        last_set_ = s;
+        KN_TRY(enqueue_build(s ^ 1));  // B(i+1) overlaps Q(i)
+        primed_ = true;
+        r_pending_ = (bool)r_;
+        ++next_;
+        ++done;
+    }
+    return flush();
+}
+
+hipError_t Pipeline::step_with(const Stage& pre, const Stage* next_pre) {
+    if (!main_) return hipErrorNotInitialized;
+    KN_TRY(graphs());
+    const int s = (int)(next_ & 1);
+    if (!primed_) {
+        // this step's input into set s, then its build
+        KN_TRY(hipStreamWaitEvent(side_, evF_[s], 0));
+        KN_TRY(pre(s, side_));
+        KN_TRY(enqueue_build(s));
+    }
+    KN_TRY(enqueue_query(s));
+    KN_TRY(flush());
+    last_set_ = s;
+    primed_ = false;
+    if (next_pre) {
+        KN_TRY(hipStreamWaitEvent(side_, evF_[s ^ 1], 0));
+        KN_TRY((*next_pre)(s ^ 1, side_));
+        KN_TRY(enqueue_build(s ^ 1));
+        primed_ = true;
+    }
+    r_pending_ = (bool)r_;
+    ++next_;
+    return flush();
+}
+
+hipError_t Pipeline::sync() {
+    if (!main_) return hipSuccess;
+    KN_TRY(hipStreamSynchronize(side_));
+    return hipStreamSynchronize(main_);
+}
+
+hipError_t Pipeline::unprime() {
+    if (!main_) return hipSuccess;
+    KN_TRY(hipStreamSynchronize(side_));
+    primed_ = false;
+    return hipSuccess;
+}
+
+}  // namespace kn

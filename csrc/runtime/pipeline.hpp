@@ -1,0 +1,86 @@
+// pipeline.hpp -- two-set software pipeline over two HIP streams (used by kn::Engine and the
+// distributed rank pipeline, kn::DistPipeline).
+//
+// The reference runs one cloud at a time: kn_prepare (bin) then kn_solve (query), serially on the
+// default stream (knearests.cu:235-392). Here step i works on buffer set s = i & 1 in up to three
+// stages, each captured once per set into a hipGraph:
+//   B(i)  side stream  produce set s (bin the cloud; distributed: route + exchange + bin)
+//   Q(i)  main stream  consume set s (the queries)
+//   R(i)  side stream  optional epilogue after Q(i) (distributed: all-reduce of the step's flag)
+// B(i+1) runs on the side stream while Q(i) fills the chip: set s^1 is free once Q(i-1) and
+// R(i-1) are done. The latency-bound binning kernels hide in the query's shadow.
+//
+// Priming. A call enqueues, per step, Q(i) and the NEXT step's build B(i+1). In resident mode
+// (every step reads the same input buffer) the pipeline stays primed between calls: a call of U
+// steps enqueues U queries and U builds and starts with a query, as a continuous stream would.
+// A changed input (or new stages) unprimes it; the next call then builds first.
+//
+// Unrolled launches (unroll U >= 2, even): U steps per graph, captured across both streams
+// (fork / join through events), so consecutive queries follow each other inside one graph launch
+// instead of paying a graph launch + cross-stream event per step.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <functional>
+#include <vector>
+
+namespace kn {
+
+class Pipeline {
+public:
+    using Stage = std::function<hipError_t(int set, hipStream_t s)>;
+    Pipeline() = default;
+    ~Pipeline() { reset(); }
+    Pipeline(const Pipeline&) = delete;
+    Pipeline& operator=(const Pipeline&) = delete;
+
+    // Stages (r may be empty). Streams stay owned by the caller. Graphs are captured lazily.
+    hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage());
+    bool ready() const { return main_ != nullptr; }
+    // Enqueue `iters` resident-mode steps; unroll >= 2 (even): whole groups of `unroll` steps go
+    // through one unrolled graph, the rest through per-step graphs.
+    hipError_t launch(int iters, int unroll = 0);
+    // One step whose input is provided by `pre` (run on the side stream before B, e.g. a copy of
+    // the step's cloud into set s's input buffer); `next_pre` != null: also the next step's input
+    // is known, so its build is enqueued now (overlapping this step's queries). Unprimes the
+    // resident state.
+    hipError_t step_with(const Stage& pre, const Stage* next_pre);
+    // R(i) of the last step when it is still pending (launch() and step_with() end with it).
+    hipError_t flush();
+    // Wait for both streams.
+    hipError_t sync();
+    // Drop the primed build (the input it read changed): waits for the side stream.
+    hipError_t unprime();
+    int last_set() const { return last_set_; }
+    long long steps() const { return next_; }
+    // Event recorded after the last step's final stage (R if present, else Q).
+    hipEvent_t last_done() const { return last_done_; }
+    // Destroy graphs and events (stages are kept? no: call init again).
+    void reset();
+
+private:
+    hipError_t graphs();          // per-set stage graphs
+    hipError_t unrolled(int start_set, int U);
+    hipError_t capture(const Stage& st, int set, hipGraphExec_t* out);
+    hipError_t enqueue_build(int set);   // side: wait set free, B(set), record evB
+    hipError_t enqueue_query(int set);   // main: wait evB, Q(set), record evQ
+    hipError_t enqueue_epilogue(int set);
+
+    hipStream_t main_ = nullptr, side_ = nullptr;
+    Stage b_, q_, r_;
+    hipGraphExec_t gB_[2] = {nullptr, nullptr}, gQ_[2] = {nullptr, nullptr}, gR_[2] = {nullptr, nullptr};
+    hipGraphExec_t gU_[2] = {nullptr, nullptr};
+    int gU_len_[2] = {0, 0};
+    hipEvent_t evB_[2] = {nullptr, nullptr};  // set built
+    hipEvent_t evQ_[2] = {nullptr, nullptr};  // set queried
+    hipEvent_t evF_[2] = {nullptr, nullptr};  // set free (after Q and R)
+    hipEvent_t last_done_ = nullptr;
+    std::vector<hipEvent_t> cap_ev_;  // fork / join events of the unrolled captures
+    long long next_ = 0;       // index of the next step to query
+    bool primed_ = false;      // B(next_) enqueued (resident input)
+    bool r_pending_ = false;   // R(next_ - 1) not yet enqueued
+    int last_set_ = -1;
+};
+
+}  // namespace kn

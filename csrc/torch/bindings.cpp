@@ -1027,7 +1027,26 @@ public:
     void solve() { TORCH_CHECK(e_->solve() == KN_OK, e_->error()); }
     void set_k(int64_t k) { TORCH_CHECK(e_->set_k((int)k) == KN_OK, e_->error()); }
     void launch_graph(int64_t iters) { TORCH_CHECK(e_->launch_graph((int)iters) == KN_OK, e_->error()); }
-    void launch_pipelined(int64_t iters) { TORCH_CHECK(e_->launch_pipelined((int)iters) == KN_OK, e_->error()); }
+    void launch_pipelined(int64_t iters, int64_t unroll) {
+        TORCH_CHECK(e_->launch_pipelined((int)iters, (int)unroll) == KN_OK, e_->error());
+    }
+    // One step of a stream of distinct clouds (same N as the prepared cloud): this step's points and
+    // optionally the next step's (binned now, while this step queries). Stream-ordered: the
+    // caller's tensors must stay unchanged until sync() (or the step after next).
+    void stream_step(torch::Tensor points, c10::optional<torch::Tensor> next) {
+        check_points(points, true);
+        TORCH_CHECK(points.size(0) == e_->n(), "stream_step: every cloud must have the prepared N points");
+        const float* np = nullptr;
+        if (next.has_value()) {
+            check_points(*next, true);
+            TORCH_CHECK(next->size(0) == e_->n(), "stream_step: every cloud must have the prepared N points");
+            np = next->data_ptr<float>();
+        }
+        const c10::DeviceGuard guard(points.device());
+        // the engine's streams must see the producer's writes
+        KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+        TORCH_CHECK(e_->stream_step(points.data_ptr<float>(), np) == KN_OK, e_->error());
+    }
     // stored -> original permutation of the engine's current grid (host int32)
     torch::Tensor permutation() {
         unsigned* p = e_->get_permutation();
@@ -1257,7 +1276,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("solve", &PyEngine::solve)
         .def("set_k", &PyEngine::set_k)
         .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
-        .def("launch_pipelined", &PyEngine::launch_pipelined, py::arg("iters") = 1)
+        .def("launch_pipelined", &PyEngine::launch_pipelined, py::arg("iters") = 1, py::arg("unroll") = -1)
+        .def("stream_step", &PyEngine::stream_step, py::arg("points"), py::arg("next") = py::none())
         .def("get_permutation", &PyEngine::permutation)
         .def("sync", &PyEngine::sync)
         .def("results", &PyEngine::results)

@@ -30,7 +30,7 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 KERNELS = ["kernels/build.hip", "kernels/query.hip", "kernels/route.hip", "kernels/tree.hip"]
 HOST = ["host/host.cpp"]
-RUNTIME = ["runtime/engine.cpp", "runtime/api.cpp", "runtime/hostio.cpp"]
+RUNTIME = ["runtime/engine.cpp", "runtime/api.cpp", "runtime/hostio.cpp", "runtime/pipeline.cpp"]
 MULTI = "runtime/multi.cpp"  # C-API multi-GPU runtime: libknearests.so only (links RCCL)
 RCCL_OK = os.path.exists(os.path.join(ROCM, "include", "rccl", "rccl.h"))
 

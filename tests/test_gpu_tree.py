@@ -191,3 +191,56 @@ def test_engine_pipeline_relabel_then_new_points(cuda, k):
     i1, d1 = e.results(cuda)
     i0, d0 = ref.results(cuda)
     assert torch.equal(i1, i0) and torch.equal(d1, d0)
+
+
+@pytest.mark.parametrize("unroll", [0, 4])
+def test_engine_stream_of_clouds(cuda, unroll):
+    """kn::Engine::stream_step: 7 DIFFERENT clouds through pipelined steps (the next cloud is
+    binned while the current one queries); every step's rows equal the kd-tree oracle's on its
+    own cloud, and a resident pipelined run afterwards solves the last cloud."""
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    k = 16
+    n = 30000
+    clouds = [uniform_cloud(n, seed=900 + j).to(cuda) for j in range(7)]
+    clouds[3] = (clouds[3] * 0.5 + 100.0).contiguous()  # another domain: the bbox is per build
+    e = C.Engine(k)
+    e.prepare(clouds[0])
+    e.launch_pipelined(2, unroll)  # a primed resident pipeline first: the stream must not use it
+    for j, c in enumerate(clouds):
+        e.stream_step(c, clouds[j + 1] if j + 1 < len(clouds) else None)
+        e.sync()
+        idx, d2 = e.results(cuda)
+        _check(c, idx, d2, k)
+        perm = e.get_permutation()
+        assert torch.equal(perm.sort().values, torch.arange(n, dtype=perm.dtype)), j
+    e.launch_pipelined(6, unroll)
+    e.sync()
+    idx, d2 = e.results(cuda)
+    _check(clouds[-1], idx, d2, k)
+
+
+@pytest.mark.parametrize("unroll", [2, 4, 8])
+def test_engine_unrolled_pipeline(cuda, unroll):
+    """Unrolled pipelined graphs (U steps per graph launch, pipeline.hpp) give the serial step's
+    rows bit for bit, for step counts that are not multiples of U, and mix with per-step launches
+    and serial graph replays."""
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    p = uniform_cloud(60000, seed=57).to(cuda)
+    e = C.Engine(16)
+    e.prepare(p)
+    e.solve()
+    idx, d2 = e.results(cuda)
+    for steps in (unroll, unroll + 1, 3 * unroll + 3, 1):
+        e.launch_pipelined(steps, unroll)
+        e.sync()
+        i2, e2 = e.results(cuda)
+        assert torch.equal(i2, idx) and torch.equal(e2, d2), steps
+    e.launch_graph(1)
+    e.launch_pipelined(2 * unroll, unroll)
+    e.sync()
+    i3, e3 = e.results(cuda)
+    assert torch.equal(i3, idx) and torch.equal(e3, d2)
