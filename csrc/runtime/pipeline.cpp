@@ -32,6 +32,7 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
             KN_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
         // both sets start free
         KN_TRY(hipEventRecord(evF_[s], main_));
+        KN_TRY(hipEventRecord(evQ_[s], main_));
     }
     KN_TRY(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming));
     KN_TRY(hipEventRecord(last_done_, main_));
@@ -131,7 +132,8 @@ hipError_t Pipeline::unrolled(int s0, int U) {
 }
 
 hipError_t Pipeline::enqueue_build(int s) {
-    KN_TRY(hipStreamWaitEvent(side_, evF_[s], 0));
+    // without an epilogue the set is free once its query is done
+    KN_TRY(hipStreamWaitEvent(side_, r_ ? evF_[s] : evQ_[s], 0));
     KN_TRY(hipGraphLaunch(gB_[s], side_));
     return hipEventRecord(evB_[s], side_);
 }
@@ -139,33 +141,32 @@ hipError_t Pipeline::enqueue_build(int s) {
 hipError_t Pipeline::enqueue_query(int s) {
     KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
     KN_TRY(hipGraphLaunch(gQ_[s], main_));
-    KN_TRY(hipEventRecord(evQ_[s], main_));
-    if (!r_) {
-        KN_TRY(hipEventRecord(evF_[s], main_));
-        KN_TRY(hipEventRecord(last_done_, main_));
-    }
-    return hipSuccess;
+    return hipEventRecord(evQ_[s], main_);
 }
 
 hipError_t Pipeline::enqueue_epilogue(int s) {
     KN_TRY(hipStreamWaitEvent(side_, evQ_[s], 0));
     KN_TRY(hipGraphLaunch(gR_[s], side_));
-    KN_TRY(hipEventRecord(evF_[s], side_));
-    return hipEventRecord(last_done_, side_);
+    return hipEventRecord(evF_[s], side_);
 }
 
 hipError_t Pipeline::flush() {
-    if (!r_pending_) return hipSuccess;
-    r_pending_ = false;
-    return enqueue_epilogue(last_set_);
+    if (r_pending_) {
+        r_pending_ = false;
+        KN_TRY(enqueue_epilogue(last_set_));
+        return hipEventRecord(last_done_, side_);
+    }
+    if (!r_ && last_set_ >= 0) return hipEventRecord(last_done_, main_);
+    return hipSuccess;
 }
 
 hipError_t Pipeline::launch(int iters, int unroll) {
     if (!main_) return hipErrorNotInitialized;
     KN_TRY(graphs());
     if (unroll < 2 || (unroll & 1)) unroll = 0;
-    if (unroll && iters >= unroll) {
-        // both start parities up front: a capture never lands inside a later (timed) call
+    if (unroll) {
+        // both start parities up front (also by a call of fewer steps, e.g. a warm-up): a capture
+        // never lands inside a later (timed) call
         KN_TRY(unrolled(0, unroll));
         KN_TRY(unrolled(1, unroll));
     }
@@ -175,20 +176,19 @@ hipError_t Pipeline::launch(int iters, int unroll) {
         if (unroll && iters - done >= unroll) {
             KN_TRY(unrolled(s, unroll));
             if (!primed_) KN_TRY(enqueue_build(s));
-            KN_TRY(flush());
+            if (r_pending_) {
+                r_pending_ = false;
+                KN_TRY(enqueue_epilogue(last_set_));
+            }
             // the graph's first query reads set s (built on the side stream); its first build
             // writes set s^1, released by the last query (main, stream order) and R (side)
             KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
-            KN_TRY(hipStreamWaitEvent(main_, evF_[s ^ 1], 0));
+            if (r_) KN_TRY(hipStreamWaitEvent(main_, evF_[s ^ 1], 0));
             KN_TRY(hipGraphLaunch(gU_[s], main_));
             // U is even: the last query used set s^1, the primed build (B(next)) wrote set s
             last_set_ = s ^ 1;
             KN_TRY(hipEventRecord(evQ_[s ^ 1], main_));
             KN_TRY(hipEventRecord(evB_[s], main_));
-            if (!r_) {
-                KN_TRY(hipEventRecord(evF_[s ^ 1], main_));
-                KN_TRY(hipEventRecord(last_done_, main_));
-            }
             primed_ = true;
             r_pending_ = (bool)r_;
             next_ += unroll;
@@ -197,7 +197,10 @@ hipError_t Pipeline::launch(int iters, int unroll) {
         }
         if (!primed_) KN_TRY(enqueue_build(s));
         KN_TRY(enqueue_query(s));
-        KN_TRY(flush());  // R(i-1) (last_set_ is still step i-1's set)
+        if (r_pending_) {  // R(i-1) (last_set_ is still step i-1's set)
+            r_pending_ = false;
+            KN_TRY(enqueue_epilogue(last_set_));
+        }
         last_set_ = s;
         KN_TRY(enqueue_build(s ^ 1));  // B(i+1) overlaps Q(i)
         primed_ = true;
@@ -214,16 +217,19 @@ hipError_t Pipeline::step_with(const Stage& pre, const Stage* next_pre) {
     const int s = (int)(next_ & 1);
     if (!primed_) {
         // this step's input into set s, then its build
-        KN_TRY(hipStreamWaitEvent(side_, evF_[s], 0));
+        KN_TRY(hipStreamWaitEvent(side_, r_ ? evF_[s] : evQ_[s], 0));
         KN_TRY(pre(s, side_));
         KN_TRY(enqueue_build(s));
     }
     KN_TRY(enqueue_query(s));
-    KN_TRY(flush());
+    if (r_pending_) {
+        r_pending_ = false;
+        KN_TRY(enqueue_epilogue(last_set_));
+    }
     last_set_ = s;
     primed_ = false;
     if (next_pre) {
-        KN_TRY(hipStreamWaitEvent(side_, evF_[s ^ 1], 0));
+        KN_TRY(hipStreamWaitEvent(side_, r_ ? evF_[s ^ 1] : evQ_[s ^ 1], 0));
         KN_TRY((*next_pre)(s ^ 1, side_));
         KN_TRY(enqueue_build(s ^ 1));
         primed_ = true;
