@@ -251,21 +251,34 @@ def run_dist(args) -> dict:
     # (CollectiveError -> non-zero exit) instead of blocking the job
     hf = {"halo_factor": args.halo_factor} if args.halo_factor else {}
     dk = DistributedKNearests(k=args.k, deterministic=args.deterministic, timeout_s=120.0,
-                              transport=HostStagedTransport() if staged else None, **hf)
+                              transport=HostStagedTransport() if staged else None,
+                              force_collectives=args.force_collectives or None, **hf)
     res = None
     part = args.layout == "partitioned"
-    for _ in range(args.warmup):
-        res = dk.solve(pts, partitioned=part)
+    # warm-up: the first step is the full (validating) step -- global domain, rank boxes, halo,
+    # split sizes; the rest are steady steps
+    res = dk.solve(pts, partitioned=part)
+    if args.warmup > 1:
+        res = dk.run_steps(pts, args.warmup - 1, resident=not args.per_call) if not args.per_call else res
+        if args.per_call:
+            for _ in range(args.warmup - 1):
+                res = dk.solve(pts, partitioned=part, async_=not args.sync_steps)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     # timed steps run asynchronously (no host synchronisation inside a step once the routing is
-    # steady); every step's device flag is checked after the timed region
+    # steady). Default: all K steps in one call to the native pipeline (kn::DistPipeline: U steps
+    # per graph launch, step i+1's route + exchange + build overlapping step i's queries, the
+    # cloud resident as on one GPU); --per-call: one solve() call per step. Every step's device
+    # flag is checked after the timed region.
     steps = []
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        steps.append(dk.solve(pts, partitioned=part, async_=not args.sync_steps))
-    t_enq = time.perf_counter() - t0  # host time to enqueue the steps (~dt: the host is the bound)
+    if args.per_call or args.sync_steps:
+        for _ in range(args.steps):
+            steps.append(dk.solve(pts, partitioned=part, async_=not args.sync_steps))
+    else:
+        steps.append(dk.run_steps(pts, args.steps, resident=True))
+    t_enq = time.perf_counter() - t0  # host time to enqueue the steps
     torch.cuda.synchronize()
     dist.barrier()
     dt = time.perf_counter() - t0
@@ -282,6 +295,14 @@ def run_dist(args) -> dict:
         torch.cuda.synchronize()
         dist.barrier()
         dt = time.perf_counter() - t0
+    # per-phase device times of one serial steady step (collective), MAX over ranks
+    phases = dk.profile_step(pts)
+    cdev0 = torch.device("cpu") if staged else dev
+    if phases:
+        keys = sorted(phases)
+        ph = torch.tensor([phases[k] for k in keys], device=cdev0, dtype=torch.float64)
+        dist.all_reduce(ph, op=dist.ReduceOp.MAX)
+        phases = {k: round(float(v), 4) for k, v in zip(keys, ph.tolist())}
     if os.environ.get("KN_HOST_MARKS"):  # host-side stage timing of the native step (stderr)
         dk.host_marks = []
         for _ in range(20):
@@ -316,7 +337,7 @@ def run_dist(args) -> dict:
     dist.all_reduce(nt)
     out = {"t": float(t.item()), "stats": res.stats if res else {}, "check": chk, "n_total": int(nt.item()),
            "rank": rank, "world": world, "invalid_async_steps": invalid,
-           "host_enqueue_ms_per_step": t_enq * 1e3 / max(1, args.steps)}
+           "host_enqueue_ms_per_step": t_enq * 1e3 / max(1, args.steps), "phases": phases}
     dist.barrier()
     dist.destroy_process_group()
     return out
@@ -450,6 +471,10 @@ def main() -> int:
     ap.add_argument("--cpu-oracle", action="store_true", help="time the CPU kd-tree path (BASELINE config 1)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="N GPUs: weak = --n points per GPU; strong = --n points in total, split over the ranks")
+    ap.add_argument("--per-call", action="store_true",
+                    help="N GPUs: one solve() call per timed step instead of one run_steps() call for all of them")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="distributed path at world 1: the rank's own rows also travel through RCCL")
     ap.add_argument("--sync-steps", action="store_true",
                     help="N GPUs: validate every step before the next (no asynchronous steady-state steps)")
     args = ap.parse_args()
@@ -487,7 +512,12 @@ def main() -> int:
                  "rounds": r["stats"].get("rounds"), "rank_grid": r["stats"].get("grid"), "layout": args.layout,
                  "steady_async": bool(r["stats"].get("steady")) and not args.sync_steps,
                  "invalid_async_steps": r["invalid_async_steps"], "path": "distributed",
-                 "host_enqueue_ms_per_step": round(r["host_enqueue_ms_per_step"], 4)}
+                 "pipelined": bool(r["stats"].get("pipelined")), "per_call": bool(args.per_call),
+                 "force_collectives": bool(args.force_collectives),
+                 "host_enqueue_ms_per_step": round(r["host_enqueue_ms_per_step"], 4),
+                 # one serial steady step's phases (event-timed, max over ranks); in the timed
+                 # pipelined steps route + exchange + build overlap the previous step's query
+                 **r["phases"]}
     else:
         r = run_native(args) if args.path == "native" else run_single(args)
         n_gpus = 1

@@ -1,0 +1,518 @@
+// dist.cpp -- see dist.hpp.
+#include "dist.hpp"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+#include "hostio.hpp"
+
+namespace kn {
+
+namespace {
+#define KN_TRY(expr)                     \
+    do {                                 \
+        hipError_t e_ = (expr);          \
+        if (e_ != hipSuccess) return e_; \
+    } while (0)
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t v) { return (v + kAlign - 1) & ~(kAlign - 1); }
+template <class T>
+T* carve(char*& p, size_t count) {
+    T* r = reinterpret_cast<T*>(p);
+    p += align_up(std::max<size_t>(count, 1) * sizeof(T));
+    return r;
+}
+ncclComm_t as_comm(RankComm* c) { return static_cast<ncclComm_t>(c->comm); }
+}  // namespace
+
+// ---------------------------------------------------------------- communicator --------
+bool comm_unique_id(unsigned char out[kCommIdBytes], std::string* err) {
+    static_assert(sizeof(ncclUniqueId) == kCommIdBytes, "ncclUniqueId is 128 bytes");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        if (err) *err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+        return false;
+    }
+    std::memcpy(out, &id, kCommIdBytes);
+    return true;
+}
+
+RankComm* comm_create(const unsigned char id[kCommIdBytes], int world, int rank, int device, std::string* err) {
+    if (world < 1 || world > kRouteMaxWorld || rank < 0 || rank >= world) {
+        if (err) *err = "bad world / rank";
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        if (err) *err = "hipSetDevice failed";
+        return nullptr;
+    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, kCommIdBytes);
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, world, uid, rank);
+    if (r != ncclSuccess) {
+        if (err) *err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+        return nullptr;
+    }
+    RankComm* c = new RankComm();
+    c->comm = comm;
+    c->world = world;
+    c->rank = rank;
+    c->device = device;
+    return c;
+}
+
+void comm_destroy(RankComm* c) {
+    if (!c) return;
+    if (c->comm && !c->aborted) (void)ncclCommDestroy(as_comm(c));
+    delete c;
+}
+
+std::string comm_async_error(RankComm* c) {
+    if (!c || !c->comm) return "no communicator";
+    if (c->aborted) return "communicator aborted";
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(as_comm(c), &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+    if (r == ncclSuccess || r == ncclInProgress) return "";
+    return std::string("RCCL async error: ") + ncclGetErrorString(r);
+}
+
+void comm_abort(RankComm* c) {
+    if (!c || !c->comm || c->aborted) return;
+    (void)ncclCommAbort(as_comm(c));
+    c->aborted = true;
+}
+
+// ---------------------------------------------------------------- pipeline ------------
+DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(comm) {
+    const int W = p_.world;
+    if (!comm_ || comm_->world != W || comm_->rank != p_.rank) { fail("communicator does not match the plan"); return; }
+    if (W < 1 || W > kRouteMaxWorld || p_.rank < 0 || p_.rank >= W || p_.k < 1 || p_.k > KN_MAX_K || p_.n < 0 ||
+        (int)p_.recv_own.size() != W || (int)p_.recv_halo.size() != W || (int)p_.cross_send.size() != W ||
+        (int)p_.cross_recv.size() != W || (int)p_.tot.size() != 2 * W || (int)p_.hdr.size() < kPlanHdr ||
+        p_.grid[0] * p_.grid[1] * p_.grid[2] != W || !p_.route || !p_.metas || (p_.n > 0 && !p_.points)) {
+        fail("inconsistent distributed plan");
+        return;
+    }
+    if (p_.self_via_comm && W != 1) { fail("self_via_comm is the world-1 forced-collective mode"); return; }
+    if (hipSetDevice(p_.device) != hipSuccess) { fail("hipSetDevice"); return; }
+    long long own = 0, halo = 0;
+    for (int s = 0; s < W; ++s) {
+        if (p_.recv_own[s] < 0 || p_.recv_halo[s] < 0 || p_.cross_send[s] < 0 || p_.cross_recv[s] < 0) {
+            fail("negative split size");
+            return;
+        }
+        own += p_.recv_own[s];
+        halo += p_.recv_halo[s];
+    }
+    if (own + halo >= (1ll << 31) - 1) { fail("too many local rows"); return; }
+    n_owned_ = (int)own;
+    rows_ = (int)(own + halo);
+    // send / receive layouts (route_scatter self-last: the other destinations in rank order, then
+    // the rank's own segment; the receive buffer holds the other sources in rank order)
+    soff_.assign(W, 0);
+    roff_.assign(W, 0);
+    long long so = 0, ro = 0;
+    for (int d = 0; d < W; ++d) {
+        if (d == p_.rank) continue;
+        soff_[d] = so;
+        roff_[d] = ro;
+        so += p_.cross_send[d];
+        ro += p_.cross_recv[d];
+    }
+    const long long nself = (long long)p_.tot[2 * p_.rank] + p_.tot[2 * p_.rank + 1];
+    if (so + nself > p_.cap) { fail("send buffer smaller than the planned rows"); return; }
+    table_ = UnpackTable{};
+    table_.world = W;
+    if (p_.self_via_comm) {
+        // world 1: the own rows travel through the communicator and the unpack like any source's
+        soff_[0] = so;  // the self segment follows the (no) other destinations
+        roff_[0] = 0;
+        recv_rows_ = (int)nself;
+        table_.seg[0] = 0;
+        table_.own[0] = p_.recv_own[0];
+        table_.own_pref[0] = 0;
+        table_.halo_pref[0] = 0;
+        table_.n_own = n_owned_;
+        table_.rows_cross = recv_rows_;
+        table_.self = -1;
+        table_.out_rows = rows_;
+        rows_cross_ = recv_rows_;
+    } else {
+        long long seg = 0, o = 0, h = 0;
+        for (int s = 0; s < W; ++s) {
+            table_.seg[s] = (int)seg;
+            table_.own[s] = p_.recv_own[s];
+            table_.own_pref[s] = (int)o;
+            table_.halo_pref[s] = (int)h;
+            if (s != p_.rank) seg += (long long)p_.recv_own[s] + p_.recv_halo[s];
+            o += p_.recv_own[s];
+            h += p_.recv_halo[s];
+        }
+        if (seg != ro) { fail("receive split sizes do not add up"); return; }
+        table_.n_own = n_owned_;
+        table_.rows_cross = (int)seg;
+        table_.self = p_.rank;
+        table_.out_rows = rows_;
+        rows_cross_ = (int)seg;
+        recv_rows_ = (int)seg;
+        if (p_.place[2] != rows_) { fail("self placement does not match the local rows"); return; }
+    }
+    // local geometry and the query plan: the same arithmetic as the torch binding's dist_local
+    const RankLocal rl = rank_local(p_.hdr.data(), p_.rank, p_.grid);
+    complete_ = rl.complete;
+    const int th[3] = {0, 0, 0};
+    AutoParams ap = auto_params(rows_, p_.k, p_.ppc, th, 0, rl.ext);
+    if (p_.dims[0] != ap.dims[0] || p_.dims[1] != ap.dims[1] || p_.dims[2] != ap.dims[2]) {
+        ap.tile[0] = std::max(1, ap.tile[0] / std::max(1, ap.xsub));  // a refined grid: isotropic
+        ap.xsub = 1;
+    }
+    const long long C = (long long)p_.dims[0] * p_.dims[1] * p_.dims[2];
+    if (p_.dims[0] < 1 || p_.dims[1] < 1 || p_.dims[2] < 1 || C >= (1ll << 31) - 1) { fail("bad local grid"); return; }
+    C_ = (int)C;
+    bproto_ = BuildBuffers{};
+    bproto_.n = rows_;
+    for (int a = 0; a < 3; ++a) bproto_.dims[a] = p_.dims[a];
+    bproto_.deterministic = p_.deterministic;
+    bproto_.use_box = 1;
+    for (int a = 0; a < 3; ++a) {
+        bproto_.box_lo[a] = (float)rl.box[a];
+        bproto_.box_hi[a] = (float)rl.box[3 + a];
+    }
+    bproto_.n_owned = n_owned_;
+    bproto_.n_zero_words = kNumCounters;
+    qproto_ = QueryBuffers{};
+    qproto_.n = rows_;
+    for (int a = 0; a < 3; ++a) qproto_.dims[a] = p_.dims[a];
+    qproto_.k = p_.k;
+    qproto_.n_queries = n_owned_;
+    qproto_.complete = complete_;
+    for (int a = 0; a < 3; ++a) qproto_.tile[a] = ap.tile[a];
+    qproto_.halo = ap.halo;
+    qproto_.xsub = ap.xsub;
+    qproto_.lds_capacity = ap.lds_capacity;
+    qproto_.use_tiles = 1;
+    qproto_.counters_zeroed = 1;
+    qproto_.exact_grid = p_.exact_grid;
+
+    // buffers: one block per set
+    const int nb = route_block_count(p_.n);
+    const size_t nbs = scan_block_count(C_) + 1;
+    const size_t K = (size_t)p_.k;
+    auto layout = [&](char* base, Set& S) {
+        char* q = base;
+        S.send = carve<float4>(q, (size_t)p_.cap);
+        S.bc = carve<int>(q, (size_t)2 * W * nb);
+        S.totals = carve<int>(q, (size_t)2 * W);
+        S.partials = carve<unsigned>(q, (size_t)6 * nb);
+        S.recv = carve<float4>(q, (size_t)recv_rows_);
+        S.lpts = carve<float>(q, (size_t)rows_ * 3);
+        S.lgids = carve<int>(q, (size_t)rows_);
+        S.bbox = carve<unsigned>(q, kBBoxWords);
+        S.geom = carve<GridGeom>(q, 1);
+        S.cell_count = carve<int>(q, (size_t)C_ + 1);
+        S.cell_scan = carve<int>(q, (size_t)C_ + 1);
+        S.block_sums = carve<int>(q, nbs);
+        S.cell_start = carve<int>(q, (size_t)C_ + 1);
+        S.bin_tmp = carve<float4>(q, (size_t)rows_);
+        S.sorted = carve<float4>(q, (size_t)rows_);
+        S.perm = carve<unsigned>(q, (size_t)rows_);
+        S.fallback = carve<unsigned>(q, (size_t)rows_);
+        S.counters = carve<unsigned>(q, kNumCounters);
+        S.uncert = carve<unsigned>(q, (size_t)n_owned_);
+        S.idx = carve<int>(q, (size_t)n_owned_ * K);
+        S.d2 = carve<float>(q, (size_t)n_owned_ * K);
+        S.flag = carve<int>(q, 1);
+        return (size_t)(q - base);
+    };
+    Set probe{};
+    const size_t bytes = layout(nullptr, probe);
+    for (int s = 0; s < 2; ++s) {
+        Set& S = set_[s];
+        void* b = nullptr;
+        if (device_malloc(&b, bytes) != hipSuccess) { fail("hipMalloc(distributed set)"); return; }
+        S.block = static_cast<char*>(b);
+        layout(S.block, S);
+        if (hipMemset(S.flag, 0, sizeof(int)) != hipSuccess) { fail("hipMemset"); return; }
+        S.tree_ws = S.tree_nodes = nullptr;
+        if (p_.use_tree) {
+            if (device_malloc(&S.tree_ws, std::max<size_t>(1, tree_workspace_bytes(rows_, p_.dims))) != hipSuccess ||
+                device_malloc(&S.tree_nodes, std::max<size_t>(1, tree_node_bytes(rows_))) != hipSuccess) {
+                fail("hipMalloc(distributed tree)");
+                return;
+            }
+        }
+    }
+    void* v = nullptr;
+    if (device_malloc(&v, sizeof(RouteParams)) != hipSuccess) { fail("hipMalloc(route)"); return; }
+    route_dev_ = v;
+    if (device_malloc(&v, (size_t)W * 8 * sizeof(double)) != hipSuccess) { fail("hipMalloc(metas)"); return; }
+    metas_dev_ = static_cast<double*>(v);
+    if (device_malloc(&v, (size_t)2 * W * sizeof(int)) != hipSuccess) { fail("hipMalloc(totals)"); return; }
+    tot_dev_ = static_cast<int*>(v);
+    if (device_malloc(&v, sizeof(int)) != hipSuccess) { fail("hipMalloc(sticky)"); return; }
+    sticky_ = static_cast<int*>(v);
+    if (hipHostMalloc(&v, sizeof(int), hipHostMallocDefault) != hipSuccess) { fail("hipHostMalloc(flag)"); return; }
+    host_flag_ = static_cast<int*>(v);
+    *host_flag_ = 0;
+    if (hipHostGetDevicePointer(&v, host_flag_, 0) != hipSuccess) { fail("hipHostGetDevicePointer"); return; }
+    host_flag_dev_ = static_cast<int*>(v);
+    if (hipMemcpy(route_dev_, p_.route, sizeof(RouteParams), hipMemcpyDeviceToDevice) != hipSuccess ||
+        hipMemcpy(metas_dev_, p_.metas, (size_t)W * 8 * sizeof(double), hipMemcpyDeviceToDevice) != hipSuccess ||
+        hipMemcpy(tot_dev_, p_.tot.data(), (size_t)2 * W * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(sticky_, 0, sizeof(int)) != hipSuccess) {
+        fail("plan upload");
+        return;
+    }
+    if (hipStreamCreateWithFlags(&main_, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess) {
+        fail("hipStreamCreate");
+        return;
+    }
+    if (hipEventCreateWithFlags(&in_ev_, hipEventDisableTiming) != hipSuccess) { fail("hipEventCreate"); return; }
+    for (int i = 0; i < 8; ++i) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { fail("hipEventCreate"); return; }
+        ring_.push_back(e);
+    }
+    auto b = [this](int s, hipStream_t st) { return stage_build(s, st); };
+    auto q = [this](int s, hipStream_t st) { return stage_query(s, st); };
+    auto r = [this](int s, hipStream_t st) { return stage_flag(s, st); };
+    if (pipe_.init(main_, side_, b, q, r) != hipSuccess) { fail("pipeline init"); return; }
+    ok_ = true;
+}
+
+DistPipeline::~DistPipeline() {
+    pipe_.reset();
+    if (main_) (void)hipStreamSynchronize(main_);
+    if (side_) (void)hipStreamSynchronize(side_);
+    for (auto& S : set_) {
+        if (S.block) (void)hipFree(S.block);
+        if (S.tree_ws) (void)hipFree(S.tree_ws);
+        if (S.tree_nodes) (void)hipFree(S.tree_nodes);
+    }
+    for (void* v : {route_dev_, (void*)metas_dev_, (void*)tot_dev_, (void*)sticky_})
+        if (v) (void)hipFree(v);
+    if (host_flag_) (void)hipHostFree(host_flag_);
+    for (auto e : ring_) (void)hipEventDestroy(e);
+    if (in_ev_) (void)hipEventDestroy(in_ev_);
+    if (main_) (void)hipStreamDestroy(main_);
+    if (side_) (void)hipStreamDestroy(side_);
+}
+
+hipError_t DistPipeline::exchange(int s, hipStream_t st) {
+    const Set& S = set_[s];
+    const int W = p_.world;
+    ncclComm_t comm = as_comm(comm_);
+    if (ncclGroupStart() != ncclSuccess) return hipErrorUnknown;
+    bool bad = false;
+    for (int d = 0; d < W && !bad; ++d) {
+        size_t sc, rc;
+        if (d == p_.rank) {
+            if (!p_.self_via_comm) continue;
+            sc = rc = (size_t)recv_rows_;
+        } else {
+            sc = (size_t)p_.cross_send[d];
+            rc = (size_t)p_.cross_recv[d];
+        }
+        if (sc && ncclSend(reinterpret_cast<const float*>(S.send + soff_[d]), sc * 4, ncclFloat, d, comm, st) != ncclSuccess)
+            bad = true;
+        if (rc && ncclRecv(reinterpret_cast<float*>(S.recv + roff_[d]), rc * 4, ncclFloat, d, comm, st) != ncclSuccess)
+            bad = true;
+    }
+    const ncclResult_t r = ncclGroupEnd();
+    return bad || r != ncclSuccess ? hipErrorUnknown : hipSuccess;
+}
+
+// marks (profile only): events recorded after the routing and after the exchange
+hipError_t DistPipeline::stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks) {
+    Set& S = set_[s];
+    const auto* rp = static_cast<const RouteParams*>(route_dev_);
+    if (p_.n > 0) {
+        KN_TRY(launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, st, S.partials));
+        if (p_.self_via_comm) {
+            KN_TRY(launch_route_scatter(p_.points, p_.ids, p_.n, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank, st));
+        } else {
+            SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
+            KN_TRY(launch_route_scatter(p_.points, p_.ids, p_.n, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank,
+                                        st, &sp));
+        }
+    } else {
+        // an empty share: nothing to route, the counts are all zero
+        KN_TRY(hipMemsetAsync(S.totals, 0, (size_t)2 * p_.world * sizeof(int), st));
+    }
+    if (marks) KN_TRY(hipEventRecord((*marks)[0], st));
+    KN_TRY(exchange(s, st));
+    if (marks) KN_TRY(hipEventRecord((*marks)[1], st));
+    if (rows_cross_ > 0) KN_TRY(launch_route_unpack(S.recv, nullptr, rows_cross_, table_, S.lpts, S.lgids, st));
+    BuildBuffers b = bproto_;
+    b.points = S.lpts;
+    b.bbox_words = S.bbox;
+    b.geom = S.geom;
+    b.cell_count = S.cell_count;
+    b.cell_scan = S.cell_scan;
+    b.block_sums = S.block_sums;
+    b.cell_start = S.cell_start;
+    b.cell_rank = reinterpret_cast<int2*>(S.bin_tmp);
+    b.bin_tmp = S.bin_tmp;
+    b.sorted = S.sorted;
+    b.perm = S.perm;
+    b.gids = S.lgids;
+    b.zero_words = S.counters;
+    KN_TRY(launch_build(b, st));
+    if (p_.use_tree && rows_ > 0) {
+        TreeView t = tree_view(S.tree_ws, rows_, p_.dims);
+        tree_attach_nodes(t, S.tree_nodes);
+        KN_TRY(launch_tree_leaves(S.sorted, S.cell_start, S.geom, t, st));
+        KN_TRY(launch_tree_nodes(t, st));
+    }
+    return hipSuccess;
+}
+
+hipError_t DistPipeline::stage_query(int s, hipStream_t st) {
+    Set& S = set_[s];
+    if (p_.use_tree) {
+        if (rows_ > 0) {
+            TreeView t = tree_view(S.tree_ws, rows_, p_.dims);
+            tree_attach_nodes(t, S.tree_nodes);
+            TreeQuery q{};
+            q.k = p_.k;
+            q.n_queries = n_owned_;
+            q.row_of = S.perm;
+            q.out_idx = reinterpret_cast<unsigned*>(S.idx);
+            q.out_dist = S.d2;
+            q.counters = S.counters;
+            KN_TRY(launch_tree_query(t, q, st));
+            // the complete-box certification the grid kernels do inline
+            KN_TRY(launch_certify_rows(S.lpts, n_owned_, p_.k, S.d2, complete_, S.geom, S.counters, S.uncert, st));
+        }
+    } else {
+        QueryBuffers q = qproto_;
+        q.sorted = S.sorted;
+        q.cell_start = S.cell_start;
+        q.geom = S.geom;
+        q.row_of = S.perm;
+        q.out_idx = reinterpret_cast<unsigned*>(S.idx);
+        q.out_dist = S.d2;
+        q.fallback_list = S.fallback;
+        q.counters = S.counters;
+        q.uncert_list = S.uncert;
+        KN_TRY(launch_query(q, st));
+    }
+    // this step's check: the share's bbox and count (routing partials) and every send count as
+    // planned, and no uncertified row
+    return launch_steady_flag_partials(S.partials, p_.n, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
+                                       S.counters, S.flag, st);
+}
+
+hipError_t DistPipeline::stage_flag(int s, hipStream_t st) {
+    Set& S = set_[s];
+    if (ncclAllReduce(S.flag, S.flag, 1, ncclInt32, ncclMax, as_comm(comm_), st) != ncclSuccess) return hipErrorUnknown;
+    return launch_flag_sink(S.flag, sticky_, host_flag_dev_, st);
+}
+
+kn_status DistPipeline::launch(int iters, int unroll, bool keep_primed, hipStream_t caller, long long* last_step) {
+    if (!ok_) return KN_ERR_STATE;
+    if (comm_->aborted) { err_ = "communicator aborted"; return KN_ERR_DEVICE; }
+    if (iters <= 0) {
+        if (last_step) *last_step = pipe_.steps() - 1;
+        return KN_OK;
+    }
+    hipError_t e = hipSuccess;
+    if (caller) {
+        // the first build reads the caller's points after the caller's earlier writes
+        e = hipEventRecord(in_ev_, caller);
+        if (e == hipSuccess) e = hipStreamWaitEvent(side_, in_ev_, 0);
+    }
+    if (e == hipSuccess) e = pipe_.launch(iters, unroll, keep_primed);
+    if (e == hipSuccess && caller) {
+        // later work on the caller's stream (e.g. refilling the points) waits for the builds
+        e = hipStreamWaitEvent(caller, pipe_.build_event(0), 0);
+        if (e == hipSuccess) e = hipStreamWaitEvent(caller, pipe_.build_event(1), 0);
+    }
+    if (e != hipSuccess) {
+        err_ = std::string("distributed pipelined launch: ") + hipGetErrorString(e);
+        return KN_ERR_DEVICE;
+    }
+    const long long last = pipe_.steps() - 1;
+    const int slot = ring_next_;
+    ring_next_ = (ring_next_ + 1) % (int)ring_.size();
+    if (hipEventRecord(ring_[slot], side_) != hipSuccess) { err_ = "hipEventRecord"; return KN_ERR_DEVICE; }
+    done_.emplace_back(last, slot);
+    while (done_.size() > ring_.size()) done_.pop_front();
+    if (last_step) *last_step = last;
+    return KN_OK;
+}
+
+kn_status DistPipeline::wait(long long step, double timeout_s, int* flag) {
+    if (!ok_) return KN_ERR_STATE;
+    hipEvent_t ev = nullptr;
+    for (const auto& d : done_)
+        if (d.first >= step) { ev = ring_[d.second]; break; }
+    if (!ev) {
+        if (done_.empty() || step > done_.back().first) { err_ = "wait() for a step not launched"; return KN_ERR_STATE; }
+        ev = ring_[done_.front().second];  // older than the ring: its flag is final (sticky)
+    }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    int polls = 0;
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) { err_ = std::string("step wait: ") + hipGetErrorString(q); return KN_ERR_DEVICE; }
+        if ((++polls & 63) == 0) {
+            // a dead or hung peer: RCCL's async error, or the deadline
+            const std::string ae = comm_async_error(comm_);
+            if (!ae.empty()) {
+                comm_abort(comm_);
+                err_ = ae;
+                return KN_ERR_DEVICE;
+            }
+            if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_s) {
+                comm_abort(comm_);
+                err_ = "distributed step did not complete within the deadline (peer dead or hung?)";
+                return KN_ERR_DEVICE;
+            }
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(polls < 256 ? 2 : 50));
+    }
+    if (flag) *flag = *reinterpret_cast<volatile int*>(host_flag_);
+    return KN_OK;
+}
+
+kn_status DistPipeline::sync() {
+    if (pipe_.sync() != hipSuccess) { err_ = "distributed pipeline sync"; return KN_ERR_DEVICE; }
+    return KN_OK;
+}
+
+kn_status DistPipeline::profile(float ms[5]) {
+    if (!ok_) return KN_ERR_STATE;
+    if (pipe_.sync() != hipSuccess || pipe_.unprime() != hipSuccess) { err_ = "sync"; return KN_ERR_DEVICE; }
+    std::vector<hipEvent_t> ev(6, nullptr);
+    for (auto& e : ev)
+        if (hipEventCreate(&e) != hipSuccess) { err_ = "hipEventCreate"; return KN_ERR_DEVICE; }
+    // the set the pipeline will build next is free (nothing primed): profile in it
+    const int s = (int)(pipe_.steps() & 1);
+    std::vector<hipEvent_t> marks = {ev[1], ev[2]};
+    hipError_t e = hipEventRecord(ev[0], main_);
+    if (e == hipSuccess) e = stage_build(s, main_, &marks);
+    if (e == hipSuccess) e = hipEventRecord(ev[3], main_);
+    if (e == hipSuccess) e = stage_query(s, main_);
+    if (e == hipSuccess) e = hipEventRecord(ev[4], main_);
+    if (e == hipSuccess) e = stage_flag(s, main_);
+    if (e == hipSuccess) e = hipEventRecord(ev[5], main_);
+    if (e == hipSuccess) e = hipStreamSynchronize(main_);
+    for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]);
+    for (auto x : ev) (void)hipEventDestroy(x);
+    if (e != hipSuccess) { err_ = std::string("profile: ") + hipGetErrorString(e); return KN_ERR_DEVICE; }
+    return KN_OK;
+}
+
+}  // namespace kn

@@ -1,0 +1,150 @@
+// dist.hpp -- one rank's pipelined distributed step over RCCL (NEW: the reference is single-GPU,
+// knearests.cu has no streams, devices or collectives).
+//
+// One process per GPU. After a validated full step (parallel/distributed.py: global domain, rank
+// boxes, halo width, split sizes), every steady step is the 1-GPU pipelined step plus the
+// communication, all in hipGraphs replayed by kn::Pipeline (pipeline.hpp):
+//   B(i)  side stream   route this rank's share (owner + halo destinations, its own rows placed
+//                       straight into the local set) -> grouped ncclSend / ncclRecv of the rows
+//                       that change rank -> unpack -> local grid build (global ids in the points)
+//   Q(i)  main stream   queries of the owned points (grid or Morton-leaf tree path, complete-box
+//                       certification) -> the step's flag (share / counts as planned, all rows
+//                       certified)
+//   R(i)  side stream   ncclAllReduce(MAX) of the flag -> sticky flag in pinned host memory
+// B(i+1), with its all-to-all, runs while Q(i) fills the chip; both RCCL calls live on the side
+// stream, in the same order on every rank (one communicator, no cross-stream collectives).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <deque>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "knearests.h"
+#include "kn/kernels.h"
+#include "kn/route.h"
+#include "kn/tree.h"
+#include "pipeline.hpp"
+
+namespace kn {
+
+// One rank's RCCL communicator (ncclComm_t behind an opaque pointer, so this header needs no RCCL
+// include). The ranks share the 128-byte unique id through their own channel (the Python layer
+// all-gathers it over torch.distributed).
+struct RankComm {
+    void* comm = nullptr;
+    int world = 0, rank = 0, device = 0;
+    bool aborted = false;
+};
+constexpr int kCommIdBytes = 128;
+bool comm_unique_id(unsigned char out[kCommIdBytes], std::string* err);
+RankComm* comm_create(const unsigned char id[kCommIdBytes], int world, int rank, int device, std::string* err);
+void comm_destroy(RankComm* c);
+// ncclCommGetAsyncError: "" when healthy
+std::string comm_async_error(RankComm* c);
+void comm_abort(RankComm* c);
+
+// The validated steady plan (a full step's routing decisions, parallel/distributed.py _steady).
+struct DistPlan {
+    int world = 1, rank = 0, k = 16, device = 0;
+    int n = 0;                       // points of this rank's share (every step)
+    const float* points = nullptr;   // device (n x 3), read in place by every step
+    const int* ids = nullptr;        // device (n) global ids, or null: id offset + i
+    const void* route = nullptr;     // device RouteParams of the validated step (copied)
+    std::vector<double> hdr;         // kPlanHdr plan header doubles
+    const double* metas = nullptr;   // device (world x 8) metas of the validated step (copied)
+    std::vector<int> tot;            // 2*world planned (owned, halo) send counts
+    int grid[3] = {1, 1, 1};         // rank grid
+    int dims[3] = {1, 1, 1};         // local grid dims of the validated step (maybe refined)
+    int use_tree = 0;
+    float ppc = 0.f;
+    int deterministic = 1;
+    int exact_grid = 0;
+    int cap = 0;                     // send buffer rows
+    std::vector<int> recv_own, recv_halo, cross_send, cross_recv;
+    int place[5] = {0, 0, 0, 0, 0};  // SelfPlace: own_base, halo_base, rows, own count, halo count
+    // world 1, forced collectives: the rank's own rows go through an RCCL self send / recv and
+    // the unpack instead of straight into the local set (exercises the exchange on one GPU)
+    int self_via_comm = 0;
+};
+
+class DistPipeline {
+public:
+    DistPipeline(const DistPlan& p, RankComm* comm);
+    ~DistPipeline();
+    DistPipeline(const DistPipeline&) = delete;
+    DistPipeline& operator=(const DistPipeline&) = delete;
+    const std::string& error() const { return err_; }
+    bool ok() const { return ok_; }
+
+    // Enqueue `iters` pipelined steps (unroll >= 2, even: steps per graph launch); *last_step = the
+    // index of the last one. The steps read the caller's points in place: `caller` (may be null)
+    // is the stream that wrote them -- the first build waits for it, and it waits (on the device)
+    // for the builds that read them. keep_primed: also enqueue the next step's build now (the
+    // caller promises the points stay unchanged until the next launch).
+    kn_status launch(int iters, int unroll, bool keep_primed, hipStream_t caller, long long* last_step);
+    // Wait (polling RCCL's async error, at most timeout_s) until step `step`'s flag is final;
+    // *flag = the sticky flag (0: every step so far valid).
+    kn_status wait(long long step, double timeout_s, int* flag);
+    kn_status sync();
+    int last_set() const { return pipe_.last_set(); }
+    // One serial step on the main stream with events between its phases (ms): route, exchange,
+    // unpack + build, query (+ certification + flag), flag all-reduce. Unprimes the pipeline.
+    kn_status profile(float ms[5]);
+
+    int rows() const { return rows_; }
+    int n_owned() const { return n_owned_; }
+    int k() const { return p_.k; }
+    // buffers of set s (the last step: last_set()); valid until the step after next
+    const int* gids(int s) const { return set_[s].lgids; }
+    const int* idx(int s) const { return set_[s].idx; }
+    const float* d2(int s) const { return set_[s].d2; }
+    const unsigned* counters(int s) const { return set_[s].counters; }
+
+private:
+    struct Set {
+        char* block;
+        float4* send; int* bc; int* totals; unsigned* partials; float4* recv;
+        float* lpts; int* lgids;
+        unsigned* bbox; GridGeom* geom; int* cell_count; int* cell_scan; int* block_sums; int* cell_start;
+        float4* bin_tmp; float4* sorted; unsigned* perm;
+        unsigned* fallback; unsigned* counters; unsigned* uncert;
+        int* idx; float* d2; int* flag;
+        void* tree_ws; void* tree_nodes;
+    };
+    hipError_t stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks = nullptr);
+    hipError_t stage_query(int s, hipStream_t st);
+    hipError_t stage_flag(int s, hipStream_t st);
+    hipError_t exchange(int s, hipStream_t st);
+    bool fail(const std::string& m) { err_ = m; ok_ = false; return false; }
+
+    DistPlan p_;
+    RankComm* comm_;
+    std::string err_;
+    bool ok_ = false;
+    int rows_ = 0, n_owned_ = 0, C_ = 0;
+    int rows_cross_ = 0, recv_rows_ = 0;
+    std::vector<long long> soff_, roff_;  // send / recv row offsets per peer
+    UnpackTable table_{};
+    BuildBuffers bproto_{};
+    QueryBuffers qproto_{};
+    CompleteBox complete_{};
+    Set set_[2]{};
+    void* route_dev_ = nullptr;
+    double* metas_dev_ = nullptr;
+    int* tot_dev_ = nullptr;
+    int* sticky_ = nullptr;
+    int* host_flag_ = nullptr;      // pinned
+    int* host_flag_dev_ = nullptr;  // its device pointer
+    hipStream_t main_ = nullptr, side_ = nullptr;
+    Pipeline pipe_;
+    // host waits: (last step covered, event) ring, recorded after each launch's last epilogue
+    std::vector<hipEvent_t> ring_;
+    hipEvent_t in_ev_ = nullptr;  // the caller's input is ready
+    std::deque<std::pair<long long, int>> done_;
+    int ring_next_ = 0;
+};
+
+}  // namespace kn

@@ -160,7 +160,7 @@ hipError_t Pipeline::flush() {
     return hipSuccess;
 }
 
-hipError_t Pipeline::launch(int iters, int unroll) {
+hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
     if (!main_) return hipErrorNotInitialized;
     KN_TRY(graphs());
     if (unroll < 2 || (unroll & 1)) unroll = 0;
@@ -173,7 +173,9 @@ hipError_t Pipeline::launch(int iters, int unroll) {
     int done = 0;
     while (done < iters) {
         const int s = (int)(next_ & 1);
-        if (unroll && iters - done >= unroll) {
+        // an unrolled graph ends with the next step's build: only when the call keeps it primed,
+        // or more steps follow in this call
+        if (unroll && iters - done >= unroll + (keep_primed ? 0 : 1)) {
             KN_TRY(unrolled(s, unroll));
             if (!primed_) KN_TRY(enqueue_build(s));
             if (r_pending_) {
@@ -202,8 +204,12 @@ hipError_t Pipeline::launch(int iters, int unroll) {
             KN_TRY(enqueue_epilogue(last_set_));
         }
         last_set_ = s;
-        KN_TRY(enqueue_build(s ^ 1));  // B(i+1) overlaps Q(i)
-        primed_ = true;
+        if (keep_primed || done + 1 < iters) {
+            KN_TRY(enqueue_build(s ^ 1));  // B(i+1) overlaps Q(i)
+            primed_ = true;
+        } else {
+            primed_ = false;
+        }
         r_pending_ = (bool)r_;
         ++next_;
         ++done;

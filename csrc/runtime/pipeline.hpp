@@ -39,8 +39,11 @@ public:
     hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage());
     bool ready() const { return main_ != nullptr; }
     // Enqueue `iters` resident-mode steps; unroll >= 2 (even): whole groups of `unroll` steps go
-    // through one unrolled graph, the rest through per-step graphs.
-    hipError_t launch(int iters, int unroll = 0);
+    // through one unrolled graph, the rest through per-step graphs. keep_primed = false: the call
+    // ends without the next step's build (its input may change before the next call).
+    hipError_t launch(int iters, int unroll = 0, bool keep_primed = true);
+    // Event recorded after the most recent build of set s (its input has been read).
+    hipEvent_t build_event(int s) const { return evB_[s]; }
     // One step whose input is provided by `pre` (run on the side stream before B, e.g. a copy of
     // the step's cloud into set s's input buffer); `next_pre` != null: also the next step's input
     // is known, so its build is enqueued now (overlapping this step's queries). Unprimes the
@@ -56,7 +59,7 @@ public:
     long long steps() const { return next_; }
     // Event recorded after the last step's final stage (R if present, else Q).
     hipEvent_t last_done() const { return last_done_; }
-    // Destroy graphs and events (stages are kept? no: call init again).
+    // Destroy graphs and events (init() again before the next launch).
     void reset();
 
 private:

@@ -17,6 +17,7 @@
 #include "kn/tree.h"
 #include "../host/host.hpp"
 #include "../runtime/engine.hpp"
+#include "../runtime/dist.hpp"
 
 #include <memory>
 
@@ -1190,6 +1191,145 @@ torch::Tensor normalize_1000(torch::Tensor points) {
 
 }  // namespace
 
+
+// ---- one rank's pipelined distributed step over RCCL (csrc/runtime/dist.hpp) -------------
+py::bytes rccl_unique_id() {
+    unsigned char id[kn::kCommIdBytes];
+    std::string err;
+    TORCH_CHECK(kn::comm_unique_id(id, &err), err);
+    return py::bytes(reinterpret_cast<const char*>(id), kn::kCommIdBytes);
+}
+
+class PyRankComm {
+public:
+    PyRankComm(py::bytes id, int64_t world, int64_t rank, int64_t device) {
+        const std::string s = id;
+        TORCH_CHECK(s.size() == (size_t)kn::kCommIdBytes, "the unique id is 128 bytes");
+        std::string err;
+        {
+            py::gil_scoped_release nogil;  // collective: blocks until every rank joined
+            c_ = kn::comm_create(reinterpret_cast<const unsigned char*>(s.data()), (int)world, (int)rank, (int)device, &err);
+        }
+        TORCH_CHECK(c_, err);
+    }
+    ~PyRankComm() { kn::comm_destroy(c_); }
+    std::string async_error() { return kn::comm_async_error(c_); }
+    void abort() { kn::comm_abort(c_); }
+    kn::RankComm* c_ = nullptr;
+};
+
+class PyDistPipe {
+public:
+    PyDistPipe(std::shared_ptr<PyRankComm> comm, torch::Tensor points, c10::optional<torch::Tensor> ids,
+               torch::Tensor plan, torch::Tensor metas, std::vector<int64_t> tot, std::vector<double> hdr,
+               std::vector<int64_t> grid, std::vector<int64_t> dims, std::vector<int64_t> recv_own,
+               std::vector<int64_t> recv_halo, std::vector<int64_t> cross_send, std::vector<int64_t> cross_recv,
+               std::vector<int64_t> place, int64_t cap, int64_t k, double ppc, bool deterministic, int64_t exact_grid,
+               int64_t use_tree, bool self_via_comm)
+        : comm_(std::move(comm)), points_(points) {
+        check_points(points, true);
+        TORCH_CHECK(plan.is_cuda() && plan.numel() == (int64_t)sizeof(kn::RouteParams), "plan must be a route plan");
+        TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous(), "metas: f64 GPU");
+        TORCH_CHECK(grid.size() == 3 && dims.size() == 3 && place.size() == 5, "grid / dims / place sizes");
+        kn::DistPlan p;
+        p.world = comm_->c_->world;
+        p.rank = comm_->c_->rank;
+        p.device = points.get_device();
+        p.k = (int)k;
+        p.n = (int)points.size(0);
+        p.points = points.data_ptr<float>();
+        if (ids.has_value()) {
+            TORCH_CHECK(ids->is_cuda() && ids->scalar_type() == torch::kInt32 && ids->numel() == points.size(0) &&
+                            ids->is_contiguous(), "ids: contiguous int32 GPU tensor of N entries");
+            ids_ = *ids;
+            p.ids = ids_.data_ptr<int>();
+        }
+        plan_ = plan;
+        metas_ = metas;
+        p.route = plan.data_ptr();
+        TORCH_CHECK(metas.numel() == 8 * (int64_t)p.world, "metas: world x 8");
+        p.metas = metas.data_ptr<double>();
+        p.hdr = hdr;
+        for (auto v : tot) p.tot.push_back((int)v);
+        for (int a = 0; a < 3; ++a) { p.grid[a] = (int)grid[a]; p.dims[a] = (int)dims[a]; }
+        for (auto v : recv_own) p.recv_own.push_back((int)v);
+        for (auto v : recv_halo) p.recv_halo.push_back((int)v);
+        for (auto v : cross_send) p.cross_send.push_back((int)v);
+        for (auto v : cross_recv) p.cross_recv.push_back((int)v);
+        for (int i = 0; i < 5; ++i) p.place[i] = (int)place[i];
+        p.cap = (int)cap;
+        p.ppc = (float)ppc;
+        p.deterministic = deterministic ? 1 : 0;
+        p.exact_grid = (int)exact_grid;
+        p.use_tree = (int)use_tree;
+        p.self_via_comm = self_via_comm ? 1 : 0;
+        const c10::DeviceGuard guard(points.device());
+        // the plan tensors (route plan, metas) are copied by the constructor: their producers first
+        KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+        d_ = std::make_unique<kn::DistPipeline>(p, comm_->c_);
+        TORCH_CHECK(d_->ok(), d_->error());
+    }
+    // enqueue `iters` steps (unroll: steps per graph launch, even >= 2, else one graph per stage)
+    // keep_primed: also enqueue the next step's build (the caller promises the points stay
+    // unchanged until the next launch); the current torch stream orders the input
+    int64_t launch(int64_t iters, int64_t unroll, bool keep_primed) {
+        long long last = -1;
+        const c10::DeviceGuard guard(points_.device());
+        const hipStream_t caller = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+        TORCH_CHECK(d_->launch((int)iters, (int)unroll, keep_primed, caller, &last) == KN_OK, d_->error());
+        return last;
+    }
+    // wait for step `step` (polls RCCL errors; deadline) -> sticky flag (0 = all steps valid)
+    int64_t wait(int64_t step, double timeout_s) {
+        int flag = -1;
+        kn_status st;
+        {
+            py::gil_scoped_release nogil;
+            st = d_->wait(step, timeout_s, &flag);
+        }
+        TORCH_CHECK(st == KN_OK, d_->error());
+        return flag;
+    }
+    void sync() { TORCH_CHECK(d_->sync() == KN_OK, d_->error()); }
+    int64_t last_set() { return d_->last_set(); }
+    // (owned global ids, idx, d2) of grid set s: views of the pipeline's buffers, overwritten by
+    // the step after next (the Python owner keeps this object alive while they are in use)
+    std::vector<torch::Tensor> outputs(int64_t s) {
+        TORCH_CHECK(s == 0 || s == 1, "set is 0 or 1");
+        auto opt = torch::TensorOptions().device(points_.device());
+        const int64_t no = d_->n_owned(), k = d_->k();
+        auto g = torch::from_blob(const_cast<int*>(d_->gids((int)s)), {no}, opt.dtype(torch::kInt32));
+        auto i = torch::from_blob(const_cast<int*>(d_->idx((int)s)), {no, k}, opt.dtype(torch::kInt32));
+        auto d = torch::from_blob(const_cast<float*>(d_->d2((int)s)), {no, k}, opt.dtype(torch::kFloat32));
+        return {g, i, d};
+    }
+    std::vector<int64_t> counters(int64_t s) {
+        TORCH_CHECK(s == 0 || s == 1, "set is 0 or 1");
+        TORCH_CHECK(d_->sync() == KN_OK, d_->error());
+        unsigned c[kn::kNumCounters];
+        KN_CHECK_HIP(hipMemcpy(c, d_->counters((int)s), sizeof(c), hipMemcpyDeviceToHost));
+        return std::vector<int64_t>(c, c + kn::kNumCounters);
+    }
+    py::dict profile() {
+        float ms[5] = {0, 0, 0, 0, 0};
+        TORCH_CHECK(d_->profile(ms) == KN_OK, d_->error());
+        py::dict r;
+        r["ms_route"] = ms[0];
+        r["ms_exchange"] = ms[1];
+        r["ms_build"] = ms[2];
+        r["ms_query"] = ms[3];
+        r["ms_flag_allreduce"] = ms[4];
+        return r;
+    }
+    int64_t rows() { return d_->rows(); }
+    int64_t n_owned() { return d_->n_owned(); }
+
+private:
+    std::shared_ptr<PyRankComm> comm_;
+    torch::Tensor points_, ids_, plan_, metas_;
+    std::unique_ptr<kn::DistPipeline> d_;
+};
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X-native k-nearest-neighbour kernels (gfx950 HIP) and CPU oracles";
     m.def("build", &build, "bin points into the grid (GPU)", py::arg("points"), py::arg("dims"),
@@ -1265,6 +1405,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("points"), py::arg("ids"), py::arg("lo"), py::arg("hi"), py::arg("grid"), py::arg("boxes"),
           py::arg("h"), py::arg("block_offsets"), py::arg("totals"), py::arg("rows"), py::arg("splits") = py::none());
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
+    m.def("rccl_unique_id", &rccl_unique_id, "multi-GPU: a new RCCL unique id (128 bytes) for RankComm");
+    py::class_<PyRankComm, std::shared_ptr<PyRankComm>>(m, "RankComm", "one rank's RCCL communicator (collective init)")
+        .def(py::init<py::bytes, int64_t, int64_t, int64_t>(), py::arg("uid"), py::arg("world"), py::arg("rank"),
+             py::arg("device"))
+        .def("async_error", &PyRankComm::async_error)
+        .def("abort", &PyRankComm::abort);
+    py::class_<PyDistPipe>(m, "DistPipe", "one rank's pipelined distributed step (route + RCCL exchange + build | "
+                                          "query | flag all-reduce), hipGraph-replayed")
+        .def(py::init<std::shared_ptr<PyRankComm>, torch::Tensor, c10::optional<torch::Tensor>, torch::Tensor,
+                      torch::Tensor, std::vector<int64_t>, std::vector<double>, std::vector<int64_t>,
+                      std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>,
+                      std::vector<int64_t>, std::vector<int64_t>, int64_t, int64_t, double, bool, int64_t, int64_t,
+                      bool>())
+        .def("launch", &PyDistPipe::launch, py::arg("iters") = 1, py::arg("unroll") = 0, py::arg("keep_primed") = false)
+        .def("wait", &PyDistPipe::wait, py::arg("step"), py::arg("timeout_s") = 300.0)
+        .def("sync", &PyDistPipe::sync)
+        .def("last_set", &PyDistPipe::last_set)
+        .def("outputs", &PyDistPipe::outputs)
+        .def("counters", &PyDistPipe::counters)
+        .def("profile", &PyDistPipe::profile)
+        .def("rows", &PyDistPipe::rows)
+        .def("n_owned", &PyDistPipe::n_owned);
     py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")
         .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t, bool, int64_t>(),
              py::arg("k") = 16, py::arg("points_per_cell") = 0.0, py::arg("tile") = std::vector<int64_t>{},

@@ -30,7 +30,7 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 
 KERNELS = ["kernels/build.hip", "kernels/query.hip", "kernels/route.hip", "kernels/tree.hip"]
 HOST = ["host/host.cpp"]
-RUNTIME = ["runtime/engine.cpp", "runtime/api.cpp", "runtime/hostio.cpp", "runtime/pipeline.cpp"]
+RUNTIME = ["runtime/engine.cpp", "runtime/api.cpp", "runtime/hostio.cpp", "runtime/pipeline.cpp", "runtime/dist.cpp"]
 MULTI = "runtime/multi.cpp"  # C-API multi-GPU runtime: libknearests.so only (links RCCL)
 RCCL_OK = os.path.exists(os.path.join(ROCM, "include", "rccl", "rccl.h"))
 
@@ -140,10 +140,12 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
     _run([HIPCC, "-shared", "-o", str(lib)] + [str(o) for o in kern + host + rt + objs["multi"]] + hiplink +
          (["-lrccl", f"-Wl,-rpath,{ROCM}/lib"] if RCCL_OK else []))
     cext = PKG / f"_C{ext}"
-    _run([HIPCC, "-shared", "-o", str(cext)] + [str(o) for o in kern + host + rt + objs["torch"]] + hiplink + tld)
+    # the extension's RCCL is torch's own (same soname, already loaded by libtorch_hip)
+    rccl = ["-lrccl"] + [f"-Wl,-rpath,{ROCM}/lib"]
+    _run([HIPCC, "-shared", "-o", str(cext)] + [str(o) for o in kern + host + rt + objs["torch"]] + hiplink + tld + rccl)
     cchk = PKG / f"_C_checked{ext}"
     _run([HIPCC, "-shared", "-o", str(cchk)] + [str(o) for o in sorted(objs["kernchk"]) + host + rt + objs["torchchk"]]
-         + hiplink + tld)
+         + hiplink + tld + rccl)
     bindir = ROOT / "bin"
     bindir.mkdir(exist_ok=True)
     exes = {}
@@ -174,7 +176,7 @@ def build_variant(name: str, hip_flags: list[str], jobs: int = 8) -> Path:
         objs = [f.result() for f in kf + hf + rf] + [bf.result()]
     out = PKG / f"_C_{name}{ext}"
     hiplink = [f"--offload-arch={ARCH}", "-fopenmp", f"-L{ROCM}/lib", "-lamdhip64"]
-    _run([HIPCC, "-shared", "-o", str(out)] + [str(o) for o in objs] + hiplink + tld)
+    _run([HIPCC, "-shared", "-o", str(out)] + [str(o) for o in objs] + hiplink + tld + ["-lrccl"])
     return out
 
 

@@ -39,7 +39,7 @@ import torch
 from ..ops import knn_ops as ops
 from .decomposition import SpatialDecomposition, balanced_splits, factor3
 from ..utils import get_logger
-from .transport import HostStagedTransport, TorchDistTransport
+from .transport import CollectiveError, HostStagedTransport, TorchDistTransport
 
 _log = get_logger("knearests.dist")
 
@@ -91,11 +91,17 @@ class DistResult:
     # hold on some rank, or some query was not certified -- the rows must not be used.
     flag: Optional[torch.Tensor] = None
     event: Optional[object] = None
+    # native pipelined steps (kn::DistPipeline): waits for the step (polling RCCL's async error
+    # under a deadline) and returns True when its sticky flag is clear; keeps the pipeline (whose
+    # buffers the rows view) alive
+    waiter: Optional[object] = None
 
     def valid(self) -> bool:
         """True when the rows are final (waits for the step's flag; no-op for synchronous steps).
         Reading it never changes the solver's state: which path the next step takes is decided
         inside solve() from the flags of earlier steps, identically on every rank."""
+        if self.waiter is not None:
+            return bool(self.waiter())
         if self.flag is None:
             return True
         if self.event is not None:
@@ -111,7 +117,8 @@ class DistributedKNearests:
     def __init__(self, k: int = 16, group=None, halo_factor: float = 2.5, points_per_cell: float = 0.0,
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
                  transport=None, device_plan: bool = True, timeout_s: Optional[float] = None,
-                 balance: str = "count", adaptive: bool = True):
+                 balance: str = "count", adaptive: bool = True, native_pipeline: Optional[bool] = None,
+                 force_collectives: Optional[bool] = None):
         self.k = int(k)
         # occupancy-adaptive local grids (GPU): a rank whose share is clustered re-bins finer, as
         # the 1-GPU engine does; steady steps reuse the validated step's grid (no extra sync)
@@ -183,6 +190,24 @@ class DistributedKNearests:
         # between replays; profiles/bench_r3_dist_world1.txt).
         self.graph_steady = None
         self._graph = None
+        # Native pipelined steady steps (round 4, csrc/runtime/dist.hpp): the rank's own RCCL
+        # communicator, route + exchange + build of step i+1 on a second stream while step i
+        # queries, the flag's all-reduce after it -- all hipGraph-replayed (the 1-GPU pipelined
+        # step plus the communication). Default on GPU ranks over torch.distributed "nccl" whenever
+        # the steady plan needs no device forwarding; KN_DIST_PIPE=0 / native_pipeline=False: the
+        # torch path above. force_collectives (KN_DIST_FORCE_COLLECTIVES=1): at world 1 the rank's
+        # own rows also travel through RCCL (self send / recv + unpack), exercising the exchange
+        # of world > 1 on one GPU.
+        import os
+
+        self.native_pipeline = native_pipeline
+        if force_collectives is None:
+            force_collectives = os.environ.get("KN_DIST_FORCE_COLLECTIVES") == "1"
+        self.force_collectives = bool(force_collectives)
+        self.pipe_unroll = int(os.environ.get("KN_DIST_UNROLL", "4"))  # steps per graph in run_steps
+        self.wait_timeout_s = float(timeout_s) if timeout_s else 300.0
+        self._rcomm = None
+        self._pipe = None
         # asynchronous steady results not yet checked by the solver. Before the next steady step
         # all but the newest are checked (their steps are long done, so this rarely waits, and it
         # bounds the host's lead to ~2 steps): an invalid one drops the steady plan. The flags
@@ -602,10 +627,118 @@ class DistributedKNearests:
         on = env == "1" or (env != "0" and self.world == 1)
         return on and isinstance(self.comm, TorchDistTransport)
 
-    def _solve_steady(self, points: torch.Tensor, ids: Optional[torch.Tensor]) -> DistResult:
-        """One step with no host synchronisation (see ``self.steady``), replayed from a hipGraph
-        when ``_use_graph``."""
+    def _use_pipe(self, points: torch.Tensor) -> bool:
         st = self._steady
+        if st is None or st.get("fwd") or not points.is_cuda:
+            return False
+        if not isinstance(self.comm, TorchDistTransport) or isinstance(self.comm, HostStagedTransport):
+            return False
+        if not getattr(self.comm, "stream_ordered", False):  # RCCL ("nccl") groups only
+            return False
+        if self.native_pipeline is not None:
+            return bool(self.native_pipeline)
+        import os
+
+        return os.environ.get("KN_DIST_PIPE", "1") != "0" and hasattr(ops.load(), "DistPipe")
+
+    def _rank_comm(self, dev: torch.device):
+        """This rank's own RCCL communicator (collective: every rank calls it at the same step;
+        the unique id travels over the process group)."""
+        if self._rcomm is None:
+            C = ops.load()
+            uid = C.rccl_unique_id() if self.rank == 0 else bytes(128)
+            t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+            parts = self.comm.all_gather(t)
+            uid0 = bytes(parts[0].cpu().tolist())
+            self._rcomm = C.RankComm(uid0, self.world, self.rank, dev.index if dev.index is not None else 0)
+        return self._rcomm
+
+    def _pipe_for(self, points: torch.Tensor, ids: Optional[torch.Tensor]):
+        """The native pipeline of the current steady plan over these input tensors (read in
+        place; other storage builds a new one)."""
+        st = self._steady
+        ids32 = ids.to(torch.int32).contiguous() if ids is not None else None
+        p = self._pipe
+        same = (p is not None and p["st"] is st and p["pts"].data_ptr() == points.data_ptr()
+                and p["n"] == points.size(0) and (p["ids"] is None) == (ids32 is None)
+                and (ids32 is None or p["ids"].data_ptr() == ids32.data_ptr()))
+        if same:
+            return p
+        self._pipe = None  # release the old pipeline's buffers first
+        C = ops.load()
+        world1_force = self.world == 1 and self.force_collectives
+        pipe = C.DistPipe(self._rank_comm(points.device), points, ids32, st["plan"], st["metas"],
+                          [int(v) for v in st["tot"].tolist()], [float(v) for v in st["hdr"]], list(st["grid"]),
+                          list(st["dims"]), list(st["recv_own"]), list(st["recv_halo"]), list(st["cross_send"]),
+                          list(st["cross_recv"]), list(st["place"]), int(st["cap"]), self.k, self.points_per_cell,
+                          bool(self.deterministic), int(st["exact_grid"]), int(st["use_tree"]), world1_force)
+        p = self._pipe = {"pipe": pipe, "st": st, "pts": points, "ids": ids32, "n": points.size(0),
+                          "outs": [pipe.outputs(0), pipe.outputs(1)], "primed": False}
+        return p
+
+    def _solve_pipe(self, points: torch.Tensor, ids: Optional[torch.Tensor], iters: int = 1,
+                    resident: bool = False) -> DistResult:
+        """``iters`` steady steps through the native pipeline (one call; unrolled graphs when
+        iters > 1). resident: keep the next step's build enqueued after the call (the caller
+        promises the points do not change before the next call)."""
+        st = self._steady
+        p = self._pipe_for(points, ids)
+        pipe = p["pipe"]
+        last = pipe.launch(iters, self.pipe_unroll if iters > 1 else 0, bool(resident))
+        gids, idx, d2 = p["outs"][pipe.last_set()]
+        stats = dict(st["stats"])
+        stats["steady"] = True
+        stats["graph"] = True
+        stats["pipelined"] = True
+        timeout = self.wait_timeout_s
+        rank = self.rank
+
+        def waiter() -> bool:
+            try:
+                return pipe.wait(last, timeout) == 0
+            except RuntimeError as e:
+                raise CollectiveError(f"rank {rank}: pipelined step failed: {e}") from e
+
+        return DistResult(gids, idx, d2, stats, waiter=waiter)
+
+    def run_steps(self, points: torch.Tensor, iters: int, ids: Optional[torch.Tensor] = None,
+                  resident: bool = False) -> DistResult:
+        """``iters`` steps of the same share in one call (benchmarks, repeated solves of a
+        resident cloud): in the steady state all of them are enqueued at once into the native
+        pipeline (U steps per graph launch, no host round trip); otherwise asynchronous
+        ``solve`` calls. Returns the last step's result; its ``valid()`` covers every step."""
+        points = points.contiguous().float()
+        if iters <= 0:
+            raise ValueError("iters must be positive")
+        if self.steady and self._steady is not None and self._use_native(points) and self.device_plan:
+            self._check_pending(keep=0)
+            if self._steady is not None and self._use_pipe(points):
+                res = self._solve_pipe(points, ids, iters, resident)
+                self._pending.append(res)
+                return res
+        res = None
+        for _ in range(iters):
+            res = self.solve(points, ids, async_=True)
+        return res
+
+    def profile_step(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None) -> dict:
+        """Per-phase device times (ms) of one serial steady step of the native pipeline
+        (collective: every rank calls it): ms_route, ms_exchange, ms_build, ms_query,
+        ms_flag_allreduce. {} when the steady native pipeline is not in use."""
+        points = points.contiguous().float()
+        if self._steady is None or not self._use_pipe(points):
+            return {}
+        self._check_pending(keep=0)
+        if self._steady is None:
+            return {}
+        return dict(self._pipe_for(points, ids)["pipe"].profile())
+
+    def _solve_steady(self, points: torch.Tensor, ids: Optional[torch.Tensor]) -> DistResult:
+        """One step with no host synchronisation (see ``self.steady``): the native pipeline
+        (``_use_pipe``), else replayed from a torch hipGraph when ``_use_graph``."""
+        st = self._steady
+        if self._use_pipe(points):
+            return self._solve_pipe(points, ids)
         if self._use_graph(points):
             g = self._graph
             ids32 = ids.to(torch.int32).contiguous() if ids is not None else None
@@ -670,6 +803,9 @@ class DistributedKNearests:
                   "the next step takes the full path", self.rank)
         self._steady = None
         self._graph = None
+        if self._pipe is not None:
+            self._pipe["pipe"].sync()
+        self._pipe = None
         self._pending.clear()
 
     def _check_pending(self, keep: int) -> None:

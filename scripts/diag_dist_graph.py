@@ -23,13 +23,13 @@ dist.init_process_group("nccl", device_id=dev)
 C = load()
 print("module", C.__name__, flush=True)
 pts = uniform_cloud(n, seed=3, device=dev)
-ref = DistributedKNearests(k=16, deterministic=False)
+ref = DistributedKNearests(k=16, deterministic=False, native_pipeline=False)
 ref.graph_steady = False
 r_full = ref.solve(pts)  # the validated full (routed) step
 r_eager = ref.solve(pts)  # steady, eager
 assert r_eager.valid() and r_eager.stats.get("steady")
 assert torch.equal(r_full.neighbors, r_eager.neighbors) and torch.equal(r_full.d2, r_eager.d2)
-dk = DistributedKNearests(k=16, deterministic=False)
+dk = DistributedKNearests(k=16, deterministic=False, native_pipeline=False)
 dk.graph_steady = True
 dk.solve(pts)  # validating step
 res = [dk.solve(pts, async_=True) for _ in range(steps)]  # capture once, then replays
@@ -49,7 +49,7 @@ moved = pts * 0.5
 bad = dk.solve(moved, async_=True)
 inval = not bad.valid()
 r_moved = dk.solve(moved)
-ref_moved = DistributedKNearests(k=16, deterministic=False).solve(moved)
+ref_moved = DistributedKNearests(k=16, deterministic=False, native_pipeline=False).solve(moved)
 same3 = torch.equal(r_moved.neighbors, ref_moved.neighbors) and torch.equal(r_moved.d2, ref_moved.d2)
 print("staged", ok2, same2, "moved share invalid", inval, "recovered", same3, flush=True)
 same = same and ok2 and same2 and inval and same3

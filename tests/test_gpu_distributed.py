@@ -524,3 +524,26 @@ def test_adaptive_halo_boost(cuda):
         for steady, ok, _, _, ids, d2 in hist:
             assert ok
             assert torch.equal(d2, od[ids.long()])
+
+
+def test_rccl_world1_native_pipeline(cuda):
+    """kn::DistPipeline at world 1 over a real RCCL communicator, plain and with forced
+    collectives (the own rows through an RCCL self send / recv + unpack): asynchronous per-call
+    steps, batched unrolled run_steps (with and without resident priming), in-place refills
+    between calls, a moved share and the per-phase profile; rows bit-identical to the torch
+    path's (scripts/diag_dist_pipe.py)."""
+    import subprocess
+    import sys
+
+    from cuda_knearests_amd.utils import REPO
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONPATH=str(REPO), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+               RANK="0", WORLD_SIZE="1")
+    r = subprocess.run([sys.executable, str(REPO / "scripts" / "diag_dist_pipe.py"), "30", "200000"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "ALL OK" in r.stdout
