@@ -154,7 +154,7 @@ void brute_knn_all(const float* pts, int n, int k, uint32_t* idx, float* d2, int
 // ----------------------------------------------------------------- CPU grid kNN -------
 void grid_knn_cpu(const float* pts, int n, int n_queries, int k, float ppc, const float clo[3],
                   const float chi[3], uint32_t* idx, float* d2, std::vector<uint32_t>* uncert,
-                  int threads) {
+                  int threads, const float* cext) {
     if (n_queries <= 0) return;
     if (!(ppc > 0.f)) ppc = 3.1f;  // same default grid density as the GPU engine
     float lo[3], hi[3];
@@ -232,7 +232,16 @@ void grid_knn_cpu(const float* pts, int n, int n_queries, int k, float ppc, cons
             if (m == std::numeric_limits<float>::infinity() || (m > 0.f && top.d[k - 1] <= m * m)) { ok = true; break; }
         }
         float m = std::numeric_limits<float>::infinity();
-        for (int a = 0; a < 3; ++a) m = std::min(m, std::min(q[a] - clo[a], chi[a] - q[a]));
+        const float wide = cext ? cext[0] : 0.f;
+        float zq = std::numeric_limits<float>::infinity();
+        if (wide > 0.f)
+            for (int a = 0; a < 3; ++a) zq = std::min(zq, std::min(q[a] - cext[2 + a], cext[5 + a] - q[a]));
+        for (int a = 0; a < 3; ++a) {
+            float lo = q[a] - clo[a], hi = chi[a] - q[a];
+            if (wide > 0.f && zq + lo + wide <= cext[1]) lo += wide;
+            if (wide > 0.f && zq + hi + wide <= cext[1]) hi += wide;
+            m = std::min(m, std::min(lo, hi));
+        }
         m -= eps;
         if (!(m == std::numeric_limits<float>::infinity() || (m > 0.f && top.d[k - 1] <= m * m))) ok = false;
         if (!ok) bad[qi] = 1;

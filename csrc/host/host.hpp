@@ -49,9 +49,12 @@ void kdtree_knn_all(const float* pts, int n, int k, uint32_t* idx, float* d2, in
 void brute_knn_all(const float* pts, int n, int k, uint32_t* idx, float* d2, int threads);
 // Queries [0, n_queries) against all n points; uncertified gets the query ids whose K-th
 // distance reaches past `complete_lo/hi` (multi-rank halo limit; pass +-inf for none).
+// complete_ext (nullable): {wide, zlim, domain lo x3, domain hi x3} of a position-dependent halo
+// (kn::CompleteBox): a face margin grows by `wide` when the query's distance to the domain plus
+// the margin + wide stays <= zlim.
 void grid_knn_cpu(const float* pts, int n, int n_queries, int k, float points_per_cell,
                   const float complete_lo[3], const float complete_hi[3], uint32_t* idx,
-                  float* d2, std::vector<uint32_t>* uncertified, int threads);
+                  float* d2, std::vector<uint32_t>* uncertified, int threads, const float* complete_ext = nullptr);
 
 // Distance-aware comparison of a kNN result (original space, rows ascending) against an
 // oracle: every row must be duplicate-free, exclude its own index, list valid ids in

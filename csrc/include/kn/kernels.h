@@ -28,9 +28,19 @@ struct GridGeom {
 
 // Box inside which the local point set is complete (all points of the global cloud that lie
 // in it are present). Single GPU: infinite. Multi-GPU: the rank's owned box grown by its halo.
+// Position-dependent halo (round 4, kn/route.h): points within the wide zone (distance <= w to
+// a face of the global domain) were routed with the edge width h_e, the others with the
+// interior width h_i <= h_e. lo / hi are the own box grown by h_i; a face's margin grows by
+// `wide` = h_e - h_i when the query's distance to the domain plus that margin stays below
+// `zlim` (w minus a rounding slack): every point of the ball it certifies then lies in the wide
+// zone. wide = 0: one width (single GPU: all zero, the margins are infinite anyway).
 struct CompleteBox {
     float lo[3];
     float hi[3];
+    float wide;
+    float zlim;
+    float dlo[3];
+    float dhi[3];
 };
 
 constexpr int kScanItems = 4096;  // elements per scan block (256 threads x 16)

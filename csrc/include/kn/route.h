@@ -20,7 +20,13 @@ struct RouteParams {
     float g[3];     // decomposition grid (px, py, pz) as floats
     int grid[3];
     int world;      // px * py * pz <= kRouteMaxWorld
-    float h2;       // squared halo send width
+    float h2;       // squared halo send width (edge width h_e: points in the wide zone)
+    // Position-dependent halo: a point farther than wz from every face of the global domain is
+    // sent with the interior width (hi2 <= h2) -- an interior query's K-th ball is a whole ball,
+    // a query near a domain face sees a truncated one (x 4^(1/3) at an edge). hi2 == h2: one width.
+    float hi2;
+    float wz;
+    float dom_hi[3];  // global domain upper corner (lower: lo)
     int id_offset;  // global id of this rank's first point (route_scatter with ids == nullptr)
     float box_lo[kRouteMaxWorld][3];  // rank boxes (same formula as SpatialDecomposition.rank_box)
     float box_hi[kRouteMaxWorld][3];
@@ -40,9 +46,10 @@ inline int route_split_count(const int g[3]) { return (g[0] + 1) + g[0] * (g[1] 
 
 // Device-side plan header (doubles) written by launch_route_plan for the host's one sync:
 constexpr int kPlanHdr = 24;
-// [0..2] global lo  [3..5] global hi  [6] h (certification halo)  [7] h_send  [8] n_total
-// [9] id offset of this rank  [10] 1 if the halo covers the whole domain  [11] domain diagonal
-// [12..14] this rank's box lo  [15..17] its box hi
+// [0..2] global lo  [3..5] global hi  [6] h (certification halo, edge width h_e)  [7] h_send
+// [8] n_total  [9] id offset of this rank  [10] 1 if the halo covers the whole domain
+// [11] domain diagonal  [12..14] this rank's box lo  [15..17] its box hi
+// [18] h_i (interior width)  [19] its send width  [20] wide-zone width w  [21] w - rounding slack
 
 // The local geometry of `rank` from its plan header -- ONE definition for every distributed
 // runtime (the torch binding's dist_local and the C-API kn_solve_multi): the complete box (own box
@@ -120,9 +127,16 @@ hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int 
 // Writes the RouteParams for decomposition `grid` (px*py*pz == world) and the plan header:
 // global domain, h = halo_factor x expected K-th neighbour radius of the whole cloud, the
 // send width (h plus rounding slack; the whole domain once h reaches its diagonal), id offset.
+// inner_factor > 0: the interior width h_i = min(h, inner_factor x that radius) for points
+// farther than w = h + h_i from the domain faces (0: one width).
 // splits: optional device array (route_split_count(grid) floats): count-balanced boxes.
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
-                             double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s);
+                             double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s,
+                             double inner_factor = 0.0);
+// Interior halo factor for K neighbours: the smallest f (steps of 0.05) for which a uniform
+// cloud's K-th neighbour distance exceeds f x the expected (K+1)-point radius with probability
+// <= 1e-12 (Poisson tail P[Poisson((K+1) f^3) <= K-1]); K=16 -> 1.55, K=1 -> 2.4, K=50 -> 1.35.
+double inner_halo_factor(int k);
 // Local meta of a rank's share: out = {lo[3], hi[3], n, 0} (doubles; +-inf box when n == 0).
 // words: kBBoxWords scratch words (kn/kernels.h). One all_gather of `out` gives the global
 // domain and the id offsets.

@@ -1141,9 +1141,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             if (gy1 < a.Y - 1) m = fminf(m, g.origin[1] + (gy1 + 1) * g.cell[1] - qy);
             if (gz0 > 0) m = fminf(m, qz - (g.origin[2] + gz0 * g.cell[2]));
             if (gz1 < a.Z - 1) m = fminf(m, g.origin[2] + (gz1 + 1) * g.cell[2] - qz);
-            m = fminf(m, complete_margin(a.complete, qx, 0));
-            m = fminf(m, complete_margin(a.complete, qy, 1));
-            m = fminf(m, complete_margin(a.complete, qz, 2));
+            m = fminf(m, complete_margin3(a.complete, qx, qy, qz));
             m -= g.eps;
         }
         const bool geo_ok = !prec_fail && (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
@@ -1509,9 +1507,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
             if (gy1 < a.Y - 1) m = fminf(m, g.origin[1] + (gy1 + 1) * g.cell[1] - qy);
             if (gz0 > 0) m = fminf(m, qz - (g.origin[2] + gz0 * g.cell[2]));
             if (gz1 < a.Z - 1) m = fminf(m, g.origin[2] + (gz1 + 1) * g.cell[2] - qz);
-            m = fminf(m, complete_margin(a.complete, qx, 0));
-            m = fminf(m, complete_margin(a.complete, qy, 1));
-            m = fminf(m, complete_margin(a.complete, qz, 2));
+            m = fminf(m, complete_margin3(a.complete, qx, qy, qz));
             m -= g.eps;
         }
         const bool geo_ok = (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
@@ -1733,8 +1729,7 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
         if (!sorted_now) compact();
         // certification against the rank's complete box (multi-GPU); needs the K-th distance
         const float dk = (cnt < k) ? INFINITY : thr;
-        const float mc = fminf(fminf(complete_margin(a.complete, qx, 0), complete_margin(a.complete, qy, 1)),
-                               complete_margin(a.complete, qz, 2)) - g.eps;
+        const float mc = complete_margin3(a.complete, qx, qy, qz) - g.eps;
         const bool cert = certified && (mc == INFINITY || (mc > 0.f && dk <= mc * mc));
         if (!cert && lane == 0) {
             const unsigned pos = atomicAdd(a.counters + 1, 1u);
@@ -1763,8 +1758,7 @@ __global__ void certify_rows_kernel(const float* __restrict__ pts, int rows, int
     if (r >= rows) return;
     const float dk = out_dist[(size_t)r * k + (k - 1)];  // INFINITY when fewer than K were found
     const float x = pts[3 * (size_t)r], y = pts[3 * (size_t)r + 1], z = pts[3 * (size_t)r + 2];
-    const float m = fminf(fminf(complete_margin(cb, x, 0), complete_margin(cb, y, 1)), complete_margin(cb, z, 2)) -
-                    geom->eps;
+    const float m = complete_margin3(cb, x, y, z) - geom->eps;
     const bool cert = (m == INFINITY) || (m > 0.f && dk <= m * m);
     if (!cert) {
         const unsigned pos = atomicAdd(counters + 1, 1u);

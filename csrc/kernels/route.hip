@@ -59,13 +59,17 @@ __device__ __forceinline__ int route_owner(const RouteParams& p, float x, float 
 __device__ __forceinline__ unsigned long long route_halo(const RouteParams& p, float x, float y, float z,
                                                          int owner) {
     unsigned long long m = 0;
+    // position-dependent width: the edge width in the wide zone near the domain faces
+    const float zp = fminf(fminf(fminf(x - p.lo[0], p.dom_hi[0] - x), fminf(y - p.lo[1], p.dom_hi[1] - y)),
+                           fminf(z - p.lo[2], p.dom_hi[2] - z));
+    const float h2 = zp <= p.wz ? p.h2 : p.hi2;
     for (int r = 0; r < p.world; ++r) {
         if (r == owner) continue;
         const float dx = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[r][0], x), 0.f), fmaxf(__fsub_rn(x, p.box_hi[r][0]), 0.f));
         const float dy = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[r][1], y), 0.f), fmaxf(__fsub_rn(y, p.box_hi[r][1]), 0.f));
         const float dz = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[r][2], z), 0.f), fmaxf(__fsub_rn(z, p.box_hi[r][2]), 0.f));
         const float d2 = __fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz));
-        if (d2 <= p.h2) m |= 1ull << r;
+        if (d2 <= h2) m |= 1ull << r;
     }
     return m;
 }
@@ -284,7 +288,7 @@ __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restr
 // One thread: global domain, halo width, rank boxes and id offset from the gathered metas.
 // Formulas follow SpatialDecomposition / DistributedKNearests (parallel/*.py) in double.
 __global__ void route_plan_kernel(const double* __restrict__ metas, int world, int rank, int gx, int gy, int gz,
-                                  int k, double halo_factor, const float* __restrict__ splits,
+                                  int k, double halo_factor, double inner_factor, const float* __restrict__ splits,
                                   RouteParams* __restrict__ p, double* __restrict__ hdr) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     double lo[3], hi[3];
@@ -315,6 +319,11 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     const double diag = sqrt(diag2);
     const bool full = h >= diag;
     const double hs = full ? 2.0 * diag + 1.0 : h * (1.0 + 1e-5) + 1e-5 * scale;
+    // interior width (position-dependent halo): h_i <= h, sent to points farther than w = h + h_i
+    // from the domain faces; the certification's zone limit keeps a rounding slack below w
+    const double hi_ = inner_factor > 0.0 ? fmin(h, inner_factor * rk) : h;
+    const double his = full ? hs : hi_ * (1.0 + 1e-5) + 1e-5 * scale;
+    const double wz = h + hi_;
     const int g[3] = {gx, gy, gz};
     for (int a = 0; a < 3; ++a) {
         const float l = (float)lo[a], u = (float)hi[a];
@@ -326,6 +335,10 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     p->world = world;
     const float hf = (float)hs;
     p->h2 = hf * hf;
+    const float hif = (float)his;
+    p->hi2 = hif * hif;
+    p->wz = (float)wz;
+    for (int a = 0; a < 3; ++a) p->dom_hi[a] = (float)hi[a];
     p->id_offset = (int)off;
     p->balanced = splits ? 1 : 0;
     const int nxs = gx + 1, nys = gx * (gy + 1), nzs = gx * gy * (gz + 1);
@@ -368,6 +381,10 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     hdr[10] = full ? 1.0 : 0.0;
     hdr[11] = diag;
     for (int i = 18; i < kPlanHdr; ++i) hdr[i] = 0.0;
+    hdr[18] = hi_;
+    hdr[19] = his;
+    hdr[20] = wz;
+    hdr[21] = wz - 1e-5 * scale;
 }
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
@@ -669,11 +686,12 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
 }
 
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
-                             double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s) {
+                             double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s,
+                             double inner_factor) {
     if (world < 1 || world > kRouteMaxWorld || grid[0] * grid[1] * grid[2] != world || rank < 0 || rank >= world)
         return hipErrorInvalidValue;
-    route_plan_kernel<<<1, 64, 0, s>>>(metas, world, rank, grid[0], grid[1], grid[2], k, halo_factor, splits, p,
-                                       hdr);
+    route_plan_kernel<<<1, 64, 0, s>>>(metas, world, rank, grid[0], grid[1], grid[2], k, halo_factor, inner_factor,
+                                       splits, p, hdr);
     return hipGetLastError();
 }
 
@@ -758,17 +776,36 @@ RankLocal rank_local(const double* hd, int rank, const int grid[3]) {
     RankLocal r{};
     const double h = hd[6], hs = hd[7];
     const bool full = hd[10] != 0.0;
+    // interior width (position-dependent halo); a header without one (0): the single width
+    const double hi_ = hd[18] > 0.0 ? hd[18] : h;
     const int c[3] = {rank % grid[0], (rank / grid[0]) % grid[1], rank / (grid[0] * grid[1])};
+    r.complete.wide = full ? 0.f : (float)(h - hi_);
+    r.complete.zlim = (float)hd[21];
     for (int a = 0; a < 3; ++a) {
         const double lo = hd[a], hi = hd[3 + a];
         const double blo = hd[12 + a], bhi = hd[15 + a];  // equal-volume or count-balanced box
-        r.complete.lo[a] = full || c[a] == 0 ? -INFINITY : (float)(blo - h);
-        r.complete.hi[a] = full || c[a] == grid[a] - 1 ? INFINITY : (float)(bhi + h);
+        r.complete.dlo[a] = (float)lo;
+        r.complete.dhi[a] = (float)hi;
+        r.complete.lo[a] = full || c[a] == 0 ? -INFINITY : (float)(blo - hi_);
+        r.complete.hi[a] = full || c[a] == grid[a] - 1 ? INFINITY : (float)(bhi + hi_);
         r.box[a] = std::max(lo, blo - hs);
         r.box[3 + a] = std::min(hi, bhi + hs);
         r.ext[a] = (float)(r.box[3 + a] - r.box[a]);
     }
     return r;
+}
+
+double inner_halo_factor(int k) {
+    k = std::max(1, k);
+    for (int i = 0; i <= 60; ++i) {
+        const double f = 1.0 + 0.05 * i;
+        const double lam = (double)(k + 1) * f * f * f;
+        // P[Poisson(lam) <= k - 1], summed in log space
+        double cdf = 0.0;
+        for (int j = 0; j < k; ++j) cdf += std::exp(-lam + j * std::log(lam) - std::lgamma(j + 1.0));
+        if (cdf <= 1e-12) return f;
+    }
+    return 4.0;
 }
 
 size_t split_hist_scratch_words(int n, const int grid[3], int stage) {

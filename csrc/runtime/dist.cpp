@@ -285,7 +285,7 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     auto b = [this](int s, hipStream_t st) { return stage_build(s, st); };
     auto q = [this](int s, hipStream_t st) { return stage_query(s, st); };
     auto r = [this](int s, hipStream_t st) { return stage_flag(s, st); };
-    if (pipe_.init(main_, side_, b, q, r) != hipSuccess) { fail("pipeline init"); return; }
+    if (pipe_.init(main_, side_, b, q, r, true) != hipSuccess) { fail("pipeline init"); return; }
     ok_ = true;
 }
 

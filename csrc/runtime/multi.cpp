@@ -326,8 +326,10 @@ kn_status solve_round(kn_multi* m, double hf, const int grid[3], bool balanced, 
     for (int i = 0; i < W; ++i) {
         RankState& R = m->r[i];
         KN_M(hipSetDevice(R.dev));
+        // position-dependent halo: the interior width scales with the round's halo factor
+        const double inner = kn::inner_halo_factor(k) * hf / std::max(1e-30, m->opt.halo_factor);
         KN_M(kn::launch_route_plan(R.metas.as<double>(), W, i, grid, k, hf, balanced ? R.splits.as<float>() : nullptr,
-                                   R.plan.as<kn::RouteParams>(), R.hdr.as<double>(), R.s));
+                                   R.plan.as<kn::RouteParams>(), R.hdr.as<double>(), R.s, inner));
         KN_M(kn::launch_route_count(R.pts.as<float>(), R.n, R.plan.as<kn::RouteParams>(), W, R.bc.as<int>(),
                                     R.totals.as<int>(), R.s));
         R.tot.assign((size_t)2 * W, 0);

@@ -20,10 +20,11 @@ void destroy(hipEvent_t& e) {
 }
 }  // namespace
 
-hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r) {
+hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r, bool capture_from_side) {
     reset();
     main_ = main;
     side_ = side;
+    capture_from_side_ = capture_from_side;
     b_ = std::move(b);
     q_ = std::move(q);
     r_ = std::move(r);
@@ -102,9 +103,11 @@ hipError_t Pipeline::unrolled(int s0, int U) {
     hipEvent_t* eq = cap_ev_.data() + 2;      // after Q(j)
     hipEvent_t* eb = cap_ev_.data() + 2 + U;  // after B(j+1)
     hipGraph_t g = nullptr;
-    KN_TRY(hipStreamBeginCapture(main_, hipStreamCaptureModeThreadLocal));
-    hipError_t e = hipEventRecord(fork, main_);
-    if (e == hipSuccess) e = hipStreamWaitEvent(side_, fork, 0);
+    // origin stream of the capture; the other one joins it through the fork event
+    hipStream_t origin = capture_from_side_ ? side_ : main_, other = capture_from_side_ ? main_ : side_;
+    KN_TRY(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
+    hipError_t e = hipEventRecord(fork, origin);
+    if (e == hipSuccess) e = hipStreamWaitEvent(other, fork, 0);
     for (int j = 0; j < U && e == hipSuccess; ++j) {
         const int s = (s0 + j) & 1;
         e = q_(s, main_);
@@ -117,9 +120,9 @@ hipError_t Pipeline::unrolled(int s0, int U) {
         if (e == hipSuccess) e = hipEventRecord(eb[j], side_);
         if (e == hipSuccess && j + 1 < U) e = hipStreamWaitEvent(main_, eb[j], 0);
     }
-    if (e == hipSuccess) e = hipEventRecord(join, side_);
-    if (e == hipSuccess) e = hipStreamWaitEvent(main_, join, 0);
-    const hipError_t ee = hipStreamEndCapture(main_, &g);
+    if (e == hipSuccess) e = hipEventRecord(join, other);
+    if (e == hipSuccess) e = hipStreamWaitEvent(origin, join, 0);
+    const hipError_t ee = hipStreamEndCapture(origin, &g);
     if (e != hipSuccess) {
         if (g) (void)hipGraphDestroy(g);
         return e;

@@ -36,7 +36,11 @@ public:
     Pipeline& operator=(const Pipeline&) = delete;
 
     // Stages (r may be empty). Streams stay owned by the caller. Graphs are captured lazily.
-    hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage());
+    // capture_from_side: unrolled captures start on the side stream (the main stream joins it):
+    // RCCL point-to-point calls in the build stage crash when captured on a JOINED stream
+    // (measured on MI355X, RCCL 2.26.6), so the stages with collectives must be on the origin.
+    hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage(),
+                    bool capture_from_side = false);
     bool ready() const { return main_ != nullptr; }
     // Enqueue `iters` resident-mode steps; unroll >= 2 (even): whole groups of `unroll` steps go
     // through one unrolled graph, the rest through per-step graphs. keep_primed = false: the call
@@ -71,6 +75,7 @@ private:
     hipError_t enqueue_epilogue(int set);
 
     hipStream_t main_ = nullptr, side_ = nullptr;
+    bool capture_from_side_ = false;
     Stage b_, q_, r_;
     hipGraphExec_t gB_[2] = {nullptr, nullptr}, gQ_[2] = {nullptr, nullptr}, gR_[2] = {nullptr, nullptr};
     hipGraphExec_t gU_[2] = {nullptr, nullptr};

@@ -40,6 +40,20 @@ void check_points(const torch::Tensor& p, bool cuda) {
     }
 }
 
+// Complete box from its Python list: [lo x3, hi x3] (one halo width) or + [wide, zlim, domain lo
+// x3, domain hi x3] (position-dependent halo, kn::CompleteBox)
+kn::CompleteBox complete_box(const std::vector<double>& c) {
+    TORCH_CHECK(c.size() == 6 || c.size() == 14, "complete must have 6 or 14 entries");
+    kn::CompleteBox b{};
+    for (int a = 0; a < 3; ++a) { b.lo[a] = (float)c[a]; b.hi[a] = (float)c[3 + a]; }
+    if (c.size() == 14) {
+        b.wide = (float)c[6];
+        b.zlim = (float)c[7];
+        for (int a = 0; a < 3; ++a) { b.dlo[a] = (float)c[8 + a]; b.dhi[a] = (float)c[11 + a]; }
+    }
+    return b;
+}
+
 // geom tensor: 16 x int32 (64 bytes) holding a kn::GridGeom
 static_assert(sizeof(kn::GridGeom) <= 64, "GridGeom must fit in 64 bytes");
 
@@ -112,7 +126,8 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
     TORCH_CHECK(geom.is_cuda() && geom.numel() == 16, "geom must be a 16-int GPU tensor");
-    TORCH_CHECK(dims.size() == 3 && tile.size() == 3 && complete.size() == 6, "bad dims/tile/complete");
+    TORCH_CHECK(dims.size() == 3 && tile.size() == 3 && (complete.size() == 6 || complete.size() == 14),
+                "bad dims/tile/complete");
     TORCH_CHECK(k >= 1 && k <= 128, "k must be in [1, 128]");
     TORCH_CHECK(cell_start.numel() == dims[0] * dims[1] * dims[2] + 1, "cell_start size does not match dims");
     const int n = (int)sorted.size(0);
@@ -151,7 +166,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                     "row_of must be an int32 GPU tensor with >= N entries");
         q.row_of = reinterpret_cast<const unsigned*>(row_of->data_ptr<int>());
     }
-    for (int a = 0; a < 3; ++a) { q.complete.lo[a] = (float)complete[a]; q.complete.hi[a] = (float)complete[3 + a]; }
+    q.complete = complete_box(complete);
     q.out_idx = reinterpret_cast<unsigned*>(out_idx.data_ptr<int>());
     q.out_dist = with_dist ? out_dist.data_ptr<float>() : nullptr;
     q.fallback_list = reinterpret_cast<unsigned*>(fallback.data_ptr<int>());
@@ -297,7 +312,8 @@ torch::Tensor to_stored_space(torch::Tensor out_orig, torch::Tensor perm) {
 // ---- multi-GPU routing (csrc/kernels/route.hip) -------------------------------------
 kn::RouteParams route_params(const std::vector<double>& lo, const std::vector<double>& hi,
                              const std::vector<int64_t>& grid, const std::vector<double>& boxes, double h,
-                             const c10::optional<std::vector<double>>& splits = c10::nullopt) {
+                             const c10::optional<std::vector<double>>& splits = c10::nullopt,
+                             double h_inner = -1.0, double wz = INFINITY) {
     TORCH_CHECK(lo.size() == 3 && hi.size() == 3 && grid.size() == 3, "lo/hi/grid must have 3 entries");
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world >= 1 && world <= kn::kRouteMaxWorld, "world size must be in [1, 64]");
@@ -314,6 +330,11 @@ kn::RouteParams route_params(const std::vector<double>& lo, const std::vector<do
     p.world = (int)world;
     const float hf = (float)h;
     p.h2 = hf * hf;
+    // position-dependent halo (h_inner < 0: one width)
+    const float hif = (float)(h_inner < 0.0 ? h : h_inner);
+    p.hi2 = hif * hif;
+    p.wz = (float)wz;
+    for (int a = 0; a < 3; ++a) p.dom_hi[a] = (float)hi[a];
     for (int r = 0; r < world; ++r)
         for (int a = 0; a < 3; ++a) {
             p.box_lo[r][a] = (float)boxes[6 * r + a];
@@ -383,20 +404,21 @@ torch::Tensor route_scatter_impl(const torch::Tensor& points, const c10::optiona
 // -> (scanned block counts, totals (world, 2) = owned / halo rows per destination)
 std::vector<torch::Tensor> route_count(torch::Tensor points, std::vector<double> lo, std::vector<double> hi,
                                        std::vector<int64_t> grid, std::vector<double> boxes, double h,
-                                       c10::optional<std::vector<double>> splits) {
+                                       c10::optional<std::vector<double>> splits, double h_inner, double wz) {
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
-    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h, splits);
+    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h, splits, h_inner, wz);
     auto dp = upload_params(p, points.device());
     return route_count_impl(points, params_ptr(dp), p.world);
 }
 
 torch::Tensor route_scatter(torch::Tensor points, torch::Tensor ids, std::vector<double> lo, std::vector<double> hi,
                             std::vector<int64_t> grid, std::vector<double> boxes, double h, torch::Tensor block_offsets,
-                            torch::Tensor totals, int64_t rows, c10::optional<std::vector<double>> splits) {
+                            torch::Tensor totals, int64_t rows, c10::optional<std::vector<double>> splits,
+                            double h_inner, double wz) {
     check_points(points, true);
     const c10::DeviceGuard guard(points.device());
-    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h, splits);
+    const kn::RouteParams p = route_params(lo, hi, grid, boxes, h, splits, h_inner, wz);
     auto dp = upload_params(p, points.device());
     return route_scatter_impl(points, ids, params_ptr(dp), p.world, block_offsets, totals, rows);
 }
@@ -413,7 +435,7 @@ const float* splits_ptr(const c10::optional<torch::Tensor>& splits, const std::v
 // Device-side plan from the all-gathered metas (world x 8 float64, on device): no host sync.
 // -> (plan (uint8 RouteParams on device), header (16,) float64 on device, see kn::kPlanHdr)
 std::vector<torch::Tensor> route_plan(torch::Tensor metas, int64_t rank, std::vector<int64_t> grid, int64_t k,
-                                      double halo_factor, c10::optional<torch::Tensor> splits) {
+                                      double halo_factor, c10::optional<torch::Tensor> splits, double inner_factor) {
     TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
                     metas.numel() % 8 == 0,
                 "metas must be a contiguous (world*8,) float64 GPU tensor");
@@ -426,7 +448,7 @@ std::vector<torch::Tensor> route_plan(torch::Tensor metas, int64_t rank, std::ve
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor,
                                        splits_ptr(splits, grid), reinterpret_cast<kn::RouteParams*>(plan.data_ptr<uint8_t>()),
-                                       hdr.data_ptr<double>(), s));
+                                       hdr.data_ptr<double>(), s, inner_factor));
     return {plan, hdr};
 }
 
@@ -458,7 +480,7 @@ torch::Tensor route_scatter_dev(torch::Tensor points, c10::optional<torch::Tenso
 // -> (plan, sync, scanned block counts, send (cap, 4))
 std::vector<torch::Tensor> route_begin(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor metas,
                                        int64_t rank, std::vector<int64_t> grid, int64_t k, double halo_factor,
-                                       int64_t cap, c10::optional<torch::Tensor> splits) {
+                                       int64_t cap, c10::optional<torch::Tensor> splits, double inner_factor) {
     check_points(points, true);
     TORCH_CHECK(cap >= 0 && cap < INT32_MAX, "cap out of range");
     TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
@@ -486,7 +508,7 @@ std::vector<torch::Tensor> route_begin(torch::Tensor points, c10::optional<torch
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor,
                                        splits_ptr(splits, grid), pp,
-                                       reinterpret_cast<double*>(sync.data_ptr<int>()), s));
+                                       reinterpret_cast<double*>(sync.data_ptr<int>()), s, inner_factor));
     KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, pp, world, bc.data_ptr<int>(), totals, s));
     KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, world, bc.data_ptr<int>(), totals,
                                           reinterpret_cast<float4*>(send.data_ptr<float>()), (int)cap, (int)rank, s));
@@ -1146,19 +1168,18 @@ std::vector<torch::Tensor> brute_knn(torch::Tensor points, int64_t k, int64_t th
 std::vector<torch::Tensor> grid_knn_cpu(torch::Tensor points, int64_t n_queries, int64_t k, double ppc,
                                         std::vector<double> complete, int64_t threads) {
     check_points(points, false);
-    TORCH_CHECK(complete.size() == 6, "complete must have 6 entries");
+    const kn::CompleteBox cb = complete_box(complete);  // 6 or 14 entries
     const int n = (int)points.size(0);
     TORCH_CHECK(n_queries >= 0 && n_queries <= n, "n_queries out of range");
     auto idx = torch::empty({n_queries, k}, torch::kInt32);
     auto d2 = torch::empty({n_queries, k}, torch::kFloat32);
-    float lo[3], hi[3];
-    for (int a = 0; a < 3; ++a) { lo[a] = (float)complete[a]; hi[a] = (float)complete[3 + a]; }
+    const float ext[8] = {cb.wide, cb.zlim, cb.dlo[0], cb.dlo[1], cb.dlo[2], cb.dhi[0], cb.dhi[1], cb.dhi[2]};
     std::vector<uint32_t> unc;
     {
         py::gil_scoped_release nogil;
-        knh::grid_knn_cpu(points.data_ptr<float>(), n, (int)n_queries, (int)k, (float)ppc, lo, hi,
+        knh::grid_knn_cpu(points.data_ptr<float>(), n, (int)n_queries, (int)k, (float)ppc, cb.lo, cb.hi,
                           reinterpret_cast<uint32_t*>(idx.data_ptr<int>()), d2.data_ptr<float>(), &unc,
-                          (int)threads);
+                          (int)threads, ext);
     }
     auto u = torch::empty({(int64_t)unc.size()}, torch::kInt32);
     for (size_t i = 0; i < unc.size(); ++i) u[i] = (int)unc[i];
@@ -1365,10 +1386,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("local_meta", &local_meta, "multi-GPU: {lo[3], hi[3], n, 0} of the local points (float64, on device)");
     m.def("route_count", &route_count, "multi-GPU routing: per-destination (owned, halo) row counts",
           py::arg("points"), py::arg("lo"), py::arg("hi"), py::arg("grid"), py::arg("boxes"), py::arg("h"),
-          py::arg("splits") = py::none());
+          py::arg("splits") = py::none(), py::arg("h_inner") = -1.0, py::arg("wz") = INFINITY);
     m.def("route_plan", &route_plan, "multi-GPU: device-side routing plan from the gathered metas (no host sync)",
           py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"), py::arg("halo_factor"),
-          py::arg("splits") = py::none());
+          py::arg("splits") = py::none(), py::arg("inner_factor") = 0.0);
+    m.def("inner_halo_factor", &kn::inner_halo_factor,
+          "multi-GPU: interior halo width in expected (K+1)-point radii (Poisson tail <= 1e-12)", py::arg("k"));
     m.def("route_count_dev", &route_count_dev, "multi-GPU: route_count with the device plan");
     m.def("route_scatter_dev", &route_scatter_dev, "multi-GPU: route_scatter with the device plan (ids=None: offset + i)",
           py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("world"), py::arg("block_offsets"),
@@ -1376,7 +1399,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("route_begin", &route_begin,
           "multi-GPU: plan + counts + scatter (self-last layout, cap rows) enqueued in one call",
           py::arg("points"), py::arg("ids"), py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"),
-          py::arg("halo_factor"), py::arg("cap"), py::arg("splits") = py::none());
+          py::arg("halo_factor"), py::arg("cap"), py::arg("splits") = py::none(), py::arg("inner_factor") = 0.0);
     m.def("query_external", &query_external,
           "multi-GPU query forwarding: exact K nearest of external points among a local grid");
     m.def("steady_flag", &steady_flag, "multi-GPU: on-device check of a sync-free steady-state step");
@@ -1403,7 +1426,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer",
           py::arg("points"), py::arg("ids"), py::arg("lo"), py::arg("hi"), py::arg("grid"), py::arg("boxes"),
-          py::arg("h"), py::arg("block_offsets"), py::arg("totals"), py::arg("rows"), py::arg("splits") = py::none());
+          py::arg("h"), py::arg("block_offsets"), py::arg("totals"), py::arg("rows"), py::arg("splits") = py::none(),
+          py::arg("h_inner") = -1.0, py::arg("wz") = INFINITY);
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     m.def("rccl_unique_id", &rccl_unique_id, "multi-GPU: a new RCCL unique id (128 bytes) for RankComm");
     py::class_<PyRankComm, std::shared_ptr<PyRankComm>>(m, "RankComm", "one rank's RCCL communicator (collective init)")

@@ -63,13 +63,22 @@ def halo_send_width(h: float, lo, hi) -> float:
     return h * (1.0 + 1e-5) + 1e-5 * scale
 
 
-def route_rows_torch(dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor, h_send: float):
+def route_rows_torch(dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor, h_send: float,
+                     h_inner: Optional[float] = None, wz: float = INF):
     """Reference router (any device): send rows [owned | halo] per destination + (world, 2) counts.
-    Same decisions and same stable order as the native router (route.hip)."""
+    Same decisions and same stable order as the native router (route.hip). Position-dependent
+    halo: points farther than ``wz`` from every domain face use the interior width ``h_inner``."""
     owner = dec.owner(points)
     rows = _pack(points, ids)
-    hf = torch.tensor(h_send, dtype=torch.float32, device=points.device)
+    dev = points.device
+    hf = torch.tensor(h_send, dtype=torch.float32, device=dev)
     h2 = hf * hf  # fp32 square, as the native router computes it
+    if h_inner is not None and h_inner != h_send:
+        hif = torch.tensor(h_inner, dtype=torch.float32, device=dev)
+        lo_t = torch.tensor(dec.lo, dtype=torch.float32, device=dev)
+        hi_t = torch.tensor(dec.hi, dtype=torch.float32, device=dev)
+        zp = torch.minimum((points - lo_t).min(1).values, (hi_t - points).min(1).values)
+        h2 = torch.where(zp <= torch.tensor(wz, dtype=torch.float32, device=dev), h2, hif * hif)
     parts, counts = [], []
     for d in range(dec.world):
         own_m = owner == d
@@ -118,7 +127,7 @@ class DistributedKNearests:
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
                  transport=None, device_plan: bool = True, timeout_s: Optional[float] = None,
                  balance: str = "count", adaptive: bool = True, native_pipeline: Optional[bool] = None,
-                 force_collectives: Optional[bool] = None):
+                 force_collectives: Optional[bool] = None, inner_halo: Optional[float] = None):
         self.k = int(k)
         # occupancy-adaptive local grids (GPU): a rank whose share is clustered re-bins finer, as
         # the 1-GPU engine does; steady steps reuse the validated step's grid (no extra sync)
@@ -130,6 +139,12 @@ class DistributedKNearests:
         self.balance = balance
         self.group = group
         self.halo_factor = float(halo_factor)
+        # Position-dependent halo (round 4): points farther than w = h_e + h_i from every face of
+        # the global domain are routed with the interior width h_i = min(h_e, inner x radius) --
+        # an interior query's K-th ball is whole, while a query near a domain face sees a truncated
+        # one (radius x 4^(1/3) at an edge), which the edge width h_e = halo_factor x radius covers.
+        # None: the K-dependent Poisson-tail factor (C.inner_halo_factor: K=16 -> 1.55); 0: one width.
+        self.inner_halo = inner_halo
         self.points_per_cell = float(points_per_cell)
         self.deterministic = deterministic
         self.max_rounds = max_rounds
@@ -216,6 +231,12 @@ class DistributedKNearests:
         self._pending = collections.deque()
 
     # ------------------------------------------------------------------ helpers ------
+    def _inner_factor(self) -> float:
+        """Interior halo factor of the current step (x the adaptive boost), 0 = one width."""
+        if self.inner_halo is not None:
+            return float(self.inner_halo) * self.halo_boost
+        return float(ops.load().inner_halo_factor(self.k)) * self.halo_boost
+
     def _a2a(self, send: torch.Tensor, send_counts: list, recv_counts: list) -> torch.Tensor:
         out = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
         self.comm.all_to_all_single(out, send, recv_counts, send_counts)
@@ -263,15 +284,18 @@ class DistributedKNearests:
     def _use_native(self, points: torch.Tensor) -> bool:
         return points.is_cuda if self.native_route is None else bool(self.native_route)
 
-    def exchange(self, dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor, h_send: float):
-        """Route points to owner + halo ranks in one all-to-all.
+    def exchange(self, dec: SpatialDecomposition, points: torch.Tensor, ids: torch.Tensor, h_send: float,
+                 h_inner: Optional[float] = None, wz: float = INF):
+        """Route points to owner + halo ranks in one all-to-all (points farther than ``wz`` from
+        the domain faces with the interior send width ``h_inner``).
         Returns (points (n,3) owned-first, global ids (n,), n_owned)."""
         ids = ids.to(torch.int32).contiguous()
+        hin = float(h_send if h_inner is None else h_inner)
         if self._use_native(points):
             C = ops.load()
             lo, hi = list(dec.lo), list(dec.hi)
             boxes = dec.boxes()
-            bc, totals = C.route_count(points, lo, hi, list(dec.grid), boxes, float(h_send), dec.splits)
+            bc, totals = C.route_count(points, lo, hi, list(dec.grid), boxes, float(h_send), dec.splits, hin, float(wz))
             recv_tot = torch.empty_like(totals)
             self.comm.all_to_all_single(recv_tot, totals)
             both = torch.cat([totals, recv_tot]).cpu()  # host sync 2 (send + receive splits)
@@ -279,11 +303,11 @@ class DistributedKNearests:
             recv_own = [int(a) for a, _ in both[self.world:].tolist()]
             recv_halo = [int(b) for _, b in both[self.world:].tolist()]
             send = C.route_scatter(points, ids, lo, hi, list(dec.grid), boxes, float(h_send), bc, totals,
-                                   sum(send_counts), dec.splits)
+                                   sum(send_counts), dec.splits, hin, float(wz))
             recv = self._a2a(send, send_counts, [a + b for a, b in zip(recv_own, recv_halo)])
             pts, gids = C.route_unpack(recv, recv_own, recv_halo)
             return pts, gids, sum(recv_own)
-        send, totals = route_rows_torch(dec, points, ids, h_send)
+        send, totals = route_rows_torch(dec, points, ids, h_send, hin, wz)
         recv_tot = torch.empty_like(totals)
         self.comm.all_to_all_single(recv_tot, totals)
         st, rt = totals.tolist(), recv_tot.tolist()
@@ -345,8 +369,9 @@ class DistributedKNearests:
             rounds += 1
             while True:
                 cap = max(self._send_cap, int(src_pts.size(0) * (1.0 + self.send_headroom)) + 1024)
+                inner = self._inner_factor() * hf / (self.halo_factor * self.halo_boost)
                 plan, sync, bc, send = C.route_begin(src_pts, src_ids, metas, rank, list(grid), self.k, hf, cap,
-                                                     splits)
+                                                     splits, inner)
                 totals = sync[nh:nh + 2 * world]
                 if spec is not None:
                     # one all-gather of {meta, counts}; the rows this rank receives are column
@@ -858,7 +883,12 @@ class DistributedKNearests:
             dec = SpatialDecomposition(self.world, lo, hi, dec.grid, sp.tolist())
         n_total = sum(counts)
         vol = max(1e-30, (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]))
-        h = self.halo_factor * ops.expected_kth_radius(n_total, self.k, vol)
+        rk = ops.expected_kth_radius(n_total, self.k, vol)
+        h = self.halo_factor * rk
+        # position-dependent halo: interior width h_i <= h (route.hip route_plan_kernel's rule)
+        inner = self._inner_factor() / self.halo_boost
+        h_in = min(h, inner * rk) if inner > 0.0 else h
+        scale = max(max(abs(v) for v in lo), max(abs(v) for v in hi), max(hi[a] - lo[a] for a in range(3)))
         diag = math.sqrt(sum((hi[a] - lo[a]) ** 2 for a in range(3)))
         blo, bhi = dec.rank_box(self.rank)
         rounds = 0
@@ -867,10 +897,15 @@ class DistributedKNearests:
             rounds += 1
             full = h >= diag
             hs = halo_send_width(h, lo, hi) if not full else 2.0 * diag + 1.0
-            pts, gids, n_owned = self.exchange(dec, src_pts, src_ids, hs)
+            his = halo_send_width(h_in, lo, hi) if not full else hs
+            wz = h + h_in
+            pts, gids, n_owned = self.exchange(dec, src_pts, src_ids, hs, his, wz)
             if rounds == 1:
                 own_pts, own_ids = pts[:n_owned], gids[:n_owned]
-            complete = dec.complete_box(self.rank, h) if not full else [-INF] * 3 + [INF] * 3
+            if full:
+                complete = [-INF] * 3 + [INF] * 3
+            else:
+                complete = (dec.complete_box(self.rank, h_in) + [h - h_in, wz - 1e-5 * scale] + list(lo) + list(hi))
             box = [max(lo[a], blo[a] - hs) for a in range(3)] + [min(hi[a], bhi[a] + hs) for a in range(3)]
             idx, d2, n_unc = self.local_solve(pts, gids, n_owned, complete, box)
             flag = n_unc.to(dev) if dev.type != "cpu" else n_unc
@@ -878,6 +913,7 @@ class DistributedKNearests:
             if int(flag.item()) == 0 or full or rounds >= self.max_rounds:  # host sync 3
                 break
             h *= 2.0
+            h_in *= 2.0
             # owned points are in place: re-route them (owner = this rank) for the wider halo
             src_pts, src_ids = own_pts, own_ids
         stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,

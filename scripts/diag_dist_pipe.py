@@ -16,6 +16,14 @@ from cuda_knearests_amd.utils import uniform_cloud
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 900000
+modes = [m == "1" for m in sys.argv[3].split(",")] if len(sys.argv) > 3 else [False, True]
+verbose = os.environ.get("KN_DIAG_VERBOSE") == "1"
+
+
+def say(*a):
+    if verbose:
+        print(*a, flush=True)
+
 for k_, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29543"), ("RANK", "0"), ("WORLD_SIZE", "1")):
     os.environ.setdefault(k_, v)
 dev = torch.device("cuda", 0)
@@ -42,15 +50,23 @@ pts_perm = pts[perm].contiguous()
 ref = reference(pts)
 ref_perm = reference(pts_perm)
 ok_all = True
-for force in (False, True):
+for force in modes:
     dk = DistributedKNearests(k=16, force_collectives=force)
     full = dk.solve(pts)
     r_full = same(full, ref)
+    say("full step done")
+    r0 = dk.solve(pts, async_=True)
+    say("first pipelined step enqueued")
+    ok0 = r0.valid()
+    say("first pipelined step valid", ok0, same(r0, ref))
     res = [dk.solve(pts, async_=True) for _ in range(steps)]
+    say("async steps enqueued")
     piped = bool(res[-1].stats.get("pipelined"))
     valid = all(r.valid() for r in res)
     rows = same(res[-1], ref)
+    say("async steps checked")
     batch = dk.run_steps(pts, 20, resident=True)
+    say("batch done")
     b_ok = batch.valid() and same(batch, ref)
     batch2 = dk.run_steps(pts, 7)  # after a primed call, an odd count without priming
     b2_ok = batch2.valid() and same(batch2, ref)
