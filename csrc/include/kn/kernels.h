@@ -156,6 +156,10 @@ struct QueryBuffers {
     int exact_grid;           // workgroups of the fallback launch; 0 = default (sized for long
                               // lists). The engine passes a small grid when the previous solve's
                               // list was short (the launch then costs ~3 us less).
+    // 0: the tile kernel then the exact finish of its fallback list; 1: the tile kernel only;
+    // 2: the exact finish only (after a mode-1 launch on the same counters / list: pipelined
+    // steps run it on the build stream, off the query stream's critical path)
+    int exact_mode;
 };
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);

@@ -1855,12 +1855,14 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     constexpr int M = KN_TOPK_MARGIN;
     const int X = q.dims[0], Y = q.dims[1], Z = q.dims[2];
     hipError_t e = hipSuccess;
-    if (!q.counters_zeroed && (e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s)) != hipSuccess)
+    if (q.exact_mode != 2 && !q.counters_zeroed &&
+        (e = hipMemsetAsync(q.counters, 0, kNumCounters * sizeof(unsigned), s)) != hipSuccess)
         return e;
     if (q.n == 0 || q.n_queries <= q.q_lo) return hipSuccess;
     // the register-resident tile path covers K <= 64; larger K use the exact ring walk
     const bool tiles = q.use_tiles && KT <= 64;
-    if (tiles) {
+    if (!tiles && q.exact_mode == 2) return hipSuccess;  // the exact kernel served every query already
+    if (tiles && q.exact_mode != 2) {
         TileArgs a;
         a.sorted = q.sorted; a.cell_start = q.cell_start; a.geom = q.geom; a.n = q.n;
         a.X = X; a.Y = Y; a.Z = Z; a.k = q.k; a.n_queries = q.n_queries; a.q_lo = q.q_lo; a.id_map = q.id_map;
@@ -1934,6 +1936,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         }
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (q.exact_mode == 1) return hipSuccess;
     }
     ExactArgs b;
     b.sorted = q.sorted; b.cell_start = q.cell_start; b.geom = q.geom; b.n = q.n;

@@ -393,27 +393,42 @@ hipError_t DistPipeline::stage_query(int s, hipStream_t st) {
             // the complete-box certification the grid kernels do inline
             KN_TRY(launch_certify_rows(S.lpts, n_owned_, p_.k, S.d2, complete_, S.geom, S.counters, S.uncert, st));
         }
-    } else {
-        QueryBuffers q = qproto_;
-        q.sorted = S.sorted;
-        q.cell_start = S.cell_start;
-        q.geom = S.geom;
-        q.row_of = S.perm;
-        q.out_idx = reinterpret_cast<unsigned*>(S.idx);
-        q.out_dist = S.d2;
-        q.fallback_list = S.fallback;
-        q.counters = S.counters;
-        q.uncert_list = S.uncert;
-        KN_TRY(launch_query(q, st));
+        return hipSuccess;
     }
-    // this step's check: the share's bbox and count (routing partials) and every send count as
-    // planned, and no uncertified row
-    return launch_steady_flag_partials(S.partials, p_.n, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
-                                       S.counters, S.flag, st);
+    // the tile kernel only: the exact finish of its fallback list opens the epilogue on the side
+    // stream, so the next step's queries follow this one's directly
+    QueryBuffers q = query_proto(s);
+    q.exact_mode = 1;
+    return launch_query(q, st);
 }
 
+QueryBuffers DistPipeline::query_proto(int s) const {
+    const Set& S = set_[s];
+    QueryBuffers q = qproto_;
+    q.sorted = S.sorted;
+    q.cell_start = S.cell_start;
+    q.geom = S.geom;
+    q.row_of = S.perm;
+    q.out_idx = reinterpret_cast<unsigned*>(S.idx);
+    q.out_dist = S.d2;
+    q.fallback_list = S.fallback;
+    q.counters = S.counters;
+    q.uncert_list = S.uncert;
+    return q;
+}
+
+// Epilogue of step s (side stream, after its queries): the exact finish of the fallback list,
+// this step's check (the share's bbox and count from the routing partials and every send count
+// as planned, no uncertified row), its MAX all-reduce and the sticky host flag.
 hipError_t DistPipeline::stage_flag(int s, hipStream_t st) {
     Set& S = set_[s];
+    if (!p_.use_tree) {
+        QueryBuffers q = query_proto(s);
+        q.exact_mode = 2;
+        KN_TRY(launch_query(q, st));
+    }
+    KN_TRY(launch_steady_flag_partials(S.partials, p_.n, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
+                                       S.counters, S.flag, st));
     if (ncclAllReduce(S.flag, S.flag, 1, ncclInt32, ncclMax, as_comm(comm_), st) != ncclSuccess) return hipErrorUnknown;
     return launch_flag_sink(S.flag, sticky_, host_flag_dev_, st);
 }

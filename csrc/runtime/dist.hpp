@@ -7,10 +7,11 @@
 //   B(i)  side stream   route this rank's share (owner + halo destinations, its own rows placed
 //                       straight into the local set) -> grouped ncclSend / ncclRecv of the rows
 //                       that change rank -> unpack -> local grid build (global ids in the points)
-//   Q(i)  main stream   queries of the owned points (grid or Morton-leaf tree path, complete-box
-//                       certification) -> the step's flag (share / counts as planned, all rows
-//                       certified)
-//   R(i)  side stream   ncclAllReduce(MAX) of the flag -> sticky flag in pinned host memory
+//   Q(i)  main stream   queries of the owned points (the tile kernel, or the Morton-leaf tree
+//                       path + complete-box certification)
+//   R(i)  side stream   exact finish of the tile kernel's fallback list -> the step's flag (share /
+//                       counts as planned, all rows certified) -> ncclAllReduce(MAX) -> sticky flag
+//                       in pinned host memory
 // B(i+1), with its all-to-all, runs while Q(i) fills the chip; both RCCL calls live on the side
 // stream, in the same order on every rank (one communicator, no cross-stream collectives).
 #pragma once
@@ -91,7 +92,8 @@ public:
     kn_status sync();
     int last_set() const { return pipe_.last_set(); }
     // One serial step on the main stream with events between its phases (ms): route, exchange,
-    // unpack + build, query (+ certification + flag), flag all-reduce. Unprimes the pipeline.
+    // unpack + build, query (tile kernel / tree + certification), epilogue (exact finish, flag,
+    // all-reduce). Unprimes the pipeline.
     kn_status profile(float ms[5]);
 
     int rows() const { return rows_; }
@@ -116,7 +118,8 @@ private:
     };
     hipError_t stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks = nullptr);
     hipError_t stage_query(int s, hipStream_t st);
-    hipError_t stage_flag(int s, hipStream_t st);
+    hipError_t stage_flag(int s, hipStream_t st);  // epilogue: exact finish, flag, all-reduce
+    QueryBuffers query_proto(int s) const;
     hipError_t exchange(int s, hipStream_t st);
     bool fail(const std::string& m) { err_ = m; ok_ = false; return false; }
 

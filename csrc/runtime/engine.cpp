@@ -432,6 +432,8 @@ kn_status Engine::ensure_outputs() {
     if (cfg_.with_distances && !out_dist_ &&
         (st = check(dmalloc(&out_dist_, nk * sizeof(float)), "hipMalloc(dist)")) != KN_OK)
         return st;
+    set_[live_].out_idx = out_idx_;
+    set_[live_].out_dist = out_dist_;
     if (use_tree_ && (st = ensure_tree()) != KN_OK) return st;
     return KN_OK;
 }
@@ -501,10 +503,12 @@ kn_status Engine::set_k(int k) {
         ap_.lds_capacity = lds_capacity_for(staged_points(ap_, ppc));
         ap_.lds_bytes = query_lds_bytes(ap_.tile, ap_.halo, ap_.lds_capacity, ap_.xsub);
     }
-    for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_})
-        if (*q) { dfree(*q); *q = nullptr; }
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     drop_pipeline(true);  // the grid stays: the next solve() queries it with the new K
+    for (void** q : {(void**)&out_idx_, (void**)&out_dist_, (void**)&knn_stored_})
+        if (*q) { dfree(*q); *q = nullptr; }
+    set_[0].out_idx = nullptr;
+    set_[0].out_dist = nullptr;
     solved_ = stored_valid_ = false;
     return KN_OK;
 }
@@ -548,7 +552,7 @@ static int pipe_prio() {
 
 Engine::GridSet Engine::members() const {
     return GridSet{points_, bbox_, geom_, cell_count_, cell_scan_, block_sums_, cell_start_, cell_rank_, bin_tmp_,
-                   sorted_, perm_, fallback_, counters_, occ_, tree_ws_, tree_nodes_};
+                   sorted_, perm_, fallback_, counters_, occ_, tree_ws_, tree_nodes_, out_idx_, out_dist_};
 }
 
 void Engine::view_set(int s) {
@@ -557,6 +561,7 @@ void Engine::view_set(int s) {
     block_sums_ = g.block_sums; cell_start_ = g.cell_start; cell_rank_ = g.cell_rank; bin_tmp_ = g.bin_tmp;
     sorted_ = g.sorted; perm_ = g.perm; fallback_ = g.fallback; counters_ = g.counters; occ_ = g.occ;
     tree_ws_ = g.tree_ws; tree_nodes_ = g.tree_nodes;
+    out_idx_ = g.out_idx; out_dist_ = g.out_dist;
     live_ = s;
 }
 
@@ -577,14 +582,18 @@ void Engine::drop_pipeline(bool keep_grid) {
         if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
         if (keep_grid && arena2_ && arena_used_)
             (void)hipMemcpyAsync(arena_, arena2_, arena_used_, hipMemcpyDeviceToDevice, stream_);
-        // the live tree buffers (same sizes in both sets) stay with the live view
+        // the live tree and result buffers (same sizes in both sets) stay with the live view
         std::swap(set_[0].tree_ws, set_[1].tree_ws);
         std::swap(set_[0].tree_nodes, set_[1].tree_nodes);
+        std::swap(set_[0].out_idx, set_[1].out_idx);
+        std::swap(set_[0].out_dist, set_[1].out_dist);
         view_set(0);
     }
     if (arena2_) { dfree(arena2_); arena2_ = nullptr; }  // dfree waits for stream_ (the copy)
     if (set_[1].tree_ws) dfree(set_[1].tree_ws);
     if (set_[1].tree_nodes) dfree(set_[1].tree_nodes);
+    if (set_[1].out_idx) dfree(set_[1].out_idx);
+    if (set_[1].out_dist) dfree(set_[1].out_dist);
     set_[1] = GridSet{};
     set_[0] = members();
     other_stale_ = true;
@@ -609,8 +618,29 @@ kn_status Engine::stage_query(int s, hipStream_t st) {
     hipStream_t ks = stream_;
     view_set(s);
     stream_ = st;
-    kn_status r = use_tree_ ? tree_query_async() : query_async(true);
+    kn_status r;
+    if (use_tree_) {
+        r = tree_query_async();
+    } else {
+        // the tile kernel only: its fallback list's exact finish is the epilogue on the build
+        // stream, so the next step's queries follow this one's without waiting for it
+        QueryBuffers q = query_buffers();
+        q.counters_zeroed = 1;
+        q.exact_mode = 1;
+        r = check(launch_query(q, stream_), "query");
+    }
     stream_ = ks;
+    view_set(keep);
+    return r;
+}
+
+kn_status Engine::stage_exact(int s, hipStream_t st) {
+    const int keep = live_;
+    view_set(s);
+    QueryBuffers q = query_buffers();
+    q.counters_zeroed = 1;
+    q.exact_mode = 2;
+    const kn_status r = check(launch_query(q, st), "exact finish");
     view_set(keep);
     return r;
 }
@@ -651,6 +681,16 @@ kn_status Engine::ensure_pipeline() {
         }
         other_stale_ = true;
     }
+    {
+        // the other set's results (per-set outputs: the exact finish of step i runs while step
+        // i+1 queries)
+        GridSet& g = set_[live_ ^ 1];
+        const size_t nk = std::max<size_t>(1, (size_t)n_ * cfg_.k);
+        if (!g.out_idx && (st = check(dmalloc(&g.out_idx, nk * sizeof(unsigned)), "hipMalloc(knn 2)")) != KN_OK) return st;
+        if (cfg_.with_distances && !g.out_dist &&
+            (st = check(dmalloc(&g.out_dist, nk * sizeof(float)), "hipMalloc(dist 2)")) != KN_OK)
+            return st;
+    }
     if (!bstream_) {
         // KN_PIPE_PRIO=1: the build stream at the device's highest priority (its latency-bound
         // kernels then take CU slots as soon as the query's workgroups free them)
@@ -662,7 +702,10 @@ kn_status Engine::ensure_pipeline() {
     if (!pipe_.ready()) {
         auto b = [this](int s, hipStream_t st2) { return stage_build(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         auto q = [this](int s, hipStream_t st2) { return stage_query(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
-        if ((st = check(pipe_.init(stream_, bstream_, b, q), "pipeline init")) != KN_OK) return st;
+        Pipeline::Stage x;
+        if (!use_tree_)  // the tree query finishes its own exact-path queries
+            x = [this](int s, hipStream_t st2) { return stage_exact(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
+        if ((st = check(pipe_.init(stream_, bstream_, b, q, x), "pipeline init")) != KN_OK) return st;
     }
     return KN_OK;
 }
@@ -696,6 +739,9 @@ kn_status Engine::launch_pipelined(int iters, int unroll) {
     if (iters <= 0) return KN_OK;
     if (unroll < 0) unroll = pipe_unroll_default();
     hipError_t e = pipe_.launch(iters, unroll);
+    // later work on stream_ (getters, serial steps) follows the last step's epilogue (its exact
+    // finish runs on the build stream)
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream_, pipe_.last_done(), 0);
     if (e != hipSuccess) {
         drop_pipeline();
         return check(e == hipErrorUnknown ? hipErrorLaunchFailure : e, "pipelined launch");
@@ -728,6 +774,7 @@ kn_status Engine::stream_step(const float* d_pts, const float* d_next) {
     Pipeline::Stage pre = copy_in(d_pts);
     Pipeline::Stage nxt = copy_in(d_next);
     hipError_t e = pipe_.step_with(pre, d_next ? &nxt : nullptr);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream_, pipe_.last_done(), 0);
     if (e != hipSuccess) {
         drop_pipeline();
         return check(e == hipErrorUnknown ? hipErrorLaunchFailure : e, "stream step");

@@ -130,12 +130,15 @@ private:
         unsigned* counters; unsigned long long* occ;
         void* tree_ws;
         void* tree_nodes;
+        unsigned* out_idx;  // per-set results (dmalloc'd): step i's rows stay while step i+1 queries
+        float* out_dist;
     };
     GridSet members() const;
     void view_set(int s);  // members <- set_[s]
     kn_status ensure_pipeline();
     kn_status stage_build(int s, hipStream_t st);
     kn_status stage_query(int s, hipStream_t st);
+    kn_status stage_exact(int s, hipStream_t st);  // the fallback list's exact finish (epilogue)
     // keep_grid: the live grid (maybe in arena2_) must survive into arena_ (set_k keeps solving it)
     void drop_pipeline(bool keep_grid = false);
     GridSet set_[2]{};

@@ -1339,7 +1339,7 @@ public:
         r["ms_exchange"] = ms[1];
         r["ms_build"] = ms[2];
         r["ms_query"] = ms[3];
-        r["ms_flag_allreduce"] = ms[4];
+        r["ms_finish"] = ms[4];  // exact finish + flag + its all-reduce
         return r;
     }
     int64_t rows() { return d_->rows(); }

@@ -749,7 +749,7 @@ class DistributedKNearests:
     def profile_step(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None) -> dict:
         """Per-phase device times (ms) of one serial steady step of the native pipeline
         (collective: every rank calls it): ms_route, ms_exchange, ms_build, ms_query,
-        ms_flag_allreduce. {} when the steady native pipeline is not in use."""
+        ms_finish. {} when the steady native pipeline is not in use."""
         points = points.contiguous().float()
         if self._steady is None or not self._use_pipe(points):
             return {}
