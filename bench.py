@@ -425,7 +425,22 @@ def run_cpu_oracle(args) -> dict:
     return {"t": dt, "n_total": pts.size(0), "check": {}}
 
 
+# The ONE JSON line goes to the original stdout; everything native libraries write to fd 1 (RCCL's
+# version banner at communicator init, HIP runtime messages) is redirected to stderr.
+_JSON_OUT = None
+
+
+def emit(line: dict) -> None:
+    out = _JSON_OUT if _JSON_OUT is not None else sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
+
+
 def main() -> int:
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     # defaults = the driver's run (--steps 20 --warmup 5)
@@ -489,7 +504,7 @@ def main() -> int:
 
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
                "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29517")] + sys.argv
-        return subprocess.call(cmd)
+        return subprocess.call(cmd, stdout=_JSON_OUT)
     if args.cpu_oracle or args.loopback:
         r = run_cpu_oracle(args) if args.cpu_oracle else run_loopback_bench(args)
         ms = r["t"] / args.steps * 1e3
@@ -501,7 +516,7 @@ def main() -> int:
                 "config": {"model": f"{kind} kNN, {r['n_total']} pts, k={args.k}", "global_batch": r["n_total"],
                            "seq_len": args.k, "parallelism": "cpu" if args.cpu_oracle else kind},
                 "check": r.get("check", {}), **({"stats": r["stats"]} if "stats" in r else {})}
-        print(json.dumps(line), flush=True)
+        emit(line)
         return 0
     if world_env > 1 or args.dist:
         r = run_dist(args)
@@ -541,7 +556,7 @@ def main() -> int:
         "vs_cpu_oracle": qps / CPU_ORACLE_QPS, "check": r.get("check", {}), "in_cell_sort": args.deterministic,
         **extra,
     }
-    print(json.dumps(line), flush=True)
+    emit(line)
     return 0
 
 

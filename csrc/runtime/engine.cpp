@@ -613,6 +613,15 @@ kn_status Engine::stage_build(int s, hipStream_t st) {
     return r;
 }
 
+// KN_PIPE_EXACT=0: the exact finish stays in the query stage (A/B of the epilogue placement)
+static bool exact_epilogue() {
+    static const bool on = [] {
+        const char* v = std::getenv("KN_PIPE_EXACT");
+        return !(v && std::atoi(v) == 0);
+    }();
+    return on;
+}
+
 kn_status Engine::stage_query(int s, hipStream_t st) {
     const int keep = live_;
     hipStream_t ks = stream_;
@@ -621,6 +630,8 @@ kn_status Engine::stage_query(int s, hipStream_t st) {
     kn_status r;
     if (use_tree_) {
         r = tree_query_async();
+    } else if (!exact_epilogue()) {
+        r = query_async(true);
     } else {
         // the tile kernel only: its fallback list's exact finish is the epilogue on the build
         // stream, so the next step's queries follow this one's without waiting for it
@@ -703,7 +714,7 @@ kn_status Engine::ensure_pipeline() {
         auto b = [this](int s, hipStream_t st2) { return stage_build(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         auto q = [this](int s, hipStream_t st2) { return stage_query(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         Pipeline::Stage x;
-        if (!use_tree_)  // the tree query finishes its own exact-path queries
+        if (!use_tree_ && exact_epilogue())  // the tree query finishes its own exact-path queries
             x = [this](int s, hipStream_t st2) { return stage_exact(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         if ((st = check(pipe_.init(stream_, bstream_, b, q, x), "pipeline init")) != KN_OK) return st;
     }

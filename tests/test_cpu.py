@@ -199,3 +199,21 @@ def test_python_cli_cpu(tmp_path):
     assert line["ok"] and line["n"] == 20626
     rows = out.read_text().splitlines()
     assert len(rows) == 20626 and len(rows[0].split()) == 8
+
+
+def test_bench_prints_one_json_line():
+    """bench.py's contract: exactly one JSON line on stdout (native libraries' own stdout prints,
+    e.g. RCCL's version banner, are redirected to stderr)."""
+    import json
+    import subprocess
+    import sys
+
+    from cuda_knearests_amd.utils import REPO
+
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--cpu-oracle", "--steps", "1", "--k", "8"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["unit"] == "queries/s" and d["value"] > 0
