@@ -13,6 +13,8 @@
 
 namespace kn {
 
+bool exact_epilogue();  // engine.cpp: KN_PIPE_EXACT
+
 namespace {
 #define KN_TRY(expr)                     \
     do {                                 \
@@ -93,7 +95,7 @@ void comm_abort(RankComm* c) {
 // ---------------------------------------------------------------- pipeline ------------
 DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(comm) {
     const int W = p_.world;
-    if (!comm_ || comm_->world != W || comm_->rank != p_.rank) { fail("communicator does not match the plan"); return; }
+    if (comm_ && (comm_->world != W || comm_->rank != p_.rank)) { fail("communicator does not match the plan"); return; }
     if (W < 1 || W > kRouteMaxWorld || p_.rank < 0 || p_.rank >= W || p_.k < 1 || p_.k > KN_MAX_K || p_.n < 0 ||
         (int)p_.recv_own.size() != W || (int)p_.recv_halo.size() != W || (int)p_.cross_send.size() != W ||
         (int)p_.cross_recv.size() != W || (int)p_.tot.size() != 2 * W || (int)p_.hdr.size() < kPlanHdr ||
@@ -285,7 +287,19 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     auto b = [this](int s, hipStream_t st) { return stage_build(s, st); };
     auto q = [this](int s, hipStream_t st) { return stage_query(s, st); };
     auto r = [this](int s, hipStream_t st) { return stage_flag(s, st); };
+    if (!comm_) {  // loopback mode: eager stages driven by the caller
+        ok_ = true;
+        return;
+    }
     if (pipe_.init(main_, side_, b, q, r, true) != hipSuccess) { fail("pipeline init"); return; }
+    // one eager (uncaptured) step: RCCL connects to the step's peers and sets up the all-reduce
+    // before any of it is captured into a graph (collective: every rank builds its pipeline at
+    // the same solve() call)
+    if (stage_build(1, main_) != hipSuccess || stage_query(1, main_) != hipSuccess || stage_flag(1, main_) != hipSuccess ||
+        hipStreamSynchronize(main_) != hipSuccess) {
+        fail("eager warm-up step of the distributed pipeline failed");
+        return;
+    }
     ok_ = true;
 }
 
@@ -308,6 +322,7 @@ DistPipeline::~DistPipeline() {
 }
 
 hipError_t DistPipeline::exchange(int s, hipStream_t st) {
+    if (!comm_) return hipSuccess;  // loopback mode: the caller moved the rows
     const Set& S = set_[s];
     const int W = p_.world;
     ncclComm_t comm = as_comm(comm_);
@@ -395,10 +410,10 @@ hipError_t DistPipeline::stage_query(int s, hipStream_t st) {
         }
         return hipSuccess;
     }
-    // the tile kernel only: the exact finish of its fallback list opens the epilogue on the side
-    // stream, so the next step's queries follow this one's directly
+    // the tile kernel and its exact finish (KN_PIPE_EXACT=1: the exact finish opens the epilogue
+    // on the side stream instead, engine.cpp exact_epilogue)
     QueryBuffers q = query_proto(s);
-    q.exact_mode = 1;
+    q.exact_mode = exact_epilogue() ? 1 : 0;
     return launch_query(q, st);
 }
 
@@ -422,19 +437,69 @@ QueryBuffers DistPipeline::query_proto(int s) const {
 // as planned, no uncertified row), its MAX all-reduce and the sticky host flag.
 hipError_t DistPipeline::stage_flag(int s, hipStream_t st) {
     Set& S = set_[s];
-    if (!p_.use_tree) {
+    if (!p_.use_tree && exact_epilogue()) {
         QueryBuffers q = query_proto(s);
         q.exact_mode = 2;
         KN_TRY(launch_query(q, st));
     }
     KN_TRY(launch_steady_flag_partials(S.partials, p_.n, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
                                        S.counters, S.flag, st));
+    if (!comm_) return hipSuccess;  // loopback mode: the caller reduces the ranks' flags
     if (ncclAllReduce(S.flag, S.flag, 1, ncclInt32, ncclMax, as_comm(comm_), st) != ncclSuccess) return hipErrorUnknown;
     return launch_flag_sink(S.flag, sticky_, host_flag_dev_, st);
 }
 
+kn_status DistPipeline::loopback_stage(int stage) {
+    if (!ok_ || comm_) return KN_ERR_STATE;
+    hipError_t e = hipSuccess;
+    if (stage == 0) {
+        // the routing half of stage_build (exchange and local build follow in stage 1)
+        Set& S = set_[0];
+        const auto* rp = static_cast<const RouteParams*>(route_dev_);
+        if (p_.n > 0) {
+            e = launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, main_, S.partials);
+            SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
+            if (e == hipSuccess)
+                e = launch_route_scatter(p_.points, p_.ids, p_.n, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank,
+                                         main_, &sp);
+        } else {
+            e = hipMemsetAsync(S.totals, 0, (size_t)2 * p_.world * sizeof(int), main_);
+        }
+    } else {
+        Set& S = set_[0];
+        if (rows_cross_ > 0) e = launch_route_unpack(S.recv, nullptr, rows_cross_, table_, S.lpts, S.lgids, main_);
+        if (e == hipSuccess) {
+            BuildBuffers b = bproto_;
+            b.points = S.lpts; b.bbox_words = S.bbox; b.geom = S.geom; b.cell_count = S.cell_count;
+            b.cell_scan = S.cell_scan; b.block_sums = S.block_sums; b.cell_start = S.cell_start;
+            b.cell_rank = reinterpret_cast<int2*>(S.bin_tmp); b.bin_tmp = S.bin_tmp; b.sorted = S.sorted;
+            b.perm = S.perm; b.gids = S.lgids; b.zero_words = S.counters;
+            e = launch_build(b, main_);
+        }
+        if (e == hipSuccess && p_.use_tree && rows_ > 0) {
+            TreeView t = tree_view(S.tree_ws, rows_, p_.dims);
+            tree_attach_nodes(t, S.tree_nodes);
+            e = launch_tree_leaves(S.sorted, S.cell_start, S.geom, t, main_);
+            if (e == hipSuccess) e = launch_tree_nodes(t, main_);
+        }
+        if (e == hipSuccess) e = stage_query(0, main_);
+        if (e == hipSuccess) e = stage_flag(0, main_);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(main_);
+    if (e != hipSuccess) { err_ = std::string("loopback stage: ") + hipGetErrorString(e); return KN_ERR_DEVICE; }
+    return KN_OK;
+}
+
+int DistPipeline::flag_local(int s) const {
+    int f = -1;
+    (void)hipStreamSynchronize(main_);
+    (void)hipMemcpy(&f, set_[s].flag, sizeof(int), hipMemcpyDeviceToHost);
+    return f;
+}
+
 kn_status DistPipeline::launch(int iters, int unroll, bool keep_primed, hipStream_t caller, long long* last_step) {
     if (!ok_) return KN_ERR_STATE;
+    if (!comm_) { err_ = "loopback pipelines run loopback_stage() only"; return KN_ERR_STATE; }
     if (comm_->aborted) { err_ = "communicator aborted"; return KN_ERR_DEVICE; }
     if (iters <= 0) {
         if (last_step) *last_step = pipe_.steps() - 1;
@@ -467,7 +532,7 @@ kn_status DistPipeline::launch(int iters, int unroll, bool keep_primed, hipStrea
 }
 
 kn_status DistPipeline::wait(long long step, double timeout_s, int* flag) {
-    if (!ok_) return KN_ERR_STATE;
+    if (!ok_ || !comm_) return KN_ERR_STATE;
     hipEvent_t ev = nullptr;
     for (const auto& d : done_)
         if (d.first >= step) { ev = ring_[d.second]; break; }
@@ -508,7 +573,7 @@ kn_status DistPipeline::sync() {
 }
 
 kn_status DistPipeline::profile(float ms[5]) {
-    if (!ok_) return KN_ERR_STATE;
+    if (!ok_ || !comm_) return KN_ERR_STATE;
     if (pipe_.sync() != hipSuccess || pipe_.unprime() != hipSuccess) { err_ = "sync"; return KN_ERR_DEVICE; }
     std::vector<hipEvent_t> ev(6, nullptr);
     for (auto& e : ev)

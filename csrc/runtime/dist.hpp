@@ -73,6 +73,10 @@ struct DistPlan {
 
 class DistPipeline {
 public:
+    // comm == nullptr: LOOPBACK mode (tests): no communicator, no graphs -- the caller drives one
+    // eager step per rank through loopback_stage() and moves the rows between the ranks' send /
+    // receive buffers itself (one process, W virtual ranks on one GPU), which checks the send /
+    // receive layouts, the unpack table and the local solve against the torch path at world > 1.
     DistPipeline(const DistPlan& p, RankComm* comm);
     ~DistPipeline();
     DistPipeline(const DistPipeline&) = delete;
@@ -95,6 +99,15 @@ public:
     // unpack + build, query (tile kernel / tree + certification), epilogue (exact finish, flag,
     // all-reduce). Unprimes the pipeline.
     kn_status profile(float ms[5]);
+
+    // loopback mode: stage 0 = route (send buffer + own rows placed), 1 = unpack + build + query
+    // + the step's local flag (no all-reduce); set 0 is used; synchronous
+    kn_status loopback_stage(int stage);
+    float4* send_rows(int s) const { return set_[s].send; }
+    float4* recv_rows(int s) const { return set_[s].recv; }
+    long long send_offset(int d) const { return soff_[d]; }
+    long long recv_offset(int src) const { return roff_[src]; }
+    int flag_local(int s) const;  // synchronous read of set s's flag word
 
     int rows() const { return rows_; }
     int n_owned() const { return n_owned_; }

@@ -613,11 +613,15 @@ kn_status Engine::stage_build(int s, hipStream_t st) {
     return r;
 }
 
-// KN_PIPE_EXACT=0: the exact finish stays in the query stage (A/B of the epilogue placement)
-static bool exact_epilogue() {
+// KN_PIPE_EXACT=1: the tile kernel's exact finish runs as an epilogue on the build stream
+// instead of right after the tile kernel on the query stream. Measured slower (900K, K=16,
+// unroll 4, interleaved on one box, profiles/r4_ab_exact.txt): 200 steps 0.2954 -> 0.3016 ms,
+// 20 steps 0.317 -> 0.324 -- the extra cross-stream dependency and the exact kernel's
+// workgroups competing with the next query cost more than its ~5 us on the query stream.
+bool exact_epilogue() {
     static const bool on = [] {
         const char* v = std::getenv("KN_PIPE_EXACT");
-        return !(v && std::atoi(v) == 0);
+        return v && std::atoi(v) == 1;
     }();
     return on;
 }

@@ -1241,20 +1241,27 @@ public:
 
 class PyDistPipe {
 public:
+    // comm = None: loopback mode (tests), world / rank from `loopback` = (world, rank)
     PyDistPipe(std::shared_ptr<PyRankComm> comm, torch::Tensor points, c10::optional<torch::Tensor> ids,
                torch::Tensor plan, torch::Tensor metas, std::vector<int64_t> tot, std::vector<double> hdr,
                std::vector<int64_t> grid, std::vector<int64_t> dims, std::vector<int64_t> recv_own,
                std::vector<int64_t> recv_halo, std::vector<int64_t> cross_send, std::vector<int64_t> cross_recv,
                std::vector<int64_t> place, int64_t cap, int64_t k, double ppc, bool deterministic, int64_t exact_grid,
-               int64_t use_tree, bool self_via_comm)
+               int64_t use_tree, bool self_via_comm, c10::optional<std::vector<int64_t>> loopback)
         : comm_(std::move(comm)), points_(points) {
         check_points(points, true);
         TORCH_CHECK(plan.is_cuda() && plan.numel() == (int64_t)sizeof(kn::RouteParams), "plan must be a route plan");
         TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous(), "metas: f64 GPU");
         TORCH_CHECK(grid.size() == 3 && dims.size() == 3 && place.size() == 5, "grid / dims / place sizes");
         kn::DistPlan p;
-        p.world = comm_->c_->world;
-        p.rank = comm_->c_->rank;
+        if (comm_) {
+            p.world = comm_->c_->world;
+            p.rank = comm_->c_->rank;
+        } else {
+            TORCH_CHECK(loopback.has_value() && loopback->size() == 2, "no communicator: loopback = (world, rank)");
+            p.world = (int)(*loopback)[0];
+            p.rank = (int)(*loopback)[1];
+        }
         p.device = points.get_device();
         p.k = (int)k;
         p.n = (int)points.size(0);
@@ -1287,9 +1294,21 @@ public:
         const c10::DeviceGuard guard(points.device());
         // the plan tensors (route plan, metas) are copied by the constructor: their producers first
         KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
-        d_ = std::make_unique<kn::DistPipeline>(p, comm_->c_);
+        d_ = std::make_unique<kn::DistPipeline>(p, comm_ ? comm_->c_ : nullptr);
         TORCH_CHECK(d_->ok(), d_->error());
     }
+    // loopback mode: one synchronous stage (0 route, 1 unpack + build + query + local flag)
+    void loopback_stage(int64_t stage) { TORCH_CHECK(d_->loopback_stage((int)stage) == KN_OK, d_->error()); }
+    // views (float32, (rows, 4)) of set 0's send rows for destination d / receive rows from source s
+    torch::Tensor send_view(int64_t d, int64_t rows) {
+        auto opt = torch::TensorOptions().device(points_.device()).dtype(torch::kFloat32);
+        return torch::from_blob(reinterpret_cast<float*>(d_->send_rows(0) + d_->send_offset((int)d)), {rows, 4}, opt);
+    }
+    torch::Tensor recv_view(int64_t src, int64_t rows) {
+        auto opt = torch::TensorOptions().device(points_.device()).dtype(torch::kFloat32);
+        return torch::from_blob(reinterpret_cast<float*>(d_->recv_rows(0) + d_->recv_offset((int)src)), {rows, 4}, opt);
+    }
+    int64_t flag_local() { return d_->flag_local(0); }
     // enqueue `iters` steps (unroll: steps per graph launch, even >= 2, else one graph per stage)
     // keep_primed: also enqueue the next step's build (the caller promises the points stay
     // unchanged until the next launch); the current torch stream orders the input
@@ -1441,7 +1460,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                       torch::Tensor, std::vector<int64_t>, std::vector<double>, std::vector<int64_t>,
                       std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>,
                       std::vector<int64_t>, std::vector<int64_t>, int64_t, int64_t, double, bool, int64_t, int64_t,
-                      bool>())
+                      bool, c10::optional<std::vector<int64_t>>>(),
+             py::arg("comm"), py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("metas"), py::arg("tot"),
+             py::arg("hdr"), py::arg("grid"), py::arg("dims"), py::arg("recv_own"), py::arg("recv_halo"),
+             py::arg("cross_send"), py::arg("cross_recv"), py::arg("place"), py::arg("cap"), py::arg("k"),
+             py::arg("ppc"), py::arg("deterministic"), py::arg("exact_grid"), py::arg("use_tree"),
+             py::arg("self_via_comm"), py::arg("loopback") = py::none())
+        .def("loopback_stage", &PyDistPipe::loopback_stage)
+        .def("send_view", &PyDistPipe::send_view)
+        .def("recv_view", &PyDistPipe::recv_view)
+        .def("flag_local", &PyDistPipe::flag_local)
         .def("launch", &PyDistPipe::launch, py::arg("iters") = 1, py::arg("unroll") = 0, py::arg("keep_primed") = false)
         .def("wait", &PyDistPipe::wait, py::arg("step"), py::arg("timeout_s") = 300.0)
         .def("sync", &PyDistPipe::sync)

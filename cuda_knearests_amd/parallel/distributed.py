@@ -696,7 +696,7 @@ class DistributedKNearests:
                           [int(v) for v in st["tot"].tolist()], [float(v) for v in st["hdr"]], list(st["grid"]),
                           list(st["dims"]), list(st["recv_own"]), list(st["recv_halo"]), list(st["cross_send"]),
                           list(st["cross_recv"]), list(st["place"]), int(st["cap"]), self.k, self.points_per_cell,
-                          bool(self.deterministic), int(st["exact_grid"]), int(st["use_tree"]), world1_force)
+                          bool(self.deterministic), int(st["exact_grid"]), int(st["use_tree"]), world1_force, None)
         p = self._pipe = {"pipe": pipe, "st": st, "pts": points, "ids": ids32, "n": points.size(0),
                           "outs": [pipe.outputs(0), pipe.outputs(1)], "primed": False}
         return p

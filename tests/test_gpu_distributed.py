@@ -547,3 +547,58 @@ def test_rccl_world1_native_pipeline(cuda):
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "ALL OK" in r.stdout
+
+
+@pytest.mark.parametrize("world,gen", [(2, "uniform"), (4, "uniform"), (8, "uniform"), (8, "clustered")])
+def test_native_pipeline_loopback_layouts(cuda, world, gen):
+    """kn::DistPipeline at world > 1 without RCCL (loopback mode, one GPU): every virtual rank's
+    pipeline routes its share, the test moves the rows between the ranks' send / receive buffers
+    exactly as the grouped ncclSend / ncclRecv would, then unpack + build + query + flag; the rows
+    are bit-identical to the torch path's steady step and every local flag is clear. This checks
+    the send / receive offsets, the unpack table and the local plan the RCCL pipeline uses."""
+    from cuda_knearests_amd._ext import load
+    from cuda_knearests_amd.parallel import DistributedKNearests, SpatialDecomposition, run_loopback
+    from cuda_knearests_amd.utils import clustered_cloud
+
+    C = load()
+    n = 60000
+    if gen == "uniform":
+        shares = []
+        for r in range(world):
+            blo, bhi = SpatialDecomposition(world, (0.0,) * 3, (1000.0,) * 3).rank_box(r)
+            u = uniform_cloud(n, seed=400 + r, device=cuda, lo=0.0, hi=1.0)
+            shares.append((u * torch.tensor([bhi[a] - blo[a] for a in range(3)], device=cuda)
+                           + torch.tensor(blo, device=cuda)).contiguous())
+    else:
+        shares = [c.contiguous() for c in clustered_cloud(n * world, seed=77).to(cuda).chunk(world)]
+
+    def body(t):
+        dk = DistributedKNearests(k=16, transport=t)
+        dk.solve(shares[t.rank])
+        r1 = dk.solve(shares[t.rank])  # steady step, torch path (loopback transport)
+        assert r1.valid() and r1.stats.get("steady")
+        return dk._steady, r1.ids.clone(), r1.neighbors.clone(), r1.d2.clone()
+
+    out = run_loopback(world, body)
+    pipes = []
+    for r, (st, _, _, _) in enumerate(out):
+        pipes.append(C.DistPipe(None, shares[r], None, st["plan"], st["metas"], [int(v) for v in st["tot"].tolist()],
+                                [float(v) for v in st["hdr"]], list(st["grid"]), list(st["dims"]), list(st["recv_own"]),
+                                list(st["recv_halo"]), list(st["cross_send"]), list(st["cross_recv"]), list(st["place"]),
+                                int(st["cap"]), 16, 0.0, True, int(st["exact_grid"]), int(st["use_tree"]), False,
+                                [world, r]))
+    for p in pipes:
+        p.loopback_stage(0)
+    for r in range(world):
+        for d in range(world):
+            m = out[r][0]["cross_send"][d]
+            if d != r and m:
+                assert out[d][0]["cross_recv"][r] == m
+                pipes[d].recv_view(r, m).copy_(pipes[r].send_view(d, m))
+    torch.cuda.synchronize()
+    for p in pipes:
+        p.loopback_stage(1)
+    for r, (st, ids, nb, d2) in enumerate(out):
+        g, i, d = pipes[r].outputs(0)
+        assert pipes[r].flag_local() == 0, r
+        assert torch.equal(g, ids) and torch.equal(i, nb) and torch.equal(d, d2), r
