@@ -107,7 +107,84 @@ hipError_t copy_h2d_staged(void* d, const void* h, size_t bytes, hipStream_t s) 
     return hipSuccess;
 }
 
+// Large device -> pageable host copies (the reference getters' malloc'd results): one pinned
+// buffer sized to the copy (grow-only, process-wide, <= kBigMax), every chunk's DMA enqueued at
+// once (the copy engine streams at PCIe rate), and a team of host threads copying each chunk out
+// as soon as its event completes -- the host copy (and its first-touch page faults, spread over
+// the threads) overlaps the DMA of the later chunks.
+namespace {
+constexpr size_t kBigChunk = 8u << 20;
+constexpr size_t kBigMax = 1ull << 30;
+constexpr int kBigEvents = (int)(kBigMax / kBigChunk);
+struct BigStage {
+    std::mutex mu;
+    void* buf = nullptr;
+    size_t cap = 0;
+    std::vector<hipEvent_t> ev;
+    int dev = -1;
+};
+BigStage& big() {
+    static BigStage* b = new BigStage();  // never destroyed: pinned memory is released at exit
+    return *b;
+}
+}  // namespace
+
+static hipError_t copy_d2h_big(void* h, const void* d, size_t bytes, hipStream_t s) {
+    BigStage& b = big();
+    std::lock_guard<std::mutex> lock(b.mu);
+    hipError_t e;
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if (b.cap < bytes) {
+        if (b.buf) (void)hipHostFree(b.buf);
+        b.buf = nullptr;
+        b.cap = 0;
+        const size_t want = std::min(kBigMax, std::max(bytes, (size_t)64 << 20));
+        if ((e = hipHostMalloc(&b.buf, want, hipHostMallocDefault)) != hipSuccess) return e;
+        b.cap = want;
+    }
+    if (b.dev != dev) {
+        for (auto x : b.ev) (void)hipEventDestroy(x);
+        b.ev.clear();
+        b.dev = dev;
+    }
+    const size_t nchunks = (bytes + kBigChunk - 1) / kBigChunk;
+    while (b.ev.size() < nchunks) {
+        hipEvent_t x = nullptr;
+        if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return e;
+        b.ev.push_back(x);
+    }
+    for (size_t c = 0; c < nchunks; ++c) {
+        const size_t off = c * kBigChunk, len = std::min(kBigChunk, bytes - off);
+        if ((e = hipMemcpyAsync((char*)b.buf + off, (const char*)d + off, len, hipMemcpyDeviceToHost, s)) != hipSuccess)
+            return e;
+        if ((e = hipEventRecord(b.ev[c], s)) != hipSuccess) return e;
+    }
+    const int nt = std::max(1, std::min(16, omp_get_max_threads()));
+    hipError_t err = hipSuccess;
+#pragma omp parallel num_threads(nt)
+    {
+        const int t = omp_get_thread_num(), T = omp_get_num_threads();
+        for (size_t c = 0; c < nchunks; ++c) {
+#pragma omp single
+            {
+                const hipError_t x = hipEventSynchronize(b.ev[c]);
+                if (x != hipSuccess) err = x;
+            }  // implicit barrier: the chunk is in pinned memory
+            if (err != hipSuccess) continue;
+            const size_t off = c * kBigChunk, len = std::min(kBigChunk, bytes - off);
+            // 4 KiB-aligned slices: every page is touched (faulted in) by one thread only
+            const size_t per = ((len + T - 1) / T + 4095) & ~(size_t)4095;
+            const size_t a = std::min(len, (size_t)t * per), z = std::min(len, a + per);
+            if (z > a) std::memcpy((char*)h + off + a, (const char*)b.buf + off + a, z - a);
+        }
+    }
+    return err;
+}
+
 hipError_t copy_d2h_staged(void* h, const void* d, size_t bytes, hipStream_t s) {
+    // big copies: the pinned whole-copy path (KN_HOST_BIG=0: off)
+    if (bytes >= (4u << 20) && bytes <= kBigMax && env_on("KN_HOST_BIG", true)) return copy_d2h_big(h, d, bytes, s);
     if (bytes < kDirectBelow || !env_on("KN_HOST_STAGE", false)) {
         hipError_t e = hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
         return e != hipSuccess ? e : hipStreamSynchronize(s);
