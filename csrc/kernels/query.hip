@@ -51,7 +51,11 @@ namespace kn {
 namespace {
 
 constexpr unsigned SENT = 0xFFFFFFFFu;
-constexpr int kWG = 256;
+// Threads per tile workgroup (A/B builds: -DKN_TILE_WG=512 with taller tiles)
+#ifndef KN_TILE_WG
+#define KN_TILE_WG 256
+#endif
+constexpr int kWG = KN_TILE_WG;
 constexpr int kWaves = kWG / 64;
 
 struct TileArgs {

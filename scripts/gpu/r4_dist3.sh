@@ -30,3 +30,7 @@ done
 cat "$O"/api_*.json
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_capi.py > "$O/tests_capi.log" 2>&1 || { tail -30 "$O/tests_capi.log"; exit 1; }
 tail -2 "$O/tests_capi.log"
+timeout -k 10 300 python3 scripts/ab_tiles.py 900000 16 5 100 > "$O/ab_tiles.log" 2>&1 || { tail -20 "$O/ab_tiles.log"; exit 1; }
+timeout -k 10 300 python3 scripts/ab_tiles.py 900000 50 3 40 > "$O/ab_tiles50.log" 2>&1 || { tail -20 "$O/ab_tiles50.log"; exit 1; }
+cat "$O/ab_tiles50.log"
+cat "$O/ab_tiles.log"
