@@ -144,12 +144,9 @@ __device__ __forceinline__ unsigned cand_key_v(const float4& p, float qx, float 
 // Sorted-array insertion of `key` into keys[0..KM) (ascending), dropping the largest:
 // new[j] = med3(old[j-1], key, old[j]) -- one v_med3_u32 per slot, all independent. Skipped
 // (uniform branch) when no lane of the wave improves; a non-improving key is a no-op anyway.
-#ifndef KN_BRANCHFREE_INSERT
-#define KN_BRANCHFREE_INSERT 0
-#endif
 template <int KM>
 __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key) {
-    if (KN_BRANCHFREE_INSERT || __builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
+    if (__builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
 #pragma unroll
         for (int j = KM - 1; j > 0; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
         keys[0] = min(keys[0], key);

@@ -91,17 +91,8 @@ struct TileArgs {
 };
 constexpr int kRowOrderMax = 128;
 
-#ifndef KN_STAGE_ROWS
-#define KN_STAGE_ROWS 0
-#endif
-#ifndef KN_YPRUNE
-#define KN_YPRUNE 1
-#endif
 #ifndef KN_LANE_UNROLL
 #define KN_LANE_UNROLL 2
-#endif
-#ifndef KN_LDS_PIPE
-#define KN_LDS_PIPE 1
 #endif
 // Lane walk region: the lane's own cell +- H, then (full mode) the rest of the staged block
 // (tile + H) for the lanes whose bound still reaches past their own box. KN_LANE_FULL: 0 never,
@@ -122,12 +113,8 @@ constexpr int kRowOrderMax = 128;
 #ifndef KN_ROW_ORDER
 #define KN_ROW_ORDER 2
 #endif
-// KN_ROW_RING=1: the other lane walks (K <= 40) take a table too, in ring order without the
-// per-lane mirror: the 3x3 rows around the query's own row first, the outer ring after (every
-// lane of a wave visits the same relative row, so the spans of one row iteration stay alike).
-#ifndef KN_ROW_RING
-#define KN_ROW_RING 0
-#endif
+// (A ring-order table without the mirror for K <= 40 lost too: K=8 +8 %, K=32 +8 %,
+// profiles/ab_r3_ring.jsonl; removed in round 4.)
 // KN_OUTER_PACK (lane walk, K <= 40, the fixed order): the 3x3 rows around the query's row stay
 // row-synchronous, the outer rows (Chebyshev ring >= 2 of the (2H+1)^2 block) are PACKED: each
 // lane marks the outer rows its bound still reaches (a 64-bit mask, distances from 8 per-lane
@@ -156,9 +143,6 @@ constexpr bool outer_pack_k() { return KN_OUTER_PACK == 1 ? KT <= 40 : (KN_OUTER
 // Re-rank of the kept keys: 1 = streaming window (O(kWin) live registers), 0 = odd-even
 // transposition over (d2, id) arrays of KM entries each plus the in-wave exact re-scan of
 // truncation near-ties (round 1).
-#ifndef KN_WINDOW_RERANK
-#define KN_WINDOW_RERANK 1
-#endif
 #ifndef KN_WIN
 #define KN_WIN 1
 #endif
@@ -251,7 +235,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
     constexpr int KM = KT + M + 1;
     constexpr bool kFull = LANE && (KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40));
-    constexpr bool kRowOrder = LANE && (KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && kFull) || KN_ROW_RING);
+    constexpr bool kRowOrder = LANE && (KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && kFull));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     KN_PH_DECL
     float4* pts = reinterpret_cast<float4*>(smem);
@@ -355,38 +339,12 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         if (threadIdx.x == 0) atomicAdd(a.counters + 2, 1u);
         return;
     }
-#if KN_STAGE_ROWS
-    // ---- 3. stage the points: rows round-robin over the waves, lanes = points of a row,
-    //         4 rows' 16-B loads in flight per wave (no per-point row search) -------------
-    for (int r0 = wid; r0 < nrows; r0 += 4 * kWaves) {
-        float4 v[4];
-        int dst[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int r = r0 + u * kWaves;
-            const int len = r < nrows ? rowbase[r + 1] - rowbase[r] : 0;
-            dst[u] = lane < len ? rowbase[r] + lane : -1;
-            if (dst[u] >= 0) v[u] = a.sorted[KN_IDX(rowst[r] + lane, a.n, 202)];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (dst[u] >= 0) pts[KN_IDX(dst[u], a.cap, 203)] = v[u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {  // rows longer than a wave (dense tiles)
-            const int r = r0 + u * kWaves;
-            const int len = r < nrows ? rowbase[r + 1] - rowbase[r] : 0;
-            for (int i = lane + 64; i < len; i += 64)
-                pts[KN_IDX(rowbase[r] + i, a.cap, 203)] = a.sorted[KN_IDX(rowst[r] + i, a.n, 202)];
-        }
-    }
-#else
     // ---- 3. stage the points (16-B coalesced loads, row found by binary search) --------
     for (int s = threadIdx.x; s < S; s += kWG) {
         int lo = 0, hi = nrows - 1;
         while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rowbase[mid] <= s) lo = mid; else hi = mid - 1; }
         pts[KN_IDX(s, a.cap, 203)] = a.sorted[KN_IDX(rowst[lo] + (s - rowbase[lo]), a.n, 202)];
     }
-#endif
     __syncthreads();
     (void)misc;
 
@@ -661,7 +619,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 if (z < rz0 || z > rz1) continue;
                 const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
                 const float dz2 = dzb * dzb;
-#if KN_YPRUNE
                 // rows of this slab any live lane can still need (bound at slab start: superset)
                 int yl0 = ry0, yl1 = ry1;
                 {
@@ -679,9 +636,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     if (Yr.x > Yr.y) continue;
                     yl0 = Yr.x; yl1 = Yr.y;
                 }
-#else
-                const int yl0 = ry0, yl1 = ry1;
-#endif
                 for (int ty_ = 0; ty_ < nyt; ++ty_) {
                     const int y = yc + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
                     if (y < yl0 || y > yl1) continue;
@@ -757,7 +711,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     st_rows += 1u;
                     st_cand += (unsigned)(s1 - s0);
                 }
-#if KN_LDS_PIPE
                 // software-pipelined: the next 4 broadcast reads are issued before the current 4
                 // candidates are scored (two register sets, no loop-carried copies); reads past
                 // s1 stay inside the workgroup's LDS and are never scored
@@ -786,24 +739,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                         if (s + 4 > s1) break;
                     }
                 }
-#else
-                // 4 broadcast LDS reads in flight, then 4 key tests / insertions
-                for (; s + 4 <= s1; s += 4) {
-                    const float4 p0 = pts[s], p1 = pts[s + 1], p2 = pts[s + 2], p3 = pts[s + 3];
-                    const unsigned k0 = cand_key(p0, qx, qy, qz, HIMASK, s, qslot);
-                    const unsigned k1 = cand_key(p1, qx, qy, qz, HIMASK, s + 1, qslot);
-                    const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, s + 2, qslot);
-                    const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, s + 3, qslot);
-                    // materialise all four keys before the first (uniform) insertion branch so
-                    // their dependent chains overlap instead of being sunk into the branches
-                    asm volatile("" ::"v"(k0), "v"(k1), "v"(k2), "v"(k3));
-                    const unsigned i0 = topk_push<KM>(keys, k0);
-                    const unsigned i1 = topk_push<KM>(keys, k1);
-                    const unsigned i2 = topk_push<KM>(keys, k2);
-                    const unsigned i3 = topk_push<KM>(keys, k3);
-                    if constexpr (kStats) st_ins += i0 + i1 + i2 + i3;
-                }
-#endif
                 for (; s < s1; ++s) {
                     const unsigned i0 = topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
                     if constexpr (kStats) st_ins += i0;
@@ -829,7 +764,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         KN_PH_MARK(kPhRerank);
         const int k = a.k;
         const bool act = in_range && live;
-#if KN_WINDOW_RERANK
         // ---- exact re-rank: streaming window ---------------------------------------------
         // keys are sorted by (truncated d2, slot); the exact (d2, id) order can differ only
         // inside a run of equal truncation buckets. A kept candidate's output position is its
@@ -1043,95 +977,6 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
         }
         KN_PH_MARK(kPhCertify);
         if (!act) continue;
-#else
-        // ---- exact re-rank of the K+M kept candidates (branch-free) ----------------------
-        float dd[KM];
-        unsigned ii[KM];
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            const bool valid = keys[j] != SENT && (keys[j] & MASK) != (unsigned)qslot;
-            const float4 p = pts[KN_IDX(valid ? (keys[j] & MASK) : 0u, (unsigned)S, 208)];
-            const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
-            const float d = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-            dd[j] = valid ? d : INFINITY;
-            ii[j] = valid ? w_id(a, __float_as_uint(p.w)) : SENT;
-        }
-        // keys are sorted by truncated distance; the exact order differs only inside equal
-        // truncation buckets (near-ties: clouds can hold several candidates within 2^-12 of
-        // each other) -> odd-even transposition rounds until no lane of the wave swaps
-        // (almost always one round; bounded by KM, after which the order is exact).
-        for (int round = 0; round < (KM + 1) / 2; ++round) {
-            bool swapped = false;
-#pragma unroll
-            for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-                for (int j = pass; j + 1 < KM; j += 2) {
-                    const bool sw = pair_less(dd[j + 1], ii[j + 1], dd[j], ii[j]);
-                    const float d0 = sw ? dd[j + 1] : dd[j], d1 = sw ? dd[j] : dd[j + 1];
-                    const unsigned i0 = sw ? ii[j + 1] : ii[j], i1 = sw ? ii[j] : ii[j + 1];
-                    dd[j] = d0; dd[j + 1] = d1; ii[j] = i0; ii[j + 1] = i1;
-                    swapped |= sw;
-                }
-            }
-            if (!__builtin_amdgcn_ballot_w64(swapped)) break;
-        }
-
-        auto kth = [&]() {
-            float v = INFINITY;
-#pragma unroll
-            for (int j = 0; j < KM; ++j) if (j == k - 1) v = dd[j];
-            return v;
-        };
-        float dK2 = kth();
-        // Precision check: everything truncated away has key >= last, i.e. exact d2 >= the
-        // floor of last's bucket. If the K-th exact distance reaches into that bucket (K-th and
-        // (K+M)-th candidates within one truncation ulp), redo this query exactly: a second,
-        // uniform pass over the same region with full (d2, id) insertion, bounded by the exact
-        // K-th distance found so far (an upper bound of the true one). Rare: only waves with
-        // such a lane pay for it, instead of a trip through the latency-bound exact kernel.
-        const unsigned last = keys[KM - 1];
-        const bool need = live && ((last != SENT && !(dK2 <= __uint_as_float(last & HIMASK))) ||
-                                   (a.flags & kQueryForceRescan));
-        if (__builtin_amdgcn_ballot_w64(need)) {
-            const float thr = need ? ((a.flags & kQueryForceRescan) ? INFINITY : dK2) : -1.f;
-            // only the lanes that need it start over; the others keep their (final) lists
-#pragma unroll
-            for (int j = 0; j < KM; ++j) {
-                dd[j] = need ? INFINITY : dd[j];
-                ii[j] = need ? SENT : ii[j];
-            }
-            scan_region([&]() { return thr; },
-                        [&](int s0, int s1) {
-                            for (int s = s0; s < s1; ++s) {
-                                const float4 p = pts[s];
-                                const float dx = p.x - qx, dy = p.y - qy, dz = p.z - qz;
-                                const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-                                const unsigned id = w_id(a, __float_as_uint(p.w));
-                                const bool take = s != qslot && d2 <= thr && pair_less(d2, id, dd[KM - 1], ii[KM - 1]);
-                                if (__builtin_amdgcn_ballot_w64(take)) {
-                                    if (take) {
-#pragma unroll
-                                        for (int j = KM - 1; j > 0; --j) {
-                                            const bool bp = pair_less(d2, id, dd[j - 1], ii[j - 1]);
-                                            const bool bc = pair_less(d2, id, dd[j], ii[j]);
-                                            const float nd = bp ? dd[j - 1] : (bc ? d2 : dd[j]);
-                                            const unsigned ni = bp ? ii[j - 1] : (bc ? id : ii[j]);
-                                            dd[j] = nd; ii[j] = ni;
-                                        }
-                                        if (pair_less(d2, id, dd[0], ii[0])) { dd[0] = d2; ii[0] = id; }
-                                    }
-                                }
-                            }
-                        });
-            if (need && in_range) atomicAdd(a.counters + 3, 1u);  // precision re-scans (diagnostic)
-            dK2 = kth();
-        }
-        int nfound = 0;
-#pragma unroll
-        for (int j = 0; j < KM; ++j) nfound += (ii[j] != SENT) ? 1 : 0;
-        if (!act) continue;
-        const bool prec_fail = false;  // the in-wave re-scan resolved it
-#endif
 
         // distance to the boundary of the scanned region (grid faces do not count: no points
         // exist beyond the grid) and to the complete box (multi-GPU halo limit)
@@ -1149,28 +994,11 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             m -= g.eps;
         }
         const bool geo_ok = !prec_fail && (nfound >= k) && (m > 0.f) && (m == INFINITY || dK2 <= m * m);
-#if !KN_WINDOW_RERANK
-        if (geo_ok) {
-            const size_t row = (size_t)w_row(a, qorig, qsidx) * (size_t)k;
-#pragma unroll
-            for (int j = 0; j < KM; ++j) {
-                if (j < k) {
-                    const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 209);
-                    a.out_idx[o] = out_id(a, ii[j]);
-                    if (a.out_dist) a.out_dist[o] = dd[j];
-                }
-            }
-        }
-#endif
         if (!geo_ok) {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
-#if KN_WINDOW_RERANK
             // the row already holds K real candidates: their K-th distance bounds the true one,
             // and the exact kernel starts its walk with it (kSeedBit)
             const bool seed = a.out_dist && nfound >= k && dK2 < INFINITY;
-#else
-            const bool seed = false;
-#endif
             a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx | (seed ? kSeedBit : 0u);
         }
     }
@@ -1878,14 +1706,12 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.cap = q.lds_capacity;
         a.flags = q.flags;
         {
-            // the distance-sorted, mirrored table for the whole-block walk (K > 40), ring order
-            // for the others (KN_ROW_RING)
+            // the distance-sorted, mirrored table for the whole-block walk (K > 40)
             constexpr bool full = KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40);
-            const bool ring = KN_ROW_RING && !(KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && full));
-            row_order_table(a.H, a.row_order, ring);
-            a.row_mirror = ring ? 0 : 1;
+            row_order_table(a.H, a.row_order, false);
+            a.row_mirror = 1;
             a.n_outer = 0;
-            if (outer_pack_k<KT>() && !full && !ring && !(KN_ROW_ORDER == 1) && a.H >= 2 &&
+            if (outer_pack_k<KT>() && !full && !(KN_ROW_ORDER == 1) && a.H >= 2 &&
                 (2 * a.H + 1) * (2 * a.H + 1) - 9 <= 64) {
                 // the distance-sorted table minus the 3x3 rows around the query's own row
                 unsigned all[32];
