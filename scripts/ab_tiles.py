@@ -14,7 +14,7 @@ k = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 100
 configs = [("", [0, 0, 0]), ("_wg512", [4, 4, 8]), ("_wg512", [4, 8, 4]), ("_wg512", [0, 0, 0]), ("", [4, 4, 8]),
-           ("_wg512", [8, 4, 4])]
+           ("_wg512", [8, 4, 4]), ("_m1", [0, 0, 0]), ("_wg512m1", [4, 4, 8])]
 dev = torch.device("cuda", 0)
 pts = uniform_cloud(n, seed=0, device=dev)
 engines = []

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Every BASELINE.json configuration on one MI355X (run through gpurun from the repo root).
-# Step counts time the steady state (the first ~30 steps after idle run ~10 % slow,
-# profiles/bench_r3_steps.txt).
+# The headline runs at the driver's 20 timed / 5 warmup steps and at 200 / 50 (the GPU's steady
+# clocks: from idle the query kernel takes 304-320 us for its first ~20 steps vs 291 us warm,
+# profiles/r4_coldstart.txt); the other rows time 100-200 steps.
 # One JSON line per configuration -> gpurun_out/bench_suite.jsonl (copy to profiles/).
 #   1. pts20K.xyz, k=8, CPU kd-tree path            (+ the same file on the GPU)
 #   2. 300K uniform, k=16, 1 GPU                     (pts300K.xyz is missing from the reference)
@@ -21,7 +22,7 @@ run() {  # run <timeout> <label> <bench args...>
   local t=$1 label=$2
   shift 2
   echo "== $label: $*" >> $ERR
-  timeout -k 10 $t python bench.py "$@" > gpurun_out/_line.json 2>> $ERR || { echo "FAIL $label"; tail -20 $ERR; exit 1; }
+  MASTER_PORT=$((29600 + RANDOM % 300)) timeout -k 10 $t python bench.py "$@" > gpurun_out/_line.json 2>> $ERR || { echo "FAIL $label"; tail -20 $ERR; exit 1; }
   python - "$label" >> $OUT <<'PY'
 import json, sys
 line = [l for l in open("gpurun_out/_line.json") if l.startswith("{")][-1]
@@ -35,7 +36,11 @@ run 200 "cfg1 pts20K k8 cpu-kdtree" --cpu-oracle --k 8 --steps 5
 run 200 "cfg1b pts20K k8 gpu" --xyz data/pts20K.xyz --k 8 --steps 200 --warmup 50
 run 200 "cfg2 300K uniform k16 gpu" --n 300000 --k 16 --steps 200 --warmup 50
 run 200 "cfg3 900K blue k16 gpu" --gen blue --n 900000 --k 16 --steps 200 --warmup 50
-run 200 "headline 900K uniform k16 gpu" --n 900000 --k 16 --steps 200 --warmup 50
+run 200 "headline 900K uniform k16 gpu, driver 20/5" --n 900000 --k 16 --steps 20 --warmup 5
+run 200 "headline 900K uniform k16 gpu, 200/50" --n 900000 --k 16 --steps 200 --warmup 50
+run 200 "900K uniform k16 gpu, stream of 4 distinct clouds" --n 900000 --k 16 --steps 200 --warmup 50 --stream-clouds 4
+run 200 "900K uniform k16 rccl world1 (native distributed pipeline)" --dist --n 900000 --k 16 --steps 200 --warmup 50
+run 200 "900K uniform k16 rccl world1, forced collectives" --dist --force-collectives --n 900000 --k 16 --steps 200 --warmup 50
 run 200 "900K uniform k50 gpu (reference K)" --n 900000 --k 50 --steps 100 --warmup 30
 run 300 "cfg4 10M uniform k32 gpu" --n 10000000 --k 32 --steps 20 --warmup 5
 run 200 "900K points on surfaces k16 gpu (occupancy-adaptive grid)" --gen surface --n 900000 --k 16 --steps 100 --warmup 20

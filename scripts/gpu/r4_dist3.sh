@@ -34,3 +34,6 @@ timeout -k 10 300 python3 scripts/ab_tiles.py 900000 16 5 100 > "$O/ab_tiles.log
 timeout -k 10 300 python3 scripts/ab_tiles.py 900000 50 3 40 > "$O/ab_tiles50.log" 2>&1 || { tail -20 "$O/ab_tiles50.log"; exit 1; }
 cat "$O/ab_tiles50.log"
 cat "$O/ab_tiles.log"
+timeout -k 10 2400 bash scripts/bench_suite.sh > "$O/suite.log" 2>&1 || { tail -20 "$O/suite.log"; exit 1; }
+cp gpurun_out/bench_suite.jsonl "$O/bench_suite.jsonl"
+tail -20 "$O/suite.log"
