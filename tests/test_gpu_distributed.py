@@ -574,8 +574,11 @@ def test_native_pipeline_loopback_layouts(cuda, world, gen):
 
     def body(t):
         dk = DistributedKNearests(k=16, transport=t)
-        dk.solve(shares[t.rank])
-        r1 = dk.solve(shares[t.rank])  # steady step, torch path (loopback transport)
+        r1 = dk.solve(shares[t.rank])
+        for _ in range(6):  # clustered: full steps widen the halo until nothing is forwarded
+            r1 = dk.solve(shares[t.rank])  # steady step, torch path (loopback transport)
+            if r1.stats.get("steady"):
+                break
         assert r1.valid() and r1.stats.get("steady")
         return dk._steady, r1.ids.clone(), r1.neighbors.clone(), r1.d2.clone()
 
