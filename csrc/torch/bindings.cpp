@@ -1449,13 +1449,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("h_inner") = -1.0, py::arg("wz") = INFINITY);
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
     m.def("rccl_unique_id", &rccl_unique_id, "multi-GPU: a new RCCL unique id (128 bytes) for RankComm");
-    py::class_<PyRankComm, std::shared_ptr<PyRankComm>>(m, "RankComm", "one rank's RCCL communicator (collective init)")
+    py::class_<PyRankComm, std::shared_ptr<PyRankComm>>(m, "RankComm", "one rank's RCCL communicator (collective init)",
+                                                          py::module_local())
         .def(py::init<py::bytes, int64_t, int64_t, int64_t>(), py::arg("uid"), py::arg("world"), py::arg("rank"),
              py::arg("device"))
         .def("async_error", &PyRankComm::async_error)
         .def("abort", &PyRankComm::abort);
     py::class_<PyDistPipe>(m, "DistPipe", "one rank's pipelined distributed step (route + RCCL exchange + build | "
-                                          "query | flag all-reduce), hipGraph-replayed")
+                                          "query | flag all-reduce), hipGraph-replayed",
+                          py::module_local())
         .def(py::init<std::shared_ptr<PyRankComm>, torch::Tensor, c10::optional<torch::Tensor>, torch::Tensor,
                       torch::Tensor, std::vector<int64_t>, std::vector<double>, std::vector<int64_t>,
                       std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>,
@@ -1479,7 +1481,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("profile", &PyDistPipe::profile)
         .def("rows", &PyDistPipe::rows)
         .def("n_owned", &PyDistPipe::n_owned);
-    py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)")
+    py::class_<PyEngine>(m, "Engine", "native single-GPU engine (own arena/stream, hipGraph replay)",
+                        py::module_local())
         .def(py::init<int64_t, double, std::vector<int64_t>, int64_t, bool, bool, bool, int64_t, bool, int64_t>(),
              py::arg("k") = 16, py::arg("points_per_cell") = 0.0, py::arg("tile") = std::vector<int64_t>{},
              py::arg("halo") = 0, py::arg("deterministic") = true, py::arg("use_tiles") = true,
