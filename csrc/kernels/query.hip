@@ -1681,10 +1681,13 @@ template <int KT>
 hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     // margin slots beyond K: a query is lost to the exact path only if the K-th and (K+M)-th
     // distances collide within one truncation ulp (~2^-(23-SB)); M=3 makes that ~1e-7/query.
+    // M = 2 up to K = 32, 1 above: at K = 50 one slot less per candidate outweighs the 3x longer
+    // exact list (900K uniform: 0.967 -> 0.884 ms/step, 110 -> 360 exact queries; at K = 16 M = 1
+    // loses, 0.294 -> 0.329; profiles/ab_r4_tiles_margin.txt). KN_TOPK_MARGIN=m forces m.
 #ifndef KN_TOPK_MARGIN
-#define KN_TOPK_MARGIN 2
+#define KN_TOPK_MARGIN -1
 #endif
-    constexpr int M = KN_TOPK_MARGIN;
+    constexpr int M = KN_TOPK_MARGIN >= 0 ? KN_TOPK_MARGIN : (KT > 32 ? 1 : 2);
     const int X = q.dims[0], Y = q.dims[1], Z = q.dims[2];
     hipError_t e = hipSuccess;
     if (q.exact_mode != 2 && !q.counters_zeroed &&

@@ -725,11 +725,12 @@ kn_status Engine::ensure_pipeline() {
     return KN_OK;
 }
 
-// Steps per graph launch of the resident pipeline: 4 (900K, K=16, 200 steps: 0.310 ms per step
-// with one graph per stage and step, 0.296 with 4 steps per graph; profiles/r4_pipe_unroll.txt)
+// Steps per graph launch of the resident pipeline: 10 (900K, K=16, 200 steps: 0.310 ms per step
+// with one graph per stage and step, 0.296 with 4 steps per graph, 0.293 with 10; at the
+// driver's 20 steps 0.318 / 0.310 for 4 / 10; profiles/r4_pipe_unroll.txt)
 static int pipe_unroll_default() {
     const char* v = std::getenv("KN_PIPE_UNROLL");
-    return v ? std::atoi(v) : 4;
+    return v ? std::atoi(v) : 10;
 }
 
 // Software-pipelined steps over two grid sets (pipeline.hpp): build(i+1) on bstream_ while

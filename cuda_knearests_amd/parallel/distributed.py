@@ -219,7 +219,7 @@ class DistributedKNearests:
         if force_collectives is None:
             force_collectives = os.environ.get("KN_DIST_FORCE_COLLECTIVES") == "1"
         self.force_collectives = bool(force_collectives)
-        self.pipe_unroll = int(os.environ.get("KN_DIST_UNROLL", "4"))  # steps per graph in run_steps
+        self.pipe_unroll = int(os.environ.get("KN_DIST_UNROLL", "10"))  # steps per graph in run_steps
         self.wait_timeout_s = float(timeout_s) if timeout_s else 300.0
         self._rcomm = None
         self._pipe = None

@@ -32,6 +32,12 @@ static double now_ms() {
         }                                                                           \
     } while (0)
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__global__ void copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n4) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(src[i], &dst[i]);
+}
+
 static void par_copy(void* dst, const void* src, size_t bytes, int nt) {
 #pragma omp parallel num_threads(nt)
     {
@@ -100,6 +106,31 @@ int main(int argc, char** argv) {
     auto timed_free = [](void* p, double* extra) { const double a = now_ms(); free(p); *extra += now_ms() - a; };
 
     run("dma_pinned", [&](double*) { CK(hipMemcpyAsync(pin, d, bytes, hipMemcpyDeviceToHost, s)); CK(hipStreamSynchronize(s)); });
+    {
+        hipStream_t ss[4];
+        for (auto& x : ss) CK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        for (int parts : {2, 4}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "dma_pinned_split%d", parts);
+            run(nm, [&](double*) {
+                const size_t per = (bytes / parts + 4095) & ~(size_t)4095;
+                for (int i = 0; i < parts; ++i) {
+                    const size_t a = std::min(bytes, (size_t)i * per), z = std::min(bytes, a + per);
+                    if (z > a) CK(hipMemcpyAsync((char*)pin + a, (const char*)d + a, z - a, hipMemcpyDeviceToHost, ss[i]));
+                }
+                for (int i = 0; i < parts; ++i) CK(hipStreamSynchronize(ss[i]));
+            });
+        }
+        for (int blocks : {64, 256, 1024}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "kernel_to_pinned_b%d", blocks);
+            run(nm, [&](double*) {
+                copy_kernel<<<blocks, 256, 0, s>>>((const u32x4*)d, (u32x4*)pin, bytes / 16);
+                CK(hipStreamSynchronize(s));
+            });
+        }
+        for (auto& x : ss) CK(hipStreamDestroy(x));
+    }
     run("dma_pageable_reused", [&](double*) { CK(hipMemcpyAsync(reused.data(), d, bytes, hipMemcpyDeviceToHost, s)); CK(hipStreamSynchronize(s)); });
     run("dma_pageable_fresh", [&](double* x) {
         void* h = malloc(bytes);
