@@ -10,6 +10,7 @@
 #pragma once
 
 #include <hip/hip_runtime_api.h>
+#include <math.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -34,6 +35,40 @@ struct GridGeom {
 // `wide` = h_e - h_i when the query's distance to the domain plus that margin stays below
 // `zlim` (w minus a rounding slack): every point of the ball it certifies then lies in the wide
 // zone. wide = 0: one width (single GPU: all zero, the margins are infinite anyway).
+// Density-adaptive halo (round 4, kn/route.h): a width field over a G^3 cell grid of the global
+// domain. Every routing, splat and certification kernel maps a point to its cell with this one
+// function, so the three agree bit for bit.
+struct FieldGeom {
+    float lo[3];
+    float inv[3];  // G / domain extent
+    int g;         // cells per axis (0: no field)
+    float rstep;   // radius certified per neighbourhood ring: level m covers r <= m * rstep
+};
+__host__ __device__ inline FieldGeom field_geom(const float lo[3], const float hi[3], int g) {
+    FieldGeom f{};
+    float inv_max = 0.f;
+    for (int a = 0; a < 3; ++a) {
+        f.lo[a] = lo[a];
+        const float ext = hi[a] - lo[a] > 1e-30f ? hi[a] - lo[a] : 1e-30f;
+        f.inv[a] = (float)g / ext;
+        inv_max = f.inv[a] > inv_max ? f.inv[a] : inv_max;
+    }
+    f.g = g;
+    // 0.2 % below a cell: a point within m * rstep of a query lies within m cells of it on every
+    // axis despite the rounding of the cell coordinates
+    f.rstep = g > 0 ? 0.998f / inv_max : 0.f;
+    return f;
+}
+__host__ __device__ inline int field_axis(const FieldGeom& f, float v, int a) {
+    int i = (int)floorf((v - f.lo[a]) * f.inv[a]);
+    i = i < 0 ? 0 : i;
+    return i > f.g - 1 ? f.g - 1 : i;
+}
+__host__ __device__ inline int field_cell(const FieldGeom& f, float x, float y, float z) {
+    return field_axis(f, x, 0) + f.g * (field_axis(f, y, 1) + f.g * field_axis(f, z, 2));
+}
+constexpr int kFieldLevels = 3;  // neighbourhood rings of the splat / certification
+
 struct CompleteBox {
     float lo[3];
     float hi[3];
@@ -41,6 +76,10 @@ struct CompleteBox {
     float zlim;
     float dlo[3];
     float dhi[3];
+    // density-adaptive halo: radius certified at each field cell (null: none). The own box
+    // (lo / hi, no halo) certifies a query's ball inside it; cfield[cell] one that reaches out.
+    const float* cfield;
+    FieldGeom fg;
 };
 
 constexpr int kScanItems = 4096;  // elements per scan block (256 threads x 16)

@@ -25,21 +25,26 @@ __device__ __forceinline__ float complete_margin(const CompleteBox& cb, float q,
 // Radius up to which the query's K-th ball is certified by the rank's complete box: the smallest
 // face margin, each face widened by cb.wide when the whole ball then stays in the wide zone
 // (position-dependent halo, CompleteBox). wide = 0 (uniform halo, single GPU): the box margin.
+// Density-adaptive halo (cb.cfield): the larger of the own-box margin and the radius the field
+// certifies at the query's cell.
 __device__ __forceinline__ float complete_margin3(const CompleteBox& cb, float x, float y, float z) {
-    if (!(cb.wide > 0.f))
-        return fminf(fminf(complete_margin(cb, x, 0), complete_margin(cb, y, 1)), complete_margin(cb, z, 2));
-    const float q[3] = {x, y, z};
-    float zq = INFINITY;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) zq = fminf(zq, fminf(q[a] - cb.dlo[a], cb.dhi[a] - q[a]));
     float m = INFINITY;
+    if (!(cb.wide > 0.f)) {
+        m = fminf(fminf(complete_margin(cb, x, 0), complete_margin(cb, y, 1)), complete_margin(cb, z, 2));
+    } else {
+        const float q[3] = {x, y, z};
+        float zq = INFINITY;
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        float lo = q[a] - cb.lo[a], hi = cb.hi[a] - q[a];  // +inf on domain faces
-        if (zq + lo + cb.wide <= cb.zlim) lo += cb.wide;
-        if (zq + hi + cb.wide <= cb.zlim) hi += cb.wide;
-        m = fminf(m, fminf(lo, hi));
+        for (int a = 0; a < 3; ++a) zq = fminf(zq, fminf(q[a] - cb.dlo[a], cb.dhi[a] - q[a]));
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            float lo = q[a] - cb.lo[a], hi = cb.hi[a] - q[a];  // +inf on domain faces
+            if (zq + lo + cb.wide <= cb.zlim) lo += cb.wide;
+            if (zq + hi + cb.wide <= cb.zlim) hi += cb.wide;
+            m = fminf(m, fminf(lo, hi));
+        }
     }
+    if (cb.cfield) m = fmaxf(m, cb.cfield[field_cell(cb.fg, x, y, z)]);
     return m;
 }
 

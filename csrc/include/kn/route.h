@@ -27,6 +27,12 @@ struct RouteParams {
     float hi2;
     float wz;
     float dom_hi[3];  // global domain upper corner (lower: lo)
+    // Density-adaptive halo (field != null): a point in field cell c is sent to every rank whose
+    // box is within field[c] (+ fslack) -- the widths splatted from the previous full step's
+    // measured K-th distances (launch_field_splat); h2 / hi2 / wz are then unused.
+    const float* field;
+    FieldGeom fg;
+    float fslack;
     int id_offset;  // global id of this rank's first point (route_scatter with ids == nullptr)
     float box_lo[kRouteMaxWorld][3];  // rank boxes (same formula as SpatialDecomposition.rank_box)
     float box_hi[kRouteMaxWorld][3];
@@ -50,6 +56,8 @@ constexpr int kPlanHdr = 24;
 // [8] n_total  [9] id offset of this rank  [10] 1 if the halo covers the whole domain
 // [11] domain diagonal  [12..14] this rank's box lo  [15..17] its box hi
 // [18] h_i (interior width)  [19] its send width  [20] wide-zone width w  [21] w - rounding slack
+// [22] 1 if the plan routes with a halo field (then [6] = [18] = 0: the complete box is the own
+//      box, the field certifies the rest)  [23] the field's largest width
 
 // The local geometry of `rank` from its plan header -- ONE definition for every distributed
 // runtime (the torch binding's dist_local and the C-API kn_solve_multi): the complete box (own box
@@ -61,7 +69,9 @@ struct RankLocal {
     double box[6];  // lo[3], hi[3]
     float ext[3];
 };
-RankLocal rank_local(const double* hdr, int rank, const int grid[3]);
+// cert_field (optional): the rank's certification field (launch_field_cert) for a field plan.
+RankLocal rank_local(const double* hdr, int rank, const int grid[3], const float* cert_field = nullptr,
+                     int field_g = 0);
 
 // Receive-side table: source s's segment starts at seg[s], holds own[s] owned rows then its
 // halo rows; owned rows of all sources go first (own_pref), then halo rows (halo_pref).
@@ -130,9 +140,27 @@ hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int 
 // inner_factor > 0: the interior width h_i = min(h, inner_factor x that radius) for points
 // farther than w = h + h_i from the domain faces (0: one width).
 // splits: optional device array (route_split_count(grid) floats): count-balanced boxes.
+// field (optional, device, field_g^3 widths): route with the density-adaptive halo field instead
+// of the global widths (unless its largest width reaches the domain diagonal).
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
                              double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s,
-                             double inner_factor = 0.0);
+                             double inner_factor = 0.0, const float* field = nullptr, int field_g = 0);
+// ---- density-adaptive halo field (round 4) ----------------------------------------------------
+// After a full step: every owned query whose K-th ball leaves the own box (own_lo / own_hi, +-inf
+// on domain faces) raises the width of every field cell within m rings of its own cell to its
+// K-th distance R (atomic max; m = the smallest ring count with R <= m * rstep, <= kFieldLevels).
+// The ranks' fields are then MAX-all-reduced. pts: the rank's local rows (owned first), d2:
+// (n_owned, k) squared distances. stat[0] += queries with fewer than K neighbours, stat[1] += queries
+// beyond kFieldLevels rings (neither can be certified by the field). slack: absolute width added
+// to R (>= the certification's rounding slack).
+hipError_t launch_field_splat(const float* pts, int n_owned, const float* d2, int k, const float own_lo[3],
+                              const float own_hi[3], const FieldGeom& fg, float slack, float* field, unsigned* stat,
+                              hipStream_t s);
+// cert[c] = max over m <= kFieldLevels of min(m * rstep, min of field over the m-ring
+// neighbourhood of c): the radius up to which a query in cell c has every point of its ball.
+hipError_t launch_field_cert(const float* field, const FieldGeom& fg, float* cert, hipStream_t s);
+// The field geometry of a plan header (global domain [0..5]) with G cells per axis.
+FieldGeom field_geom_hdr(const double* hdr, int g);
 // Interior halo factor for K neighbours: the smallest f (steps of 0.05) for which a uniform
 // cloud's K-th neighbour distance exceeds f x the expected (K+1)-point radius with probability
 // <= 1e-12 (Poisson tail P[Poisson((K+1) f^3) <= K-1]); K=16 -> 1.55, K=1 -> 2.4, K=50 -> 1.35.

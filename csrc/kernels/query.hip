@@ -1681,13 +1681,16 @@ template <int KT>
 hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     // margin slots beyond K: a query is lost to the exact path only if the K-th and (K+M)-th
     // distances collide within one truncation ulp (~2^-(23-SB)); M=3 makes that ~1e-7/query.
-    // M = 2 up to K = 32, 1 above: at K = 50 one slot less per candidate outweighs the 3x longer
-    // exact list (900K uniform: 0.967 -> 0.884 ms/step, 110 -> 360 exact queries; at K = 16 M = 1
-    // loses, 0.294 -> 0.329; profiles/ab_r4_tiles_margin.txt). KN_TOPK_MARGIN=m forces m.
+    // The lane-walk kernel (the default) takes M = 1 above K = 32: at K = 50 one slot less per
+    // candidate outweighs the 3x longer exact list (900K uniform: 0.967 -> 0.884 ms/step, 110 ->
+    // 360 exact queries; at K = 16 M = 1 loses, 0.294 -> 0.329; profiles/ab_r4_tiles_margin.txt).
+    // The union-stream and staging-free kernels keep M = 2 (the stream kernel's rows differ from
+    // the oracle with M = 1 at K = 50). KN_TOPK_MARGIN=m forces m for the lane walk.
 #ifndef KN_TOPK_MARGIN
 #define KN_TOPK_MARGIN -1
 #endif
-    constexpr int M = KN_TOPK_MARGIN >= 0 ? KN_TOPK_MARGIN : (KT > 32 ? 1 : 2);
+    constexpr int M = 2;
+    constexpr int ML = KN_TOPK_MARGIN >= 0 ? KN_TOPK_MARGIN : (KT > 32 ? 1 : 2);
     const int X = q.dims[0], Y = q.dims[1], Z = q.dims[2];
     hipError_t e = hipSuccess;
     if (q.exact_mode != 2 && !q.counters_zeroed &&
@@ -1754,9 +1757,9 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             if constexpr (KT <= 64) {
                 (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M, false>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M, true>,
+                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, ML, true>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, M, true, true>,
+                (void)hipFuncSetAttribute((const void*)knn_tile_kernel<KT, ML, true, true>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
             }
             attr_set = true;
@@ -1764,8 +1767,8 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         if constexpr (KT <= 64) {
             const bool wide = kWin2 > 0 && (q.flags & kQueryWide);
             if (query_algo(q.flags, q.k) != kAlgoLane) knn_tile_kernel<KT, M, false><<<nt, kWG, lds, s>>>(a);
-            else if (wide) knn_tile_kernel<KT, M, true, true><<<nt, kWG, lds, s>>>(a);
-            else knn_tile_kernel<KT, M, true><<<nt, kWG, lds, s>>>(a);
+            else if (wide) knn_tile_kernel<KT, ML, true, true><<<nt, kWG, lds, s>>>(a);
+            else knn_tile_kernel<KT, ML, true><<<nt, kWG, lds, s>>>(a);
         }
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;

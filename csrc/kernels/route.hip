@@ -59,10 +59,17 @@ __device__ __forceinline__ int route_owner(const RouteParams& p, float x, float 
 __device__ __forceinline__ unsigned long long route_halo(const RouteParams& p, float x, float y, float z,
                                                          int owner) {
     unsigned long long m = 0;
-    // position-dependent width: the edge width in the wide zone near the domain faces
-    const float zp = fminf(fminf(fminf(x - p.lo[0], p.dom_hi[0] - x), fminf(y - p.lo[1], p.dom_hi[1] - y)),
-                           fminf(z - p.lo[2], p.dom_hi[2] - z));
-    const float h2 = zp <= p.wz ? p.h2 : p.hi2;
+    float h2;
+    if (p.field) {
+        // density-adaptive halo: the width of the point's field cell
+        const float w = fmaf(p.field[field_cell(p.fg, x, y, z)], 1.0001f, p.fslack);
+        h2 = w * w;
+    } else {
+        // position-dependent width: the edge width in the wide zone near the domain faces
+        const float zp = fminf(fminf(fminf(x - p.lo[0], p.dom_hi[0] - x), fminf(y - p.lo[1], p.dom_hi[1] - y)),
+                               fminf(z - p.lo[2], p.dom_hi[2] - z));
+        h2 = zp <= p.wz ? p.h2 : p.hi2;
+    }
     for (int r = 0; r < p.world; ++r) {
         if (r == owner) continue;
         const float dx = __fadd_rn(fmaxf(__fsub_rn(p.box_lo[r][0], x), 0.f), fmaxf(__fsub_rn(x, p.box_hi[r][0]), 0.f));
@@ -295,7 +302,15 @@ __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restr
 // Formulas follow SpatialDecomposition / DistributedKNearests (parallel/*.py) in double.
 __global__ void route_plan_kernel(const double* __restrict__ metas, int world, int rank, int gx, int gy, int gz,
                                   int k, double halo_factor, double inner_factor, const float* __restrict__ splits,
-                                  RouteParams* __restrict__ p, double* __restrict__ hdr) {
+                                  RouteParams* __restrict__ p, double* __restrict__ hdr,
+                                  const float* __restrict__ field, int field_g) {
+    // the halo field's largest width (one wave; widths >= 0 order as their bits)
+    unsigned fmax_bits = 0u;
+    if (field) {
+        const int cells = field_g * field_g * field_g;
+        for (int c = threadIdx.x; c < cells; c += 64) fmax_bits = max(fmax_bits, __float_as_uint(field[c]));
+        fmax_bits = wave_max_u32(fmax_bits);
+    }
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     double lo[3], hi[3];
     double ntot = 0.0, off = 0.0;
@@ -321,14 +336,21 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     }
     vol = fmax(vol, 1e-30);
     const double rk = cbrt(3.0 * (k + 1) * vol / (4.0 * M_PI * fmax(1.0, ntot)));
-    const double h = halo_factor * rk;
     const double diag = sqrt(diag2);
+    // halo field: the send width of a cell is its field value (x 1.0001 + fslack); the complete
+    // box is the own box (certification width 0) plus the field's certified radii. A field whose
+    // widest cell reaches the diagonal falls back to the global widths.
+    const double fslack = 1e-5 * scale;
+    const double fmax = (double)__uint_as_float(fmax_bits);
+    const bool use_field = field && field_g > 0 && fmax * 1.0001 + fslack < diag;
+    const double h = use_field ? 0.0 : halo_factor * rk;
     const bool full = h >= diag;
-    const double hs = full ? 2.0 * diag + 1.0 : h * (1.0 + 1e-5) + 1e-5 * scale;
+    const double hs = use_field ? fmax * 1.0001 + 2.0 * fslack
+                    : full ? 2.0 * diag + 1.0 : h * (1.0 + 1e-5) + 1e-5 * scale;
     // interior width (position-dependent halo): h_i <= h, sent to points farther than w = h + h_i
     // from the domain faces; the certification's zone limit keeps a rounding slack below w
     const double hi_ = inner_factor > 0.0 ? fmin(h, inner_factor * rk) : h;
-    const double his = full ? hs : hi_ * (1.0 + 1e-5) + 1e-5 * scale;
+    const double his = full || use_field ? hs : hi_ * (1.0 + 1e-5) + 1e-5 * scale;
     const double wz = h + hi_;
     const int g[3] = {gx, gy, gz};
     for (int a = 0; a < 3; ++a) {
@@ -345,6 +367,13 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     p->hi2 = hif * hif;
     p->wz = (float)wz;
     for (int a = 0; a < 3; ++a) p->dom_hi[a] = (float)hi[a];
+    p->field = use_field ? field : nullptr;
+    {
+        const float fl[3] = {(float)lo[0], (float)lo[1], (float)lo[2]};
+        const float fh[3] = {(float)hi[0], (float)hi[1], (float)hi[2]};
+        p->fg = field_geom(fl, fh, use_field ? field_g : 0);
+    }
+    p->fslack = (float)fslack;
     p->id_offset = (int)off;
     p->balanced = splits ? 1 : 0;
     const int nxs = gx + 1, nys = gx * (gy + 1), nzs = gx * gy * (gz + 1);
@@ -391,6 +420,68 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     hdr[19] = his;
     hdr[20] = wz;
     hdr[21] = wz - 1e-5 * scale;
+    hdr[22] = use_field ? 1.0 : 0.0;
+    hdr[23] = use_field ? fmax : 0.0;
+}
+
+// ---- density-adaptive halo field ------------------------------------------------------------
+__global__ void field_splat_kernel(const float* __restrict__ pts, int n_owned, const float* __restrict__ d2, int k,
+                                   float3 olo, float3 ohi, FieldGeom fg, float slack, unsigned* __restrict__ field,
+                                   unsigned* __restrict__ stat) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_owned) return;
+    const float dk = d2[(size_t)j * k + (k - 1)];
+    if (!(dk < INFINITY)) {  // fewer than K neighbours in the whole cloud
+        atomicAdd(stat + 0, 1u);
+        return;
+    }
+    const float x = pts[3 * (size_t)j], y = pts[3 * (size_t)j + 1], z = pts[3 * (size_t)j + 2];
+    const float margin = fminf(fminf(fminf(x - olo.x, ohi.x - x), fminf(y - olo.y, ohi.y - y)),
+                               fminf(z - olo.z, ohi.z - z));
+    // R: the K-th distance rounded up, plus the slack the certification subtracts
+    const float R = fmaf(sqrtf(dk), 1.000001f, slack);
+    if (R <= margin) return;  // the ball stays in the own box
+    int m = 1;
+    while (m < kFieldLevels && R > (float)m * fg.rstep) ++m;
+    if (R > (float)m * fg.rstep) atomicAdd(stat + 1, 1u);  // past the field's reach: forwarded
+    const int cx = field_axis(fg, x, 0), cy = field_axis(fg, y, 1), cz = field_axis(fg, z, 2);
+    const unsigned rb = __float_as_uint(R);
+    for (int zz = max(0, cz - m); zz <= min(fg.g - 1, cz + m); ++zz)
+        for (int yy = max(0, cy - m); yy <= min(fg.g - 1, cy + m); ++yy)
+            for (int xx = max(0, cx - m); xx <= min(fg.g - 1, cx + m); ++xx)
+                atomicMax(field + (xx + fg.g * (yy + fg.g * zz)), rb);
+}
+
+__global__ void field_cert_kernel(const float* __restrict__ field, FieldGeom fg, float* __restrict__ cert) {
+    const int G = fg.g;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= G * G * G) return;
+    const int cx = c % G, cy = (c / G) % G, cz = c / (G * G);
+    float mn[kFieldLevels + 1];
+#pragma unroll
+    for (int m = 0; m <= kFieldLevels; ++m) mn[m] = INFINITY;
+    constexpr int L = kFieldLevels;
+    for (int dz = -L; dz <= L; ++dz) {
+        const int zz = cz + dz;
+        if (zz < 0 || zz >= G) continue;
+        for (int dy = -L; dy <= L; ++dy) {
+            const int yy = cy + dy;
+            if (yy < 0 || yy >= G) continue;
+            for (int dx = -L; dx <= L; ++dx) {
+                const int xx = cx + dx;
+                if (xx < 0 || xx >= G) continue;
+                const int ring = max(max(abs(dx), abs(dy)), abs(dz));
+                const float v = field[xx + G * (yy + G * zz)];
+#pragma unroll
+                for (int m = 1; m <= L; ++m)
+                    if (ring <= m) mn[m] = fminf(mn[m], v);
+            }
+        }
+    }
+    float r = 0.f;
+#pragma unroll
+    for (int m = 1; m <= L; ++m) r = fmaxf(r, fminf(mn[m], (float)m * fg.rstep));
+    cert[c] = r;
 }
 
 inline unsigned cdiv(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
@@ -693,12 +784,37 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
 
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
                              double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s,
-                             double inner_factor) {
+                             double inner_factor, const float* field, int field_g) {
     if (world < 1 || world > kRouteMaxWorld || grid[0] * grid[1] * grid[2] != world || rank < 0 || rank >= world)
         return hipErrorInvalidValue;
+    if (field && (field_g < 1 || field_g > 256)) return hipErrorInvalidValue;
     route_plan_kernel<<<1, 64, 0, s>>>(metas, world, rank, grid[0], grid[1], grid[2], k, halo_factor, inner_factor,
-                                       splits, p, hdr);
+                                       splits, p, hdr, field, field ? field_g : 0);
     return hipGetLastError();
+}
+
+hipError_t launch_field_splat(const float* pts, int n_owned, const float* d2, int k, const float own_lo[3],
+                              const float own_hi[3], const FieldGeom& fg, float slack, float* field, unsigned* stat,
+                              hipStream_t s) {
+    if (fg.g < 1 || fg.g > 256 || k < 1 || n_owned < 0) return hipErrorInvalidValue;
+    if (n_owned > 0)
+        field_splat_kernel<<<cdiv((size_t)n_owned, 256), 256, 0, s>>>(
+            pts, n_owned, d2, k, make_float3(own_lo[0], own_lo[1], own_lo[2]),
+            make_float3(own_hi[0], own_hi[1], own_hi[2]), fg, slack, reinterpret_cast<unsigned*>(field), stat);
+    return hipGetLastError();
+}
+
+hipError_t launch_field_cert(const float* field, const FieldGeom& fg, float* cert, hipStream_t s) {
+    if (fg.g < 1 || fg.g > 256) return hipErrorInvalidValue;
+    const size_t cells = (size_t)fg.g * fg.g * fg.g;
+    field_cert_kernel<<<cdiv(cells, 256), 256, 0, s>>>(field, fg, cert);
+    return hipGetLastError();
+}
+
+FieldGeom field_geom_hdr(const double* hd, int g) {
+    const float lo[3] = {(float)hd[0], (float)hd[1], (float)hd[2]};
+    const float hi[3] = {(float)hd[3], (float)hd[4], (float)hd[5]};
+    return field_geom(lo, hi, g);
 }
 
 hipError_t launch_route_unpack(const float4* recv, const float4* self_rows, int rows, const UnpackTable& t,
@@ -778,8 +894,13 @@ hipError_t launch_fwd_merge(int world, int F, int k, const unsigned* uncert, con
     return hipGetLastError();
 }
 
-RankLocal rank_local(const double* hd, int rank, const int grid[3]) {
+RankLocal rank_local(const double* hd, int rank, const int grid[3], const float* cert_field, int field_g) {
     RankLocal r{};
+    if (hd[22] != 0.0 && cert_field && field_g > 0) {
+        // a field plan ([6] = [18] = 0 below: the complete box is the own box)
+        r.complete.cfield = cert_field;
+        r.complete.fg = field_geom_hdr(hd, field_g);
+    }
     const double h = hd[6], hs = hd[7];
     const bool full = hd[10] != 0.0;
     // interior width (position-dependent halo); a header without one (0): the single width

@@ -168,7 +168,7 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
         if (p_.place[2] != rows_) { fail("self placement does not match the local rows"); return; }
     }
     // local geometry and the query plan: the same arithmetic as the torch binding's dist_local
-    const RankLocal rl = rank_local(p_.hdr.data(), p_.rank, p_.grid);
+    const RankLocal rl = rank_local(p_.hdr.data(), p_.rank, p_.grid, p_.cert_field, p_.field_g);
     complete_ = rl.complete;
     const int th[3] = {0, 0, 0};
     AutoParams ap = auto_params(rows_, p_.k, p_.ppc, th, 0, rl.ext);

@@ -69,6 +69,10 @@ struct DistPlan {
     // world 1, forced collectives: the rank's own rows go through an RCCL self send / recv and
     // the unpack instead of straight into the local set (exercises the exchange on one GPU)
     int self_via_comm = 0;
+    // halo field plan (hdr[22] != 0): the certified radii of the field cells (device, G^3 floats,
+    // alive as long as the pipeline); the route plan holds the width field's pointer itself
+    const float* cert_field = nullptr;
+    int field_g = 0;
 };
 
 class DistPipeline {

@@ -114,14 +114,15 @@ std::vector<torch::Tensor> build(torch::Tensor points, std::vector<int64_t> dims
     return build_impl(points, dims, deterministic, box);
 }
 
-std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom,
-                                 std::vector<int64_t> dims, int64_t k, int64_t n_queries,
-                                 c10::optional<torch::Tensor> id_map, std::vector<double> complete,
-                                 std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
-                                 bool use_tiles, bool with_dist, int64_t flags,
-                                 c10::optional<torch::Tensor> row_of, int64_t exact_grid = 0,
-                                 c10::optional<torch::Tensor> zeroed_counters = c10::nullopt, int64_t q_lo = 0,
-                                 int64_t xsub = 1) {
+// cbp (internal callers): the complete box itself (e.g. with a halo field), overriding `complete`
+std::vector<torch::Tensor> query_impl(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom,
+                                      std::vector<int64_t> dims, int64_t k, int64_t n_queries,
+                                      c10::optional<torch::Tensor> id_map, std::vector<double> complete,
+                                      std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
+                                      bool use_tiles, bool with_dist, int64_t flags,
+                                      c10::optional<torch::Tensor> row_of, int64_t exact_grid,
+                                      c10::optional<torch::Tensor> zeroed_counters, int64_t q_lo,
+                                      int64_t xsub, const kn::CompleteBox* cbp) {
     TORCH_CHECK(sorted.is_cuda() && sorted.dim() == 2 && sorted.size(1) == 4 && sorted.scalar_type() == torch::kFloat32,
                 "sorted must be a (N,4) float32 GPU tensor");
     TORCH_CHECK(cell_start.is_cuda() && cell_start.scalar_type() == torch::kInt32, "cell_start must be int32 GPU");
@@ -166,7 +167,7 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
                     "row_of must be an int32 GPU tensor with >= N entries");
         q.row_of = reinterpret_cast<const unsigned*>(row_of->data_ptr<int>());
     }
-    q.complete = complete_box(complete);
+    q.complete = cbp ? *cbp : complete_box(complete);
     q.out_idx = reinterpret_cast<unsigned*>(out_idx.data_ptr<int>());
     q.out_dist = with_dist ? out_dist.data_ptr<float>() : nullptr;
     q.fallback_list = reinterpret_cast<unsigned*>(fallback.data_ptr<int>());
@@ -188,6 +189,18 @@ std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start,
     KN_CHECK_HIP(kn::launch_query(q, s));
     if (!with_dist) out_dist = torch::empty({0}, sorted.options());
     return {out_idx, out_dist, counters, uncert, fallback};
+}
+
+std::vector<torch::Tensor> query(torch::Tensor sorted, torch::Tensor cell_start, torch::Tensor geom,
+                                 std::vector<int64_t> dims, int64_t k, int64_t n_queries,
+                                 c10::optional<torch::Tensor> id_map, std::vector<double> complete,
+                                 std::vector<int64_t> tile, int64_t halo, int64_t lds_capacity,
+                                 bool use_tiles, bool with_dist, int64_t flags,
+                                 c10::optional<torch::Tensor> row_of, int64_t exact_grid = 0,
+                                 c10::optional<torch::Tensor> zeroed_counters = c10::nullopt, int64_t q_lo = 0,
+                                 int64_t xsub = 1) {
+    return query_impl(sorted, cell_start, geom, dims, k, n_queries, id_map, complete, tile, halo, lds_capacity,
+                      use_tiles, with_dist, flags, row_of, exact_grid, zeroed_counters, q_lo, xsub, nullptr);
 }
 
 // Morton-leaf tree over a built grid's points (kn/tree.h): (workspace, node buffer, leaf count).
@@ -432,10 +445,23 @@ const float* splits_ptr(const c10::optional<torch::Tensor>& splits, const std::v
     return splits->data_ptr<float>();
 }
 
+// (pointer, G) of an optional halo-field tensor (G^3 float32 widths or certified radii, on the GPU)
+static std::pair<float*, int> field_arg(const c10::optional<torch::Tensor>& f) {
+    if (!f.has_value()) return {nullptr, 0};
+    TORCH_CHECK(f->is_cuda() && f->scalar_type() == torch::kFloat32 && f->is_contiguous(),
+                "a halo field must be a contiguous float32 GPU tensor");
+    const int64_t n = f->numel();
+    const int g = (int)std::lround(std::cbrt((double)n));
+    TORCH_CHECK(g >= 1 && g <= 256 && (int64_t)g * g * g == n, "a halo field holds G^3 floats, G in [1, 256]");
+    return {f->data_ptr<float>(), g};
+}
+
 // Device-side plan from the all-gathered metas (world x 8 float64, on device): no host sync.
 // -> (plan (uint8 RouteParams on device), header (16,) float64 on device, see kn::kPlanHdr)
 std::vector<torch::Tensor> route_plan(torch::Tensor metas, int64_t rank, std::vector<int64_t> grid, int64_t k,
-                                      double halo_factor, c10::optional<torch::Tensor> splits, double inner_factor) {
+                                      double halo_factor, c10::optional<torch::Tensor> splits, double inner_factor,
+                                      c10::optional<torch::Tensor> field) {
+    const auto fa = field_arg(field);
     TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
                     metas.numel() % 8 == 0,
                 "metas must be a contiguous (world*8,) float64 GPU tensor");
@@ -448,7 +474,7 @@ std::vector<torch::Tensor> route_plan(torch::Tensor metas, int64_t rank, std::ve
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor,
                                        splits_ptr(splits, grid), reinterpret_cast<kn::RouteParams*>(plan.data_ptr<uint8_t>()),
-                                       hdr.data_ptr<double>(), s, inner_factor));
+                                       hdr.data_ptr<double>(), s, inner_factor, fa.first, fa.second));
     return {plan, hdr};
 }
 
@@ -480,8 +506,10 @@ torch::Tensor route_scatter_dev(torch::Tensor points, c10::optional<torch::Tenso
 // -> (plan, sync, scanned block counts, send (cap, 4))
 std::vector<torch::Tensor> route_begin(torch::Tensor points, c10::optional<torch::Tensor> ids, torch::Tensor metas,
                                        int64_t rank, std::vector<int64_t> grid, int64_t k, double halo_factor,
-                                       int64_t cap, c10::optional<torch::Tensor> splits, double inner_factor) {
+                                       int64_t cap, c10::optional<torch::Tensor> splits, double inner_factor,
+                                       c10::optional<torch::Tensor> field) {
     check_points(points, true);
+    const auto fa = field_arg(field);
     TORCH_CHECK(cap >= 0 && cap < INT32_MAX, "cap out of range");
     TORCH_CHECK(metas.is_cuda() && metas.scalar_type() == torch::kFloat64 && metas.is_contiguous() &&
                     metas.numel() % 8 == 0 && metas.numel() >= 8,
@@ -508,7 +536,8 @@ std::vector<torch::Tensor> route_begin(torch::Tensor points, c10::optional<torch
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
     KN_CHECK_HIP(kn::launch_route_plan(metas.data_ptr<double>(), world, (int)rank, g, (int)k, halo_factor,
                                        splits_ptr(splits, grid), pp,
-                                       reinterpret_cast<double*>(sync.data_ptr<int>()), s, inner_factor));
+                                       reinterpret_cast<double*>(sync.data_ptr<int>()), s, inner_factor, fa.first,
+                                       fa.second));
     KN_CHECK_HIP(kn::launch_route_count(points.data_ptr<float>(), n, pp, world, bc.data_ptr<int>(), totals, s));
     KN_CHECK_HIP(kn::launch_route_scatter(points.data_ptr<float>(), idp, n, pp, world, bc.data_ptr<int>(), totals,
                                           reinterpret_cast<float4*>(send.data_ptr<float>()), (int)cap, (int)rank, s));
@@ -592,6 +621,49 @@ std::vector<torch::Tensor> route_unpack_split(torch::Tensor recv, torch::Tensor 
     return {pts, gids};
 }
 
+// Density-adaptive halo field (kn/route.h): splat this rank's measured K-th distances into
+// `field` (G^3 float32, zeroed by the caller, then MAX-all-reduced over the ranks). pts: the local
+// rows (owned first), d2: (n_owned, k). -> stat (2 int32 on device: queries with < K neighbours,
+// queries beyond the field's reach).
+torch::Tensor field_splat(torch::Tensor pts, int64_t n_owned, torch::Tensor d2, int64_t k, std::vector<double> hdr,
+                          int64_t rank, std::vector<int64_t> grid, torch::Tensor field) {
+    check_points(pts, true);
+    TORCH_CHECK(grid.size() == 3 && hdr.size() >= (size_t)kn::kPlanHdr, "grid must have 3 entries, hdr kPlanHdr");
+    TORCH_CHECK(n_owned >= 0 && n_owned <= pts.size(0), "n_owned out of range");
+    TORCH_CHECK(d2.is_cuda() && d2.scalar_type() == torch::kFloat32 && d2.is_contiguous() && d2.numel() >= n_owned * k,
+                "d2 must be a contiguous (n_owned, k) float32 GPU tensor");
+    const auto fa = field_arg(field);
+    const c10::DeviceGuard guard(pts.device());
+    const int gi[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
+    const int c[3] = {(int)(rank % gi[0]), (int)((rank / gi[0]) % gi[1]), (int)(rank / (gi[0] * gi[1]))};
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {  // the own box, unbounded on domain faces (rank_local with h = 0)
+        lo[a] = c[a] == 0 ? -INFINITY : (float)hdr[12 + a];
+        hi[a] = c[a] == gi[a] - 1 ? INFINITY : (float)hdr[15 + a];
+    }
+    const kn::FieldGeom fg = kn::field_geom_hdr(hdr.data(), fa.second);
+    double scale = 0.0;
+    for (int a = 0; a < 3; ++a) scale = std::max({scale, std::fabs(hdr[a]), std::fabs(hdr[3 + a]), hdr[3 + a] - hdr[a]});
+    auto stat = torch::zeros({2}, pts.options().dtype(torch::kInt32));
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    // slack 4e-6 x scale >= the local grids' certification slack (2e-6 x their extent)
+    KN_CHECK_HIP(kn::launch_field_splat(pts.data_ptr<float>(), (int)n_owned, d2.data_ptr<float>(), (int)k, lo, hi, fg,
+                                        (float)(4e-6 * scale), fa.first,
+                                        reinterpret_cast<unsigned*>(stat.data_ptr<int>()), s));
+    return stat;
+}
+
+// Certified radius of every field cell (launch_field_cert) for a plan header's domain.
+torch::Tensor field_cert(torch::Tensor field, std::vector<double> hdr) {
+    TORCH_CHECK(hdr.size() >= 6, "hdr needs the domain");
+    const auto fa = field_arg(field);
+    const c10::DeviceGuard guard(field.device());
+    auto cert = torch::empty_like(field);
+    const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+    KN_CHECK_HIP(kn::launch_field_cert(fa.first, kn::field_geom_hdr(hdr.data(), fa.second), cert.data_ptr<float>(), s));
+    return cert;
+}
+
 // The whole post-sync half of a distributed step in one call: unpack (self-last layout) ->
 // rank box / complete box / local grid box from the plan header -> tile plan -> grid build ->
 // queries of the owned points. Same arithmetic as the Python local path
@@ -605,8 +677,10 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
                                       c10::optional<std::vector<int64_t>> dims_hint = c10::nullopt,
                                       c10::optional<torch::Tensor> pre_pts = c10::nullopt,
                                       c10::optional<torch::Tensor> pre_gids = c10::nullopt,
-                                      int64_t use_tree = -1) {
-    TORCH_CHECK(grid.size() == 3 && hdr.size() >= 18, "grid must have 3 entries, hdr >= 18");
+                                      int64_t use_tree = -1,
+                                      c10::optional<torch::Tensor> field_cert = c10::nullopt) {
+    TORCH_CHECK(grid.size() == 3 && hdr.size() >= (size_t)kn::kPlanHdr, "grid must have 3 entries, hdr kPlanHdr");
+    const auto fc = field_arg(field_cert);
     const int64_t world = grid[0] * grid[1] * grid[2];
     TORCH_CHECK(world == (int64_t)recv_own.size(), "grid does not match the source table");
     std::vector<torch::Tensor> pg;
@@ -645,7 +719,7 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     // the rank's box / complete box / local grid box from the plan header (kn::rank_local, shared
     // with the C-API multi-GPU runtime)
     const int gi[3] = {(int)grid[0], (int)grid[1], (int)grid[2]};
-    const kn::RankLocal rl = kn::rank_local(hdr.data(), (int)rank, gi);
+    const kn::RankLocal rl = kn::rank_local(hdr.data(), (int)rank, gi, fc.first, fc.second);
     std::vector<double> complete(6), box(rl.box, rl.box + 6);
     for (int a = 0; a < 3; ++a) {
         complete[a] = (double)rl.complete.lo[a];
@@ -700,8 +774,8 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
         auto tb = tree_build_impl(g[0], g[1], g[3], dims, false);
         auto tq = tree_query(std::get<0>(tb), std::get<1>(tb), dims, npts, k, n_owned, c10::nullopt, true, 0, g[2]);
         auto uncert = torch::empty({std::max<int64_t>(1, n_owned)}, pg[1].options());
-        kn::CompleteBox cb;
-        for (int a = 0; a < 3; ++a) { cb.lo[a] = (float)complete[a]; cb.hi[a] = (float)complete[3 + a]; }
+        // the rank's whole complete box (wide zone, halo field), as the grid kernels below
+        const kn::CompleteBox cb = rl.complete;
         KN_CHECK_HIP(kn::launch_certify_rows(pg[0].data_ptr<float>(), (int)n_owned, (int)k, tq[1].data_ptr<float>(), cb,
                                              reinterpret_cast<const kn::GridGeom*>(g[3].data_ptr<int>()),
                                              reinterpret_cast<unsigned*>(tq[2].data_ptr<int>()),
@@ -714,8 +788,8 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
         ap.tile[0] = std::max(1, ap.tile[0] / std::max(1, ap.xsub));
         ap.xsub = 1;
     }
-    auto q = query(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
-                   ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid, counters, 0, ap.xsub);
+    auto q = query_impl(g[0], g[1], g[3], dims, k, n_owned, c10::nullopt, complete, {ap.tile[0], ap.tile[1], ap.tile[2]},
+                        ap.halo, ap.lds_capacity, true, true, 0, g[2], exact_grid, counters, 0, ap.xsub, &rl.complete);
     // + the local grid (global-id mode) and the uncertified list, for query forwarding
     return {pg[0], pg[1], q[0], q[1], q[2], g[0], g[1], g[3], g[2], q[3], dims_t, tree_t};
 }
@@ -1247,7 +1321,8 @@ public:
                std::vector<int64_t> grid, std::vector<int64_t> dims, std::vector<int64_t> recv_own,
                std::vector<int64_t> recv_halo, std::vector<int64_t> cross_send, std::vector<int64_t> cross_recv,
                std::vector<int64_t> place, int64_t cap, int64_t k, double ppc, bool deterministic, int64_t exact_grid,
-               int64_t use_tree, bool self_via_comm, c10::optional<std::vector<int64_t>> loopback)
+               int64_t use_tree, bool self_via_comm, c10::optional<std::vector<int64_t>> loopback,
+               c10::optional<torch::Tensor> field, c10::optional<torch::Tensor> field_cert)
         : comm_(std::move(comm)), points_(points) {
         check_points(points, true);
         TORCH_CHECK(plan.is_cuda() && plan.numel() == (int64_t)sizeof(kn::RouteParams), "plan must be a route plan");
@@ -1291,6 +1366,17 @@ public:
         p.exact_grid = (int)exact_grid;
         p.use_tree = (int)use_tree;
         p.self_via_comm = self_via_comm ? 1 : 0;
+        // halo field plan: the route plan points at the width field, the complete box at the
+        // certified radii; both stay alive with the pipeline
+        TORCH_CHECK(field.has_value() == field_cert.has_value(), "field and field_cert go together");
+        if (field.has_value()) {
+            const auto fc = field_arg(field_cert);
+            TORCH_CHECK(field_arg(field).second == fc.second, "field / field_cert sizes differ");
+            field_ = *field;
+            field_cert_ = *field_cert;
+            p.cert_field = fc.first;
+            p.field_g = fc.second;
+        }
         const c10::DeviceGuard guard(points.device());
         // the plan tensors (route plan, metas) are copied by the constructor: their producers first
         KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
@@ -1366,7 +1452,7 @@ public:
 
 private:
     std::shared_ptr<PyRankComm> comm_;
-    torch::Tensor points_, ids_, plan_, metas_;
+    torch::Tensor points_, ids_, plan_, metas_, field_, field_cert_;
     std::unique_ptr<kn::DistPipeline> d_;
 };
 
@@ -1408,7 +1494,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("splits") = py::none(), py::arg("h_inner") = -1.0, py::arg("wz") = INFINITY);
     m.def("route_plan", &route_plan, "multi-GPU: device-side routing plan from the gathered metas (no host sync)",
           py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"), py::arg("halo_factor"),
-          py::arg("splits") = py::none(), py::arg("inner_factor") = 0.0);
+          py::arg("splits") = py::none(), py::arg("inner_factor") = 0.0, py::arg("field") = py::none());
+    m.def("field_splat", &field_splat,
+          "multi-GPU halo field: splat the owned queries' K-th distances into a G^3 width field (in place)",
+          py::arg("pts"), py::arg("n_owned"), py::arg("d2"), py::arg("k"), py::arg("hdr"), py::arg("rank"),
+          py::arg("grid"), py::arg("field"));
+    m.def("field_cert", &field_cert, "multi-GPU halo field: certified radius of every field cell",
+          py::arg("field"), py::arg("hdr"));
     m.def("inner_halo_factor", &kn::inner_halo_factor,
           "multi-GPU: interior halo width in expected (K+1)-point radii (Poisson tail <= 1e-12)", py::arg("k"));
     m.def("route_count_dev", &route_count_dev, "multi-GPU: route_count with the device plan");
@@ -1418,7 +1510,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("route_begin", &route_begin,
           "multi-GPU: plan + counts + scatter (self-last layout, cap rows) enqueued in one call",
           py::arg("points"), py::arg("ids"), py::arg("metas"), py::arg("rank"), py::arg("grid"), py::arg("k"),
-          py::arg("halo_factor"), py::arg("cap"), py::arg("splits") = py::none(), py::arg("inner_factor") = 0.0);
+          py::arg("halo_factor"), py::arg("cap"), py::arg("splits") = py::none(), py::arg("inner_factor") = 0.0,
+          py::arg("field") = py::none());
     m.def("query_external", &query_external,
           "multi-GPU query forwarding: exact K nearest of external points among a local grid");
     m.def("steady_flag", &steady_flag, "multi-GPU: on-device check of a sync-free steady-state step");
@@ -1440,7 +1533,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("recv"), py::arg("self_rows"), py::arg("recv_own"), py::arg("recv_halo"), py::arg("rank"),
           py::arg("grid"), py::arg("hdr"), py::arg("k"), py::arg("ppc"), py::arg("deterministic"),
           py::arg("exact_grid") = 0, py::arg("adaptive") = false, py::arg("dims_hint") = py::none(),
-          py::arg("pre_pts") = py::none(), py::arg("pre_gids") = py::none(), py::arg("use_tree") = -1);
+          py::arg("pre_pts") = py::none(), py::arg("pre_gids") = py::none(), py::arg("use_tree") = -1,
+          py::arg("field_cert") = py::none());
     m.def("route_unpack_split", &route_unpack_split,
           "multi-GPU: unpack other sources' rows + this rank's own segment (self-last layout)");
     m.def("route_scatter", &route_scatter, "multi-GPU routing: build the all-to-all send buffer",
@@ -1462,12 +1556,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                       torch::Tensor, std::vector<int64_t>, std::vector<double>, std::vector<int64_t>,
                       std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>,
                       std::vector<int64_t>, std::vector<int64_t>, int64_t, int64_t, double, bool, int64_t, int64_t,
-                      bool, c10::optional<std::vector<int64_t>>>(),
+                      bool, c10::optional<std::vector<int64_t>>, c10::optional<torch::Tensor>,
+                      c10::optional<torch::Tensor>>(),
              py::arg("comm"), py::arg("points"), py::arg("ids"), py::arg("plan"), py::arg("metas"), py::arg("tot"),
              py::arg("hdr"), py::arg("grid"), py::arg("dims"), py::arg("recv_own"), py::arg("recv_halo"),
              py::arg("cross_send"), py::arg("cross_recv"), py::arg("place"), py::arg("cap"), py::arg("k"),
              py::arg("ppc"), py::arg("deterministic"), py::arg("exact_grid"), py::arg("use_tree"),
-             py::arg("self_via_comm"), py::arg("loopback") = py::none())
+             py::arg("self_via_comm"), py::arg("loopback") = py::none(), py::arg("field") = py::none(),
+             py::arg("field_cert") = py::none())
         .def("loopback_stage", &PyDistPipe::loopback_stage)
         .def("send_view", &PyDistPipe::send_view)
         .def("recv_view", &PyDistPipe::recv_view)

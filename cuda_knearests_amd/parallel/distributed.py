@@ -220,6 +220,21 @@ class DistributedKNearests:
             force_collectives = os.environ.get("KN_DIST_FORCE_COLLECTIVES") == "1"
         self.force_collectives = bool(force_collectives)
         self.pipe_unroll = int(os.environ.get("KN_DIST_UNROLL", "10"))  # steps per graph in run_steps
+        # Density-adaptive halo field (round 4, GPU ranks on the native router, world > 1): after a
+        # full step routed with the global widths, every owned query whose K-th ball leaves its own
+        # box raises the send width of the field cells within a few cells of it to its K-th
+        # distance (C.field_splat; the ranks' fields are MAX-all-reduced). The next full step routes
+        # each point with its cell's width and certifies a query when its K-th distance is within
+        # the radius the field guarantees at its cell (C.field_cert) or its ball stays in its own
+        # box; that step becomes the steady plan. Widths follow the measured distances, so dense
+        # clusters cut by a rank boundary ship a thin halo and sparse regions a wide one (CPU study
+        # of 8 x 900K, scripts/halo_study.py: clustered 30 % -> 8.8 %, uniform 12.8 % -> 6.2 %
+        # halo rows at G = 64). A field step that still forwards queries splats again (max-merged);
+        # after three such steps the field is dropped for the global widths. halo_field_g: cells
+        # per axis (KN_HALO_FIELD_G, default 64; 0 disables).
+        self.halo_field_g = int(os.environ.get("KN_HALO_FIELD_G", "64"))
+        self._field = None  # the width field (G^3 float32 on the device) of the next full step
+        self._field_retries = 0
         self.wait_timeout_s = float(timeout_s) if timeout_s else 300.0
         self._rcomm = None
         self._pipe = None
@@ -370,8 +385,10 @@ class DistributedKNearests:
             while True:
                 cap = max(self._send_cap, int(src_pts.size(0) * (1.0 + self.send_headroom)) + 1024)
                 inner = self._inner_factor() * hf / (self.halo_factor * self.halo_boost)
+                # the halo field routes the first round (growth rounds widen the global widths)
+                fld = self._field if rounds == 1 else None
                 plan, sync, bc, send = C.route_begin(src_pts, src_ids, metas, rank, list(grid), self.k, hf, cap,
-                                                     splits, inner)
+                                                     splits, inner, fld)
                 totals = sync[nh:nh + 2 * world]
                 if spec is not None:
                     # one all-gather of {meta, counts}; the rows this rank receives are column
@@ -417,6 +434,9 @@ class DistributedKNearests:
                 self._spec = (metas, meta_host, tuple(grid), splits)
             spec = None  # growth rounds re-route with the normal exchange
             h, hs, full = hv[6], hv[7], hv[10] != 0.0
+            # a field plan: the certified radius of every field cell, for this plan's domain
+            used_field = hv[22] != 0.0 and fld is not None
+            cert = C.field_cert(fld, hv[:HDR]) if used_field else None
             tot = [int(x) for x in hv[HDR:HDR + 2 * world]]
             rtot = [int(x) for x in hv[HDR + 2 * world:HDR + 4 * world]] if world > 1 else tot
             send_counts = [tot[2 * d] + tot[2 * d + 1] for d in range(world)]
@@ -438,7 +458,7 @@ class DistributedKNearests:
             # local_solve with SpatialDecomposition's boxes)
             pts, gids, idx, d2, counters, *local_grid = C.dist_local(
                 recv, send[x:x + send_counts[rank]], recv_own, recv_halo, rank, list(grid), hv[:HDR], self.k,
-                self.points_per_cell, self.deterministic, 0, self.adaptive)
+                self.points_per_cell, self.deterministic, 0, self.adaptive, field_cert=cert)
             mark(("local_enqueued", time.perf_counter()))
             n_owned = sum(recv_own)
             if rounds == 1:
@@ -461,7 +481,9 @@ class DistributedKNearests:
             growth += 1
             _log.info("rank %d: uncertified queries, growth round %d with halo factor %.3g", rank, rounds + 1, hf)
             src_pts, src_ids = own_pts, own_ids
-        stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned), "halo_width": h, "rounds": rounds,
+        field_next = self._update_field(points, pts, n_owned, d2, hv, grid, used_field, n_fwd, growth, full)
+        stats = {"n_owned": n_owned, "n_halo": int(pts.size(0) - n_owned),
+                 "halo_width": hv[23] if used_field else h, "halo_field": bool(used_field), "rounds": rounds,
                  "grid": tuple(grid), "forwarded": n_fwd, "exact_path": int(counters[0].item()),
                  "local_dims": tuple(int(v) for v in local_grid[5].tolist()),
                  "local_tree": bool(local_grid[6].item())}
@@ -471,7 +493,8 @@ class DistributedKNearests:
             self.halo_boost *= 1.6
             _log.info("rank %d: %d queries forwarded; halo factor for the next steps %.3g", rank, n_fwd,
                       self.halo_factor * self.halo_boost)
-        if growth == 0 and not full and self.steady and not widen and 2 * n_fwd <= self.fwd_slots_max:
+        if growth == 0 and not full and self.steady and not widen and not field_next and \
+                2 * n_fwd <= self.fwd_slots_max:
             # validated single-round step: the steady-state assumption for the next ones
             self._steady = {
                 "fwd": n_fwd > 0,  # device forwarding in the steady steps
@@ -490,12 +513,42 @@ class DistributedKNearests:
                 "n": int(points.size(0)), "ids": ids is not None, "stats": dict(stats),
                 # fallback launch sized from the validated step's list (short list: 256 WGs)
                 "exact_grid": 256 if int(counters[0].item()) < 4096 else 0,
+                # halo field plan: the width field (the route plan points at it) and its radii
+                "field": fld if used_field else None, "field_cert": cert,
             }
             if world == 1:  # ids of the world-1 steady step (no routing) when the caller gives none
                 self._steady["gids1"] = torch.arange(points.size(0), dtype=torch.int32, device=points.device)
         else:
             self._steady = None
         return DistResult(own_ids, idx, d2, stats)
+
+    def _update_field(self, points, pts, n_owned, d2, hv, grid, used_field, n_fwd, growth, full) -> bool:
+        """Halo field after a full step (collective: every rank takes the same branch). Returns
+        True when a new field was made for the next full step (this step is then not the steady
+        plan)."""
+        G = self.halo_field_g
+        if G <= 0 or self.world == 1 or not points.is_cuda or full or growth:
+            return False
+        if used_field and n_fwd == 0:
+            self._field_retries = 0
+            return False  # the field plan certified every query: it becomes the steady plan
+        if used_field:
+            self._field_retries += 1
+            if self._field_retries > 3:  # a changing cloud outruns the field: global widths
+                self._field = None
+                self._field_retries = 0
+                return False
+        C = ops.load()
+        F = self._field.clone() if (used_field and self._field is not None) else \
+            torch.zeros(G * G * G, dtype=torch.float32, device=pts.device)
+        stat = C.field_splat(pts, n_owned, d2, self.k, hv[:HDR], self.rank, list(grid), F)
+        self.comm.all_reduce_max(F)
+        self.comm.all_reduce_max(stat)
+        if int(stat[0].item()) > 0:  # a query with fewer than K neighbours in the whole cloud
+            self._field = None
+            return False
+        self._field = F
+        return True
 
     def _forward_round(self, hv, grid, pts, gids, idx, d2, counters, local_grid, splits=None) -> int:
         """Query forwarding for the uncertified queries of a round (targeted second round,
@@ -616,7 +669,8 @@ class DistributedKNearests:
         pts, gids, idx, d2, counters, *lg = C.dist_local(recv, send[:0], st["recv_own"], st["recv_halo"],
                                                          rank, list(st["grid"]), st["hdr"], self.k,
                                                          self.points_per_cell, self.deterministic, st["exact_grid"],
-                                                         False, st["dims"], lpts, lgids, st["use_tree"])
+                                                         False, st["dims"], lpts, lgids, st["use_tree"],
+                                                         field_cert=st.get("field_cert"))
         check = counters  # the flag's word [1]: uncertified queries (no forwarding) or slot overflow
         if world > 1 and st.get("fwd"):
             # uncertified queries answered inside the step: fixed-capacity forwarding slots and
@@ -696,7 +750,8 @@ class DistributedKNearests:
                           [int(v) for v in st["tot"].tolist()], [float(v) for v in st["hdr"]], list(st["grid"]),
                           list(st["dims"]), list(st["recv_own"]), list(st["recv_halo"]), list(st["cross_send"]),
                           list(st["cross_recv"]), list(st["place"]), int(st["cap"]), self.k, self.points_per_cell,
-                          bool(self.deterministic), int(st["exact_grid"]), int(st["use_tree"]), world1_force, None)
+                          bool(self.deterministic), int(st["exact_grid"]), int(st["use_tree"]), world1_force, None,
+                          st.get("field"), st.get("field_cert"))
         p = self._pipe = {"pipe": pipe, "st": st, "pts": points, "ids": ids32, "n": points.size(0),
                           "outs": [pipe.outputs(0), pipe.outputs(1)], "primed": False}
         return p

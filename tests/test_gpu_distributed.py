@@ -589,7 +589,7 @@ def test_native_pipeline_loopback_layouts(cuda, world, gen):
                                 [float(v) for v in st["hdr"]], list(st["grid"]), list(st["dims"]), list(st["recv_own"]),
                                 list(st["recv_halo"]), list(st["cross_send"]), list(st["cross_recv"]), list(st["place"]),
                                 int(st["cap"]), 16, 0.0, True, int(st["exact_grid"]), int(st["use_tree"]), False,
-                                [world, r]))
+                                [world, r], st.get("field"), st.get("field_cert")))
     for p in pipes:
         p.loopback_stage(0)
     for r in range(world):
