@@ -266,6 +266,112 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
     }
 }
 
+__global__ __launch_bounds__(kRT) void route_fused_kernel(const float* __restrict__ pts, const int* __restrict__ ids,
+                                                          int n, const RouteParams* __restrict__ pp, FusedRoute fr,
+                                                          int* __restrict__ cursors, float4* __restrict__ send,
+                                                          SelfPlace sp, unsigned* __restrict__ partials, int nb) {
+    const RouteParams& p = *pp;
+    __shared__ int bcnt[2 * kRouteMaxWorld];            // the block's rows per column -> its base
+    __shared__ int wcnt[kRT / 64][2 * kRouteMaxWorld];  // per-wave counts of the current round
+    __shared__ unsigned red[6][kRT / 64];
+    const int cols = 2 * p.world;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const bool lead = lane == 0;
+    for (int c = threadIdx.x; c < cols; c += kRT) bcnt[c] = 0;
+    __syncthreads();
+    // pass 1: classify (kept in registers), bbox, block counts
+    int o[kRounds];
+    unsigned long long m[kRounds];
+    float px[kRounds], py[kRounds], pz[kRounds];
+    unsigned bw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
+        o[r] = -1;
+        m[r] = 0;
+        px[r] = py[r] = pz[r] = 0.f;
+        if (i < n) {
+            const size_t i3 = 3 * (size_t)i;
+            const float x = pts[i3], y = pts[i3 + 1], z = pts[i3 + 2];
+            px[r] = x; py[r] = y; pz[r] = z;
+            bw[0] = max(bw[0], ~meta_ord(x)); bw[1] = max(bw[1], ~meta_ord(y)); bw[2] = max(bw[2], ~meta_ord(z));
+            bw[3] = max(bw[3], meta_ord(x)); bw[4] = max(bw[4], meta_ord(y)); bw[5] = max(bw[5], meta_ord(z));
+            o[r] = route_owner(p, x, y, z);
+            m[r] = route_halo(p, x, y, z, o[r]);
+        }
+        for (int d = 0; d < p.world; ++d) {
+            const unsigned long long bo = __builtin_amdgcn_ballot_w64(o[r] == d);
+            const unsigned long long bh = __builtin_amdgcn_ballot_w64((m[r] >> d) & 1ull);
+            if (lead && bo) atomicAdd(&bcnt[2 * d], __builtin_popcountll(bo));
+            if (lead && bh) atomicAdd(&bcnt[2 * d + 1], __builtin_popcountll(bh));
+        }
+    }
+    if (partials) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const unsigned v = wave_max_u32(bw[a]);
+            if (lead) red[a][wid] = v;
+        }
+    }
+    __syncthreads();
+    // the block's rows of every column: one global atomic per (block, column)
+    for (int c = threadIdx.x; c < cols; c += kRT) bcnt[c] = bcnt[c] ? atomicAdd(cursors + c, bcnt[c]) : 0;
+    if (partials && threadIdx.x < 6) {
+        unsigned v = red[threadIdx.x][0];
+        for (int w = 1; w < kRT / 64; ++w) v = max(v, red[threadIdx.x][w]);
+        partials[(size_t)threadIdx.x * nb + blockIdx.x] = v;
+    }
+    __syncthreads();
+    // pass 2: rows (in-wave rank from the ballot, earlier waves of the round from LDS)
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
+        for (int d = 0; d < p.world; ++d) {
+            const unsigned long long bo = __builtin_amdgcn_ballot_w64(o[r] == d);
+            const unsigned long long bh = __builtin_amdgcn_ballot_w64((m[r] >> d) & 1ull);
+            if (lead) {
+                wcnt[wid][2 * d] = __builtin_popcountll(bo);
+                wcnt[wid][2 * d + 1] = __builtin_popcountll(bh);
+            }
+        }
+        __syncthreads();
+        if (o[r] >= 0) {
+            const int gid = ids ? ids[i] : p.id_offset + i;
+            const float4 row = make_float4(px[r], py[r], pz[r], __int_as_float(gid));
+            for (int d = 0; d < p.world; ++d) {
+                const bool po = o[r] == d, ph = (m[r] >> d) & 1ull;
+                const unsigned long long bo = __builtin_amdgcn_ballot_w64(po);
+                const unsigned long long bh = __builtin_amdgcn_ballot_w64(ph);
+                if (!(po || ph)) continue;
+                const int c = 2 * d + (po ? 0 : 1);
+                int j = bcnt[c];
+                for (int w = 0; w < wid; ++w) j += wcnt[w][c];
+                j += __builtin_popcountll((po ? bo : bh) & lt);
+                if (j >= fr.cap[c]) continue;  // more rows than planned: dropped, the flag fails
+                if (fr.base[c] < 0) {
+                    const int loc = sp.own_base + j;  // self placement (owned rows only)
+                    if (loc < 0 || loc >= sp.rows) continue;
+                    const size_t l3 = 3 * (size_t)KN_IDX(loc, sp.rows, 404);
+                    sp.pts[l3] = px[r];
+                    sp.pts[l3 + 1] = py[r];
+                    sp.pts[l3 + 2] = pz[r];
+                    sp.gids[loc] = gid;
+                } else {
+                    send[fr.base[c] + j] = row;
+                }
+            }
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < cols; c += kRT) {
+            int t = 0;
+            for (int w = 0; w < kRT / 64; ++w) t += wcnt[w][c];
+            bcnt[c] += t;
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restrict__ recv,
                                                            const float4* __restrict__ self_rows, int rows,
                                                            UnpackTable t, float* __restrict__ pts,
@@ -779,6 +885,27 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
     if (n > 0)
         route_scatter_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, block_offsets, nb, totals, send, send_rows,
                                                 self_last, sp);
+    return hipGetLastError();
+}
+
+hipError_t launch_route_fused(const float* pts, const int* ids, int n, const RouteParams* p, int world,
+                              const FusedRoute& fr, int* cursors, float4* send, const SelfPlace* self_place,
+                              unsigned* partials, hipStream_t s) {
+    if (world < 1 || world > kRouteMaxWorld) return hipErrorInvalidValue;
+    SelfPlace sp{};
+    for (int c = 0; c < 2 * world; ++c) {
+        if (fr.cap[c] < 0) return hipErrorInvalidValue;
+        if (fr.base[c] < 0 && (c & 1)) return hipErrorInvalidValue;  // self placement: owned rows only
+        if (fr.base[c] < 0 && fr.cap[c] > 0 && !self_place) return hipErrorInvalidValue;
+    }
+    if (self_place) {
+        if (!self_place->pts || !self_place->gids) return hipErrorInvalidValue;
+        sp = *self_place;
+    }
+    hipError_t e = hipMemsetAsync(cursors, 0, (size_t)2 * world * sizeof(int), s);
+    if (e != hipSuccess || n <= 0) return e;
+    const int nb = route_block_count(n);
+    route_fused_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, fr, cursors, send, sp, partials, nb);
     return hipGetLastError();
 }
 

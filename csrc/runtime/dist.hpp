@@ -151,6 +151,7 @@ private:
     BuildBuffers bproto_{};
     QueryBuffers qproto_{};
     CompleteBox complete_{};
+    FusedRoute fused_{};
     Set set_[2]{};
     void* route_dev_ = nullptr;
     double* metas_dev_ = nullptr;
