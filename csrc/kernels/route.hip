@@ -266,27 +266,37 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
     }
 }
 
+// Single-pass chained scan over the blocks (decoupled look-back): a block takes the next CHUNK
+// of points by ticket, so it only ever waits for chunks that earlier-started blocks hold (forward
+// progress without co-residency assumptions), and the rows keep the input order of the
+// count + scan + scatter path. status[chunk * cols + c] = count | flag << 30 (1: the chunk's own
+// count, 2: the inclusive prefix through it); one word carries value and flag together.
+constexpr unsigned kLbAgg = 1u << 30, kLbInc = 2u << 30, kLbMask = kLbAgg - 1u;
 __global__ __launch_bounds__(kRT) void route_fused_kernel(const float* __restrict__ pts, const int* __restrict__ ids,
                                                           int n, const RouteParams* __restrict__ pp, FusedRoute fr,
-                                                          int* __restrict__ cursors, float4* __restrict__ send,
-                                                          SelfPlace sp, unsigned* __restrict__ partials, int nb) {
+                                                          int* __restrict__ totals, unsigned* __restrict__ status,
+                                                          float4* __restrict__ send, SelfPlace sp,
+                                                          unsigned* __restrict__ partials, int nb) {
     const RouteParams& p = *pp;
-    __shared__ int bcnt[2 * kRouteMaxWorld];            // the block's rows per column -> its base
+    __shared__ int bcnt[2 * kRouteMaxWorld];            // the chunk's rows per column -> its base
     __shared__ int wcnt[kRT / 64][2 * kRouteMaxWorld];  // per-wave counts of the current round
     __shared__ unsigned red[6][kRT / 64];
+    __shared__ int chunk_s;
     const int cols = 2 * p.world;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const bool lead = lane == 0;
     for (int c = threadIdx.x; c < cols; c += kRT) bcnt[c] = 0;
+    if (threadIdx.x == 0) chunk_s = atomicAdd(reinterpret_cast<int*>(status) + (size_t)nb * cols, 1);
     __syncthreads();
-    // pass 1: classify (kept in registers), bbox, block counts
+    const int chunk = chunk_s;
+    // pass 1: classify (kept in registers), bbox, chunk counts
     int o[kRounds];
     unsigned long long m[kRounds];
     float px[kRounds], py[kRounds], pz[kRounds];
     unsigned bw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
-        const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
+        const int i = chunk * kRouteItems + r * kRT + threadIdx.x;
         o[r] = -1;
         m[r] = 0;
         px[r] = py[r] = pz[r] = 0.f;
@@ -314,19 +324,38 @@ __global__ __launch_bounds__(kRT) void route_fused_kernel(const float* __restric
         }
     }
     __syncthreads();
-    // the block's rows of every column: one global atomic per (block, column)
-    for (int c = threadIdx.x; c < cols; c += kRT) bcnt[c] = bcnt[c] ? atomicAdd(cursors + c, bcnt[c]) : 0;
+    // publish the chunk's counts, look back for its prefix (one thread per column)
+    if (threadIdx.x < cols) {
+        const int c = threadIdx.x;
+        const unsigned cnt = (unsigned)bcnt[c];
+        unsigned* st = status + (size_t)chunk * cols + c;
+        unsigned prefix = 0;
+        if (chunk > 0) {
+            __hip_atomic_store(st, cnt | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int j = chunk - 1; j >= 0; --j) {
+                unsigned v;
+                do {
+                    v = __hip_atomic_load(status + (size_t)j * cols + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } while (!(v & (kLbAgg | kLbInc)));
+                prefix += v & kLbMask;
+                if (v & kLbInc) break;
+            }
+        }
+        __hip_atomic_store(st, (prefix + cnt) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bcnt[c] = (int)prefix;
+        if (chunk == nb - 1) totals[c] = (int)(prefix + cnt);  // the step's per-column totals
+    }
     if (partials && threadIdx.x < 6) {
         unsigned v = red[threadIdx.x][0];
         for (int w = 1; w < kRT / 64; ++w) v = max(v, red[threadIdx.x][w]);
-        partials[(size_t)threadIdx.x * nb + blockIdx.x] = v;
+        partials[(size_t)threadIdx.x * nb + chunk] = v;
     }
     __syncthreads();
     // pass 2: rows (in-wave rank from the ballot, earlier waves of the round from LDS)
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int r = 0; r < kRounds; ++r) {
-        const int i = blockIdx.x * kRouteItems + r * kRT + threadIdx.x;
+        const int i = chunk * kRouteItems + r * kRT + threadIdx.x;
         for (int d = 0; d < p.world; ++d) {
             const unsigned long long bo = __builtin_amdgcn_ballot_w64(o[r] == d);
             const unsigned long long bh = __builtin_amdgcn_ballot_w64((m[r] >> d) & 1ull);
@@ -888,10 +917,12 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
     return hipGetLastError();
 }
 
+size_t route_fused_scratch_words(int n, int world) { return (size_t)2 * world * route_block_count(n) + 1; }
+
 hipError_t launch_route_fused(const float* pts, const int* ids, int n, const RouteParams* p, int world,
-                              const FusedRoute& fr, int* cursors, float4* send, const SelfPlace* self_place,
-                              unsigned* partials, hipStream_t s) {
-    if (world < 1 || world > kRouteMaxWorld) return hipErrorInvalidValue;
+                              const FusedRoute& fr, int* totals, unsigned* scratch, float4* send,
+                              const SelfPlace* self_place, unsigned* partials, hipStream_t s) {
+    if (world < 1 || world > kRouteMaxWorld || n >= (int)kLbMask) return hipErrorInvalidValue;
     SelfPlace sp{};
     for (int c = 0; c < 2 * world; ++c) {
         if (fr.cap[c] < 0) return hipErrorInvalidValue;
@@ -902,10 +933,13 @@ hipError_t launch_route_fused(const float* pts, const int* ids, int n, const Rou
         if (!self_place->pts || !self_place->gids) return hipErrorInvalidValue;
         sp = *self_place;
     }
-    hipError_t e = hipMemsetAsync(cursors, 0, (size_t)2 * world * sizeof(int), s);
+    hipError_t e = hipMemsetAsync(totals, 0, (size_t)2 * world * sizeof(int), s);
     if (e != hipSuccess || n <= 0) return e;
+    // look-back status words + the chunk ticket
+    if ((e = hipMemsetAsync(scratch, 0, route_fused_scratch_words(n, world) * sizeof(unsigned), s)) != hipSuccess)
+        return e;
     const int nb = route_block_count(n);
-    route_fused_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, fr, cursors, send, sp, partials, nb);
+    route_fused_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, fr, totals, scratch, send, sp, partials, nb);
     return hipGetLastError();
 }
 

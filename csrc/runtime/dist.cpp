@@ -235,7 +235,7 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     auto layout = [&](char* base, Set& S) {
         char* q = base;
         S.send = carve<float4>(q, (size_t)p_.cap);
-        S.bc = carve<int>(q, (size_t)2 * W * nb);
+        S.bc = carve<int>(q, route_fused_scratch_words(p_.n, W));  // block counts / look-back status
         S.totals = carve<int>(q, (size_t)2 * W);
         S.partials = carve<unsigned>(q, (size_t)6 * nb);
         S.recv = carve<float4>(q, (size_t)recv_rows_);
@@ -376,8 +376,9 @@ hipError_t DistPipeline::stage_build(int s, hipStream_t st, const std::vector<hi
     const auto* rp = static_cast<const RouteParams*>(route_dev_);
     if (p_.n > 0 && route_fused()) {
         const SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
-        KN_TRY(launch_route_fused(p_.points, p_.ids, p_.n, rp, p_.world, fused_, S.totals, S.send,
-                                  p_.self_via_comm ? nullptr : &sp, S.partials, st));
+        KN_TRY(launch_route_fused(p_.points, p_.ids, p_.n, rp, p_.world, fused_, S.totals,
+                                  reinterpret_cast<unsigned*>(S.bc), S.send, p_.self_via_comm ? nullptr : &sp,
+                                  S.partials, st));
     } else if (p_.n > 0) {
         KN_TRY(launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, st, S.partials));
         if (p_.self_via_comm) {
@@ -486,8 +487,8 @@ kn_status DistPipeline::loopback_stage(int stage) {
         const auto* rp = static_cast<const RouteParams*>(route_dev_);
         if (p_.n > 0 && route_fused()) {
             const SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
-            e = launch_route_fused(p_.points, p_.ids, p_.n, rp, p_.world, fused_, S.totals, S.send, &sp, S.partials,
-                                   main_);
+            e = launch_route_fused(p_.points, p_.ids, p_.n, rp, p_.world, fused_, S.totals,
+                                   reinterpret_cast<unsigned*>(S.bc), S.send, &sp, S.partials, main_);
         } else if (p_.n > 0) {
             e = launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, main_, S.partials);
             SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
