@@ -6,6 +6,7 @@
 #pragma once
 
 #include <hip/hip_runtime_api.h>
+#include <stddef.h>
 
 #include "kn/kernels.h"
 
@@ -27,6 +28,7 @@ struct RouteParams {
     float hi2;
     float wz;
     float dom_hi[3];  // global domain upper corner (lower: lo)
+    int pad0;         // explicit padding (plans are compared byte for byte): always 0
     // Density-adaptive halo (field != null): a point in field cell c is sent to every rank whose
     // box is within field[c] (+ fslack) -- the widths splatted from the previous full step's
     // measured K-th distances (launch_field_splat); h2 / hi2 / wz are then unused.
@@ -47,6 +49,9 @@ struct RouteParams {
     float ys[2 * kRouteMaxWorld];
     float zs[2 * kRouteMaxWorld];
 };
+static_assert(sizeof(RouteParams) == offsetof(RouteParams, zs) + sizeof(float) * 2 * kRouteMaxWorld,
+              "RouteParams has hidden tail padding");
+static_assert(offsetof(RouteParams, field) == offsetof(RouteParams, pad0) + sizeof(int), "RouteParams padding");
 // floats in a splits array for decomposition grid g (kd layout above)
 inline int route_split_count(const int g[3]) { return (g[0] + 1) + g[0] * (g[1] + 1) + g[0] * g[1] * (g[2] + 1); }
 

@@ -502,6 +502,7 @@ __global__ void route_plan_kernel(const double* __restrict__ metas, int world, i
     p->hi2 = hif * hif;
     p->wz = (float)wz;
     for (int a = 0; a < 3; ++a) p->dom_hi[a] = (float)hi[a];
+    p->pad0 = 0;
     p->field = use_field ? field : nullptr;
     {
         const float fl[3] = {(float)lo[0], (float)lo[1], (float)lo[2]};
