@@ -127,7 +127,8 @@ class DistributedKNearests:
                  deterministic: bool = True, max_rounds: int = 8, native_route: Optional[bool] = None,
                  transport=None, device_plan: bool = True, timeout_s: Optional[float] = None,
                  balance: str = "count", adaptive: bool = True, native_pipeline: Optional[bool] = None,
-                 force_collectives: Optional[bool] = None, inner_halo: Optional[float] = None):
+                 force_collectives: Optional[bool] = None, inner_halo: Optional[float] = None,
+                 halo_field: Optional[int] = None):
         self.k = int(k)
         # occupancy-adaptive local grids (GPU): a rank whose share is clustered re-bins finer, as
         # the 1-GPU engine does; steady steps reuse the validated step's grid (no extra sync)
@@ -230,9 +231,10 @@ class DistributedKNearests:
         # clusters cut by a rank boundary ship a thin halo and sparse regions a wide one (CPU study
         # of 8 x 900K, scripts/halo_study.py: clustered 30 % -> 8.8 %, uniform 12.8 % -> 6.2 %
         # halo rows at G = 64). A field step that still forwards queries splats again (max-merged);
-        # after three such steps the field is dropped for the global widths. halo_field_g: cells
-        # per axis (KN_HALO_FIELD_G, default 64; 0 disables).
-        self.halo_field_g = int(os.environ.get("KN_HALO_FIELD_G", "64"))
+        # after three such steps the field is dropped for the global widths. The steady state thus
+        # starts after the second full step. halo_field_g: cells per axis (halo_field, else
+        # KN_HALO_FIELD_G, default 64; 0 disables).
+        self.halo_field_g = int(os.environ.get("KN_HALO_FIELD_G", "64")) if halo_field is None else int(halo_field)
         self._field = None  # the width field (G^3 float32 on the device) of the next full step
         self._field_retries = 0
         self.wait_timeout_s = float(timeout_s) if timeout_s else 300.0

@@ -372,7 +372,7 @@ def test_steady_state_async_steps(cuda, world):
     def body(t):
         m = owner == t.rank
         ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
-        dk = DistributedKNearests(k=k, transport=t)
+        dk = DistributedKNearests(k=k, transport=t, halo_field=0)  # steady after ONE full step
         r0 = dk.solve(cloud[m].contiguous().to(cuda), ids)
         r1 = dk.solve(cloud[m].contiguous().to(cuda), ids, async_=True)
         ok1 = r1.valid()
@@ -409,7 +409,7 @@ def test_adaptive_local_grid_clustered(cuda):
         def body(t):
             m = owner == t.rank
             ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
-            dk = DistributedKNearests(k=k, transport=t, adaptive=adaptive)
+            dk = DistributedKNearests(k=k, transport=t, adaptive=adaptive, halo_field=0)
             r0 = dk.solve(cloud[m].contiguous().to(cuda), ids)
             r1 = dk.solve(cloud[m].contiguous().to(cuda), ids, async_=True)
             ok = r1.valid()
@@ -473,7 +473,7 @@ def test_steady_forwarding_on_device(cuda, world, gen, hf):
         m = owner == t.rank
         ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
         pts = cloud[m].contiguous().to(cuda)
-        dk = DistributedKNearests(k=k, transport=t, halo_factor=hf)
+        dk = DistributedKNearests(k=k, transport=t, halo_factor=hf, halo_field=0)
         dk.halo_boost_max = 1.0  # no adaptive halo: the steady steps forward on the device
         r0 = dk.solve(pts, ids)
         outs = []
@@ -508,7 +508,7 @@ def test_adaptive_halo_boost(cuda):
         m = owner == t.rank
         ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
         pts = cloud[m].contiguous().to(cuda)
-        dk = DistributedKNearests(k=k, transport=t, halo_factor=0.6)
+        dk = DistributedKNearests(k=k, transport=t, halo_factor=0.6, halo_field=0)
         hist = []
         for _ in range(6):
             r = dk.solve(pts, ids, async_=True)
@@ -605,3 +605,51 @@ def test_native_pipeline_loopback_layouts(cuda, world, gen):
         g, i, d = pipes[r].outputs(0)
         assert pipes[r].flag_local() == 0, r
         assert torch.equal(g, ids) and torch.equal(i, nb) and torch.equal(d, d2), r
+
+
+@pytest.mark.parametrize("world,gen", [(4, "uniform"), (8, "clustered")])
+def test_halo_field(cuda, world, gen):
+    """Density-adaptive halo field (route.hip field_splat / field_cert): the first full step routes
+    with the global widths and splats the measured K-th distances; the second routes each point
+    with its field cell's width (fewer halo rows), certifies every query and becomes the steady
+    plan; the steady steps are valid, exact and equal to the field step's rows; a moved cloud
+    fails the steady check and the synchronous solve recovers the exact rows."""
+    import cuda_knearests_amd as kn
+    from cuda_knearests_amd.parallel import DistributedKNearests, run_loopback
+    from cuda_knearests_amd.utils import clustered_cloud
+
+    n, k = 40000 * world, 16
+    cloud = uniform_cloud(n, seed=61) if gen == "uniform" else clustered_cloud(n, seed=62)
+    moved = cloud.clone()
+    moved[:, 1] = moved[:, 1] * 0.8 + 11.0
+    owner = torch.arange(n) % world
+
+    def body(t):
+        m = owner == t.rank
+        ids = torch.nonzero(m).flatten().to(torch.int32).to(cuda)
+        pts = cloud[m].contiguous().to(cuda)
+        dk = DistributedKNearests(k=k, transport=t)
+        r0 = dk.solve(pts, ids)
+        r1 = dk.solve(pts, ids)
+        r2 = dk.solve(pts, ids, async_=True)
+        ok2 = r2.valid()
+        r3 = dk.solve(moved[m].contiguous().to(cuda), ids, async_=True)
+        ok3 = r3.valid()
+        r4 = dk.solve(moved[m].contiguous().to(cuda), ids)
+        return (dict(r0.stats), dict(r1.stats), ok2, bool(r2.stats.get("steady")), ok3,
+                r1.ids.cpu(), r1.neighbors.cpu(), r1.d2.cpu(), r2.ids.cpu(), r2.neighbors.cpu(), r2.d2.cpu(),
+                r4.ids.cpu(), r4.d2.cpu())
+
+    out = run_loopback(world, body)
+    _, od = kn.knn_cpu(cloud, k, "kdtree")
+    _, odm = kn.knn_cpu(moved, k, "kdtree")
+    halo0 = sum(o[0]["n_halo"] for o in out)
+    halo1 = sum(o[1]["n_halo"] for o in out)
+    for s0, s1, ok2, steady2, ok3, i1, n1, d1, i2, n2, d2, i4, d4 in out:
+        assert not s0["halo_field"] and s1["halo_field"] and s1["forwarded"] == 0, (s0, s1)
+        assert ok2 and steady2 and not ok3
+        assert torch.equal(d1, od[i1.long()])
+        assert_knn_exact(cloud, i1.long(), n1, d1, od[i1.long()])
+        assert torch.equal(i1, i2) and torch.equal(n1, n2) and torch.equal(d1, d2)
+        assert torch.equal(d4, odm[i4.long()])
+    assert halo1 < halo0, (halo1, halo0)
