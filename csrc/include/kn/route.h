@@ -135,8 +135,8 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
 // classifies a chunk of points, gets its rows' offsets in every (destination, kind) column from a
 // single-pass chained scan over the chunks (decoupled look-back), and writes them at base[c] +
 // offset -- rows past cap[c] (a step that differs from the plan) are dropped, so nothing is
-// written out of bounds. base[2*d] < 0: destination d's owned rows go straight to the local rows
-// (self placement, sp). Same rows in the same order as count + scan + scatter, which it replaces
+// written out of bounds. base[c] < 0: column c (the rank's own owned or halo rows) goes straight
+// to the local rows (self placement, sp). Same rows in the same order as count + scan + scatter, which it replaces
 // (48 + 9 + 28 us at 900K concurrent with the queries). totals (2*world ints): the step's
 // actual column totals, checked by the steady flag against the plan. scratch:
 // route_fused_scratch_words(n, world) words (zeroed by the launcher). partials: the share's bbox

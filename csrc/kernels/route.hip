@@ -379,7 +379,9 @@ __global__ __launch_bounds__(kRT) void route_fused_kernel(const float* __restric
                 j += __builtin_popcountll((po ? bo : bh) & lt);
                 if (j >= fr.cap[c]) continue;  // more rows than planned: dropped, the flag fails
                 if (fr.base[c] < 0) {
-                    const int loc = sp.own_base + j;  // self placement (owned rows only)
+                    // self placement: owned rows after the other sources' owned rows, halo rows
+                    // (the rank's points that another rank owns) after theirs
+                    const int loc = (c & 1) ? sp.halo_base + j : sp.own_base + j;
                     if (loc < 0 || loc >= sp.rows) continue;
                     const size_t l3 = 3 * (size_t)KN_IDX(loc, sp.rows, 404);
                     sp.pts[l3] = px[r];
@@ -927,7 +929,6 @@ hipError_t launch_route_fused(const float* pts, const int* ids, int n, const Rou
     SelfPlace sp{};
     for (int c = 0; c < 2 * world; ++c) {
         if (fr.cap[c] < 0) return hipErrorInvalidValue;
-        if (fr.base[c] < 0 && (c & 1)) return hipErrorInvalidValue;  // self placement: owned rows only
         if (fr.base[c] < 0 && fr.cap[c] > 0 && !self_place) return hipErrorInvalidValue;
     }
     if (self_place) {

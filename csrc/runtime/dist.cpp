@@ -152,8 +152,10 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
         const long long b = p_.self_via_comm && d == p_.rank ? so : soff_[d];
         fused_.base[2 * d] = self ? -1 : (int)b;
         fused_.cap[2 * d] = own_d;
-        fused_.base[2 * d + 1] = self ? 0 : (int)(b + own_d);
-        fused_.cap[2 * d + 1] = self ? 0 : halo_d;  // a rank is never its own halo destination
+        // self: a share can hold points another rank owns that are halo of this rank (they
+        // enter the local rows after the other sources' halo rows)
+        fused_.base[2 * d + 1] = self ? -1 : (int)(b + own_d);
+        fused_.cap[2 * d + 1] = halo_d;
     }
     table_ = UnpackTable{};
     table_.world = W;

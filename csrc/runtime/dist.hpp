@@ -121,6 +121,8 @@ public:
     const int* idx(int s) const { return set_[s].idx; }
     const float* d2(int s) const { return set_[s].d2; }
     const unsigned* counters(int s) const { return set_[s].counters; }
+    const int* totals(int s) const { return set_[s].totals; }
+    const unsigned* partials(int s) const { return set_[s].partials; }
 
 private:
     struct Set {

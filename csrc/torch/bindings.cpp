@@ -1337,6 +1337,7 @@ public:
             p.world = (int)(*loopback)[0];
             p.rank = (int)(*loopback)[1];
         }
+        comm_world_ = p.world;
         p.device = points.get_device();
         p.k = (int)k;
         p.n = (int)points.size(0);
@@ -1395,6 +1396,18 @@ public:
         return torch::from_blob(reinterpret_cast<float*>(d_->recv_rows(0) + d_->recv_offset((int)src)), {rows, 4}, opt);
     }
     int64_t flag_local() { return d_->flag_local(0); }
+    // diagnostics (loopback mode): set 0's query counters and routed column totals
+    std::vector<int64_t> debug_words() {
+        (void)d_->flag_local(0);  // synchronises the pipeline's stream
+        std::vector<unsigned> c(kn::kNumCounters);
+        const int W = (int)comm_world_;
+        std::vector<int> t((size_t)2 * W);
+        KN_CHECK_HIP(hipMemcpy(c.data(), d_->counters(0), c.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+        KN_CHECK_HIP(hipMemcpy(t.data(), d_->totals(0), t.size() * sizeof(int), hipMemcpyDeviceToHost));
+        std::vector<int64_t> out(c.begin(), c.end());
+        out.insert(out.end(), t.begin(), t.end());
+        return out;
+    }
     // enqueue `iters` steps (unroll: steps per graph launch, even >= 2, else one graph per stage)
     // keep_primed: also enqueue the next step's build (the caller promises the points stay
     // unchanged until the next launch); the current torch stream orders the input
@@ -1453,6 +1466,7 @@ public:
 private:
     std::shared_ptr<PyRankComm> comm_;
     torch::Tensor points_, ids_, plan_, metas_, field_, field_cert_;
+    int64_t comm_world_ = 1;
     std::unique_ptr<kn::DistPipeline> d_;
 };
 
@@ -1568,6 +1582,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("send_view", &PyDistPipe::send_view)
         .def("recv_view", &PyDistPipe::recv_view)
         .def("flag_local", &PyDistPipe::flag_local)
+        .def("debug_words", &PyDistPipe::debug_words)
         .def("launch", &PyDistPipe::launch, py::arg("iters") = 1, py::arg("unroll") = 0, py::arg("keep_primed") = false)
         .def("wait", &PyDistPipe::wait, py::arg("step"), py::arg("timeout_s") = 300.0)
         .def("sync", &PyDistPipe::sync)

@@ -59,4 +59,4 @@ for r, (st, ids, nb, d2, stats) in enumerate(out):
     g, i, d = pipes[r].outputs(0)
     print(f"rank {r}: flag {pipes[r].flag_local()} field {st.get('field') is not None} tot {st['tot'].tolist()} "
           f"rows equal {torch.equal(g, ids) and torch.equal(i, nb) and torch.equal(d, d2)} "
-          f"halo {stats.get('n_halo')} width {stats.get('halo_width'):.3f}", flush=True)
+          f"halo {stats.get('n_halo')} width {stats.get('halo_width'):.3f} words {pipes[r].debug_words()}", flush=True)
