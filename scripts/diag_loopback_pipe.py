@@ -34,7 +34,20 @@ def body(t):
         r1 = dk.solve(shares[t.rank])
         if r1.stats.get("steady"):
             break
-    return dk._steady, r1.ids.clone(), r1.neighbors.clone(), r1.d2.clone(), dict(r1.stats)
+    # the torch steady path by hand (distributed.py _steady_body, world > 1): its query counters
+    st = dk._steady
+    pts_in = shares[t.rank]
+    totals, send, partials, lpts, lgids = C.route_steady(pts_in, None, st["plan"], world, st["cap"], t.rank,
+                                                         st["place"])
+    recv = dk._a2a(send[:st["x"]], st["cross_send"], st["cross_recv"])
+    _, _, _, _, counters, *_ = C.dist_local(recv, send[:0], st["recv_own"], st["recv_halo"], t.rank,
+                                            list(st["grid"]), st["hdr"], dk.k, dk.points_per_cell, dk.deterministic,
+                                            st["exact_grid"], False, st["dims"], lpts, lgids, st["use_tree"],
+                                            field_cert=st.get("field_cert"))
+    stats = dict(r1.stats)
+    stats["torch_counters"] = counters[:8].tolist()
+    stats["valid"] = r1.valid()
+    return dk._steady, r1.ids.clone(), r1.neighbors.clone(), r1.d2.clone(), stats
 
 
 out = run_loopback(world, body)
@@ -59,4 +72,4 @@ for r, (st, ids, nb, d2, stats) in enumerate(out):
     g, i, d = pipes[r].outputs(0)
     print(f"rank {r}: flag {pipes[r].flag_local()} field {st.get('field') is not None} tot {st['tot'].tolist()} "
           f"rows equal {torch.equal(g, ids) and torch.equal(i, nb) and torch.equal(d, d2)} "
-          f"halo {stats.get('n_halo')} width {stats.get('halo_width'):.3f} words {pipes[r].debug_words()}", flush=True)
+          f"halo {stats.get('n_halo')} width {stats.get('halo_width'):.3f} words {pipes[r].debug_words()} torch {stats['torch_counters']} valid {stats['valid']}", flush=True)
