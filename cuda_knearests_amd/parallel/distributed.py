@@ -541,8 +541,19 @@ class DistributedKNearests:
                 self._field_retries = 0
                 return False
         C = ops.load()
-        F = self._field.clone() if (used_field and self._field is not None) else \
-            torch.zeros(G * G * G, dtype=torch.float32, device=pts.device)
+        # cells per axis: the largest K-th distance must fit in the field's reach (3 rings of
+        # cells: 3 x 0.998 x the smallest cell edge), else such queries could never be certified
+        dk = d2[:n_owned, self.k - 1] if n_owned else d2.new_zeros(1)
+        rmax = torch.where(torch.isfinite(dk), dk, torch.zeros_like(dk)).max().sqrt().reshape(1).float()
+        self.comm.all_reduce_max(rmax)
+        ext_min = min(hv[3 + a] - hv[a] for a in range(3))
+        r = float(rmax.item())
+        G = min(G, int(math.floor(3 * 0.998 * ext_min / (r * 1.02))) if r > 0.0 else G)
+        if G < 4:  # cells wider than a quarter of the domain: the global widths do as well
+            self._field = None
+            return False
+        F = self._field.clone() if (used_field and self._field is not None and self._field.numel() == G ** 3) \
+            else torch.zeros(G * G * G, dtype=torch.float32, device=pts.device)
         stat = C.field_splat(pts, n_owned, d2, self.k, hv[:HDR], self.rank, list(grid), F)
         self.comm.all_reduce_max(F)
         self.comm.all_reduce_max(stat)
