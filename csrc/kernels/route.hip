@@ -324,26 +324,33 @@ __global__ __launch_bounds__(kRT) void route_fused_kernel(const float* __restric
         }
     }
     __syncthreads();
-    // publish the chunk's counts, look back for its prefix (one thread per column)
-    if (threadIdx.x < cols) {
-        const int c = threadIdx.x;
+    // publish the chunk's counts and look back for its prefix: one wave per column, each lane
+    // reading one of the 64 preceding chunks' status words, so one round trip covers 64 chunks
+    for (int c = wid; c < cols; c += kRT / 64) {
         const unsigned cnt = (unsigned)bcnt[c];
         unsigned* st = status + (size_t)chunk * cols + c;
+        if (chunk > 0 && lead) __hip_atomic_store(st, cnt | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned prefix = 0;
-        if (chunk > 0) {
-            __hip_atomic_store(st, cnt | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int j = chunk - 1; j >= 0; --j) {
-                unsigned v;
+        for (int j0 = chunk - 1; j0 >= 0; j0 -= 64) {
+            const int j = j0 - lane;
+            unsigned v = kLbInc;  // before chunk 0: an inclusive prefix of 0 ends the look-back
+            if (j >= 0) {
                 do {
                     v = __hip_atomic_load(status + (size_t)j * cols + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 } while (!(v & (kLbAgg | kLbInc)));
-                prefix += v & kLbMask;
-                if (v & kLbInc) break;
             }
+            // the nearest inclusive prefix ends the sum: lanes up to it contribute
+            const unsigned long long inc = __builtin_amdgcn_ballot_w64((v & kLbInc) != 0u);
+            const int stop = inc ? __builtin_ctzll(inc) : 64;
+            const int part = lane <= stop ? (int)(v & kLbMask) : 0;
+            prefix += (unsigned)__builtin_amdgcn_readlane(wave_inclusive_scan_add(part), 63);
+            if (inc) break;
         }
-        __hip_atomic_store(st, (prefix + cnt) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bcnt[c] = (int)prefix;
-        if (chunk == nb - 1) totals[c] = (int)(prefix + cnt);  // the step's per-column totals
+        if (lead) {
+            __hip_atomic_store(st, (prefix + cnt) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bcnt[c] = (int)prefix;
+            if (chunk == nb - 1) totals[c] = (int)(prefix + cnt);  // the step's per-column totals
+        }
     }
     if (partials && threadIdx.x < 6) {
         unsigned v = red[threadIdx.x][0];
