@@ -1397,13 +1397,14 @@ public:
     }
     int64_t flag_local() { return d_->flag_local(0); }
     // diagnostics (loopback mode): set 0's query counters and routed column totals
-    std::vector<int64_t> debug_words() {
-        (void)d_->flag_local(0);  // synchronises the pipeline's stream
+    std::vector<int64_t> debug_words(int64_t set) {
+        TORCH_CHECK(set == 0 || set == 1, "set must be 0 or 1");
+        KN_CHECK_HIP(hipDeviceSynchronize());
         std::vector<unsigned> c(kn::kNumCounters);
         const int W = (int)comm_world_;
         std::vector<int> t((size_t)2 * W);
-        KN_CHECK_HIP(hipMemcpy(c.data(), d_->counters(0), c.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
-        KN_CHECK_HIP(hipMemcpy(t.data(), d_->totals(0), t.size() * sizeof(int), hipMemcpyDeviceToHost));
+        KN_CHECK_HIP(hipMemcpy(c.data(), d_->counters((int)set), c.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+        KN_CHECK_HIP(hipMemcpy(t.data(), d_->totals((int)set), t.size() * sizeof(int), hipMemcpyDeviceToHost));
         std::vector<int64_t> out(c.begin(), c.end());
         out.insert(out.end(), t.begin(), t.end());
         return out;
@@ -1582,7 +1583,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("send_view", &PyDistPipe::send_view)
         .def("recv_view", &PyDistPipe::recv_view)
         .def("flag_local", &PyDistPipe::flag_local)
-        .def("debug_words", &PyDistPipe::debug_words)
+        .def("debug_words", &PyDistPipe::debug_words, py::arg("set") = 0)
         .def("launch", &PyDistPipe::launch, py::arg("iters") = 1, py::arg("unroll") = 0, py::arg("keep_primed") = false)
         .def("wait", &PyDistPipe::wait, py::arg("step"), py::arg("timeout_s") = 300.0)
         .def("sync", &PyDistPipe::sync)

@@ -82,7 +82,12 @@ for force in modes:
         outs.append((r, i % 2))
         if len(outs) == 2:  # check before the set is reused by the step after next
             for rr, which in outs:
-                assert rr.valid()
+                if not rr.valid():
+                    p = dk2._pipe["pipe"]
+                    st = dk2._steady
+                    print(f"refill step invalid (force {force}, step {i}): planned tot {st['tot'].tolist()} "
+                          f"set0 {p.debug_words(0)} set1 {p.debug_words(1)} last_set {p.last_set()}", flush=True)
+                    sys.exit(1)
             refill = all(same(rr, ref_perm if w else ref) for rr, w in outs)
             outs = []
             if not refill:
