@@ -85,8 +85,14 @@ for force in modes:
                 if not rr.valid():
                     p = dk2._pipe["pipe"]
                     st = dk2._steady
-                    print(f"refill step invalid (force {force}, step {i}): planned tot {st['tot'].tolist()} "
-                          f"set0 {p.debug_words(0)} set1 {p.debug_words(1)} last_set {p.last_set()}", flush=True)
+                    msg = (f"refill step invalid (force {force}, step {i}, which {which}): planned tot "
+                           f"{st['tot'].tolist()} set0 {p.debug_words(0)} set1 {p.debug_words(1)} "
+                           f"last_set {p.last_set()} flags {[x.valid() for x, _ in outs]}")
+                    print(msg, flush=True)
+                    os.makedirs("gpurun_out", exist_ok=True)
+                    with open("gpurun_out/diag_refill.txt", "a") as f:
+                        f.write(msg + "\n")
+                    dist.destroy_process_group()
                     sys.exit(1)
             refill = all(same(rr, ref_perm if w else ref) for rr, w in outs)
             outs = []
