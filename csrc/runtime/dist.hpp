@@ -122,6 +122,8 @@ public:
     const float* d2(int s) const { return set_[s].d2; }
     const unsigned* counters(int s) const { return set_[s].counters; }
     const int* totals(int s) const { return set_[s].totals; }
+    const int* block_words(int s) const { return set_[s].bc; }
+    int share_rows() const { return p_.n; }
     const unsigned* partials(int s) const { return set_[s].partials; }
 
 private:
