@@ -15,11 +15,12 @@ namespace kn {
 
 bool exact_epilogue();
 
-// One-pass steady routing (launch_route_fused); KN_ROUTE_FUSED=0: count + scan + scatter (A/B)
+// One-pass steady routing (launch_route_fused) when KN_ROUTE_FUSED=1 (A/B); default: count + scan
+// + scatter
 static bool route_fused() {
     static const bool on = [] {
         const char* v = std::getenv("KN_ROUTE_FUSED");
-        return !v || std::atoi(v) != 0;
+        return v && std::atoi(v) != 0;
     }();
     return on;
 }  // engine.cpp: KN_PIPE_EXACT
