@@ -929,6 +929,14 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
 
 size_t route_fused_scratch_words(int n, int world) { return (size_t)2 * world * route_block_count(n) + 1; }
 
+// zeroes the look-back words + ticket and the totals (a kernel node: a captured hipMemsetAsync of
+// this odd size left stale words behind in graph replays)
+__global__ void route_fused_reset_kernel(unsigned* __restrict__ scratch, int words, int* __restrict__ totals,
+                                         int cols) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < words; i += gridDim.x * blockDim.x) scratch[i] = 0u;
+    if (blockIdx.x == 0 && (int)threadIdx.x < cols) totals[threadIdx.x] = 0;
+}
+
 hipError_t launch_route_fused(const float* pts, const int* ids, int n, const RouteParams* p, int world,
                               const FusedRoute& fr, int* totals, unsigned* scratch, float4* send,
                               const SelfPlace* self_place, unsigned* partials, hipStream_t s) {
@@ -942,11 +950,10 @@ hipError_t launch_route_fused(const float* pts, const int* ids, int n, const Rou
         if (!self_place->pts || !self_place->gids) return hipErrorInvalidValue;
         sp = *self_place;
     }
-    hipError_t e = hipMemsetAsync(totals, 0, (size_t)2 * world * sizeof(int), s);
+    const int words = (int)route_fused_scratch_words(n, world);
+    route_fused_reset_kernel<<<std::min((words + 255) / 256, 64), 256, 0, s>>>(scratch, words, totals, 2 * world);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess || n <= 0) return e;
-    // look-back status words + the chunk ticket
-    if ((e = hipMemsetAsync(scratch, 0, route_fused_scratch_words(n, world) * sizeof(unsigned), s)) != hipSuccess)
-        return e;
     const int nb = route_block_count(n);
     route_fused_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, fr, totals, scratch, send, sp, partials, nb);
     return hipGetLastError();
