@@ -180,6 +180,10 @@ typedef struct {
     int min_owned, max_owned;  /* owned points per rank                                    */
     int device_allocations; /* device allocations made by the last solve (0 once buffers fit) */
     float ms_total;         /* host wall time of the last kn_solve_multi                      */
+    int host_syncs;         /* host synchronisation points of the last kn_solve_multi: meta,
+                               route counts, local solves, rows (+1 per kd split level of a new
+                               count-balanced plan; a solve whose ranks' bboxes and counts are
+                               unchanged reuses the splits; + forwarding)                        */
 } kn_multi_stats;
 kn_status kn_get_multi_stats(kn_multi *m, kn_multi_stats *out);
 

@@ -142,6 +142,11 @@ struct kn_multi {
     std::vector<unsigned> idx;
     std::vector<float> dist;
     bool solved = false;
+    int host_syncs = 0;
+    // plan reuse: the count-balanced kd splits of the last solve stay valid while every rank's
+    // meta (bbox, count) is unchanged -- a repeated solve skips the split histograms' syncs
+    std::vector<double> plan_metas;
+    bool splits_valid = false;
 #ifdef KN_HAVE_RCCL
     std::vector<ncclComm_t> comms;
 #endif
@@ -189,6 +194,7 @@ void free_buf(DBuf& b) {
 
 kn_status sync_all(kn_multi* m) {
     for (auto& R : m->r) { KN_M(hipSetDevice(R.dev)); KN_M(hipStreamSynchronize(R.s)); }
+    ++m->host_syncs;
     return KN_OK;
 }
 
@@ -253,6 +259,10 @@ kn_status phase_meta(kn_multi* m, double lo[3], double hi[3], int grid[3]) {
         KN_M(hipMemcpyAsync(&metas[(size_t)8 * i], R.meta.p, 8 * sizeof(double), hipMemcpyDeviceToHost, R.s));
     }
     KN_TRY(sync_all(m));
+    if (metas != m->plan_metas) {  // a rank's bbox or count changed: the splits are re-planned
+        m->plan_metas = metas;
+        m->splits_valid = false;
+    }
     for (int a = 0; a < 3; ++a) { lo[a] = INFINITY; hi[a] = -INFINITY; }
     for (int i = 0; i < W; ++i)
         for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], metas[8 * i + a]); hi[a] = std::max(hi[a], metas[8 * i + 3 + a]); }
@@ -534,25 +544,33 @@ kn_status forward(kn_multi* m) {
 // 8. rows in original order
 kn_status gather(kn_multi* m) {
     const int k = m->cfg.k;
+    const int W = (int)m->r.size();
     m->idx.assign((size_t)m->n * k, 0xFFFFFFFFu);
     m->dist.assign((size_t)m->n * k, INFINITY);
-    for (auto& R : m->r) {
+    // every rank's rows copied back at once, ONE sync for all of them
+    std::vector<std::vector<int>> g(W);
+    std::vector<std::vector<unsigned>> ix(W);
+    std::vector<std::vector<float>> ds(W);
+    for (int i = 0; i < W; ++i) {
+        RankState& R = m->r[i];
         KN_M(hipSetDevice(R.dev));
         const int n_owned = R.n_owned;
-        std::vector<int> g(n_owned);
-        std::vector<unsigned> ix((size_t)n_owned * k);
-        std::vector<float> ds((size_t)n_owned * k);
+        g[i].resize(n_owned);
+        ix[i].resize((size_t)n_owned * k);
+        ds[i].resize((size_t)n_owned * k);
         if (n_owned) {
-            KN_M(hipMemcpyAsync(g.data(), R.lgids.p, n_owned * sizeof(int), hipMemcpyDeviceToHost, R.s));
-            KN_M(hipMemcpyAsync(ix.data(), R.out_idx.p, ix.size() * sizeof(unsigned), hipMemcpyDeviceToHost, R.s));
-            KN_M(hipMemcpyAsync(ds.data(), R.out_dist.p, ds.size() * sizeof(float), hipMemcpyDeviceToHost, R.s));
+            KN_M(hipMemcpyAsync(g[i].data(), R.lgids.p, n_owned * sizeof(int), hipMemcpyDeviceToHost, R.s));
+            KN_M(hipMemcpyAsync(ix[i].data(), R.out_idx.p, ix[i].size() * sizeof(unsigned), hipMemcpyDeviceToHost, R.s));
+            KN_M(hipMemcpyAsync(ds[i].data(), R.out_dist.p, ds[i].size() * sizeof(float), hipMemcpyDeviceToHost, R.s));
         }
-        KN_M(hipStreamSynchronize(R.s));
-        for (int j = 0; j < n_owned; ++j) {
-            if (g[j] < 0 || g[j] >= m->n) { m->err = "global id out of range"; return KN_ERR_DEVICE; }
-            const size_t dst = (size_t)g[j] * k;
-            std::memcpy(&m->idx[dst], &ix[(size_t)j * k], k * sizeof(unsigned));
-            std::memcpy(&m->dist[dst], &ds[(size_t)j * k], k * sizeof(float));
+    }
+    KN_TRY(sync_all(m));
+    for (int i = 0; i < W; ++i) {
+        for (int j = 0; j < m->r[i].n_owned; ++j) {
+            if (g[i][j] < 0 || g[i][j] >= m->n) { m->err = "global id out of range"; return KN_ERR_DEVICE; }
+            const size_t dst = (size_t)g[i][j] * k;
+            std::memcpy(&m->idx[dst], &ix[i][(size_t)j * k], k * sizeof(unsigned));
+            std::memcpy(&m->dist[dst], &ds[i][(size_t)j * k], k * sizeof(float));
         }
     }
     return KN_OK;
@@ -562,9 +580,13 @@ kn_status solve(kn_multi* m) {
     const int W = (int)m->r.size();
     double lo[3], hi[3];
     int grid[3];
+    m->host_syncs = 0;
     KN_TRY(phase_meta(m, lo, hi, grid));
     m->balanced = m->opt.balance != 0 && W > 1 && grid[0] * grid[1] <= kn::kRouteMaxWorld;
-    if (m->balanced) KN_TRY(phase_splits(m, lo, hi, grid));
+    if (m->balanced && !m->splits_valid) {
+        KN_TRY(phase_splits(m, lo, hi, grid));
+        m->splits_valid = true;  // the ranks' `splits` buffers hold them until a meta changes
+    }
     double hf = m->opt.halo_factor;
     m->forwarded = 0;
     for (int round = 0; round < m->opt.max_rounds; ++round) {
@@ -747,6 +769,7 @@ kn_status kn_get_multi_stats(kn_multi* m, kn_multi_stats* out) {
     for (auto& R : m->r) { s.min_owned = std::min(s.min_owned, R.n_owned); s.max_owned = std::max(s.max_owned, R.n_owned); }
     s.device_allocations = m->allocations;
     s.ms_total = m->ms_total;
+    s.host_syncs = m->host_syncs;
     *out = s;
     return KN_OK;
 }

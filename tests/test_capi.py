@@ -38,7 +38,7 @@ class KnMultiOptions(C.Structure):
 class KnMultiStats(C.Structure):
     _fields_ = [("ranks", C.c_int), ("rounds", C.c_int), ("halo_points", C.c_int), ("forwarded", C.c_int),
                 ("uses_rccl", C.c_int), ("balanced", C.c_int), ("min_owned", C.c_int), ("max_owned", C.c_int),
-                ("device_allocations", C.c_int), ("ms_total", C.c_float)]
+                ("device_allocations", C.c_int), ("ms_total", C.c_float), ("host_syncs", C.c_int)]
 
 
 def _lib():
@@ -298,10 +298,11 @@ def test_capi_multi_balanced_forwarding_persistent():
     assert st.balanced == 1 and st.rounds == 1 and st.forwarded > 0
     assert st.max_owned <= 2 * st.min_owned < 2 * vol_ratio * st.min_owned
     check(cloud, od)
-    # the same solve again: every buffer fits
+    # the same solve again: every buffer fits, the kd splits are reused (no split histograms)
     assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
     lib.kn_get_multi_stats(m, C.byref(st))
     assert st.device_allocations == 0, st.device_allocations
+    syncs_repeat = st.host_syncs
     check(cloud, od)
     # forwarding off: halo growth rounds instead, same rows
     opt.forward = 0
@@ -317,6 +318,8 @@ def test_capi_multi_balanced_forwarding_persistent():
     opt.forward = 1
     assert lib.kn_set_multi_options(m, C.byref(opt)) == 0
     assert lib.kn_solve_multi(m) == 0, lib.kn_last_error()
+    lib.kn_get_multi_stats(m, C.byref(st))
+    assert st.host_syncs > syncs_repeat, (st.host_syncs, syncs_repeat)  # moved: the splits are re-planned
     _, od2 = kn.knn_cpu(moved, k, "kdtree")
     check(moved, od2)
     h = C.c_void_p(m)
