@@ -51,11 +51,10 @@ namespace kn {
 namespace {
 
 constexpr unsigned SENT = 0xFFFFFFFFu;
-// Threads per tile workgroup (A/B builds: -DKN_TILE_WG=512 with taller tiles)
-#ifndef KN_TILE_WG
-#define KN_TILE_WG 256
-#endif
-constexpr int kWG = KN_TILE_WG;
+// Threads per tile workgroup. 512 threads with taller tiles lost the round-4 A/B at every tile
+// shape (900K K=16 0.294 -> 0.325-0.360 ms/step, K=50 0.967 -> 0.944-1.147;
+// profiles/ab_r4_tiles_margin.txt)
+constexpr int kWG = 256;
 constexpr int kWaves = kWG / 64;
 
 struct TileArgs {

@@ -1,5 +1,7 @@
-"""In-process interleaved A/B of tile plans / workgroup sizes on the pipelined engine step (900K
-uniform): configs = (extension suffix, tile hint in cells). Rows must equal the baseline's.
+"""In-process interleaved A/B of tile plans on the pipelined engine step (900K uniform): configs =
+(extension suffix, tile hint in cells). Variant extensions come from
+cuda_knearests_amd._build.build_variant(name, flags) (round 4: -DKN_TILE_WG=512, since removed,
+and -DKN_TOPK_MARGIN=1; profiles/ab_r4_tiles_margin.txt). Rows must equal the baseline's.
 usage: python scripts/ab_tiles.py [n] [k] [rounds] [steps]"""
 import importlib
 import sys
