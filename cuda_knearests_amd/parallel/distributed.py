@@ -799,19 +799,23 @@ class DistributedKNearests:
         """``iters`` steps of the same share in one call (benchmarks, repeated solves of a
         resident cloud): in the steady state all of them are enqueued at once into the native
         pipeline (U steps per graph launch, no host round trip); otherwise asynchronous
-        ``solve`` calls. Returns the last step's result; its ``valid()`` covers every step."""
+        ``solve`` calls until the steady state is reached (e.g. the halo-field step after the
+        first full step), then the rest through the pipeline. Returns the last step's result;
+        its ``valid()`` covers every pipelined step."""
         points = points.contiguous().float()
         if iters <= 0:
             raise ValueError("iters must be positive")
-        if self.steady and self._steady is not None and self._use_native(points) and self.device_plan:
-            self._check_pending(keep=0)
-            if self._steady is not None and self._use_pipe(points):
-                res = self._solve_pipe(points, ids, iters, resident)
-                self._pending.append(res)
-                return res
         res = None
-        for _ in range(iters):
+        left = iters
+        while left > 0:
+            if self.steady and self._steady is not None and self._use_native(points) and self.device_plan:
+                self._check_pending(keep=0)
+                if self._steady is not None and self._use_pipe(points):
+                    res = self._solve_pipe(points, ids, left, resident)
+                    self._pending.append(res)
+                    return res
             res = self.solve(points, ids, async_=True)
+            left -= 1
         return res
 
     def profile_step(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None) -> dict:
