@@ -403,6 +403,7 @@ def run_loopback_bench(args) -> dict:
     halo = [r.stats["n_halo"] for r in out]
     return {"t": dt, "n_total": sum(s.size(0) for s in shares), "check": chk,
             "stats": {**{k: st[k] for k in ("n_halo", "halo_width", "rounds", "grid")},
+                      "halo_field": bool(st.get("halo_field")),
                       "forwarded": sum(int(r.stats.get("forwarded", 0)) for r in out),
                       "steady": all(bool(r.stats.get("steady")) for r in out),
                       "owned_max_over_mean": max(owned) / (sum(owned) / len(owned)),
@@ -524,6 +525,7 @@ def main() -> int:
             return 0
         n_gpus = r["world"]
         extra = {"halo_width": r["stats"].get("halo_width"), "n_halo_rank0": r["stats"].get("n_halo"),
+                 "halo_field": bool(r["stats"].get("halo_field")),
                  "rounds": r["stats"].get("rounds"), "rank_grid": r["stats"].get("grid"), "layout": args.layout,
                  "steady_async": bool(r["stats"].get("steady")) and not args.sync_steps,
                  "invalid_async_steps": r["invalid_async_steps"], "path": "distributed",
