@@ -231,12 +231,14 @@ class DistributedKNearests:
         # clusters cut by a rank boundary ship a thin halo and sparse regions a wide one (CPU study
         # of 8 x 900K, scripts/halo_study.py: clustered 30 % -> 8.8 %, uniform 12.8 % -> 6.2 %
         # halo rows at G = 64). A field step that still forwards queries splats again (max-merged);
-        # after three such steps the field is dropped for the global widths. The steady state thus
-        # starts after the second full step. halo_field_g: cells per axis (halo_field, else
+        # after three such steps the field is dropped for the global widths, and so is a field whose
+        # halo is not smaller than the global widths' (sparse outliers force coarse cells: small
+        # clustered clouds). The steady state thus starts after the second full step. halo_field_g: cells per axis (halo_field, else
         # KN_HALO_FIELD_G, default 64; 0 disables).
         self.halo_field_g = int(os.environ.get("KN_HALO_FIELD_G", "64")) if halo_field is None else int(halo_field)
         self._field = None  # the width field (G^3 float32 on the device) of the next full step
         self._field_retries = 0
+        self._field_ref_halo = 0  # halo rows (all ranks) of the last full step with the global widths
         self.wait_timeout_s = float(timeout_s) if timeout_s else 300.0
         self._rcomm = None
         self._pipe = None
@@ -531,9 +533,22 @@ class DistributedKNearests:
         G = self.halo_field_g
         if G <= 0 or self.world == 1 or not points.is_cuda or full or growth:
             return False
+        # the step's halo rows over all ranks (the field must beat the global widths' halo)
+        nh = torch.tensor([int(pts.size(0) - n_owned)], dtype=torch.int64, device=pts.device)
+        halo_all = sum(int(x.item()) for x in self.comm.all_gather(nh))
         if used_field and n_fwd == 0:
             self._field_retries = 0
+            if halo_all >= self._field_ref_halo:
+                # sparse outliers forced cells so coarse that the field ships more than the global
+                # widths (small clustered clouds): back to the global widths for good
+                _log.info("rank %d: halo field %d rows >= global %d: global widths", self.rank, halo_all,
+                          self._field_ref_halo)
+                self.halo_field_g = 0
+                self._field = None
+                return True  # one more full step with the global widths, then steady
             return False  # the field plan certified every query: it becomes the steady plan
+        if not used_field:
+            self._field_ref_halo = halo_all
         if used_field:
             self._field_retries += 1
             if self._field_retries > 3:  # a changing cloud outruns the field: global widths
