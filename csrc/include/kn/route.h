@@ -131,24 +131,6 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
                                 const int* block_offsets, const int* totals, float4* send, int send_rows,
                                 int self_last, hipStream_t s,
                                 const SelfPlace* self_place = nullptr);
-// Steady-state routing in ONE pass (validated plan: every column's base row is known): each block
-// classifies a chunk of points, gets its rows' offsets in every (destination, kind) column from a
-// single-pass chained scan over the chunks (decoupled look-back), and writes them at base[c] +
-// offset -- rows past cap[c] (a step that differs from the plan) are dropped, so nothing is
-// written out of bounds. base[c] < 0: column c (the rank's own owned or halo rows) goes straight
-// to the local rows (self placement, sp). Same rows in the same order as count + scan + scatter, which it replaces
-// (48 + 9 + 28 us at 900K concurrent with the queries). totals (2*world ints): the step's
-// actual column totals, checked by the steady flag against the plan. scratch:
-// route_fused_scratch_words(n, world) words (zeroed by the launcher). partials: the share's bbox
-// per chunk (route_count's layout).
-struct FusedRoute {
-    int base[2 * kRouteMaxWorld];
-    int cap[2 * kRouteMaxWorld];
-};
-size_t route_fused_scratch_words(int n, int world);
-hipError_t launch_route_fused(const float* pts, const int* ids, int n, const RouteParams* p, int world,
-                              const FusedRoute& fr, int* totals, unsigned* scratch, float4* send,
-                              const SelfPlace* self_place, unsigned* partials, hipStream_t s);
 // rows = t.rows_cross + rows of the self buffer (self_rows may be null when t.self < 0)
 // sorted[i].w = gid[perm[i]] | (perm[i] >= n_owned ? 0x80000000 : 0): prepares a rank's grid
 // for the query kernels' global-id mode (QueryBuffers::row_of = perm).

@@ -266,150 +266,6 @@ __global__ __launch_bounds__(kRT) void route_scatter_kernel(const float* __restr
     }
 }
 
-// Single-pass chained scan over the blocks (decoupled look-back): a block takes the next CHUNK
-// of points by ticket, so it only ever waits for chunks that earlier-started blocks hold (forward
-// progress without co-residency assumptions), and the rows keep the input order of the
-// count + scan + scatter path. status[chunk * cols + c] = count | flag << 30 (1: the chunk's own
-// count, 2: the inclusive prefix through it); one word carries value and flag together.
-constexpr unsigned kLbAgg = 1u << 30, kLbInc = 2u << 30, kLbMask = kLbAgg - 1u;
-__global__ __launch_bounds__(kRT) void route_fused_kernel(const float* __restrict__ pts, const int* __restrict__ ids,
-                                                          int n, const RouteParams* __restrict__ pp, FusedRoute fr,
-                                                          int* __restrict__ totals, unsigned* __restrict__ status,
-                                                          float4* __restrict__ send, SelfPlace sp,
-                                                          unsigned* __restrict__ partials, int nb) {
-    const RouteParams& p = *pp;
-    __shared__ int bcnt[2 * kRouteMaxWorld];            // the chunk's rows per column -> its base
-    __shared__ int wcnt[kRT / 64][2 * kRouteMaxWorld];  // per-wave counts of the current round
-    __shared__ unsigned red[6][kRT / 64];
-    __shared__ int chunk_s;
-    const int cols = 2 * p.world;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const bool lead = lane == 0;
-    for (int c = threadIdx.x; c < cols; c += kRT) bcnt[c] = 0;
-    if (threadIdx.x == 0) chunk_s = atomicAdd(reinterpret_cast<int*>(status) + (size_t)nb * cols, 1);
-    __syncthreads();
-    const int chunk = chunk_s;
-    // pass 1: classify (kept in registers), bbox, chunk counts
-    int o[kRounds];
-    unsigned long long m[kRounds];
-    float px[kRounds], py[kRounds], pz[kRounds];
-    unsigned bw[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-        const int i = chunk * kRouteItems + r * kRT + threadIdx.x;
-        o[r] = -1;
-        m[r] = 0;
-        px[r] = py[r] = pz[r] = 0.f;
-        if (i < n) {
-            const size_t i3 = 3 * (size_t)i;
-            const float x = pts[i3], y = pts[i3 + 1], z = pts[i3 + 2];
-            px[r] = x; py[r] = y; pz[r] = z;
-            bw[0] = max(bw[0], ~meta_ord(x)); bw[1] = max(bw[1], ~meta_ord(y)); bw[2] = max(bw[2], ~meta_ord(z));
-            bw[3] = max(bw[3], meta_ord(x)); bw[4] = max(bw[4], meta_ord(y)); bw[5] = max(bw[5], meta_ord(z));
-            o[r] = route_owner(p, x, y, z);
-            m[r] = route_halo(p, x, y, z, o[r]);
-        }
-        for (int d = 0; d < p.world; ++d) {
-            const unsigned long long bo = __builtin_amdgcn_ballot_w64(o[r] == d);
-            const unsigned long long bh = __builtin_amdgcn_ballot_w64((m[r] >> d) & 1ull);
-            if (lead && bo) atomicAdd(&bcnt[2 * d], __builtin_popcountll(bo));
-            if (lead && bh) atomicAdd(&bcnt[2 * d + 1], __builtin_popcountll(bh));
-        }
-    }
-    if (partials) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const unsigned v = wave_max_u32(bw[a]);
-            if (lead) red[a][wid] = v;
-        }
-    }
-    __syncthreads();
-    // publish the chunk's counts and look back for its prefix: one wave per column, each lane
-    // reading one of the 64 preceding chunks' status words, so one round trip covers 64 chunks
-    for (int c = wid; c < cols; c += kRT / 64) {
-        const unsigned cnt = (unsigned)bcnt[c];
-        unsigned* st = status + (size_t)chunk * cols + c;
-        if (chunk > 0 && lead) __hip_atomic_store(st, cnt | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned prefix = 0;
-        for (int j0 = chunk - 1; j0 >= 0; j0 -= 64) {
-            const int j = j0 - lane;
-            unsigned v = kLbInc;  // before chunk 0: an inclusive prefix of 0 ends the look-back
-            if (j >= 0) {
-                do {
-                    v = __hip_atomic_load(status + (size_t)j * cols + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } while (!(v & (kLbAgg | kLbInc)));
-            }
-            // the nearest inclusive prefix ends the sum: lanes up to it contribute
-            const unsigned long long inc = __builtin_amdgcn_ballot_w64((v & kLbInc) != 0u);
-            const int stop = inc ? __builtin_ctzll(inc) : 64;
-            const int part = lane <= stop ? (int)(v & kLbMask) : 0;
-            prefix += (unsigned)__builtin_amdgcn_readlane(wave_inclusive_scan_add(part), 63);
-            if (inc) break;
-        }
-        if (lead) {
-            __hip_atomic_store(st, (prefix + cnt) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bcnt[c] = (int)prefix;
-            if (chunk == nb - 1) totals[c] = (int)(prefix + cnt);  // the step's per-column totals
-        }
-    }
-    if (partials && threadIdx.x < 6) {
-        unsigned v = red[threadIdx.x][0];
-        for (int w = 1; w < kRT / 64; ++w) v = max(v, red[threadIdx.x][w]);
-        partials[(size_t)threadIdx.x * nb + chunk] = v;
-    }
-    __syncthreads();
-    // pass 2: rows (in-wave rank from the ballot, earlier waves of the round from LDS)
-    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
-        const int i = chunk * kRouteItems + r * kRT + threadIdx.x;
-        for (int d = 0; d < p.world; ++d) {
-            const unsigned long long bo = __builtin_amdgcn_ballot_w64(o[r] == d);
-            const unsigned long long bh = __builtin_amdgcn_ballot_w64((m[r] >> d) & 1ull);
-            if (lead) {
-                wcnt[wid][2 * d] = __builtin_popcountll(bo);
-                wcnt[wid][2 * d + 1] = __builtin_popcountll(bh);
-            }
-        }
-        __syncthreads();
-        if (o[r] >= 0) {
-            const int gid = ids ? ids[i] : p.id_offset + i;
-            const float4 row = make_float4(px[r], py[r], pz[r], __int_as_float(gid));
-            for (int d = 0; d < p.world; ++d) {
-                const bool po = o[r] == d, ph = (m[r] >> d) & 1ull;
-                const unsigned long long bo = __builtin_amdgcn_ballot_w64(po);
-                const unsigned long long bh = __builtin_amdgcn_ballot_w64(ph);
-                if (!(po || ph)) continue;
-                const int c = 2 * d + (po ? 0 : 1);
-                int j = bcnt[c];
-                for (int w = 0; w < wid; ++w) j += wcnt[w][c];
-                j += __builtin_popcountll((po ? bo : bh) & lt);
-                if (j >= fr.cap[c]) continue;  // more rows than planned: dropped, the flag fails
-                if (fr.base[c] < 0) {
-                    // self placement: owned rows after the other sources' owned rows, halo rows
-                    // (the rank's points that another rank owns) after theirs
-                    const int loc = (c & 1) ? sp.halo_base + j : sp.own_base + j;
-                    if (loc < 0 || loc >= sp.rows) continue;
-                    const size_t l3 = 3 * (size_t)KN_IDX(loc, sp.rows, 404);
-                    sp.pts[l3] = px[r];
-                    sp.pts[l3 + 1] = py[r];
-                    sp.pts[l3 + 2] = pz[r];
-                    sp.gids[loc] = gid;
-                } else {
-                    send[fr.base[c] + j] = row;
-                }
-            }
-        }
-        __syncthreads();
-        for (int c = threadIdx.x; c < cols; c += kRT) {
-            int t = 0;
-            for (int w = 0; w < kRT / 64; ++w) t += wcnt[w][c];
-            bcnt[c] += t;
-        }
-        __syncthreads();
-    }
-}
-
 __global__ __launch_bounds__(kRT) void route_unpack_kernel(const float4* __restrict__ recv,
                                                            const float4* __restrict__ self_rows, int rows,
                                                            UnpackTable t, float* __restrict__ pts,
@@ -927,37 +783,6 @@ hipError_t launch_route_scatter(const float* pts, const int* ids, int n, const R
     return hipGetLastError();
 }
 
-size_t route_fused_scratch_words(int n, int world) { return (size_t)2 * world * route_block_count(n) + 1; }
-
-// zeroes the look-back words + ticket and the totals (a kernel node: a captured hipMemsetAsync of
-// this odd size left stale words behind in graph replays)
-__global__ void route_fused_reset_kernel(unsigned* __restrict__ scratch, int words, int* __restrict__ totals,
-                                         int cols) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < words; i += gridDim.x * blockDim.x) scratch[i] = 0u;
-    if (blockIdx.x == 0 && (int)threadIdx.x < cols) totals[threadIdx.x] = 0;
-}
-
-hipError_t launch_route_fused(const float* pts, const int* ids, int n, const RouteParams* p, int world,
-                              const FusedRoute& fr, int* totals, unsigned* scratch, float4* send,
-                              const SelfPlace* self_place, unsigned* partials, hipStream_t s) {
-    if (world < 1 || world > kRouteMaxWorld || n >= (int)kLbMask) return hipErrorInvalidValue;
-    SelfPlace sp{};
-    for (int c = 0; c < 2 * world; ++c) {
-        if (fr.cap[c] < 0) return hipErrorInvalidValue;
-        if (fr.base[c] < 0 && fr.cap[c] > 0 && !self_place) return hipErrorInvalidValue;
-    }
-    if (self_place) {
-        if (!self_place->pts || !self_place->gids) return hipErrorInvalidValue;
-        sp = *self_place;
-    }
-    const int words = (int)route_fused_scratch_words(n, world);
-    route_fused_reset_kernel<<<std::min((words + 255) / 256, 64), 256, 0, s>>>(scratch, words, totals, 2 * world);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || n <= 0) return e;
-    const int nb = route_block_count(n);
-    route_fused_kernel<<<nb, kRT, 0, s>>>(pts, ids, n, p, fr, totals, scratch, send, sp, partials, nb);
-    return hipGetLastError();
-}
 
 hipError_t launch_route_plan(const double* metas, int world, int rank, const int grid[3], int k,
                              double halo_factor, const float* splits, RouteParams* p, double* hdr, hipStream_t s,

@@ -15,15 +15,7 @@ namespace kn {
 
 bool exact_epilogue();
 
-// One-pass steady routing (launch_route_fused) when KN_ROUTE_FUSED=1 (A/B); default: count + scan
-// + scatter
-static bool route_fused() {
-    static const bool on = [] {
-        const char* v = std::getenv("KN_ROUTE_FUSED");
-        return v && std::atoi(v) != 0;
-    }();
-    return on;
-}  // engine.cpp: KN_PIPE_EXACT
+  // engine.cpp: KN_PIPE_EXACT
 
 namespace {
 #define KN_TRY(expr)                     \
@@ -141,23 +133,6 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     }
     const long long nself = (long long)p_.tot[2 * p_.rank] + p_.tot[2 * p_.rank + 1];
     if (so + nself > p_.cap) { fail("send buffer smaller than the planned rows"); return; }
-    // one-pass steady routing (launch_route_fused): every column's base row and planned size
-    fused_ = FusedRoute{};
-    for (int d = 0; d < W; ++d) {
-        const int own_d = p_.tot[2 * d], halo_d = p_.tot[2 * d + 1];
-        if (own_d < 0 || halo_d < 0 || (d != p_.rank && (long long)own_d + halo_d != p_.cross_send[d])) {
-            fail("planned send counts do not match the split sizes");
-            return;
-        }
-        const bool self = d == p_.rank && !p_.self_via_comm;
-        const long long b = p_.self_via_comm && d == p_.rank ? so : soff_[d];
-        fused_.base[2 * d] = self ? -1 : (int)b;
-        fused_.cap[2 * d] = own_d;
-        // self: a share can hold points another rank owns that are halo of this rank (they
-        // enter the local rows after the other sources' halo rows)
-        fused_.base[2 * d + 1] = self ? -1 : (int)(b + own_d);
-        fused_.cap[2 * d + 1] = halo_d;
-    }
     table_ = UnpackTable{};
     table_.world = W;
     if (p_.self_via_comm) {
@@ -238,7 +213,7 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     auto layout = [&](char* base, Set& S) {
         char* q = base;
         S.send = carve<float4>(q, (size_t)p_.cap);
-        S.bc = carve<int>(q, route_fused_scratch_words(p_.n, W));  // block counts / look-back status
+        S.bc = carve<int>(q, (size_t)2 * W * nb);
         S.totals = carve<int>(q, (size_t)2 * W);
         S.partials = carve<unsigned>(q, (size_t)6 * nb);
         S.recv = carve<float4>(q, (size_t)recv_rows_);
@@ -377,12 +352,7 @@ hipError_t DistPipeline::exchange(int s, hipStream_t st) {
 hipError_t DistPipeline::stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks) {
     Set& S = set_[s];
     const auto* rp = static_cast<const RouteParams*>(route_dev_);
-    if (p_.n > 0 && route_fused()) {
-        const SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
-        KN_TRY(launch_route_fused(p_.points, p_.ids, p_.n, rp, p_.world, fused_, S.totals,
-                                  reinterpret_cast<unsigned*>(S.bc), S.send, p_.self_via_comm ? nullptr : &sp,
-                                  S.partials, st));
-    } else if (p_.n > 0) {
+    if (p_.n > 0) {
         KN_TRY(launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, st, S.partials));
         if (p_.self_via_comm) {
             KN_TRY(launch_route_scatter(p_.points, p_.ids, p_.n, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank, st));
@@ -488,11 +458,7 @@ kn_status DistPipeline::loopback_stage(int stage) {
         // the routing half of stage_build (exchange and local build follow in stage 1)
         Set& S = set_[0];
         const auto* rp = static_cast<const RouteParams*>(route_dev_);
-        if (p_.n > 0 && route_fused()) {
-            const SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
-            e = launch_route_fused(p_.points, p_.ids, p_.n, rp, p_.world, fused_, S.totals,
-                                   reinterpret_cast<unsigned*>(S.bc), S.send, &sp, S.partials, main_);
-        } else if (p_.n > 0) {
+        if (p_.n > 0) {
             e = launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, main_, S.partials);
             SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
             if (e == hipSuccess)

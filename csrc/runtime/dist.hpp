@@ -122,7 +122,6 @@ public:
     const float* d2(int s) const { return set_[s].d2; }
     const unsigned* counters(int s) const { return set_[s].counters; }
     const int* totals(int s) const { return set_[s].totals; }
-    const int* block_words(int s) const { return set_[s].bc; }
     int share_rows() const { return p_.n; }
     const unsigned* partials(int s) const { return set_[s].partials; }
 
@@ -155,7 +154,6 @@ private:
     BuildBuffers bproto_{};
     QueryBuffers qproto_{};
     CompleteBox complete_{};
-    FusedRoute fused_{};
     Set set_[2]{};
     void* route_dev_ = nullptr;
     double* metas_dev_ = nullptr;

@@ -1407,15 +1407,6 @@ public:
         KN_CHECK_HIP(hipMemcpy(t.data(), d_->totals((int)set), t.size() * sizeof(int), hipMemcpyDeviceToHost));
         std::vector<int64_t> out(c.begin(), c.end());
         out.insert(out.end(), t.begin(), t.end());
-        // the fused router's look-back words: [ticket, words without the inclusive flag, first
-        // such word's index, its value]
-        const size_t nw = kn::route_fused_scratch_words(d_->share_rows(), W);
-        std::vector<unsigned> bw(nw);
-        KN_CHECK_HIP(hipMemcpy(bw.data(), d_->block_words((int)set), nw * sizeof(unsigned), hipMemcpyDeviceToHost));
-        int64_t bad = 0, first = -1, fv = 0;
-        for (size_t i = 0; i + 1 < nw; ++i)
-            if (!(bw[i] & (2u << 30))) { if (first < 0) { first = (int64_t)i; fv = bw[i]; } ++bad; }
-        out.insert(out.end(), {(int64_t)bw[nw - 1], bad, first, fv});
         return out;
     }
     // enqueue `iters` steps (unroll: steps per graph launch, even >= 2, else one graph per stage)
