@@ -120,14 +120,8 @@ def run_native(args) -> dict:
     # then run at the GPU's steady clocks (from idle the query kernel takes 304-320 us for its
     # first ~20 steps vs 291 us warm, profiles/r4_coldstart.txt)
     idx0, d20 = e.results(dev)
-    idx0, d20 = idx0.clone(), d20.clone()
-
-    def check_eager():
-        c = brute_check(pts, torch.arange(pts.size(0), device=dev), idx0, d20, args.k) if not args.no_check else {}
-        log(f"check (eager rows) {c}")
-        return c
-
-    chk = check_eager() if args.check_order == "before" else {}
+    chk = brute_check(pts, torch.arange(pts.size(0), device=dev), idx0, d20, args.k) if not args.no_check else {}
+    log(f"check (eager rows) {chk}")
     if args.stream_clouds:
         # a stream of distinct clouds (kn::Engine::stream_step): every step copies ITS cloud into
         # the free grid set, bins and queries it; the next cloud is binned while this one queries
@@ -148,11 +142,6 @@ def run_native(args) -> dict:
     launch(args.warmup)
     e.sync()
     log("warmup done")
-    if args.check_order == "after":
-        # the eager rows' check between the warm-up and the timed steps (--check-order before: ahead
-        # of the warm-up): see the option's help
-        chk = check_eager()
-        torch.cuda.synchronize()
     t0 = time.perf_counter()
     launch(args.steps)
     e.sync()
@@ -477,9 +466,6 @@ def main() -> int:
     ap.add_argument("--path", choices=["native", "torch"], default="native",
                     help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--check-order", choices=("before", "after"), default="before",
-                    help="1 GPU: run the brute-force check of the eager rows before the warm-up steps or "
-                         "between them and the timed steps")
     ap.add_argument("--dist", action="store_true",
                     help="use the distributed (routing + RCCL) path even at world size 1")
     ap.add_argument("--deterministic", action="store_true",
