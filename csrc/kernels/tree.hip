@@ -482,18 +482,13 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         const int node = __builtin_amdgcn_readfirstlane(stk[sp]);
         const unsigned last = keys[KM - 1];
         const float ub = last == SENT ? INFINITY : __uint_as_float(last | kMask);
-#ifndef KN_TREE_POP_RETEST
-#define KN_TREE_POP_RETEST 0
-#endif
-        if (KN_TREE_POP_RETEST && node < a.P) {  // A/B: the round-3 re-test of every popped node
-            const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
-            if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
-        }
         if (node >= a.P) {
             // a leaf is re-tested against the bounds tightened since its push (a visit stages and
             // scores its points); an inner node is not: its children are tested below anyway,
             // and a child's box lies inside its parent's, so skipping the parent's re-test prunes
-            // the same subtrees one dependent box load sooner
+            // the same subtrees one dependent box load sooner (900K K=16: clustered 1.578 ->
+            // 1.453 ms/step, surfaces 0.972 -> 0.930, the same leaf visits and rows;
+            // profiles/ab_r4_tree_pop_retest.txt)
             const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
             if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
             const int lf = node - a.P;
