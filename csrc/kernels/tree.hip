@@ -444,9 +444,10 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     bool over = false;
 
     // stage leaf lf in the wave's LDS slice and stream its points to every lane (broadcast reads)
-    // pv: this lane's point of the leaf (lane < cnt), loaded by the caller
-    auto visit_loaded = [&](int b, int cnt, const float4& pv) __attribute__((always_inline)) {
-        if (lane < cnt) buf[lane] = pv;
+    auto visit = [&](int lf) __attribute__((always_inline)) {
+        const int b = (int)a.leaf_start[lf];
+        const int cnt = (int)a.leaf_start[lf + 1] - b;
+        if (lane < cnt) buf[lane] = a.pts[KN_IDX(b + lane, a.n, 402)];
         if (lane == 0) vis[nv] = b;
         __builtin_amdgcn_wave_barrier();
         const int sb = nv << kLeafBits;
@@ -457,12 +458,6 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         }
         ++nv;
         __builtin_amdgcn_wave_barrier();
-    };
-    auto visit = [&](int lf) __attribute__((always_inline)) {
-        const int b = (int)a.leaf_start[lf];
-        const int cnt = (int)a.leaf_start[lf + 1] - b;
-        const float4 pv = lane < cnt ? a.pts[KN_IDX(b + lane, a.n, 402)] : make_float4(0.f, 0.f, 0.f, 0.f);
-        visit_loaded(b, cnt, pv);
     };
     // the leaves holding the wave's own 64 points first: every lane starts the traversal with a
     // bound from ~64 nearby candidates (small leaves alone leave the early bounds loose, and a
@@ -494,29 +489,12 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             // the same subtrees one dependent box load sooner (900K K=16: clustered 1.578 ->
             // 1.453 ms/step, surfaces 0.972 -> 0.930, the same leaf visits and rows;
             // profiles/ab_r4_tree_pop_retest.txt)
+            const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
+            if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
             const int lf = node - a.P;
-            // the leaf's range is loaded with its box and its points before the test resolves
-            // (two dependent rounds per visited leaf instead of three; a pruned leaf's load is
-            // wasted)
-#ifndef KN_TREE_HOIST
-#define KN_TREE_HOIST 1
-#endif
-            if (KN_TREE_HOIST) {
-                const int b = (int)a.leaf_start[lf];
-                const int cnt = (int)a.leaf_start[lf + 1] - b;
-                const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
-                const float4 pv = lane < cnt ? a.pts[KN_IDX(b + lane, a.n, 402)] : make_float4(0.f, 0.f, 0.f, 0.f);
-                if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
-                if (lf >= l0 && lf <= l1) continue;  // visited first
-                if (nv == kMaxVisit) { over = true; break; }
-                visit_loaded(b, cnt, pv);
-            } else {
-                const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
-                if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
-                if (lf >= l0 && lf <= l1) continue;  // visited first
-                if (nv == kMaxVisit) { over = true; break; }
-                visit(lf);
-            }
+            if (lf >= l0 && lf <= l1) continue;  // visited first
+            if (nv == kMaxVisit) { over = true; break; }
+            visit(lf);
             continue;
         }
         const int c0 = 2 * node;
