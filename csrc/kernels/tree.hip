@@ -498,6 +498,49 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             continue;
         }
         const int c0 = 2 * node;
+#ifndef KN_TREE_SKIP2
+#define KN_TREE_SKIP2 1
+#endif
+        if (KN_TREE_SKIP2 && c0 < a.P) {
+            // the children are inner nodes: test the four grandchildren directly (a grandchild's
+            // box lies inside its parent's, so one that passes has a passing parent) -- one
+            // dependent round of box loads per two levels. Grandchild g is empty when its first
+            // leaf lies past L (the left child's left child never is).
+            const int g0 = 2 * c0;
+            float gd[4];
+            unsigned long long need = 0ull;  // bit j: grandchild j is entered
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int g = g0 + j;
+                gd[j] = (j == 0 || first_leaf(g, a.logP) < L) ? box_d2(qx, qy, qz, a.nlo[g], a.nhi[g]) : INFINITY;
+                if (__builtin_amdgcn_ballot_w64(live && gd[j] < INFINITY && gd[j] * kShrink <= ub)) need |= 1ull << j;
+            }
+            // near-first: the grandchild nearest for most live lanes goes on top
+            int am = 0;
+#pragma unroll
+            for (int j = 1; j < 4; ++j) am = gd[j] < gd[am] ? j : am;
+            int ord[4], vote[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                vote[j] = __builtin_popcountll(__builtin_amdgcn_ballot_w64(live && am == j));
+                ord[j] = j;
+            }
+#pragma unroll
+            for (int i = 1; i < 4; ++i)  // ascending votes: the most-voted pushed last (top)
+#pragma unroll
+                for (int j = i; j > 0; --j)
+                    if (vote[ord[j]] < vote[ord[j - 1]]) { const int t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = ord[i];
+                if ((need >> j) & 1ull) {
+                    if (lane == 0) stk[sp] = g0 + j;
+                    ++sp;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
         // the left child shares the node's first leaf (non-empty); the right one may lie past L
         const float b0 = box_d2(qx, qy, qz, a.nlo[c0], a.nhi[c0]);
         const float b1 = first_leaf(c0 + 1, a.logP) < L ? box_d2(qx, qy, qz, a.nlo[c0 + 1], a.nhi[c0 + 1]) : INFINITY;
