@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "kn/knn_device.h"
 #include "kn/tree.h"
@@ -23,7 +24,7 @@ constexpr int kVisitBits = 13 - kLeafBits;    // key slot = visit index | point 
 constexpr int kMaxVisit = 1 << kVisitBits;    // leaves a wave may visit before its queries go exact
 constexpr unsigned kMask = (1u << (kVisitBits + kLeafBits)) - 1u;
 static_assert((1 << kLeafBits) == kTreeLeaf, "leaf size");
-constexpr int kStack = 64;                    // traversal stack (depth <= log2(P) + 1)
+constexpr int kStack = 128;  // traversal stack: <= 7 pending siblings per 3 levels (fan 8) of log2(P) <= 31
 constexpr int kTCap = 256;                    // exact-finish candidate buffer per wave (u64 keys)
 constexpr int kSortPasses = 3;                // odd-even passes of the exact re-rank (then checked)
 // A point inside a box can compute a squared distance a few ulps below the box's: nodes are
@@ -498,47 +499,56 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             continue;
         }
         const int c0 = 2 * node;
-#ifndef KN_TREE_SKIP2
-#define KN_TREE_SKIP2 1
+#ifndef KN_TREE_FAN
+#define KN_TREE_FAN 8
 #endif
-        if (KN_TREE_SKIP2 && c0 < a.P) {
-            // the children are inner nodes: test the four grandchildren directly (a grandchild's
-            // box lies inside its parent's, so one that passes has a passing parent) -- one
-            // dependent round of box loads per two levels. Grandchild g is empty when its first
-            // leaf lies past L (the left child's left child never is).
-            const int g0 = 2 * c0;
-            float gd[4];
-            unsigned long long need = 0ull;  // bit j: grandchild j is entered
+        // descendants `levels` below an inner node, tested and pushed directly (a descendant's box
+        // lies inside its ancestors', so one that passes has passing ancestors): one dependent
+        // round of box loads per `levels` levels instead of per level. A node is empty when its
+        // first leaf lies past L (the leftmost descendant never is).
+        auto enter_descendants = [&](auto fan_c) __attribute__((always_inline)) {
+            constexpr int FAN = decltype(fan_c)::value;
+            const int g0 = node * FAN;
+            float gd[FAN];
+            unsigned need = 0u;  // bit j: descendant j is entered
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < FAN; ++j) {
                 const int g = g0 + j;
                 gd[j] = (j == 0 || first_leaf(g, a.logP) < L) ? box_d2(qx, qy, qz, a.nlo[g], a.nhi[g]) : INFINITY;
-                if (__builtin_amdgcn_ballot_w64(live && gd[j] < INFINITY && gd[j] * kShrink <= ub)) need |= 1ull << j;
+                if (__builtin_amdgcn_ballot_w64(live && gd[j] < INFINITY && gd[j] * kShrink <= ub)) need |= 1u << j;
             }
-            // near-first: the grandchild nearest for most live lanes goes on top
+            // near-first: the descendant nearest for most live lanes goes on top
             int am = 0;
 #pragma unroll
-            for (int j = 1; j < 4; ++j) am = gd[j] < gd[am] ? j : am;
-            int ord[4], vote[4];
+            for (int j = 1; j < FAN; ++j) am = gd[j] < gd[am] ? j : am;
+            int ord[FAN], vote[FAN];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                vote[j] = __builtin_popcountll(__builtin_amdgcn_ballot_w64(live && am == j));
+            for (int j = 0; j < FAN; ++j) {
+                vote[j] = (need >> j) & 1u ? __builtin_popcountll(__builtin_amdgcn_ballot_w64(live && am == j)) : -1;
                 ord[j] = j;
             }
 #pragma unroll
-            for (int i = 1; i < 4; ++i)  // ascending votes: the most-voted pushed last (top)
+            for (int i = 1; i < FAN; ++i)  // ascending votes: the most-voted pushed last (top)
 #pragma unroll
                 for (int j = i; j > 0; --j)
                     if (vote[ord[j]] < vote[ord[j - 1]]) { const int t = ord[j]; ord[j] = ord[j - 1]; ord[j - 1] = t; }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < FAN; ++i) {
                 const int j = ord[i];
-                if ((need >> j) & 1ull) {
+                if ((need >> j) & 1u) {
                     if (lane == 0) stk[sp] = g0 + j;
                     ++sp;
                 }
             }
             __builtin_amdgcn_wave_barrier();
+        };
+        if (sp + KN_TREE_FAN > kStack) { over = true; break; }  // (unreachable for P <= 2^31) exact path
+        if (KN_TREE_FAN >= 8 && 2 * c0 < a.P) {  // the grandchildren are inner nodes
+            enter_descendants(std::integral_constant<int, 8>());
+            continue;
+        }
+        if (KN_TREE_FAN >= 4 && c0 < a.P) {  // the children are inner nodes
+            enter_descendants(std::integral_constant<int, 4>());
             continue;
         }
         // the left child shares the node's first leaf (non-empty); the right one may lie past L
