@@ -24,7 +24,7 @@ constexpr int kVisitBits = 13 - kLeafBits;    // key slot = visit index | point 
 constexpr int kMaxVisit = 1 << kVisitBits;    // leaves a wave may visit before its queries go exact
 constexpr unsigned kMask = (1u << (kVisitBits + kLeafBits)) - 1u;
 static_assert((1 << kLeafBits) == kTreeLeaf, "leaf size");
-constexpr int kStack = 128;  // traversal stack: <= 7 pending siblings per 3 levels (fan 8) of log2(P) <= 31
+constexpr int kStack = 64;  // traversal stack: <= 3 pending siblings per 2 levels of log2(P) <= 31
 constexpr int kTCap = 256;                    // exact-finish candidate buffer per wave (u64 keys)
 constexpr int kSortPasses = 3;                // odd-even passes of the exact re-rank (then checked)
 // A point inside a box can compute a squared distance a few ulps below the box's: nodes are
@@ -499,13 +499,12 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             continue;
         }
         const int c0 = 2 * node;
-#ifndef KN_TREE_FAN
-#define KN_TREE_FAN 8
-#endif
-        // descendants `levels` below an inner node, tested and pushed directly (a descendant's box
-        // lies inside its ancestors', so one that passes has passing ancestors): one dependent
-        // round of box loads per `levels` levels instead of per level. A node is empty when its
-        // first leaf lies past L (the leftmost descendant never is).
+        // the grandchildren of an inner node whose children are inner nodes, tested and pushed
+        // directly (a grandchild's box lies inside its parent's, so one that passes has a passing
+        // parent): one dependent round of box loads per two levels instead of per level. A node is
+        // empty when its first leaf lies past L (the leftmost descendant never is). 900K K=16:
+        // clustered 1.479 -> 1.449 ms/step, surfaces 0.951 -> 0.825; three levels (8 boxes per
+        // round) lost, 2.11 / 1.16 (profiles/ab_r4_tree_fan.txt)
         auto enter_descendants = [&](auto fan_c) __attribute__((always_inline)) {
             constexpr int FAN = decltype(fan_c)::value;
             const int g0 = node * FAN;
@@ -542,12 +541,8 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             }
             __builtin_amdgcn_wave_barrier();
         };
-        if (sp + KN_TREE_FAN > kStack) { over = true; break; }  // (unreachable for P <= 2^31) exact path
-        if (KN_TREE_FAN >= 8 && 2 * c0 < a.P) {  // the grandchildren are inner nodes
-            enter_descendants(std::integral_constant<int, 8>());
-            continue;
-        }
-        if (KN_TREE_FAN >= 4 && c0 < a.P) {  // the children are inner nodes
+        if (sp + 4 > kStack) { over = true; break; }  // (unreachable for P <= 2^31) exact path
+        if (c0 < a.P) {  // the children are inner nodes
             enter_descendants(std::integral_constant<int, 4>());
             continue;
         }
