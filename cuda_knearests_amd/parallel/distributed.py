@@ -790,7 +790,18 @@ class DistributedKNearests:
         iters > 1). resident: keep the next step's build enqueued after the call (the caller
         promises the points do not change before the next call)."""
         st = self._steady
-        p = self._pipe_for(points, ids)
+        try:
+            p = self._pipe_for(points, ids)
+        except RuntimeError as e:
+            # the native pipeline could not be built (communicator or plan check): the torch
+            # steady path instead, for good (every rank builds the same plan, so all take this)
+            _log.warning("rank %d: native pipeline unavailable (%s); torch steady path", self.rank, e)
+            self.native_pipeline = False
+            self._pipe = None
+            res = None
+            for _ in range(iters):
+                res = self._solve_steady(points, ids)
+            return res
         pipe = p["pipe"]
         last = pipe.launch(iters, self.pipe_unroll if iters > 1 else 0, bool(resident))
         gids, idx, d2 = p["outs"][pipe.last_set()]
