@@ -907,9 +907,23 @@ unsigned* Engine::get_permutation() {
     return d2h(perm_, (size_t)n_, stream_);
 }
 unsigned* Engine::get_knearests_stored() {
+    // KN_GET_TRACE=1: the getter's phases on stderr (stored-space conversion, host copy)
+    static const bool trace = [] {
+        const char* v = std::getenv("KN_GET_TRACE");
+        return v && std::atoi(v) != 0;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
     unsigned* d = d_knn_stored();
     if (!d) { if (err_.empty()) fail(KN_ERR_STATE, "not solved"); return nullptr; }
-    return d2h(d, (size_t)n_ * cfg_.k, stream_);
+    const auto t1 = std::chrono::steady_clock::now();
+    unsigned* h = d2h(d, (size_t)n_ * cfg_.k, stream_);
+    if (trace) {
+        const auto t2 = std::chrono::steady_clock::now();
+        fprintf(stderr, "get_knearests: to_stored %.3f ms, copy %.3f ms\n",
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(t2 - t1).count());
+    }
+    return h;
 }
 float* Engine::get_distances_stored() {
     if (!out_dist_) { fail(KN_ERR_STATE, "distances disabled"); return nullptr; }

@@ -5,6 +5,8 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -115,7 +117,9 @@ hipError_t copy_h2d_staged(void* d, const void* h, size_t bytes, hipStream_t s) 
 // destination's 2 MiB-aligned interior is advised to transparent huge pages first: a freshly
 // malloc'd result faults one 2 MiB page per first touch instead of 512 4 KiB ones (61 MB copy-out
 // with 8 threads 0.74-0.81 ms vs 3.6-4.4 ms, its free() 2.4-3.0 vs 4.8-7.2 ms; DMA 1.08 ms at
-// 56 GB/s; scripts/hostio_probe.cpp, profiles/r4_hostio_probe.txt).
+// 56 GB/s; scripts/hostio_probe.cpp, profiles/r4_hostio_probe.txt). The destination is faulted
+// in before the first chunk lands (900K K=16 getter 1.69 -> 1.54 ms median, faster in all 6
+// interleaved pairs; profiles/api_r4_getter_prefault.jsonl).
 namespace {
 constexpr size_t kBigChunk = 16u << 20;
 constexpr size_t kHuge = 2u << 20;
@@ -140,6 +144,11 @@ BigStage& big() {
 }  // namespace
 
 static hipError_t copy_d2h_big(void* h, const void* d, size_t bytes, hipStream_t s) {
+    // KN_GET_TRACE=1: enqueue / first chunk ready / last chunk ready / done, on stderr
+    static const bool trace = env_on("KN_GET_TRACE", false);
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    clk::time_point t_enq, t_first, t_last;
     BigStage& b = big();
     std::lock_guard<std::mutex> lock(b.mu);
     hipError_t e;
@@ -170,20 +179,26 @@ static hipError_t copy_d2h_big(void* h, const void* d, size_t bytes, hipStream_t
             return e;
         if ((e = hipEventRecord(b.ev[c], s)) != hipSuccess) return e;
     }
+    t_enq = clk::now();
     advise_huge(h, bytes);
-    // 8 threads: the copy-out's best on MI355X hosts (16 contend for the page-fault path)
-    const int nt = std::max(1, std::min(8, omp_get_max_threads()));
+    // 8 threads: the copy-out's best on MI355X hosts (16 contend for the page-fault path;
+    // KN_COPY_THREADS, A/B)
+    static const int copy_threads = [] {
+        const char* v = std::getenv("KN_COPY_THREADS");
+        const int t = v ? std::atoi(v) : 8;
+        return (t >= 1 && t <= 64) ? t : 8;
+    }();
+    // KN_COPY_PREFAULT (default on): every thread first faults in its slices of the destination
+    // (one store per 4 KiB page) while the first chunk's DMA is still in flight, so the copy-out
+    // of each chunk runs at the memcpy rate of mapped pages instead of zeroing fresh huge pages
+    // behind the DMA
+    static const bool prefault = env_on("KN_COPY_PREFAULT", true);
+    const int nt = std::max(1, std::min(copy_threads, omp_get_max_threads()));
     hipError_t err = hipSuccess;
 #pragma omp parallel num_threads(nt)
     {
         const int t = omp_get_thread_num(), T = omp_get_num_threads();
-        for (size_t c = 0; c < nchunks; ++c) {
-#pragma omp single
-            {
-                const hipError_t x = hipEventSynchronize(b.ev[c]);
-                if (x != hipSuccess) err = x;
-            }  // implicit barrier: the chunk is in pinned memory
-            if (err != hipSuccess) continue;
+        auto slice = [&](size_t c, uintptr_t* a, uintptr_t* z) {
             const size_t off = c * kBigChunk, len = std::min(kBigChunk, bytes - off);
             // slices cut at 2 MiB boundaries of the destination address: every huge page is
             // touched (faulted in) by one thread only
@@ -193,9 +208,32 @@ static hipError_t copy_d2h_big(void* h, const void* d, size_t bytes, hipStream_t
                 if (i >= T) return end;
                 return std::min(end, (beg + (uintptr_t)i * per + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
             };
-            const uintptr_t a = cut(t), z = cut(t + 1);
+            *a = cut(t);
+            *z = cut(t + 1);
+        };
+        if (prefault)
+            for (size_t c = 0; c < nchunks; ++c) {
+                uintptr_t a, z;
+                slice(c, &a, &z);
+                for (uintptr_t p = a; p < z; p = (p & ~(uintptr_t)4095) + 4096) *(volatile char*)p = 0;
+            }
+        for (size_t c = 0; c < nchunks; ++c) {
+#pragma omp single
+            {
+                const hipError_t x = hipEventSynchronize(b.ev[c]);
+                if (x != hipSuccess) err = x;
+                if (trace) (c == 0 ? t_first : t_last) = clk::now();
+            }  // implicit barrier: the chunk is in pinned memory
+            if (err != hipSuccess) continue;
+            uintptr_t a, z;
+            slice(c, &a, &z);
             if (z > a) std::memcpy((void*)a, (const char*)b.buf + (a - (uintptr_t)h), z - a);
         }
+    }
+    if (trace) {
+        auto ms = [&](clk::time_point t) { return std::chrono::duration<double, std::milli>(t - t0).count(); };
+        fprintf(stderr, "copy_d2h_big %.1f MB: enqueued %.3f, chunk0 %.3f, last %.3f, done %.3f ms\n", bytes / 1e6,
+                ms(t_enq), ms(t_first), nchunks > 1 ? ms(t_last) : ms(t_first), ms(clk::now()));
     }
     return err;
 }
