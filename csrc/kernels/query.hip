@@ -123,13 +123,20 @@ constexpr int kRowOrderMax = 128;
 // iterations per wave at K=16 -> 26 over 3.8). Interleaved A/B, 900K uniform, identical rows
 // (profiles/ab_r3_outer_pack.jsonl): query K=12 -5 %, K=16 -2 %, K=24 -17 %, K=32 -3 %, K=40 -6 %,
 // blue noise K=16 -5 %, 300K K=16 -12 %; K=8 +9 % (its outer rows are almost never needed, the
-// mask costs more): 0 = off, 1 = every K <= 40 bucket, 2 = the K buckets 12..40 (default).
+// mask costs more): 0 = off, 1 = every K <= 40 bucket, 2 = the K buckets 12..40 and 64 (default),
+// 3 = the K buckets 12..64. Round 4, the whole-block walk (K > 40) packing its outer ring instead
+// of the distance-sorted table (interleaved, identical rows, profiles/ab_r4_outer_pack_k64.txt):
+// K=64 1.189 -> 1.128 ms/step, but K=50 0.912 -> 0.932 (the sorted table stays there).
 // Oracle check on clustered clouds (profiles/diag_r3_outer_pack_oracle.txt).
 #ifndef KN_OUTER_PACK
 #define KN_OUTER_PACK 2
 #endif
 template <int KT>
-constexpr bool outer_pack_k() { return KN_OUTER_PACK == 1 ? KT <= 40 : (KN_OUTER_PACK == 2 && KT >= 12 && KT <= 40); }
+constexpr bool outer_pack_k() {
+    return KN_OUTER_PACK == 1 ? KT <= 40
+         : KN_OUTER_PACK == 2 ? ((KT >= 12 && KT <= 40) || KT == 64)
+         : KN_OUTER_PACK == 3 ? (KT >= 12 && KT <= 64) : false;
+}
 // Default AutoParams::xsub of the tile path for K <= KN_XSUB_MAX_K. Interleaved A/B at 900K
 // uniform (profiles/ab_r3_xsub.jsonl): xsub 2 query K=8 0.207 -> 0.198, K=16 0.305 -> 0.292 ms
 // (build +3 us), K=32 +2 %, K=50 +4 %; xsub 4 at K=16 0.318 -> 0.301 but build +11 us.
@@ -234,7 +241,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
     constexpr int KM = KT + M + 1;
     constexpr bool kFull = LANE && (KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40));
-    constexpr bool kRowOrder = LANE && (KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && kFull));
+    // (KN_OUTER_PACK=3: the whole-block walk packs its outer rows instead of the sorted table)
+    constexpr bool kRowOrder = LANE && (KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && kFull && !outer_pack_k<KT>()));
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     KN_PH_DECL
     float4* pts = reinterpret_cast<float4*>(smem);
@@ -1711,12 +1719,12 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.cap = q.lds_capacity;
         a.flags = q.flags;
         {
-            // the distance-sorted, mirrored table for the whole-block walk (K > 40)
-            constexpr bool full = KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40);
+            // the distance-sorted, mirrored table for the whole-block walk (K > 40), or the
+            // outer-ring rows of the packed walk
             row_order_table(a.H, a.row_order, false);
             a.row_mirror = 1;
             a.n_outer = 0;
-            if (outer_pack_k<KT>() && !full && !(KN_ROW_ORDER == 1) && a.H >= 2 &&
+            if (outer_pack_k<KT>() && !(KN_ROW_ORDER == 1) && a.H >= 2 &&
                 (2 * a.H + 1) * (2 * a.H + 1) - 9 <= 64) {
                 // the distance-sorted table minus the 3x3 rows around the query's own row
                 unsigned all[32];

@@ -70,7 +70,8 @@ def test_stream_kernel_vs_oracle(cuda, k, gen):
 
 
 @pytest.mark.parametrize("k,gen", [(1, "uniform"), (8, "blue"), (16, "uniform"), (32, "uniform"), (50, "uniform"),
-                                   (64, "uniform"), (16, "clustered"), (50, "clustered"), (48, "blue")])
+                                   (64, "uniform"), (16, "clustered"), (50, "clustered"), (48, "blue"),
+                                   (64, "clustered"), (60, "blue")])
 def test_lane_walk_vs_union_stream(cuda, k, gen):
     # per-lane walk (flags bit 3, the default) vs the wave-uniform union stream (bit 2) of the
     # same LDS-staged tile kernel: oracle-exact and bit-identical to each other
