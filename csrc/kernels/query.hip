@@ -131,6 +131,9 @@ constexpr int kRowOrderMax = 128;
 #ifndef KN_OUTER_PACK
 #define KN_OUTER_PACK 2
 #endif
+// (Round 4: the packed walk's 3x3 inner rows in the mirrored expected-distance order instead of
+// centre-out z/y lost at every K: K=16 +1.3 %, K=32 +0.8 %, K=50 +2 %, K=64 +2.5 %;
+// profiles/ab_r4_pack_inner_sorted.txt. Removed.)
 template <int KT>
 constexpr bool outer_pack_k() {
     return KN_OUTER_PACK == 1 ? KT <= 40
