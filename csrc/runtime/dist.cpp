@@ -13,7 +13,7 @@
 
 namespace kn {
 
-bool exact_epilogue();
+bool exact_epilogue(int k);
 
   // engine.cpp: KN_PIPE_EXACT
 
@@ -415,7 +415,7 @@ hipError_t DistPipeline::stage_query(int s, hipStream_t st) {
     // the tile kernel and its exact finish (KN_PIPE_EXACT=1: the exact finish opens the epilogue
     // on the side stream instead, engine.cpp exact_epilogue)
     QueryBuffers q = query_proto(s);
-    q.exact_mode = exact_epilogue() ? 1 : 0;
+    q.exact_mode = exact_epilogue(p_.k) ? 1 : 0;
     return launch_query(q, st);
 }
 
@@ -439,7 +439,7 @@ QueryBuffers DistPipeline::query_proto(int s) const {
 // as planned, no uncertified row), its MAX all-reduce and the sticky host flag.
 hipError_t DistPipeline::stage_flag(int s, hipStream_t st) {
     Set& S = set_[s];
-    if (!p_.use_tree && exact_epilogue()) {
+    if (!p_.use_tree && exact_epilogue(p_.k)) {
         QueryBuffers q = query_proto(s);
         q.exact_mode = 2;
         KN_TRY(launch_query(q, st));

@@ -613,17 +613,19 @@ kn_status Engine::stage_build(int s, hipStream_t st) {
     return r;
 }
 
-// KN_PIPE_EXACT=1: the tile kernel's exact finish runs as an epilogue on the build stream
-// instead of right after the tile kernel on the query stream. Measured slower (900K, K=16,
-// unroll 4, interleaved on one box, profiles/r4_ab_exact.txt): 200 steps 0.2954 -> 0.3016 ms,
-// 20 steps 0.317 -> 0.324 -- the extra cross-stream dependency and the exact kernel's
-// workgroups competing with the next query cost more than its ~5 us on the query stream.
-bool exact_epilogue() {
-    static const bool on = [] {
+// The tile kernel's exact finish as an epilogue on the build stream instead of right after the
+// tile kernel on the query stream: default for 32 < K <= 64 (the lane walk's top-K margin of 1
+// slot there sends ~360 of 900K queries to the exact kernel, ~38 us), where it wins -- 900K K=50
+// 200 steps 0.913 -> 0.855 ms, 20 steps 0.90 -> 0.868 (interleaved processes on one box,
+// profiles/ab_r4_exact_k50.txt). At K=16 (~5 us of exact work) it loses: 0.2954 -> 0.3016 ms,
+// the extra cross-stream dependency and the exact kernel's workgroups competing with the next
+// query cost more (profiles/r4_ab_exact.txt). KN_PIPE_EXACT=0 / 1 forces it off / on.
+bool exact_epilogue(int k) {
+    static const int mode = [] {
         const char* v = std::getenv("KN_PIPE_EXACT");
-        return v && std::atoi(v) == 1;
+        return v ? std::atoi(v) : -1;
     }();
-    return on;
+    return mode == 1 || (mode < 0 && k > 32 && k <= 64);
 }
 
 kn_status Engine::stage_query(int s, hipStream_t st) {
@@ -634,7 +636,7 @@ kn_status Engine::stage_query(int s, hipStream_t st) {
     kn_status r;
     if (use_tree_) {
         r = tree_query_async();
-    } else if (!exact_epilogue()) {
+    } else if (!exact_epilogue(cfg_.k)) {
         r = query_async(true);
     } else {
         // the tile kernel only: its fallback list's exact finish is the epilogue on the build
@@ -718,7 +720,7 @@ kn_status Engine::ensure_pipeline() {
         auto b = [this](int s, hipStream_t st2) { return stage_build(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         auto q = [this](int s, hipStream_t st2) { return stage_query(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         Pipeline::Stage x;
-        if (!use_tree_ && exact_epilogue())  // the tree query finishes its own exact-path queries
+        if (!use_tree_ && exact_epilogue(cfg_.k))  // the tree query finishes its own exact-path queries
             x = [this](int s, hipStream_t st2) { return stage_exact(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         if ((st = check(pipe_.init(stream_, bstream_, b, q, x), "pipeline init")) != KN_OK) return st;
     }
