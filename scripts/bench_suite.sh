@@ -42,6 +42,8 @@ run 200 "900K uniform k16 gpu, stream of 4 distinct clouds" --n 900000 --k 16 --
 run 200 "900K uniform k16 rccl world1 (native distributed pipeline)" --dist --n 900000 --k 16 --steps 200 --warmup 50
 run 200 "900K uniform k16 rccl world1, forced collectives" --dist --force-collectives --n 900000 --k 16 --steps 200 --warmup 50
 run 200 "900K uniform k50 gpu (reference K)" --n 900000 --k 50 --steps 100 --warmup 30
+run 200 "900K uniform k50 gpu, driver 20/5" --n 900000 --k 50 --steps 20 --warmup 5
+run 200 "900K uniform k64 gpu" --n 900000 --k 64 --steps 100 --warmup 30
 run 300 "cfg4 10M uniform k32 gpu" --n 10000000 --k 32 --steps 20 --warmup 5
 run 200 "900K points on surfaces k16 gpu (occupancy-adaptive grid)" --gen surface --n 900000 --k 16 --steps 100 --warmup 20
 run 300 "900K clustered k16 gpu (occupancy-adaptive grid)" --gen clustered --n 900000 --k 16 --steps 100 --warmup 20
