@@ -614,18 +614,20 @@ kn_status Engine::stage_build(int s, hipStream_t st) {
 }
 
 // The tile kernel's exact finish as an epilogue on the build stream instead of right after the
-// tile kernel on the query stream: default for 32 < K <= 64 (the lane walk's top-K margin of 1
-// slot there sends ~360 of 900K queries to the exact kernel, ~38 us), where it wins -- 900K K=50
-// 200 steps 0.913 -> 0.855 ms, 20 steps 0.90 -> 0.868 (interleaved processes on one box,
-// profiles/ab_r4_exact_k50.txt). At K=16 (~5 us of exact work) it loses: 0.2954 -> 0.3016 ms,
-// the extra cross-stream dependency and the exact kernel's workgroups competing with the next
-// query cost more (profiles/r4_ab_exact.txt). KN_PIPE_EXACT=0 / 1 forces it off / on.
+// tile kernel on the query stream: default for the K buckets 32..64, where it wins -- 900K K=50
+// (the lane walk's 1-slot top-K margin sends ~360 queries to the exact kernel, ~38 us) 200
+// steps 0.913 -> 0.855 ms, 20 steps 0.90 -> 0.868 (interleaved processes on one box,
+// profiles/ab_r4_exact_k50.txt); K=32 0.518 -> 0.500 (profiles/ab_r4_m1_epilogue.txt). At K=16
+// and K=24 it loses (0.2946 -> 0.2976, 0.396 -> 0.403; r3: 0.2954 -> 0.3016,
+// profiles/r4_ab_exact.txt): the extra cross-stream dependency and the exact kernel's workgroups
+// competing with the next query cost more than the few us of exact work. KN_PIPE_EXACT=0 / 1
+// forces it off / on.
 bool exact_epilogue(int k) {
     static const int mode = [] {
         const char* v = std::getenv("KN_PIPE_EXACT");
         return v ? std::atoi(v) : -1;
     }();
-    return mode == 1 || (mode < 0 && k > 32 && k <= 64);
+    return mode == 1 || (mode < 0 && k > 24 && k <= 64);
 }
 
 kn_status Engine::stage_query(int s, hipStream_t st) {
