@@ -3,8 +3,8 @@
 cuda_knearests_amd._build.build_variant(name, flags) (round 4: -DKN_TILE_WG=512, since removed,
 and -DKN_TOPK_MARGIN=1; profiles/ab_r4_tiles_margin.txt). Rows must equal the baseline's.
 usage: python scripts/ab_tiles.py [n] [k] [rounds] [steps] [variants]
-variants: comma-separated extension suffixes ("base" = _C) on the auto tile plan, replacing the
-built-in tile configs (e.g. "base,_op3")."""
+variants: comma-separated extension suffixes ("base" = _C), optionally with a tile hint
+("base@4x4x8"; none = the auto plan), replacing the built-in configs (e.g. "base,_op3")."""
 import importlib
 import sys
 import time
@@ -20,7 +20,11 @@ steps = int(sys.argv[4]) if len(sys.argv) > 4 else 100
 configs = [("", [0, 0, 0]), ("_wg512", [4, 4, 8]), ("_wg512", [4, 8, 4]), ("_wg512", [0, 0, 0]), ("", [4, 4, 8]),
            ("_wg512", [8, 4, 4]), ("_m1", [0, 0, 0]), ("_wg512m1", [4, 4, 8])]
 if len(sys.argv) > 5:
-    configs = [("" if v == "base" else v, [0, 0, 0]) for v in sys.argv[5].split(",")]
+    # "<suffix>[@TXxTYxTZ]": e.g. "base,base@4x4x8,_op3"
+    def _cfg(v):
+        suf, _, t = v.partition("@")
+        return ("" if suf == "base" else suf, [int(x) for x in t.split("x")] if t else [0, 0, 0])
+    configs = [_cfg(v) for v in sys.argv[5].split(",")]
 dev = torch.device("cuda", 0)
 pts = uniform_cloud(n, seed=0, device=dev)
 engines = []
