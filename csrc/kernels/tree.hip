@@ -415,6 +415,9 @@ __global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, 
 }
 
 // ---- query: one wave per 64 consecutive points of the Morton order (lanes = queries) -------------
+// (Round 4: asking the compiler for 6 / 8 waves per SIMD at K <= 16 (82 -> 80 / 64 VGPRs, 3 / 12
+// spilled) was mixed -- clustered 1.440 -> 1.422 / 1.404 ms, surfaces 0.825 -> 0.854 / 0.853;
+// profiles/ab_r4_tree_waves.txt -- and is not used.)
 template <int KT, int M>
 __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     constexpr int KM = KT + M + 1;  // + 1: the query itself enters its own list at d2 = 0
