@@ -213,6 +213,10 @@ def run_dist(args) -> dict:
     from cuda_knearests_amd.parallel import DistributedKNearests
     from cuda_knearests_amd.utils import uniform_cloud
 
+    from cuda_knearests_amd._ext import load as _load_ext
+
+    # a native backtrace if anything in the native stack (RCCL included) faults
+    _load_ext().install_crash_handler()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("KN_SAME_DEVICE"):  # rehearsal: every rank on cuda:0 (1-GPU box)
         local = 0
@@ -530,6 +534,10 @@ def main() -> int:
                  "steady_async": bool(r["stats"].get("steady")) and not args.sync_steps,
                  "invalid_async_steps": r["invalid_async_steps"], "path": "distributed",
                  "pipelined": bool(r["stats"].get("pipelined")), "per_call": bool(args.per_call),
+                 # how the native pipeline ran: "graph" (hipGraphs, RCCL captured) or "eager"
+                 # (the same stages enqueued per step; the default at world > 1)
+                 "dist_mode": r["stats"].get("pipe_mode"),
+                 "capture_fallbacks": r["stats"].get("capture_fallbacks"),
                  "force_collectives": bool(args.force_collectives),
                  "host_enqueue_ms_per_step": round(r["host_enqueue_ms_per_step"], 4),
                  # one serial steady step's phases (event-timed, max over ranks); in the timed

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -293,17 +294,72 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
         ok_ = true;
         return;
     }
-    if (pipe_.init(main_, side_, b, q, r, true) != hipSuccess) { fail("pipeline init"); return; }
-    // one eager (uncaptured) step: RCCL connects to the step's peers and sets up the all-reduce
-    // before any of it is captured into a graph (collective: every rank builds its pipeline at
-    // the same solve() call)
-    if (stage_build(1, main_) != hipSuccess || stage_query(1, main_) != hipSuccess || stage_flag(1, main_) != hipSuccess ||
-        hipStreamSynchronize(main_) != hipSuccess) {
-        fail("eager warm-up step of the distributed pipeline failed");
-        return;
-    }
+    // KN_DIST_CAPTURE_JOINED=1 (diagnostics): start unrolled captures on the main stream, so the
+    // RCCL calls of the build stage are captured on a JOINED stream (the round-4 segfault)
+    const char* joined = std::getenv("KN_DIST_CAPTURE_JOINED");
+    if (pipe_.init(main_, side_, b, q, r, !(joined && joined[0] == '1')) != hipSuccess) { fail("pipeline init"); return; }
+    // RCCL stages run eagerly until prepare_graphs() captured them (set_eager(false) below)
+    pipe_.set_eager(true);
     ok_ = true;
 }
+
+kn_status DistPipeline::poll(hipEvent_t ev, double timeout_s, const char* what) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    int polls = 0;
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return KN_OK;
+        if (q != hipErrorNotReady) { err_ = std::string(what) + ": " + hipGetErrorString(q); return KN_ERR_DEVICE; }
+        if ((++polls & 63) == 0) {
+            // a dead or hung peer: RCCL's async error, or the deadline
+            const std::string ae = comm_ ? comm_async_error(comm_) : std::string();
+            if (!ae.empty()) {
+                comm_abort(comm_);
+                err_ = ae;
+                return KN_ERR_DEVICE;
+            }
+            if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_s) {
+                if (comm_) comm_abort(comm_);
+                err_ = std::string(what) + " did not complete within the deadline (peer dead or hung?)";
+                return KN_ERR_DEVICE;
+            }
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(polls < 256 ? 2 : 50));
+    }
+}
+
+kn_status DistPipeline::warmup(double timeout_s) {
+    if (!ok_ || !comm_) return KN_ERR_STATE;
+    if (warm_) return KN_OK;
+    // one eager (uncaptured) step on set 1: RCCL connects to the step's peers and sets up the
+    // all-reduce before anything is captured (collective: every rank calls it at the same step)
+    hipError_t e = stage_build(1, main_);
+    if (e == hipSuccess) e = stage_query(1, main_);
+    if (e == hipSuccess) e = stage_flag(1, main_);
+    if (e == hipSuccess) e = hipEventRecord(ring_[0], main_);
+    if (e != hipSuccess) { err_ = std::string("eager warm-up step: ") + hipGetErrorString(e); return KN_ERR_DEVICE; }
+    const kn_status st = poll(ring_[0], timeout_s, "eager warm-up step");
+    if (st == KN_OK) warm_ = true;
+    return st;
+}
+
+kn_status DistPipeline::prepare_graphs(int unroll) {
+    if (!ok_ || !comm_) return KN_ERR_STATE;
+    if (!warm_) { err_ = "prepare_graphs() before warmup()"; return KN_ERR_STATE; }
+    pipe_.set_eager(false);
+    // test hook: an injected capture failure (the fallback path of tests/test_gpu_distributed.py)
+    const char* inj = std::getenv("KN_DIST_CAPTURE_FAIL");
+    hipError_t e = (inj && inj[0] == '1') ? hipErrorStreamCaptureUnsupported : pipe_.prepare(unroll);
+    if (e != hipSuccess) {
+        pipe_.set_eager(true);
+        err_ = std::string("graph capture of the distributed step: ") + hipGetErrorString(e);
+        return KN_ERR_DEVICE;
+    }
+    return KN_OK;
+}
+
+void DistPipeline::set_eager(bool eager) { pipe_.set_eager(eager); }
 
 DistPipeline::~DistPipeline() {
     pipe_.reset();
@@ -503,6 +559,7 @@ kn_status DistPipeline::launch(int iters, int unroll, bool keep_primed, hipStrea
     if (!ok_) return KN_ERR_STATE;
     if (!comm_) { err_ = "loopback pipelines run loopback_stage() only"; return KN_ERR_STATE; }
     if (comm_->aborted) { err_ = "communicator aborted"; return KN_ERR_DEVICE; }
+    if (!warm_) { err_ = "launch() before warmup()"; return KN_ERR_STATE; }
     if (iters <= 0) {
         if (last_step) *last_step = pipe_.steps() - 1;
         return KN_OK;
@@ -542,29 +599,8 @@ kn_status DistPipeline::wait(long long step, double timeout_s, int* flag) {
         if (done_.empty() || step > done_.back().first) { err_ = "wait() for a step not launched"; return KN_ERR_STATE; }
         ev = ring_[done_.front().second];  // older than the ring: its flag is final (sticky)
     }
-    using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
-    int polls = 0;
-    for (;;) {
-        const hipError_t q = hipEventQuery(ev);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) { err_ = std::string("step wait: ") + hipGetErrorString(q); return KN_ERR_DEVICE; }
-        if ((++polls & 63) == 0) {
-            // a dead or hung peer: RCCL's async error, or the deadline
-            const std::string ae = comm_async_error(comm_);
-            if (!ae.empty()) {
-                comm_abort(comm_);
-                err_ = ae;
-                return KN_ERR_DEVICE;
-            }
-            if (std::chrono::duration<double>(clk::now() - t0).count() > timeout_s) {
-                comm_abort(comm_);
-                err_ = "distributed step did not complete within the deadline (peer dead or hung?)";
-                return KN_ERR_DEVICE;
-            }
-        }
-        std::this_thread::sleep_for(std::chrono::microseconds(polls < 256 ? 2 : 50));
-    }
+    const kn_status st = poll(ev, timeout_s, "distributed step");
+    if (st != KN_OK) return st;
     if (flag) *flag = *reinterpret_cast<volatile int*>(host_flag_);
     return KN_OK;
 }

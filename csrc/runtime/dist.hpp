@@ -88,6 +88,19 @@ public:
     const std::string& error() const { return err_; }
     bool ok() const { return ok_; }
 
+    // Construction is LOCAL (plan checks, allocation, streams): nothing collective runs, so a rank
+    // whose construction fails can tell its peers before any of them enters a collective.
+    // warmup(): one eager step (collective; RCCL connects to the step's peers), waited for under
+    // the deadline while polling RCCL's async error. Required before launch().
+    kn_status warmup(double timeout_s);
+    // Capture every stage graph and both unrolled graphs now (nothing runs). On failure the
+    // pipeline stays eager and an error is returned; callers all-reduce the outcome and pick one
+    // mode for every rank. Until this succeeds the stages run eagerly (the default at world > 1:
+    // RCCL point-to-point calls inside graphs have never run on more than one rank here).
+    kn_status prepare_graphs(int unroll);
+    void set_eager(bool eager);
+    bool eager() const { return pipe_.eager(); }
+    int capture_fallbacks() const { return pipe_.fallbacks(); }
     // Enqueue `iters` pipelined steps (unroll >= 2, even: steps per graph launch); *last_step = the
     // index of the last one. The steps read the caller's points in place: `caller` (may be null)
     // is the stream that wrote them -- the first build waits for it, and it waits (on the device)
@@ -140,6 +153,8 @@ private:
     hipError_t stage_query(int s, hipStream_t st);
     hipError_t stage_flag(int s, hipStream_t st);  // epilogue: exact finish, flag, all-reduce
     QueryBuffers query_proto(int s) const;
+    // wait for `ev`, polling RCCL's async error; past the deadline the communicator is aborted
+    kn_status poll(hipEvent_t ev, double timeout_s, const char* what);
     hipError_t exchange(int s, hipStream_t st);
     bool fail(const std::string& m) { err_ = m; ok_ = false; return false; }
 
@@ -147,6 +162,7 @@ private:
     RankComm* comm_;
     std::string err_;
     bool ok_ = false;
+    bool warm_ = false;
     int rows_ = 0, n_owned_ = 0, C_ = 0;
     int rows_cross_ = 0, recv_rows_ = 0;
     std::vector<long long> soff_, roff_;  // send / recv row offsets per peer

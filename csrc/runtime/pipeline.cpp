@@ -1,6 +1,8 @@
 // pipeline.cpp -- see pipeline.hpp.
 #include "pipeline.hpp"
 
+#include <cstdlib>
+
 namespace kn {
 
 namespace {
@@ -37,6 +39,16 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
     }
     KN_TRY(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming));
     KN_TRY(hipEventRecord(last_done_, main_));
+    static const int qstreams = [] {
+        const char* v = std::getenv("KN_PIPE_QSTREAMS");
+        return v ? std::atoi(v) : 1;
+    }();
+    if (qstreams >= 2) {
+        int lo = 0, hi = 0;
+        KN_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        (void)hi;
+        KN_TRY(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, lo));
+    }
     return hipSuccess;
 }
 
@@ -54,6 +66,11 @@ void Pipeline::reset() {
         destroy(evF_[s]);
     }
     destroy(last_done_);
+    if (aux_) {
+        (void)hipStreamSynchronize(aux_);
+        (void)hipStreamDestroy(aux_);
+        aux_ = nullptr;
+    }
     for (auto& e : cap_ev_) destroy(e);
     cap_ev_.clear();
     main_ = side_ = nullptr;
@@ -78,6 +95,7 @@ hipError_t Pipeline::capture(const Stage& st, int set, hipGraphExec_t* out) {
 }
 
 hipError_t Pipeline::graphs() {
+    if (eager_) return hipSuccess;
     for (int s = 0; s < 2; ++s) {
         if (!gB_[s]) KN_TRY(capture(b_, s, &gB_[s]));
         if (!gQ_[s]) KN_TRY(capture(q_, s, &gQ_[s]));
@@ -93,35 +111,44 @@ hipError_t Pipeline::unrolled(int s0, int U) {
     if (gU_[s0] && gU_len_[s0] == U) return hipSuccess;
     destroy(gU_[s0]);
     gU_len_[s0] = 0;
-    const size_t need = 2 * (size_t)U + 2;
+    const size_t need = 2 * (size_t)U + 3;
     while (cap_ev_.size() < need) {
         hipEvent_t e = nullptr;
         KN_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         cap_ev_.push_back(e);
     }
-    hipEvent_t fork = cap_ev_[0], join = cap_ev_[1];
-    hipEvent_t* eq = cap_ev_.data() + 2;      // after Q(j)
-    hipEvent_t* eb = cap_ev_.data() + 2 + U;  // after B(j+1)
+    hipEvent_t fork = cap_ev_[0], join = cap_ev_[1], join2 = cap_ev_[2];
+    hipEvent_t* eq = cap_ev_.data() + 3;      // after Q(j)
+    hipEvent_t* eb = cap_ev_.data() + 3 + U;  // after B(j+1)
     hipGraph_t g = nullptr;
     // origin stream of the capture; the other one joins it through the fork event
     hipStream_t origin = capture_from_side_ ? side_ : main_, other = capture_from_side_ ? main_ : side_;
+    // query streams: Q(j) on qst[j & 1]. With the second query stream (KN_PIPE_QSTREAMS=2), the
+    // queries of consecutive steps (different grid sets, different outputs) depend only on their
+    // own builds, so step j+1's workgroups fill the CUs that step j's tail leaves idle instead of
+    // waiting for its last workgroup and the kernel boundary
+    hipStream_t qst[2] = {main_, aux_ ? aux_ : main_};
     KN_TRY(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
     hipError_t e = hipEventRecord(fork, origin);
     if (e == hipSuccess) e = hipStreamWaitEvent(other, fork, 0);
+    if (e == hipSuccess && aux_) e = hipStreamWaitEvent(aux_, fork, 0);
     for (int j = 0; j < U && e == hipSuccess; ++j) {
         const int s = (s0 + j) & 1;
-        e = q_(s, main_);
-        if (e == hipSuccess) e = hipEventRecord(eq[j], main_);
+        hipStream_t qs = qst[j & 1];
+        if (j >= 1) e = hipStreamWaitEvent(qs, eb[j - 1], 0);  // B(j) (built during Q(j-1))
+        if (e == hipSuccess) e = q_(s, qs);
+        if (e == hipSuccess) e = hipEventRecord(eq[j], qs);
         if (e == hipSuccess && j >= 1) {
             e = hipStreamWaitEvent(side_, eq[j - 1], 0);
             if (e == hipSuccess && r_) e = r_(s ^ 1, side_);
         }
         if (e == hipSuccess) e = b_(s ^ 1, side_);
         if (e == hipSuccess) e = hipEventRecord(eb[j], side_);
-        if (e == hipSuccess && j + 1 < U) e = hipStreamWaitEvent(main_, eb[j], 0);
     }
     if (e == hipSuccess) e = hipEventRecord(join, other);
     if (e == hipSuccess) e = hipStreamWaitEvent(origin, join, 0);
+    if (e == hipSuccess && aux_) e = hipEventRecord(join2, aux_);
+    if (e == hipSuccess && aux_) e = hipStreamWaitEvent(origin, join2, 0);
     const hipError_t ee = hipStreamEndCapture(origin, &g);
     if (e != hipSuccess) {
         if (g) (void)hipGraphDestroy(g);
@@ -134,23 +161,61 @@ hipError_t Pipeline::unrolled(int s0, int U) {
     return e;
 }
 
+// Eager mode runs the stage bodies directly on the streams (same stages, same event order as
+// the graphs): nothing is captured, so a stage whose calls cannot be captured (RCCL at world > 1
+// by default, dist.cpp) or whose capture failed still runs.
 hipError_t Pipeline::enqueue_build(int s) {
     // without an epilogue the set is free once its query is done
     KN_TRY(hipStreamWaitEvent(side_, r_ ? evF_[s] : evQ_[s], 0));
-    KN_TRY(hipGraphLaunch(gB_[s], side_));
+    KN_TRY(eager_ ? b_(s, side_) : hipGraphLaunch(gB_[s], side_));
     return hipEventRecord(evB_[s], side_);
 }
 
 hipError_t Pipeline::enqueue_query(int s) {
     KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
-    KN_TRY(hipGraphLaunch(gQ_[s], main_));
+    KN_TRY(eager_ ? q_(s, main_) : hipGraphLaunch(gQ_[s], main_));
     return hipEventRecord(evQ_[s], main_);
 }
 
 hipError_t Pipeline::enqueue_epilogue(int s) {
     KN_TRY(hipStreamWaitEvent(side_, evQ_[s], 0));
-    KN_TRY(hipGraphLaunch(gR_[s], side_));
+    KN_TRY(eager_ ? r_(s, side_) : hipGraphLaunch(gR_[s], side_));
     return hipEventRecord(evF_[s], side_);
+}
+
+hipError_t Pipeline::prepare(int unroll) {
+    if (!main_) return hipErrorNotInitialized;
+    if (eager_) return hipSuccess;
+    KN_TRY(graphs());
+    if (unroll >= 2 && !(unroll & 1)) {
+        KN_TRY(unrolled(0, unroll));
+        KN_TRY(unrolled(1, unroll));
+    }
+    return hipSuccess;
+}
+
+void Pipeline::set_eager(bool eager) {
+    if (eager == eager_) return;
+    if (main_) (void)hipStreamSynchronize(main_);
+    if (side_) (void)hipStreamSynchronize(side_);
+    // a failed capture may have left a stream in capture mode: end it (the graph is dropped)
+    for (hipStream_t st : {main_, side_}) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+            hipGraph_t g = nullptr;
+            (void)hipStreamEndCapture(st, &g);
+            if (g) (void)hipGraphDestroy(g);
+        }
+    }
+    (void)hipGetLastError();
+    for (int s = 0; s < 2; ++s) {
+        destroy(gB_[s]);
+        destroy(gQ_[s]);
+        destroy(gR_[s]);
+        destroy(gU_[s]);
+        gU_len_[s] = 0;
+    }
+    eager_ = eager;
 }
 
 hipError_t Pipeline::flush() {
@@ -163,15 +228,25 @@ hipError_t Pipeline::flush() {
     return hipSuccess;
 }
 
+hipError_t Pipeline::fallback_if(hipError_t e) {
+    if (e == hipSuccess) return e;
+    // a capture or instantiation failed (nothing ran): the same stages eagerly from now on
+    set_eager(true);
+    ++fallbacks_;
+    return hipSuccess;
+}
+
 hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
     if (!main_) return hipErrorNotInitialized;
-    KN_TRY(graphs());
-    if (unroll < 2 || (unroll & 1)) unroll = 0;
+    KN_TRY(fallback_if(graphs()));
+    if (unroll < 2 || (unroll & 1) || eager_) unroll = 0;
     if (unroll) {
         // both start parities up front (also by a call of fewer steps, e.g. a warm-up): a capture
         // never lands inside a later (timed) call
-        KN_TRY(unrolled(0, unroll));
-        KN_TRY(unrolled(1, unroll));
+        hipError_t e = unrolled(0, unroll);
+        if (e == hipSuccess) e = unrolled(1, unroll);
+        KN_TRY(fallback_if(e));
+        if (eager_) unroll = 0;
     }
     int done = 0;
     while (done < iters) {
@@ -179,7 +254,6 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
         // an unrolled graph ends with the next step's build: only when the call keeps it primed,
         // or more steps follow in this call
         if (unroll && iters - done >= unroll + (keep_primed ? 0 : 1)) {
-            KN_TRY(unrolled(s, unroll));
             if (!primed_) KN_TRY(enqueue_build(s));
             if (r_pending_) {
                 r_pending_ = false;
@@ -190,10 +264,15 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
             KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
             if (r_) KN_TRY(hipStreamWaitEvent(main_, evF_[s ^ 1], 0));
             KN_TRY(hipGraphLaunch(gU_[s], main_));
-            // U is even: the last query used set s^1, the primed build (B(next)) wrote set s
+            // U is even: the last query used set s^1, the primed build (B(next)) wrote set s.
+            // Every per-set event is re-recorded after the graph: its queries read both sets and
+            // its last epilogue inside it (R(U-2)) released set s, so a later step_with() or build
+            // of either set waits for the whole graph (not for a stale pre-graph event)
             last_set_ = s ^ 1;
             KN_TRY(hipEventRecord(evQ_[s ^ 1], main_));
+            KN_TRY(hipEventRecord(evQ_[s], main_));
             KN_TRY(hipEventRecord(evB_[s], main_));
+            if (r_) KN_TRY(hipEventRecord(evF_[s], main_));
             primed_ = true;
             r_pending_ = (bool)r_;
             next_ += unroll;
@@ -222,7 +301,7 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
 
 hipError_t Pipeline::step_with(const Stage& pre, const Stage* next_pre) {
     if (!main_) return hipErrorNotInitialized;
-    KN_TRY(graphs());
+    KN_TRY(fallback_if(graphs()));
     const int s = (int)(next_ & 1);
     if (!primed_) {
         // this step's input into set s, then its build

@@ -46,6 +46,17 @@ public:
     // through one unrolled graph, the rest through per-step graphs. keep_primed = false: the call
     // ends without the next step's build (its input may change before the next call).
     hipError_t launch(int iters, int unroll = 0, bool keep_primed = true);
+    // Capture every stage graph (and both unrolled graphs when unroll >= 2, even) now, without
+    // running anything: a capture error surfaces here, before any step is enqueued, so a caller
+    // can decide (collectively, over several ranks) to run eagerly instead. No-op in eager mode.
+    hipError_t prepare(int unroll);
+    // Eager mode: the stage bodies are enqueued directly on the two streams at every step (same
+    // stages, same event order, nothing captured). Switching waits for both streams and drops the
+    // captured graphs (ending a capture a failed stage left open).
+    void set_eager(bool eager);
+    bool eager() const { return eager_; }
+    // captures that failed inside launch() / step_with() and switched the pipeline to eager mode
+    int fallbacks() const { return fallbacks_; }
     // Event recorded after the most recent build of set s (its input has been read).
     hipEvent_t build_event(int s) const { return evB_[s]; }
     // One step whose input is provided by `pre` (run on the side stream before B, e.g. a copy of
@@ -68,6 +79,7 @@ public:
 
 private:
     hipError_t graphs();          // per-set stage graphs
+    hipError_t fallback_if(hipError_t capture_error);
     hipError_t unrolled(int start_set, int U);
     hipError_t capture(const Stage& st, int set, hipGraphExec_t* out);
     hipError_t enqueue_build(int set);   // side: wait set free, B(set), record evB
@@ -75,7 +87,10 @@ private:
     hipError_t enqueue_epilogue(int set);
 
     hipStream_t main_ = nullptr, side_ = nullptr;
+    hipStream_t aux_ = nullptr;  // second query stream of the unrolled graphs (KN_PIPE_QSTREAMS=2)
     bool capture_from_side_ = false;
+    bool eager_ = false;
+    int fallbacks_ = 0;
     Stage b_, q_, r_;
     hipGraphExec_t gB_[2] = {nullptr, nullptr}, gQ_[2] = {nullptr, nullptr}, gR_[2] = {nullptr, nullptr};
     hipGraphExec_t gU_[2] = {nullptr, nullptr};

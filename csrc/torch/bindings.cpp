@@ -7,7 +7,12 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/extension.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -1287,6 +1292,41 @@ torch::Tensor normalize_1000(torch::Tensor points) {
 }  // namespace
 
 
+// ---- crash diagnostics -----------------------------------------------------------------
+// A native backtrace on SIGSEGV / SIGBUS / SIGFPE / SIGILL (faulthandler prints only the Python
+// frames): the frames go to stderr with backtrace_symbols_fd (async-signal-safe), then the previous
+// disposition is restored and the signal re-raised, so the process still dies as it would have.
+namespace crash {
+struct sigaction g_prev[32];
+void handler(int sig, siginfo_t* info, void*) {
+    const char hdr[] = "\n[cuda_knearests_amd] fatal signal; native backtrace:\n";
+    (void)!write(2, hdr, sizeof(hdr) - 1);
+    char buf[64];
+    const int n = std::snprintf(buf, sizeof(buf), "signal %d, fault address %p\n", sig, info ? info->si_addr : nullptr);
+    if (n > 0) (void)!write(2, buf, (size_t)n);
+    void* frames[64];
+    const int nf = backtrace(frames, 64);
+    backtrace_symbols_fd(frames, nf, 2);
+    sigaction(sig, &g_prev[sig], nullptr);
+    raise(sig);
+}
+bool install() {
+    static bool done = false;
+    if (done) return true;
+    void* warm[2];
+    (void)backtrace(warm, 2);  // loads libgcc's unwinder now, not inside the handler
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = handler;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL})
+        if (sigaction(sig, &sa, &g_prev[sig]) != 0) return false;
+    done = true;
+    return true;
+}
+}  // namespace crash
+
 // ---- one rank's pipelined distributed step over RCCL (csrc/runtime/dist.hpp) -------------
 py::bytes rccl_unique_id() {
     unsigned char id[kn::kCommIdBytes];
@@ -1381,9 +1421,28 @@ public:
         const c10::DeviceGuard guard(points.device());
         // the plan tensors (route plan, metas) are copied by the constructor: their producers first
         KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
-        d_ = std::make_unique<kn::DistPipeline>(p, comm_ ? comm_->c_ : nullptr);
+        d_ = std::make_shared<kn::DistPipeline>(p, comm_ ? comm_->c_ : nullptr);
         TORCH_CHECK(d_->ok(), d_->error());
     }
+    // one eager step, collective (every rank calls it after all constructed their pipelines);
+    // waits under the deadline with the GIL released
+    void warmup(double timeout_s) {
+        kn_status st;
+        {
+            py::gil_scoped_release nogil;
+            st = d_->warmup(timeout_s);
+        }
+        TORCH_CHECK(st == KN_OK, d_->error());
+    }
+    // capture the step's graphs now (nothing runs); False: capture failed, the pipeline is eager
+    bool prepare_graphs(int64_t unroll) {
+        const c10::DeviceGuard guard(points_.device());
+        return d_->prepare_graphs((int)unroll) == KN_OK;
+    }
+    void set_eager(bool eager) { d_->set_eager(eager); }
+    std::string mode() { return d_->eager() ? "eager" : "graph"; }
+    int64_t capture_fallbacks() { return d_->capture_fallbacks(); }
+    std::string error() { return d_->error(); }
     // loopback mode: one synchronous stage (0 route, 1 unpack + build + query + local flag)
     void loopback_stage(int64_t stage) { TORCH_CHECK(d_->loopback_stage((int)stage) == KN_OK, d_->error()); }
     // views (float32, (rows, 4)) of set 0's send rows for destination d / receive rows from source s
@@ -1416,7 +1475,13 @@ public:
         long long last = -1;
         const c10::DeviceGuard guard(points_.device());
         const hipStream_t caller = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-        TORCH_CHECK(d_->launch((int)iters, (int)unroll, keep_primed, caller, &last) == KN_OK, d_->error());
+        kn_status st;
+        {
+            // eager mode enqueues RCCL calls: never hold the GIL across them
+            py::gil_scoped_release nogil;
+            st = d_->launch((int)iters, (int)unroll, keep_primed, caller, &last);
+        }
+        TORCH_CHECK(st == KN_OK, d_->error());
         return last;
     }
     // wait for step `step` (polls RCCL errors; deadline) -> sticky flag (0 = all steps valid)
@@ -1433,14 +1498,18 @@ public:
     void sync() { TORCH_CHECK(d_->sync() == KN_OK, d_->error()); }
     int64_t last_set() { return d_->last_set(); }
     // (owned global ids, idx, d2) of grid set s: views of the pipeline's buffers, overwritten by
-    // the step after next (the Python owner keeps this object alive while they are in use)
+    // the step after next. Each view holds a reference to the pipeline (its deleter), so the
+    // buffers outlive every tensor that views them, whatever the Python side drops
     std::vector<torch::Tensor> outputs(int64_t s) {
         TORCH_CHECK(s == 0 || s == 1, "set is 0 or 1");
         auto opt = torch::TensorOptions().device(points_.device());
         const int64_t no = d_->n_owned(), k = d_->k();
-        auto g = torch::from_blob(const_cast<int*>(d_->gids((int)s)), {no}, opt.dtype(torch::kInt32));
-        auto i = torch::from_blob(const_cast<int*>(d_->idx((int)s)), {no, k}, opt.dtype(torch::kInt32));
-        auto d = torch::from_blob(const_cast<float*>(d_->d2((int)s)), {no, k}, opt.dtype(torch::kFloat32));
+        std::shared_ptr<kn::DistPipeline> keep = d_;
+        std::shared_ptr<PyRankComm> keepc = comm_;
+        auto owner = [keep, keepc](void*) {};
+        auto g = torch::from_blob(const_cast<int*>(d_->gids((int)s)), {no}, owner, opt.dtype(torch::kInt32));
+        auto i = torch::from_blob(const_cast<int*>(d_->idx((int)s)), {no, k}, owner, opt.dtype(torch::kInt32));
+        auto d = torch::from_blob(const_cast<float*>(d_->d2((int)s)), {no, k}, owner, opt.dtype(torch::kFloat32));
         return {g, i, d};
     }
     std::vector<int64_t> counters(int64_t s) {
@@ -1468,7 +1537,7 @@ private:
     std::shared_ptr<PyRankComm> comm_;
     torch::Tensor points_, ids_, plan_, metas_, field_, field_cert_;
     int64_t comm_world_ = 1;
-    std::unique_ptr<kn::DistPipeline> d_;
+    std::shared_ptr<kn::DistPipeline> d_;
 };
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -1557,6 +1626,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("h"), py::arg("block_offsets"), py::arg("totals"), py::arg("rows"), py::arg("splits") = py::none(),
           py::arg("h_inner") = -1.0, py::arg("wz") = INFINITY);
     m.def("route_unpack", &route_unpack, "multi-GPU routing: received rows -> owned-first points + global ids");
+    m.def("install_crash_handler", &crash::install,
+          "print a native backtrace on SIGSEGV/SIGBUS/SIGFPE/SIGILL, then die as before");
     m.def("rccl_unique_id", &rccl_unique_id, "multi-GPU: a new RCCL unique id (128 bytes) for RankComm");
     py::class_<PyRankComm, std::shared_ptr<PyRankComm>>(m, "RankComm", "one rank's RCCL communicator (collective init)",
                                                           py::module_local())
@@ -1584,6 +1655,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("recv_view", &PyDistPipe::recv_view)
         .def("flag_local", &PyDistPipe::flag_local)
         .def("debug_words", &PyDistPipe::debug_words, py::arg("set") = 0)
+        .def("warmup", &PyDistPipe::warmup, py::arg("timeout_s") = 300.0)
+        .def("prepare_graphs", &PyDistPipe::prepare_graphs, py::arg("unroll"))
+        .def("set_eager", &PyDistPipe::set_eager)
+        .def("mode", &PyDistPipe::mode)
+        .def("capture_fallbacks", &PyDistPipe::capture_fallbacks)
+        .def("error", &PyDistPipe::error)
         .def("launch", &PyDistPipe::launch, py::arg("iters") = 1, py::arg("unroll") = 0, py::arg("keep_primed") = false)
         .def("wait", &PyDistPipe::wait, py::arg("step"), py::arg("timeout_s") = 300.0)
         .def("sync", &PyDistPipe::sync)

@@ -192,6 +192,8 @@ class DistributedKNearests:
         # boost is collective (n_fwd is all-reduced), kept across steps.
         self.halo_boost = 1.0
         self.halo_boost_max = 4.0
+        self.boost_decay_after = 2  # clean validated full steps in a row before the boost decays
+        self._boost_clean = 0
         # hipGraph replay of the steady step (torch.cuda.CUDAGraph): the default at world 1 (round
         # 3; no collective inside the captured step), opt-in above (KN_DIST_GRAPH=1 or
         # graph_steady = True: capturing RCCL collectives cannot be exercised on a one-GPU box);
@@ -242,6 +244,7 @@ class DistributedKNearests:
         self.wait_timeout_s = float(timeout_s) if timeout_s else 300.0
         self._rcomm = None
         self._pipe = None
+        self.pipe_mode = None  # "graph" / "eager": how the native pipeline runs (set when built)
         # asynchronous steady results not yet checked by the solver. Before the next steady step
         # all but the newest are checked (their steps are long done, so this rarely waits, and it
         # bounds the host's lead to ~2 steps): an invalid one drops the steady plan. The flags
@@ -495,8 +498,20 @@ class DistributedKNearests:
         widen = n_fwd > 0 and self.halo_boost * 1.6 <= self.halo_boost_max + 1e-9
         if widen:
             self.halo_boost *= 1.6
+            self._boost_clean = 0
             _log.info("rank %d: %d queries forwarded; halo factor for the next steps %.3g", rank, n_fwd,
                       self.halo_factor * self.halo_boost)
+        elif n_fwd == 0 and growth == 0 and self.halo_boost > 1.0:
+            # the boost decays once the cloud no longer needs it: after boost_decay_after validated
+            # full steps in a row that forwarded nothing (n_fwd is all-reduced and growth follows the
+            # all-reduced flag, so every rank decays together), one x1.6 step back toward 1
+            self._boost_clean += 1
+            if self._boost_clean >= self.boost_decay_after:
+                self.halo_boost = max(1.0, self.halo_boost / 1.6)
+                self._boost_clean = 0
+                _log.info("rank %d: halo boost decays to %.3g", rank, self.halo_boost)
+        else:
+            self._boost_clean = 0
         if growth == 0 and not full and self.steady and not widen and not field_next and \
                 2 * n_fwd <= self.fwd_slots_max:
             # validated single-round step: the steady-state assumption for the next ones
@@ -760,9 +775,34 @@ class DistributedKNearests:
             self._rcomm = C.RankComm(uid0, self.world, self.rank, dev.index if dev.index is not None else 0)
         return self._rcomm
 
+    def _agree(self, ok: bool, dev: torch.device) -> bool:
+        """True when ``ok`` holds on EVERY rank (a MAX all-reduce of the failure bit): decisions
+        that change which collectives a rank issues are taken by all ranks together."""
+        bad = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+        self.comm.all_reduce_max(bad)
+        return int(bad.item()) == 0
+
+    def _capture_mode(self) -> bool:
+        """Graph capture of the native pipeline's stages (RCCL calls included): KN_DIST_CAPTURE=1
+        always, =0 never; default at world 1 only. At world > 1 the stages run eagerly on the two
+        streams (same order and overlap, one enqueue per kernel): captured multi-peer RCCL
+        point-to-point has never run on more than one rank here, and an eager RCCL step is the
+        library's ordinary use."""
+        import os
+
+        env = os.environ.get("KN_DIST_CAPTURE")
+        if env in ("0", "1"):
+            return env == "1"
+        return self.world == 1
+
     def _pipe_for(self, points: torch.Tensor, ids: Optional[torch.Tensor]):
         """The native pipeline of the current steady plan over these input tensors (read in
-        place; other storage builds a new one)."""
+        place; other storage builds a new one). Collective when it builds: construction is local,
+        then every rank learns whether all ranks constructed theirs before any enters the eager
+        warm-up step (so one rank's local failure -- an allocation, a plan check -- sends all ranks
+        to the torch path together instead of leaving its peers blocked in a collective), and the
+        graph capture's outcome is agreed on the same way (any failure: every rank runs eagerly).
+        Returns None when the native pipeline is unavailable on some rank."""
         st = self._steady
         ids32 = ids.to(torch.int32).contiguous() if ids is not None else None
         p = self._pipe
@@ -774,12 +814,35 @@ class DistributedKNearests:
         self._pipe = None  # release the old pipeline's buffers first
         C = ops.load()
         world1_force = self.world == 1 and self.force_collectives
-        pipe = C.DistPipe(self._rank_comm(points.device), points, ids32, st["plan"], st["metas"],
-                          [int(v) for v in st["tot"].tolist()], [float(v) for v in st["hdr"]], list(st["grid"]),
-                          list(st["dims"]), list(st["recv_own"]), list(st["recv_halo"]), list(st["cross_send"]),
-                          list(st["cross_recv"]), list(st["place"]), int(st["cap"]), self.k, self.points_per_cell,
-                          bool(self.deterministic), int(st["exact_grid"]), int(st["use_tree"]), world1_force, None,
-                          st.get("field"), st.get("field_cert"))
+        pipe, err = None, ""
+        try:
+            rc = self._rank_comm(points.device)
+            pipe = C.DistPipe(rc, points, ids32, st["plan"], st["metas"],
+                              [int(v) for v in st["tot"].tolist()], [float(v) for v in st["hdr"]], list(st["grid"]),
+                              list(st["dims"]), list(st["recv_own"]), list(st["recv_halo"]), list(st["cross_send"]),
+                              list(st["cross_recv"]), list(st["place"]), int(st["cap"]), self.k, self.points_per_cell,
+                              bool(self.deterministic), int(st["exact_grid"]), int(st["use_tree"]), world1_force, None,
+                              st.get("field"), st.get("field_cert"))
+        except RuntimeError as e:
+            err = str(e)
+        if not self._agree(pipe is not None, points.device):
+            _log.warning("rank %d: native pipeline unavailable on some rank (%s); torch steady path", self.rank,
+                         err or "a peer failed")
+            return None
+        try:
+            pipe.warmup(self.wait_timeout_s)  # collective eager step under the deadline
+        except RuntimeError as e:
+            raise CollectiveError(f"rank {self.rank}: native pipeline warm-up step failed: {e}") from e
+        mode = "eager"
+        if self._capture_mode():
+            ok = pipe.prepare_graphs(self.pipe_unroll)
+            if not ok:
+                _log.warning("rank %d: graph capture of the native pipeline failed (%s)", self.rank, pipe.error())
+            if self._agree(ok, points.device):
+                mode = "graph"
+            else:
+                pipe.set_eager(True)
+        self.pipe_mode = mode
         p = self._pipe = {"pipe": pipe, "st": st, "pts": points, "ids": ids32, "n": points.size(0),
                           "outs": [pipe.outputs(0), pipe.outputs(1)], "primed": False}
         return p
@@ -790,12 +853,10 @@ class DistributedKNearests:
         iters > 1). resident: keep the next step's build enqueued after the call (the caller
         promises the points do not change before the next call)."""
         st = self._steady
-        try:
-            p = self._pipe_for(points, ids)
-        except RuntimeError as e:
-            # the native pipeline could not be built (communicator or plan check): the torch
-            # steady path instead, for good (every rank builds the same plan, so all take this)
-            _log.warning("rank %d: native pipeline unavailable (%s); torch steady path", self.rank, e)
+        p = self._pipe_for(points, ids)
+        if p is None:
+            # the native pipeline could not be built on every rank: the torch steady path, for good
+            # (decided collectively in _pipe_for, so every rank takes it)
             self.native_pipeline = False
             self._pipe = None
             res = None
@@ -803,12 +864,19 @@ class DistributedKNearests:
                 res = self._solve_steady(points, ids)
             return res
         pipe = p["pipe"]
-        last = pipe.launch(iters, self.pipe_unroll if iters > 1 else 0, bool(resident))
+        try:
+            last = pipe.launch(iters, self.pipe_unroll if iters > 1 else 0, bool(resident))
+        except RuntimeError as e:
+            # an enqueue failed after the peers may have issued this step's collectives: the group
+            # cannot continue (wait() would time out); fail loudly on this rank
+            raise CollectiveError(f"rank {self.rank}: pipelined launch failed: {e}") from e
         gids, idx, d2 = p["outs"][pipe.last_set()]
         stats = dict(st["stats"])
         stats["steady"] = True
-        stats["graph"] = True
+        stats["graph"] = pipe.mode() == "graph"
         stats["pipelined"] = True
+        stats["pipe_mode"] = pipe.mode()
+        stats["capture_fallbacks"] = int(pipe.capture_fallbacks())
         timeout = self.wait_timeout_s
         rank = self.rank
 
@@ -854,7 +922,11 @@ class DistributedKNearests:
         self._check_pending(keep=0)
         if self._steady is None:
             return {}
-        return dict(self._pipe_for(points, ids)["pipe"].profile())
+        p = self._pipe_for(points, ids)
+        if p is None:
+            self.native_pipeline = False
+            return {}
+        return dict(p["pipe"].profile())
 
     def _solve_steady(self, points: torch.Tensor, ids: Optional[torch.Tensor]) -> DistResult:
         """One step with no host synchronisation (see ``self.steady``): the native pipeline

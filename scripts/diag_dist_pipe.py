@@ -4,7 +4,10 @@ self send / recv + unpack): per-call asynchronous steps, batched run_steps (unro
 resident priming), in-place refills of the input between calls (caller-stream ordering), a moved
 share (flag fails, the synchronous call recovers), per-phase profile. Rows are compared bit for
 bit with the torch-path reference (DistributedKNearests(native_pipeline=False)).
-usage: python scripts/diag_dist_pipe.py [steps] [n]"""
+Every combination runs in three pipeline modes: captured hipGraphs (KN_DIST_CAPTURE=1), eager
+stages (=0, the default at world > 1) and an injected capture failure (KN_DIST_CAPTURE_FAIL=1),
+which must fall back to the eager mode and stay exact.
+usage: python scripts/diag_dist_pipe.py [steps] [n] [force modes, e.g. 0,1] [capture modes, e.g. 1,0,fail]"""
 import os
 import sys
 
@@ -17,6 +20,7 @@ from cuda_knearests_amd.utils import uniform_cloud
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 900000
 modes = [m == "1" for m in sys.argv[3].split(",")] if len(sys.argv) > 3 else [False, True]
+caps = sys.argv[4].split(",") if len(sys.argv) > 4 else ["1", "0", "fail"]
 verbose = os.environ.get("KN_DIAG_VERBOSE") == "1"
 
 
@@ -50,7 +54,10 @@ pts_perm = pts[perm].contiguous()
 ref = reference(pts)
 ref_perm = reference(pts_perm)
 ok_all = True
-for force in modes:
+for cap, force in [(c, f) for c in caps for f in modes]:
+    os.environ["KN_DIST_CAPTURE"] = "0" if cap == "0" else "1"
+    os.environ["KN_DIST_CAPTURE_FAIL"] = "1" if cap == "fail" else "0"
+    want_mode = "graph" if cap == "1" else "eager"
     dk = DistributedKNearests(k=16, force_collectives=force)
     full = dk.solve(pts)
     r_full = same(full, ref)
@@ -104,9 +111,12 @@ for force in modes:
     bad = dk.solve(moved, async_=True)
     inval = not bad.valid()
     rec = same(dk.solve(moved), reference(moved))
-    print(f"force {force} full {r_full} pipelined {piped} valid {valid} rows {rows} batch {b_ok} {b2_ok} "
-          f"refill {refill} moved share invalid {inval} recovered {rec} profile {prof}", flush=True)
-    ok_all = ok_all and r_full and piped and valid and rows and b_ok and b2_ok and refill and inval and rec and prof_ok
+    mode_ok = dk2.pipe_mode == want_mode and batch.stats.get("pipe_mode") == want_mode
+    print(f"capture {cap} force {force} mode {batch.stats.get('pipe_mode')} full {r_full} pipelined {piped} "
+          f"valid {valid} rows {rows} batch {b_ok} {b2_ok} refill {refill} moved share invalid {inval} "
+          f"recovered {rec} profile {prof}", flush=True)
+    ok_all = (ok_all and r_full and piped and valid and rows and b_ok and b2_ok and refill and inval and rec and prof_ok
+              and mode_ok)
 print("ALL OK" if ok_all else "FAILED", flush=True)
 dist.destroy_process_group()
 sys.exit(0 if ok_all else 1)

@@ -221,6 +221,34 @@ def test_engine_stream_of_clouds(cuda, unroll):
     _check(clouds[-1], idx, d2, k)
 
 
+@pytest.mark.parametrize("k", [16, 50])
+def test_engine_stream_after_unrolled(cuda, k):
+    """A stream step issued right after an UNROLLED resident launch, with no sync in between
+    (the unrolled graph's last queries and its primed build use both grid sets, so the
+    stream step's copy into a set must wait for the whole graph, not for a pre-graph event).
+    K=16 has no epilogue (nothing on the side stream follows the graph), K=50 has one. Every
+    stream step's rows equal the oracle's on its own cloud."""
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    unroll = 4
+    n = 40000
+    base = uniform_cloud(n, seed=41).to(cuda)
+    clouds = [uniform_cloud(n, seed=950 + j).to(cuda) for j in range(3)]
+    e = C.Engine(k)
+    e.prepare(base)
+    for rep in range(2):
+        e.launch_pipelined(2 * unroll, unroll)  # unrolled graphs, primed at the end
+        for j, c in enumerate(clouds):
+            e.stream_step(c, clouds[j + 1] if j + 1 < len(clouds) else None)
+            if j == 0:
+                continue  # first result checked after the next step was enqueued as well
+            e.sync()
+            idx, d2 = e.results(cuda)
+            _check(c, idx, d2, k)
+        e.prepare(base)
+
+
 @pytest.mark.parametrize("unroll", [2, 4, 8])
 def test_engine_unrolled_pipeline(cuda, unroll):
     """Unrolled pipelined graphs (U steps per graph launch, pipeline.hpp) give the serial step's
