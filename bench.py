@@ -213,10 +213,6 @@ def run_dist(args) -> dict:
     from cuda_knearests_amd.parallel import DistributedKNearests
     from cuda_knearests_amd.utils import uniform_cloud
 
-    from cuda_knearests_amd._ext import load as _load_ext
-
-    # a native backtrace if anything in the native stack (RCCL included) faults
-    _load_ext().install_crash_handler()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("KN_SAME_DEVICE"):  # rehearsal: every rank on cuda:0 (1-GPU box)
         local = 0
@@ -498,6 +494,11 @@ def main() -> int:
     ap.add_argument("--sync-steps", action="store_true",
                     help="N GPUs: validate every step before the next (no asynchronous steady-state steps)")
     args = ap.parse_args()
+    if not args.cpu_oracle:
+        # a native backtrace if anything in the native stack (HIP runtime, RCCL) faults
+        from cuda_knearests_amd._ext import load as _load_ext
+
+        _load_ext().install_crash_handler()
     if os.environ.get("KN_BENCH_WATCHDOG"):
         import faulthandler
 

@@ -149,12 +149,44 @@ __device__ __forceinline__ unsigned cand_key_v(const float4& p, float qx, float 
 // Sorted-array insertion of `key` into keys[0..KM) (ascending), dropping the largest:
 // new[j] = med3(old[j-1], key, old[j]) -- one v_med3_u32 per slot, all independent. Skipped
 // (uniform branch) when no lane of the wave improves; a non-improving key is a no-op anyway.
-template <int KM>
+//
+// Split networks (KN_TOPK_SPLIT): slots below the lowest insertion position of the wave's
+// inserting lanes do not change, so when every inserting lane's key is >= keys[LO-1] (a uniform
+// ballot) the network starts at LO. A new candidate inside the K-th ball is uniformly placed in
+// it, i.e. at a uniform rank: late in a walk, when few lanes insert at once, the wave's lowest
+// position is often in the upper half. Numpy lockstep replay of the lane walk
+// (scripts/sim_wave_order.py machinery, /tmp replays recorded in DESIGN.md): med3 slots per wave
+// K=16 -8 % (half) / -6 % (quarters), K=50 -13 % / -17 %. 0 = one network, 1 = halves,
+// 2 = quarters.
+#ifndef KN_TOPK_SPLIT
+#define KN_TOPK_SPLIT 0
+#endif
+template <int KM, int LO>
+__device__ __forceinline__ void topk_net(unsigned (&keys)[KM], unsigned key) {
+#pragma unroll
+    for (int j = KM - 1; j > LO; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
+    if constexpr (LO == 0) keys[0] = min(keys[0], key);
+    else keys[LO] = med3_u32(keys[LO - 1], key, keys[LO]);
+}
+template <int KM, int SPLIT = KN_TOPK_SPLIT>
 __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key) {
     if (__builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
-#pragma unroll
-        for (int j = KM - 1; j > 0; --j) keys[j] = med3_u32(keys[j - 1], key, keys[j]);
-        keys[0] = min(keys[0], key);
+        if constexpr (SPLIT == 0 || KM < 8) {
+            topk_net<KM, 0>(keys, key);
+        } else if constexpr (SPLIT == 1) {
+            constexpr int H = KM / 2;
+            if (__builtin_amdgcn_ballot_w64(key < keys[H - 1])) topk_net<KM, 0>(keys, key);
+            else topk_net<KM, H>(keys, key);
+        } else {
+            constexpr int Q = KM / 4, H = KM / 2, T = (3 * KM) / 4;
+            if (__builtin_amdgcn_ballot_w64(key < keys[H - 1])) {
+                if (__builtin_amdgcn_ballot_w64(key < keys[Q - 1])) topk_net<KM, 0>(keys, key);
+                else topk_net<KM, Q>(keys, key);
+            } else {
+                if (__builtin_amdgcn_ballot_w64(key < keys[T - 1])) topk_net<KM, H>(keys, key);
+                else topk_net<KM, T>(keys, key);
+            }
+        }
         return 1u;
     }
     return 0u;

@@ -56,7 +56,7 @@ struct TreeView {
     unsigned* info;       // [0] = L after launch_tree_leaves (device; the query kernels read it)
     float4* tmp_pts;      // n: points in cell order (before the sub-cell order)
     unsigned* tmp_vals;   // n
-    unsigned* cell_code;  // n: Morton code of each point's cell
+    unsigned long long* cell_code;  // n: Morton code of each point's cell (brick code << 9 | in-brick code)
     uint2* cell_span;     // n: tree range [first, end) of each point's cell
     unsigned* bcount;     // padded brick space + 1: brick counts, scanned in place to bases
     unsigned* scan_sums;  // block sums of the device scans
@@ -70,6 +70,12 @@ struct TreeView {
 
 // dims: the grid's dims (host copy of GridGeom::dims)
 size_t tree_workspace_bytes(int n, const int dims[3]);
+// The Morton brick codes hold 10 bits of brick coordinate per axis (8 cells a brick): grids of at
+// most 8,192 cells per axis. Larger grids stay on the grid path (callers check this).
+constexpr int kTreeMaxAxisCells = 8192;
+inline bool tree_supports(const int dims[3]) {
+    return dims[0] <= kTreeMaxAxisCells && dims[1] <= kTreeMaxAxisCells && dims[2] <= kTreeMaxAxisCells;
+}
 TreeView tree_view(void* ws, int n, const int dims[3]);
 // Phase 1 (stream-ordered, no host sync): the grid's sorted points in the Morton order of their
 // cells, leaf boundaries; the leaf count lands in t.info[0] on the device.

@@ -79,6 +79,8 @@ typedef struct {
     int uncertified_queries;  /* queries with fewer than K neighbours in the cloud  */
     float ms_build;           /* bbox + count + scan + scatter (device time)        */
     float ms_solve;           /* tiled query + fallback (device time)               */
+    int range_allocations;    /* device allocations made by kn_solve_range so far (grow-only
+                                 scratch: 1 for any sequence of equal or shrinking batches) */
 } kn_stats;
 
 /* The problem handle. Field names follow the reference struct (reference knearests.h:3-16);

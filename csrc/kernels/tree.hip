@@ -142,7 +142,8 @@ __global__ __launch_bounds__(64) void brick_count_kernel(const int* __restrict__
 __global__ __launch_bounds__(256) void brick_scatter_kernel(const float4* __restrict__ in, const int* __restrict__ cell_start,
                                                             const GridGeom* __restrict__ geom, int nbx, int nby,
                                                             const unsigned* __restrict__ bbase, float4* __restrict__ tmp_pts,
-                                                            unsigned* __restrict__ tmp_vals, unsigned* __restrict__ cell_code,
+                                                            unsigned* __restrict__ tmp_vals,
+                                                            unsigned long long* __restrict__ cell_code,
                                                             uint2* __restrict__ cell_span) {
     __shared__ int s_base[kBrickCells + 1];
     __shared__ int s_start[kBrickCells];
@@ -188,7 +189,9 @@ __global__ __launch_bounds__(256) void brick_scatter_kernel(const float4* __rest
         const unsigned dst = out0 + (unsigned)j;
         tmp_pts[dst] = in[src];
         tmp_vals[dst] = src;
-        cell_code[dst] = (bcode << (3 * kBrickBits)) | (unsigned)lo;  // the cell's Morton code (<= 30 bits)
+        // the cell's Morton code: up to 30 brick bits + 9 in-brick bits (64-bit: an axis of more than
+        // 1,024 cells -- 128 bricks -- takes the brick code past 23 bits)
+        cell_code[dst] = ((unsigned long long)bcode << (3 * kBrickBits)) | (unsigned long long)lo;
         cell_span[dst] = make_uint2(out0 + (unsigned)s_base[lo], out0 + (unsigned)s_base[lo + 1]);
     }
 }
@@ -198,21 +201,26 @@ __global__ __launch_bounds__(256) void brick_scatter_kernel(const float4* __rest
 // ~20 %). One thread per point ranks it by counting over its cell's points: sum of count^2 work
 // (~8n for an occupancy-adaptive grid), spread evenly over the points -- done per brick, the
 // few bricks holding a cluster's core serialised it (230 us at 900K clustered).
-__device__ __forceinline__ unsigned subcell_code(const GridGeom& g, const float4& p, unsigned cc) {
-    const int cx = (int)compact3(cc), cy = (int)compact3(cc >> 1), cz = (int)compact3(cc >> 2);
+__device__ __forceinline__ unsigned subcell_code(const GridGeom& g, const float4& p, unsigned long long cc) {
+    // cell coordinates: brick coordinates (the high bits) * 8 + the in-brick Morton bits
+    const unsigned bc = (unsigned)(cc >> (3 * kBrickBits)), ic = (unsigned)cc & (kBrickCells - 1);
+    const int cx = (int)((compact3(bc) << kBrickBits) | compact3(ic));
+    const int cy = (int)((compact3(bc >> 1) << kBrickBits) | compact3(ic >> 1));
+    const int cz = (int)((compact3(bc >> 2) << kBrickBits) | compact3(ic >> 2));
     const int sx = clampi((int)((p.x - (g.origin[0] + cx * g.cell[0])) * g.inv_cell[0] * 8.f), 0, 7);
     const int sy = clampi((int)((p.y - (g.origin[1] + cy * g.cell[1])) * g.inv_cell[1] * 8.f), 0, 7);
     const int sz = clampi((int)((p.z - (g.origin[2] + cz * g.cell[2])) * g.inv_cell[2] * 8.f), 0, 7);
     return spread10((unsigned)sx) | (spread10((unsigned)sy) << 1) | (spread10((unsigned)sz) << 2);
 }
 __global__ __launch_bounds__(256) void subcell_rank_kernel(const float4* __restrict__ tmp_pts, const unsigned* __restrict__ tmp_vals,
-                                                           const unsigned* __restrict__ cell_code, const uint2* __restrict__ cell_span,
+                                                           const unsigned long long* __restrict__ cell_code,
+                                                           const uint2* __restrict__ cell_span,
                                                            const GridGeom* __restrict__ geom, int n, float4* __restrict__ pts,
                                                            unsigned* __restrict__ vals, unsigned long long* __restrict__ codes) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const GridGeom g = *geom;
-    const unsigned cc = cell_code[j];
+    const unsigned long long cc = cell_code[j];
     const uint2 sp = cell_span[j];
     const float4 p = tmp_pts[j];
     const unsigned sc = subcell_code(g, p, cc);
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(256) void subcell_rank_kernel(const float4* __restr
     const unsigned dst = sp.x + r;
     pts[dst] = p;
     vals[dst] = tmp_vals[j];
-    codes[dst] = ((unsigned long long)cc << 9) | sc;
+    codes[dst] = (cc << 9) | sc;  // <= 48 bits
 }
 
 // ---- device-wide scan of u32 (block sums -> one-workgroup scan of the sums -> block scans) ------
@@ -876,7 +884,8 @@ size_t tree_workspace_bytes(int n, const int dims[3]) {
     b += align256((size_t)n * 4);                // vals
     b += align256(16);                           // info
     b += align256((size_t)n * 16);               // tmp_pts
-    b += 2 * align256((size_t)n * 4);            // tmp_vals, cell_code
+    b += align256((size_t)n * 4);                // tmp_vals
+    b += align256((size_t)n * 8);                // cell_code (u64)
     b += align256((size_t)n * 8);                // cell_span
     b += align256((NB + 1) * 4);                 // brick counts -> bases
     b += align256(sums * 4);                     // scan block sums
@@ -901,7 +910,7 @@ TreeView tree_view(void* ws, int n, const int dims[3]) {
     t.info = reinterpret_cast<unsigned*>(take(16));
     t.tmp_pts = reinterpret_cast<float4*>(take((size_t)n * 16));
     t.tmp_vals = reinterpret_cast<unsigned*>(take((size_t)n * 4));
-    t.cell_code = reinterpret_cast<unsigned*>(take((size_t)n * 4));
+    t.cell_code = reinterpret_cast<unsigned long long*>(take((size_t)n * 8));
     t.cell_span = reinterpret_cast<uint2*>(take((size_t)n * 8));
     for (int a = 0; a < 3; ++a) t.dims[a] = dims[a];
     t.nbricks_pad = brick_space(dims, t.nbricks);
@@ -924,6 +933,7 @@ hipError_t launch_tree_leaves(const float4* in, const int* cell_start, const Gri
                               hipStream_t s) {
     const int n = t.n;
     if (n <= 0) return hipSuccess;
+    if (!tree_supports(t.dims)) return hipErrorInvalidValue;
     hipError_t e;
     // Morton order of the cells (brick counts -> brick bases -> per-brick cell scan + copy)
     const unsigned nreal = (unsigned)(t.nbricks[0] * t.nbricks[1] * t.nbricks[2]);

@@ -130,11 +130,14 @@ kn_status kn_solve_range(kn_problem* kn, int first, int count, unsigned int* out
     if (count > 0 && !out_ids) { g_err = "null output"; return KN_ERR_INVALID_ARGUMENT; }
     if (count == 0) return KN_OK;
     const size_t nk = (size_t)count * e->k();
-    unsigned* d_idx = nullptr;
-    float* d_d2 = nullptr;
+    // the batch buffers are the engine's grow-only scratch: a sequence of batches allocates once
+    // (no synchronising hipMalloc / hipFree per batch)
+    const size_t bi = (nk * sizeof(unsigned) + 255) & ~(size_t)255;
+    char* scr = static_cast<char*>(e->scratch(bi + (out_d2 ? nk * sizeof(float) : 0)));
+    unsigned* d_idx = scr ? reinterpret_cast<unsigned*>(scr) : nullptr;
+    float* d_d2 = (scr && out_d2) ? reinterpret_cast<float*>(scr + bi) : nullptr;
     kn_status s = KN_OK;
-    if (hipMalloc(&d_idx, nk * sizeof(unsigned)) != hipSuccess ||
-        (out_d2 && hipMalloc(&d_d2, nk * sizeof(float)) != hipSuccess)) {
+    if (!scr) {
         g_err = "hipMalloc(query range)";
         s = KN_ERR_DEVICE;
     }
@@ -144,8 +147,6 @@ kn_status kn_solve_range(kn_problem* kn, int first, int count, unsigned int* out
         g_err = "D2H (query range)";
         s = KN_ERR_DEVICE;
     }
-    if (d_idx) (void)hipFree(d_idx);
-    if (d_d2) (void)hipFree(d_d2);
     return s;
 }
 

@@ -361,6 +361,21 @@ kn_status DistPipeline::prepare_graphs(int unroll) {
 
 void DistPipeline::set_eager(bool eager) { pipe_.set_eager(eager); }
 
+kn_status DistPipeline::rebind(const float* points, const int* ids) {
+    if (!ok_) return KN_ERR_STATE;
+    if ((p_.ids == nullptr) != (ids == nullptr) || (p_.n > 0 && !points)) {
+        err_ = "rebind: input layout differs from the plan";
+        return KN_ERR_INVALID_ARGUMENT;
+    }
+    if (points == p_.points && ids == p_.ids) return KN_OK;
+    if (!pipe_.eager()) pipe_.set_eager(true);
+    // a primed build read the old input: the next launch rebuilds from the new one
+    if (pipe_.unprime() != hipSuccess) { err_ = "rebind: sync"; return KN_ERR_DEVICE; }
+    p_.points = points;
+    p_.ids = ids;
+    return KN_OK;
+}
+
 DistPipeline::~DistPipeline() {
     pipe_.reset();
     if (main_) (void)hipStreamSynchronize(main_);

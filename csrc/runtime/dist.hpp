@@ -100,6 +100,12 @@ public:
     kn_status prepare_graphs(int unroll);
     void set_eager(bool eager);
     bool eager() const { return pipe_.eager(); }
+    // Read the steps' input from other device buffers (same n; ids null <=> built without ids):
+    // a caller passing a fresh tensor every step keeps its pipeline. Eager stages read the new
+    // pointers at once; captured graphs hold the old ones, so a graph-mode pipeline switches to
+    // eager (one wait for both streams, once). The launch() caller-stream ordering still covers
+    // the old buffers' last reads.
+    kn_status rebind(const float* points, const int* ids);
     int capture_fallbacks() const { return pipe_.fallbacks(); }
     // Enqueue `iters` pipelined steps (unroll >= 2, even: steps per graph launch); *last_step = the
     // index of the last one. The steps read the caller's points in place: `caller` (may be null)

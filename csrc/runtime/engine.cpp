@@ -54,6 +54,7 @@ void Engine::release() {
     if (points3_) { dfree(points3_); points3_ = nullptr; }
     if (tree_ws_) { dfree(tree_ws_); tree_ws_ = nullptr; }
     if (tree_nodes_) { dfree(tree_nodes_); tree_nodes_ = nullptr; }
+    if (scratch_) { dfree(scratch_); scratch_ = nullptr; scratch_bytes_ = 0; }
     // the (idle) stream and its events go back to the pool; the reference leaks its events (D6)
     if (stream_) {
         (void)hipStreamSynchronize(stream_);
@@ -88,6 +89,17 @@ void Engine::dfree(void* p) {
     if (it == dsize_.end()) { (void)hipFree(p); return; }
     arena_release(cfg_.device, p, it->second);
     dsize_.erase(it);
+}
+
+void* Engine::scratch(size_t bytes) {
+    if (bytes <= scratch_bytes_) return scratch_;
+    if (scratch_) { dfree(scratch_); scratch_ = nullptr; scratch_bytes_ = 0; }
+    void* p = nullptr;
+    if (dmalloc(&p, bytes) != hipSuccess) return nullptr;
+    scratch_ = p;
+    scratch_bytes_ = bytes;
+    ++scratch_allocs_;
+    return p;
 }
 
 kn_status Engine::fail(kn_status s, const std::string& msg) {
@@ -390,7 +402,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
     // size (900K clustered, K=16: grid query 7.5 ms, tree 1.6 ms + 0.27 ms build; surfaces
     // 1.27 vs 0.96 + 0.27; profiles/diag_r2_tree.jsonl): the tree path takes it.
     refined_ = refined;
-    use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined));
+    use_tree_ = cfg_.use_tiles && (cfg_.algo == 2 || (cfg_.algo == 0 && refined)) && tree_supports(ap_.dims);
     if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
     drop_pipeline();  // grid or tree step of the new plan
     if (cfg_.verbose) fprintf(stderr, "kn_firstbuild: %.3f msec\n", ms_build_);
@@ -976,6 +988,7 @@ kn_status Engine::stats(kn_stats* out, std::vector<int>* hist) {
     out->uncertified_queries = solved_ ? (int)c[1] : 0;
     out->ms_build = ms_build_;
     out->ms_solve = ms_solve_;
+    out->range_allocations = (int)scratch_allocs_;
     if (hist) hist->assign(v.begin() + 3, v.end());
     // the stats kernel used cell_count_ as scratch: it is rebuilt by every build
     return KN_OK;
@@ -1072,7 +1085,7 @@ Engine* Engine::load(const char* path, const EngineConfig& cfg, std::string* err
     }
     // the refined state travels with the grid: algo auto serves a refined grid with the tree
     e->refined_ = v2 && (hdr[11] & kPlanRefined);
-    e->use_tree_ = c.use_tiles && (c.algo == 2 || (c.algo == 0 && e->refined_));
+    e->use_tree_ = c.use_tiles && (c.algo == 2 || (c.algo == 0 && e->refined_)) && tree_supports(e->ap_.dims);
     bool ok = hipMemcpy(e->geom_, &g, sizeof(g), hipMemcpyHostToDevice) == hipSuccess &&
               (n == 0 || hipMemcpy(e->sorted_, s.data(), (size_t)n * sizeof(float4), hipMemcpyHostToDevice) == hipSuccess) &&
               (n == 0 || hipMemcpy(e->perm_, perm.data(), (size_t)n * sizeof(unsigned), hipMemcpyHostToDevice) == hipSuccess) &&

@@ -53,6 +53,10 @@ public:
     // Queries [first, first + count) only, into caller device buffers (count x K; d_dist may be
     // null): batched solves of clouds whose whole N x K result does not fit on the device.
     kn_status solve_range(int first, int count, unsigned* d_idx, float* d_dist);
+    // Grow-only device scratch owned by the engine (kn_solve_range's batch buffers): a batched
+    // solve allocates once, at its first (largest-so-far) batch, not per batch. nullptr on failure.
+    void* scratch(size_t bytes);
+    size_t scratch_allocations() const { return scratch_allocs_; }
     kn_status set_k(int k);
     // Capture build+solve into a graph once, then replay it `iters` times (bench path).
     kn_status run_graph(int iters, float* ms_per_iter);
@@ -162,6 +166,8 @@ private:
     size_t arena_bytes_ = 0;
     // result / tree buffers through the process-wide device block cache (hostio.hpp)
     std::unordered_map<void*, size_t> dsize_;
+    void* scratch_ = nullptr;
+    size_t scratch_bytes_ = 0, scratch_allocs_ = 0;
     hipError_t dmalloc(void** p, size_t bytes);
     template <class T>
     hipError_t dmalloc(T** p, size_t bytes) { return dmalloc(reinterpret_cast<void**>(p), bytes); }

@@ -769,7 +769,8 @@ std::vector<torch::Tensor> dist_local(torch::Tensor recv, torch::Tensor self_row
     }
     // use_tree: -1 auto (the local grid had to be refined: a share too non-uniform for one cell
     // size, as kn::Engine decides on one GPU), 0 grid, 1 tree
-    const bool tree = use_tree < 0 ? refined : use_tree != 0;
+    const int dims3[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
+    const bool tree = (use_tree < 0 ? refined : use_tree != 0) && kn::tree_supports(dims3);
     auto dims_t = torch::tensor({dims[0], dims[1], dims[2]}, torch::kInt64);
     auto tree_t = torch::tensor({(int64_t)(tree ? 1 : 0)}, torch::kInt64);
     if (tree && npts > 0) {
@@ -1440,6 +1441,23 @@ public:
         return d_->prepare_graphs((int)unroll) == KN_OK;
     }
     void set_eager(bool eager) { d_->set_eager(eager); }
+    // new input tensors for the following steps (same n, same ids presence); keeps them alive
+    void rebind(torch::Tensor points, c10::optional<torch::Tensor> ids) {
+        check_points(points, true);
+        TORCH_CHECK(points.size(0) == points_.size(0) && points.get_device() == points_.get_device(),
+                    "rebind: same number of points on the same device");
+        TORCH_CHECK(ids.has_value() == ids_.defined(), "rebind: ids given iff the pipeline was built with ids");
+        const int* ip = nullptr;
+        if (ids.has_value()) {
+            TORCH_CHECK(ids->is_cuda() && ids->scalar_type() == torch::kInt32 && ids->numel() == points.size(0) &&
+                            ids->is_contiguous(), "ids: contiguous int32 GPU tensor of N entries");
+            ip = ids->data_ptr<int>();
+        }
+        const c10::DeviceGuard guard(points.device());
+        TORCH_CHECK(d_->rebind(points.data_ptr<float>(), ip) == KN_OK, d_->error());
+        points_ = points;
+        if (ids.has_value()) ids_ = *ids;
+    }
     std::string mode() { return d_->eager() ? "eager" : "graph"; }
     int64_t capture_fallbacks() { return d_->capture_fallbacks(); }
     std::string error() { return d_->error(); }
@@ -1658,6 +1676,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("warmup", &PyDistPipe::warmup, py::arg("timeout_s") = 300.0)
         .def("prepare_graphs", &PyDistPipe::prepare_graphs, py::arg("unroll"))
         .def("set_eager", &PyDistPipe::set_eager)
+        .def("rebind", &PyDistPipe::rebind, py::arg("points"), py::arg("ids") = py::none())
         .def("mode", &PyDistPipe::mode)
         .def("capture_fallbacks", &PyDistPipe::capture_fallbacks)
         .def("error", &PyDistPipe::error)

@@ -811,6 +811,13 @@ class DistributedKNearests:
                 and (ids32 is None or p["ids"].data_ptr() == ids32.data_ptr()))
         if same:
             return p
+        if (p is not None and p["st"] is st and p["n"] == points.size(0) and (p["ids"] is None) == (ids32 is None)):
+            # other storage of the same shape (a caller passing a fresh tensor every step): the
+            # pipeline reads the new tensors from now on (local: no collective, no rebuild)
+            p["pipe"].rebind(points, ids32)
+            p["pts"], p["ids"] = points, ids32
+            self.pipe_mode = p["pipe"].mode()
+            return p
         self._pipe = None  # release the old pipeline's buffers first
         C = ops.load()
         world1_force = self.world == 1 and self.force_collectives

@@ -105,6 +105,17 @@ for cap, force in [(c, f) for c in caps for f in modes]:
             outs = []
             if not refill:
                 break
+    # a fresh tensor every step (same shape): the pipeline is rebound, not rebuilt
+    dk3 = DistributedKNearests(k=16, force_collectives=force)
+    dk3.solve(pts)
+    fresh = True
+    first_pipe = None
+    for i in range(4):
+        r = dk3.solve(pts.clone(), async_=True)
+        fresh = fresh and r.valid() and same(r, ref)
+        if i == 0:
+            first_pipe = dk3._pipe["pipe"] if dk3._pipe else None
+    fresh = fresh and dk3._pipe is not None and dk3._pipe["pipe"] is first_pipe
     prof = dk.profile_step(pts)
     prof_ok = all(v >= 0.0 for v in prof.values()) and len(prof) == 5
     moved = pts * 0.5
@@ -113,10 +124,10 @@ for cap, force in [(c, f) for c in caps for f in modes]:
     rec = same(dk.solve(moved), reference(moved))
     mode_ok = dk2.pipe_mode == want_mode and batch.stats.get("pipe_mode") == want_mode
     print(f"capture {cap} force {force} mode {batch.stats.get('pipe_mode')} full {r_full} pipelined {piped} "
-          f"valid {valid} rows {rows} batch {b_ok} {b2_ok} refill {refill} moved share invalid {inval} "
+          f"valid {valid} rows {rows} batch {b_ok} {b2_ok} refill {refill} fresh {fresh} moved share invalid {inval} "
           f"recovered {rec} profile {prof}", flush=True)
     ok_all = (ok_all and r_full and piped and valid and rows and b_ok and b2_ok and refill and inval and rec and prof_ok
-              and mode_ok)
+              and mode_ok and fresh)
 print("ALL OK" if ok_all else "FAILED", flush=True)
 dist.destroy_process_group()
 sys.exit(0 if ok_all else 1)

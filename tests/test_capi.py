@@ -28,7 +28,7 @@ class KnStats(C.Structure):
     _fields_ = [("num_points", C.c_int), ("k", C.c_int), ("dims", C.c_int * 3), ("num_cells", C.c_int),
                 ("min_cell", C.c_int), ("max_cell", C.c_int), ("avg_cell", C.c_float), ("empty_cells", C.c_int),
                 ("fallback_queries", C.c_int), ("uncertified_queries", C.c_int), ("ms_build", C.c_float),
-                ("ms_solve", C.c_float)]
+                ("ms_solve", C.c_float), ("range_allocations", C.c_int)]
 
 
 class KnMultiOptions(C.Structure):
@@ -173,6 +173,9 @@ def test_capi_solve_range_batches():
         assert lib.kn_solve_range(prob, first, cnt, ids[first:].ctypes.data, d2[first:].ctypes.data) == 0, \
             lib.kn_last_error()
     assert lib.kn_solve_range(prob, n - 5, 10, ids.ctypes.data, None) != 0  # out of range
+    st = KnStats()
+    assert lib.kn_get_stats(prob, C.byref(st)) == 0
+    assert st.range_allocations == 1, st.range_allocations  # one grow-only scratch for all batches
     assert lib.kn_solve_ex(prob) == 0
     g = lib.kn_get_neighbors(prob)
     whole = np.ctypeslib.as_array(g, shape=(n * k,)).reshape(n, k).copy()

@@ -221,6 +221,26 @@ def test_engine_stream_of_clouds(cuda, unroll):
     _check(clouds[-1], idx, d2, k)
 
 
+def test_tree_long_axis(cuda):
+    """Tree path on a grid with more than 1,024 cells along one axis (the cells'
+    Morton codes overflowed 32 bits past 128 bricks): a uniform 1000 x 8 x 8 slab, forced onto the
+    tree, equals the oracle."""
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    k = 16
+    n = 400000
+    g = torch.Generator().manual_seed(17)
+    p = (torch.rand(n, 3, generator=g) * torch.tensor([1000.0, 8.0, 8.0])).contiguous()
+    e = C.Engine(k, algo=2)
+    e.prepare(p.to(cuda))
+    e.solve()
+    info = e.info()
+    assert info["algo"] == "tree" and max(info["dims"]) > 1024, info
+    idx, d2 = e.results(cuda)
+    _check(p, idx, d2, k)
+
+
 @pytest.mark.parametrize("k", [16, 50])
 def test_engine_stream_after_unrolled(cuda, k):
     """A stream step issued right after an UNROLLED resident launch, with no sync in between
