@@ -123,17 +123,28 @@ def run_native(args) -> dict:
     chk = brute_check(pts, torch.arange(pts.size(0), device=dev), idx0, d20, args.k) if not args.no_check else {}
     log(f"check (eager rows) {chk}")
     if args.stream_clouds:
-        # a stream of distinct clouds (kn::Engine::stream_step): every step copies ITS cloud into
-        # the free grid set, bins and queries it; the next cloud is binned while this one queries
+        # a stream of distinct clouds: every step bins and queries ITS cloud (step i: cloud i % M)
+        # and writes its rows to its own output buffers. Default: kn::Engine::stream_batch (one
+        # graph per power-of-two chunk of steps, step i+1's copy-in + build under step i's
+        # queries); --stream-mode step: one stream_step() call per step (per-stage graphs)
         clouds = [pts] + [make_cloud(args, dev, 104729 * j) for j in range(1, args.stream_clouds)]
         M = len(clouds)
         state = {"i": 0}
+        if args.stream_mode == "batch":
+            oidx = [torch.empty(args.n, args.k, dtype=torch.int32, device=dev) for _ in range(M)]
+            od2 = [torch.empty(args.n, args.k, dtype=torch.float32, device=dev) for _ in range(M)]
 
-        def launch(n):
-            for _ in range(n):
-                i = state["i"]
-                e.stream_step(clouds[i % M], clouds[(i + 1) % M])
-                state["i"] = i + 1
+            def launch(n):
+                i0 = state["i"]
+                sel = [(i0 + t) % M for t in range(n)]
+                e.stream_batch([clouds[j] for j in sel], [oidx[j] for j in sel], [od2[j] for j in sel])
+                state["i"] = i0 + n
+        else:
+            def launch(n):
+                for _ in range(n):
+                    i = state["i"]
+                    e.stream_step(clouds[i % M], clouds[(i + 1) % M])
+                    state["i"] = i + 1
     elif args.pipeline:
         def launch(n):
             e.launch_pipelined(n, args.unroll)
@@ -147,7 +158,11 @@ def run_native(args) -> dict:
     e.sync()
     dt = time.perf_counter() - t0
     log(f"timed {args.steps} steps: {dt * 1e3 / args.steps:.3f} ms/step")
-    idx, d2 = e.results(dev)
+    if args.stream_clouds and args.stream_mode == "batch":
+        j = (state["i"] - 1) % M
+        idx, d2 = oidx[j], od2[j]
+    else:
+        idx, d2 = e.results(dev)
     if args.stream_clouds:
         last = clouds[(state["i"] - 1) % M]
         if not args.no_check:
@@ -463,6 +478,9 @@ def main() -> int:
     ap.add_argument("--stream-clouds", type=int, default=0,
                     help="native 1-GPU path: cycle M distinct clouds (a new cloud every step, copied into the free "
                          "grid set, binned and queried) instead of re-solving one resident cloud")
+    ap.add_argument("--stream-mode", choices=["batch", "step"], default="batch",
+                    help="--stream-clouds: one stream_batch() call for all steps (graphs of many steps) or one "
+                         "stream_step() call per step")
     ap.add_argument("--path", choices=["native", "torch"], default="native",
                     help="1 GPU: native C++ runtime (hipGraph) or the torch-op path (torch.cuda graphs)")
     ap.add_argument("--no-check", action="store_true")
@@ -551,7 +569,8 @@ def main() -> int:
                  "grid": r.get("dims"), "query_algo": r.get("algo", "grid"),
                  "exact_path_queries": r["info"].get("exact_path"), "graph": not args.no_graph, "path": args.path,
                  "pipelined": bool(args.pipeline), "unroll": args.unroll,
-                 **({"stream_clouds": args.stream_clouds} if args.stream_clouds else {})}
+                 **({"stream_clouds": args.stream_clouds, "stream_mode": args.stream_mode}
+                    if args.stream_clouds else {})}
     ms = r["t"] / args.steps * 1e3
     qps = r["n_total"] * args.steps / r["t"]
     line = {

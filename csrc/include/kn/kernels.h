@@ -158,6 +158,13 @@ struct BinPlan {
 };
 bool bin_plan(int n, int num_cells, BinPlan* out);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t stream);
+
+// Batched streams of clouds (Engine::stream_batch): write `count` (<= kPtrTableMax) pointers into
+// the device table `dst` (kernel arguments carry them: the host array may go at once), and copy
+// n floats from the buffer whose address sits in the device slot `src_ref`.
+constexpr int kPtrTableMax = 96;
+hipError_t launch_set_ptr_table(void* const* ptrs, int count, void** dst, hipStream_t stream);
+hipError_t launch_copy_from_ref(const float* const* src_ref, float* dst, size_t n, hipStream_t stream);
 // The deterministic in-cell order (by original index) of launch_build, alone (rank of each point
 // in its cell, O(N x mean cell occupancy) parallel work; tmp: N float4 scratch). The occupancy-
 // adaptive build bins its probe grids without it (a clustered cloud's first grid has cells of
@@ -182,6 +189,11 @@ struct QueryBuffers {
     CompleteBox complete;
     unsigned* out_idx;        // n_queries x k   (row = original index), UINT_MAX = empty
     float* out_dist;          // optional n_queries x k squared distances
+    // optional: device slots holding the output pointers, read by the kernels at launch time
+    // instead of out_idx / out_dist (a graph captured once writes each replay's rows where the
+    // slot points: batched streams of clouds, Engine::stream_batch)
+    unsigned* const* out_idx_ref = nullptr;
+    float* const* out_dist_ref = nullptr;
     unsigned* fallback_list;  // n   (stored indices of queries needing the exact path)
     unsigned* counters;       // kNumCounters words, see below
     unsigned* uncert_list;    // optional n_queries: original indices of uncertified queries

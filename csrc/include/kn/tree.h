@@ -96,6 +96,8 @@ struct TreeQuery {
                               // halo bit, output row = row_of[stored index]; multi-GPU ranks)
     unsigned* out_idx;        // n_queries x k, row = original index
     float* out_dist;          // optional
+    unsigned* const* out_idx_ref = nullptr;  // optional pointer slots (QueryBuffers::out_idx_ref)
+    float* const* out_dist_ref = nullptr;
     unsigned* counters;       // kNumCounters words: [0] exact-finish queries, [2] waves over the
                               // visit cap, [3] queries whose re-rank stayed unsorted, [4] queries
                               // whose K-th is not below the truncation floor, [5] leaves

@@ -850,4 +850,47 @@ hipError_t launch_cell_stats(const int* cell_start, int num_cells, int* out, int
     return hipGetLastError();
 }
 
+// ---- pointer tables of batched streams of clouds (Engine::stream_batch) ----------------------
+// A graph captured once per batch length reads its steps' input / output pointers from a device
+// table; one tiny kernel writes the table (its values travel as kernel arguments, so the host
+// array need not outlive the enqueue) before each graph launch, stream-ordered.
+struct PtrTable {
+    void* p[kPtrTableMax];
+};
+__global__ void set_ptr_table_kernel(PtrTable t, int count, void** dst) {
+    const int i = threadIdx.x;
+    if (i < count) dst[i] = t.p[i];
+}
+// dst[0, n) = (*src_ref)[0, n): 16-byte vector copy where the source is aligned, else scalar
+__global__ __launch_bounds__(256) void copy_from_ref_kernel(const float* const* src_ref, float* __restrict__ dst,
+                                                            size_t n) {
+    const float* src = *src_ref;
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
+        const size_t n4 = n / 4;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (size_t i = tid; i < n4; i += stride) d4[i] = s4[i];
+        for (size_t i = 4 * n4 + tid; i < n; i += stride) dst[i] = src[i];
+    } else {
+        for (size_t i = tid; i < n; i += stride) dst[i] = src[i];
+    }
+}
+
+hipError_t launch_set_ptr_table(void* const* ptrs, int count, void** dst, hipStream_t s) {
+    if (count < 0 || count > kPtrTableMax) return hipErrorInvalidValue;
+    if (count == 0) return hipSuccess;
+    PtrTable t{};
+    for (int i = 0; i < count; ++i) t.p[i] = ptrs[i];
+    set_ptr_table_kernel<<<1, kPtrTableMax, 0, s>>>(t, count, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_from_ref(const float* const* src_ref, float* dst, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned grid = std::max(1u, std::min(cdiv(n / 4 + 1, 256), 2048u));
+    copy_from_ref_kernel<<<grid, 256, 0, s>>>(src_ref, dst, n);
+    return hipGetLastError();
+}
+
 }  // namespace kn

@@ -71,6 +71,8 @@ struct TileArgs {
     CompleteBox complete;
     unsigned* out_idx;
     float* out_dist;
+    unsigned* const* out_idx_ref;  // non-null: the output pointers are read from these slots
+    float* const* out_dist_ref;
     unsigned* fallback_list;
     unsigned* counters;
     int TX, TY, TZ, H;
@@ -154,6 +156,9 @@ constexpr bool outer_pack_k() {
 // truncation near-ties (round 1).
 #ifndef KN_WIN
 #define KN_WIN 1
+#endif
+#ifndef KN_RERANK_UNROLL
+#define KN_RERANK_UNROLL 0
 #endif
 constexpr int kWin = KN_WIN;  // exact re-rank window: same-bucket neighbours within +-kWin
 // Second, wider window for the lanes whose bucket runs overflow +-kWin but fit +-kWin2 (point
@@ -240,12 +245,21 @@ __device__ unsigned long long g_phase[kPhN];
 // the ~535 the union stream feeds every lane, at the price of divergent trip counts.
 template <int KT, int M, bool LANE, bool WIDE = false>
 __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
+    // output pointers: the launch's, or read from device slots (graph replays of a batched
+    // stream of clouds); locals, so the kernel argument block stays read-only
+    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
+    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
     // K + M margin slots + 1: the query itself is not filtered in the hot loop (that cost 3
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
     constexpr int KM = KT + M + 1;
     constexpr bool kFull = LANE && (KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40));
     // (KN_OUTER_PACK=3: the whole-block walk packs its outer rows instead of the sorted table)
     constexpr bool kRowOrder = LANE && (KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && kFull && !outer_pack_k<KT>()));
+    // row-cut square roots: the bare v_sqrt_f32 (kn/wave.h sqrt_bound) for the walks of K <= 40
+    // (900K, interleaved A/B: K=16 query -2.5 %, K=32 -3 %); the whole-block walk (K > 40) keeps
+    // the correctly rounded sqrtf, which measured 11 % FASTER there (K=50 0.949 -> 0.838 ms) with
+    // identical rows and near-identical code (profiles/ab_r5_query_variants.txt)
+    auto rsqrt = [](float x) __attribute__((always_inline)) { return kFull ? sqrtf(x) : sqrt_bound(x); };
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     KN_PH_DECL
     float4* pts = reinterpret_cast<float4*>(smem);
@@ -460,7 +474,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     if (tau == INFINITY) {
                         lx0 = hx0; lx1 = hx1;
                     } else {
-                        const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                        const float rr = rsqrt(tau - dyz2) * 1.000001f + g.eps;
                         lx0 = max(hx0, cell_coord(g, 0, qx - rr) - sx0);
                         lx1 = min(hx1, cell_coord(g, 0, qx + rr) - sx0);
                     }
@@ -487,7 +501,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                         if (tau == INFINITY) {
                             lx0 = hx0; lx1 = hx1;
                         } else {
-                            const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                            const float rr = rsqrt(tau - dyz2) * 1.000001f + g.eps;
                             lx0 = max(hx0, cell_coord(g, 0, qx - rr) - sx0);
                             lx1 = min(hx1, cell_coord(g, 0, qx + rr) - sx0);
                         }
@@ -540,7 +554,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                         const float dyz2 = fmaf(dyb, dyb, dzb * dzb);
                         const float tau = lane_tau();
                         if (dyz2 <= tau) {
-                            const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                            const float rr = rsqrt(tau - dyz2) * 1.000001f + g.eps;
                             lx0 = max(hx0, cell_coord(g, 0, qx - rr) - sx0);
                             lx1 = min(hx1, cell_coord(g, 0, qx + rr) - sx0);
                         }
@@ -606,7 +620,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                             if (tau == INFINITY) {
                                 lx0 = rx0; lx1 = rx1;
                             } else {
-                                const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                                const float rr = rsqrt(tau - dyz2) * 1.000001f + g.eps;
                                 lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
                                 lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
                             }
@@ -637,7 +651,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     if (tz == INFINITY) {
                         ly0 = ry0; ly1 = ry1;
                     } else if (dz2 <= tz) {
-                        const float rr = sqrtf(tz - dz2) * 1.000001f + g.eps;
+                        const float rr = rsqrt(tz - dz2) * 1.000001f + g.eps;
                         ly0 = max(ry0, cell_coord(g, 1, qy - rr) - sy0);
                         ly1 = min(ry1, cell_coord(g, 1, qy + rr) - sy0);
                     }
@@ -656,7 +670,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     if (tau == INFINITY) {
                         lx0 = rx0; lx1 = rx1;
                     } else if (dyz2 <= tau) {
-                        const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                        const float rr = rsqrt(tau - dyz2) * 1.000001f + g.eps;
                         lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
                         lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
                     }
@@ -827,8 +841,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 #pragma unroll
             for (int t = 0; t < NW; ++t) ld((t >= W && t - W < KM) ? keys[t - W] : SENT, t);
             int base = 0;
-#pragma unroll 1
-            for (int j = 0; j < KM; ++j) {
+            auto entry = [&](int j) __attribute__((always_inline)) {
+                (void)j;
                 const bool vj = wk[W] != SENT;
                 int pos = base;
 #pragma unroll
@@ -843,8 +857,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 }
                 if (vj && act && pos < k) {
                     const size_t o = KN_IDX(row + pos, (size_t)a.n_queries * k, 209);
-                    a.out_idx[o] = out_id(a, wi[W]);
-                    if (a.out_dist) a.out_dist[o] = wd[W];
+                    o_idx[o] = out_id(a, wi[W]);
+                    if (o_dist) o_dist[o] = wd[W];
                 }
                 dK2 = (vj && pos == k - 1) ? wd[W] : dK2;
                 base += vj ? 1 : 0;
@@ -855,6 +869,15 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 #pragma unroll
                 for (int t = 0; t + 1 < KM; ++t) keys[t] = keys[t + 1];
                 keys[KM - 1] = SENT;
+            };
+            // KN_RERANK_UNROLL: the K buckets with KM <= 24 unroll the walk, so the key shifts and
+            // window rotations become register renames instead of ~KM + 3 * NW moves per entry
+            if constexpr (KN_RERANK_UNROLL && KM <= 24) {
+#pragma unroll
+                for (int j = 0; j < KM; ++j) entry(j);
+            } else {
+#pragma unroll 1
+                for (int j = 0; j < KM; ++j) entry(j);
             }
             nfound = base;
         };
@@ -879,8 +902,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                 const int r = 64 * e + lane;
                 if (r < k && v[e] != ~0ull) {
                     const size_t o = KN_IDX(rowL + r, (size_t)a.n_queries * k, 214);
-                    a.out_idx[o] = out_id(a, (unsigned)v[e]);
-                    if (a.out_dist) a.out_dist[o] = __uint_as_float((unsigned)(v[e] >> 32));
+                    o_idx[o] = out_id(a, (unsigned)v[e]);
+                    if (o_dist) o_dist[o] = __uint_as_float((unsigned)(v[e] >> 32));
                 }
             }
             float dk = INFINITY;
@@ -948,7 +971,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
                     const float dyb = slab_dist(g, 1, qyL, sy0 + y, sy0 + y);
                     const float dyz2 = fmaf(dyb, dyb, dz2);
                     if (!(dyz2 <= thr)) continue;
-                    const float rr = sqrtf(thr - dyz2) * 1.000001f + g.eps;
+                    const float rr = rsqrt(thr - dyz2) * 1.000001f + g.eps;
                     const int lx0 = max(x0, cell_coord(g, 0, qxL - rr) - sx0);
                     const int lx1 = min(x1, cell_coord(g, 0, qxL + rr) - sx0);
                     if (lx0 > lx1) continue;
@@ -1008,7 +1031,7 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
             const unsigned pos = atomicAdd(a.counters + 0, 1u);
             // the row already holds K real candidates: their K-th distance bounds the true one,
             // and the exact kernel starts its walk with it (kSeedBit)
-            const bool seed = a.out_dist && nfound >= k && dK2 < INFINITY;
+            const bool seed = o_dist && nfound >= k && dK2 < INFINITY;
             a.fallback_list[KN_IDX(pos, (unsigned)a.n, 210)] = qsidx | (seed ? kSeedBit : 0u);
         }
     }
@@ -1044,6 +1067,10 @@ constexpr int kStreamSlotBits = 11;  // stream positions per chunk: 2048
 template <int KT, int M>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_WPE, 8))) void knn_stream_kernel(
     TileArgs a) {
+    // output pointers: the launch's, or read from device slots (graph replays of a batched
+    // stream of clouds); locals, so the kernel argument block stays read-only
+    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
+    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
     constexpr int KM = KT + M + 1;
     constexpr unsigned MASK = (1u << kStreamSlotBits) - 1u;
     constexpr unsigned HIMASK = ~MASK;
@@ -1141,7 +1168,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
             if (tau == INFINITY) {
                 lx0 = rx0; lx1 = rx1;
             } else if (dyz2 <= tau) {
-                const float rr = sqrtf(tau - dyz2) * 1.000001f + g.eps;
+                const float rr = sqrt_bound(tau - dyz2) * 1.000001f + g.eps;
                 lx0 = max(rx0, cell_coord(g, 0, qx - rr) - sx0);
                 lx1 = min(rx1, cell_coord(g, 0, qx + rr) - sx0);
             }
@@ -1359,8 +1386,8 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
             for (int j = 0; j < KM; ++j) {
                 if (j < k) {
                     const size_t o = KN_IDX(row + j, (size_t)a.n_queries * k, 228);
-                    a.out_idx[o] = out_id(a, ii[j]);
-                    if (a.out_dist) a.out_dist[o] = dd[j];
+                    o_idx[o] = out_id(a, ii[j]);
+                    if (o_dist) o_dist[o] = dd[j];
                 }
             }
         } else {
@@ -1384,6 +1411,8 @@ struct ExactArgs {
     CompleteBox complete;
     unsigned* out_idx;
     float* out_dist;
+    unsigned* const* out_idx_ref;
+    float* const* out_dist_ref;
     const unsigned* list;      // stored indices (nullptr: all stored points)
     const unsigned* list_count;
     unsigned* counters;        // [1] uncertified count
@@ -1414,6 +1443,10 @@ constexpr int kXCap = 256;
 #define KN_EXACT_GRID 1024
 #endif  // per-wave candidate buffer (u64 keys); >= K + 64 for K <= 128
 __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
+    // output pointers: the launch's, or read from device slots (graph replays of a batched
+    // stream of clouds); locals, so the kernel argument block stays read-only
+    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
+    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
     __shared__ unsigned long long s_buf[4][kXCap];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long* buf = s_buf[wid];
@@ -1425,7 +1458,7 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
         // external queries (multi-GPU forwarding): a point of another rank, self = same global id
         const unsigned entry = a.ext ? ~0u : (unsigned)__builtin_amdgcn_readfirstlane(
             (int)(a.list ? a.list[KN_IDX(t, a.n, 311)] : (unsigned)t));
-        const bool seeded = !a.ext && a.list && (entry & kSeedBit) && a.out_dist;
+        const bool seeded = !a.ext && a.list && (entry & kSeedBit) && o_dist;
         const unsigned sidx = a.ext ? ~0u : (entry & ~kSeedBit);
         const float4 qp = a.ext ? a.ext[(size_t)t * a.ext_stride] : a.sorted[KN_IDX(sidx, (unsigned)a.n, 312)];
         const unsigned qw = __float_as_uint(qp.w);
@@ -1446,7 +1479,7 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
             // the tile kernel's K-th distance for this row (K real points within it): every true
             // neighbour passes d2 <= thr from the first shell on, rows are cut by the ball at once
             const float s0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
-                a.out_dist[KN_IDX((size_t)qorig * (size_t)k + (size_t)(k - 1), (size_t)a.n_queries * k, 317)])));
+                o_dist[KN_IDX((size_t)qorig * (size_t)k + (size_t)(k - 1), (size_t)a.n_queries * k, 317)])));
             if (s0 >= 0.f && s0 < INFINITY) thr = s0;
         }
         // sort buf[0, cnt), keep the first min(cnt, k), thr = K-th distance once K are held
@@ -1511,7 +1544,7 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
                     const float dyb = slab_dist(g, 1, qy, y, y), dzb = slab_dist(g, 2, qz, z, z);
                     const float dyz2 = fmaf(dyb, dyb, dzb * dzb);
                     if (!(dyz2 <= thr)) return false;
-                    const float rr = sqrtf(thr - dyz2) * 1.000001f + g.eps;
+                    const float rr = sqrt_bound(thr - dyz2) * 1.000001f + g.eps;
                     xa = max(xa, cell_coord(g, 0, qx - rr));
                     xb = min(xb, cell_coord(g, 0, qx + rr));
                     if (xa > xb) return false;
@@ -1582,8 +1615,8 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
             const size_t o = KN_IDX((size_t)qorig * (size_t)k + j, (size_t)a.n_queries * k, 315);
             const unsigned long long v = (j < cnt) ? buf[j] : ~0ull;
             const bool empty = (v == ~0ull);
-            a.out_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
-            if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
+            o_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
+            if (o_dist) o_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -1716,6 +1749,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.X = X; a.Y = Y; a.Z = Z; a.k = q.k; a.n_queries = q.n_queries; a.q_lo = q.q_lo; a.id_map = q.id_map;
         a.row_of = q.row_of;
         a.complete = q.complete; a.out_idx = q.out_idx; a.out_dist = q.out_dist;
+        a.out_idx_ref = q.out_idx_ref; a.out_dist_ref = q.out_dist_ref;
         a.fallback_list = q.fallback_list; a.counters = q.counters;
         a.TX = q.tile[0]; a.TY = q.tile[1]; a.TZ = q.tile[2]; a.H = q.halo;
         a.Hx = q.halo * std::max(1, q.xsub);
@@ -1789,6 +1823,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     b.X = X; b.Y = Y; b.Z = Z; b.k = q.k; b.n_queries = q.n_queries; b.q_lo = q.q_lo; b.id_map = q.id_map;
     b.row_of = q.row_of;
     b.complete = q.complete; b.out_idx = q.out_idx; b.out_dist = q.out_dist;
+    b.out_idx_ref = q.out_idx_ref; b.out_dist_ref = q.out_dist_ref;
     b.list = tiles ? q.fallback_list : nullptr;
     b.list_count = q.counters + 0;
     b.counters = q.counters;

@@ -68,9 +68,12 @@ struct TArgs {
     const unsigned* src;     // tree point -> input (grid slot) index: row_of is indexed by grid slot
     unsigned* out_idx;
     float* out_dist;
+    unsigned* const* out_idx_ref;  // non-null: output pointers read from these slots at launch
+    float* const* out_dist_ref;
     unsigned* counters;
     int flags;
 };
+
 
 __device__ __forceinline__ unsigned ordf(float f) {
     const unsigned u = __float_as_uint(f);
@@ -377,8 +380,11 @@ __global__ __launch_bounds__(256) void leaf_box_kernel(const float4* __restrict_
         const unsigned ly = wave_min_u32(v ? ordf(p.y) : SENT), hy = wave_max_u32(v ? ordf(p.y) : 0u);
         const unsigned lz = wave_min_u32(v ? ordf(p.z) : SENT), hz = wave_max_u32(v ? ordf(p.z) : 0u);
         if (lane == 0) {
-            nlo[P + leaf] = make_float4(unordf(lx), unordf(ly), unordf(lz), 0.f);
-            nhi[P + leaf] = make_float4(unordf(hx), unordf(hy), unordf(hz), 0.f);
+            // w words: the leaf's first point and count, so a traversal that tests the leaf's box
+            // has its point range in the same load (no dependent leaf_start round before the points)
+            const unsigned b0 = leaf_start[leaf], cnt = leaf_start[leaf + 1] - b0;
+            nlo[P + leaf] = make_float4(unordf(lx), unordf(ly), unordf(lz), __uint_as_float(b0));
+            nhi[P + leaf] = make_float4(unordf(hx), unordf(hy), unordf(hz), __uint_as_float(cnt));
         }
     }
 }
@@ -428,6 +434,10 @@ __global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, 
 // profiles/ab_r4_tree_waves.txt -- and is not used.)
 template <int KT, int M>
 __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
+    // output pointers: the launch's, or read from device slots (graph replays of a batched
+    // stream of clouds); locals, so the kernel argument block stays read-only
+    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
+    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
     constexpr int KM = KT + M + 1;  // + 1: the query itself enters its own list at d2 = 0
     __shared__ float4 s_pts[4][kTreeLeaf];
     __shared__ int s_visit[4][kMaxVisit];  // first point of each visited leaf
@@ -455,10 +465,9 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
     int nv = 0;
     bool over = false;
 
-    // stage leaf lf in the wave's LDS slice and stream its points to every lane (broadcast reads)
-    auto visit = [&](int lf) __attribute__((always_inline)) {
-        const int b = (int)a.leaf_start[lf];
-        const int cnt = (int)a.leaf_start[lf + 1] - b;
+    // stage the leaf of points [b, b + cnt) in the wave's LDS slice and stream its points to every
+    // lane (broadcast reads)
+    auto visit_range = [&](int b, int cnt) __attribute__((always_inline)) {
         if (lane < cnt) buf[lane] = a.pts[KN_IDX(b + lane, a.n, 402)];
         if (lane == 0) vis[nv] = b;
         __builtin_amdgcn_wave_barrier();
@@ -470,6 +479,10 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
         }
         ++nv;
         __builtin_amdgcn_wave_barrier();
+    };
+    auto visit = [&](int lf) __attribute__((always_inline)) {
+        const int b = (int)a.leaf_start[lf];
+        visit_range(b, (int)a.leaf_start[lf + 1] - b);
     };
     // the leaves holding the wave's own 64 points first: every lane starts the traversal with a
     // bound from ~64 nearby candidates (small leaves alone leave the early bounds loose, and a
@@ -501,12 +514,15 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
             // the same subtrees one dependent box load sooner (900K K=16: clustered 1.578 ->
             // 1.453 ms/step, surfaces 0.972 -> 0.930, the same leaf visits and rows;
             // profiles/ab_r4_tree_pop_retest.txt)
-            const float bd = box_d2(qx, qy, qz, a.nlo[node], a.nhi[node]);
+            const float4 blo = a.nlo[node], bhi = a.nhi[node];
+            const float bd = box_d2(qx, qy, qz, blo, bhi);
             if (!__builtin_amdgcn_ballot_w64(live && bd < INFINITY && bd * kShrink <= ub)) continue;
             const int lf = node - a.P;
             if (lf >= l0 && lf <= l1) continue;  // visited first
             if (nv == kMaxVisit) { over = true; break; }
-            visit(lf);
+            // the point range rides in the box's w words (leaf_box_kernel)
+            visit_range(__builtin_amdgcn_readfirstlane((int)__float_as_uint(blo.w)),
+                        __builtin_amdgcn_readfirstlane((int)__float_as_uint(bhi.w)));
             continue;
         }
         const int c0 = 2 * node;
@@ -665,8 +681,8 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
                 const size_t o = KN_IDX((size_t)row * (size_t)k + j, (size_t)a.n_queries * k, 406);
                 const unsigned long long v = has_self ? e[j + 1] : e[j];
                 const bool empty = v == ~0ull;
-                a.out_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
-                if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
+                o_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
+                if (o_dist) o_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
             }
         }
     }
@@ -677,6 +693,10 @@ __global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
 // ballot-compacted into the wave's LDS buffer, which is bitonic-sorted by (d2, id) and cut to K
 // (thr = K-th distance) when it could overflow -- the semantics of query.hip's exact kernel.
 __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
+    // output pointers: the launch's, or read from device slots (graph replays of a batched
+    // stream of clouds); locals, so the kernel argument block stays read-only
+    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
+    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
     __shared__ unsigned long long s_buf[4][kTCap];
     __shared__ int s_stack[4][kStack];
     __shared__ float s_sbd[4][kStack];  // box distance of each stacked node (computed by its parent)
@@ -842,8 +862,8 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
             const size_t o = KN_IDX((size_t)row * (size_t)k + j, (size_t)a.n_queries * k, 415);
             const unsigned long long v = (j < cnt) ? buf[j] : ~0ull;
             const bool empty = (v == ~0ull);
-            a.out_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
-            if (a.out_dist) a.out_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
+            o_idx[o] = empty ? SENT : out_id(a, (unsigned)v);
+            if (o_dist) o_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -975,6 +995,7 @@ hipError_t launch_tree_query(const TreeView& t, const TreeQuery& q, hipStream_t 
     a.Lp = t.info; a.n = t.n; a.P = t.P; a.logP = tree_log2(t.P);
     a.k = q.k; a.n_queries = q.n_queries; a.q_lo = 0; a.id_map = q.id_map;
     a.row_of = q.row_of; a.src = t.vals; a.out_idx = q.out_idx; a.out_dist = q.out_dist; a.counters = q.counters;
+    a.out_idx_ref = q.out_idx_ref; a.out_dist_ref = q.out_dist_ref;
     a.flags = q.flags;
     constexpr int M = 2;
     const unsigned grid = cdiv(cdiv(t.n, 64), 4);

@@ -250,6 +250,10 @@ QueryBuffers Engine::query_buffers() const {
     for (int a = 0; a < 3; ++a) { q.complete.lo[a] = -INFINITY; q.complete.hi[a] = INFINITY; }
     q.out_idx = out_idx_;
     q.out_dist = out_dist_;
+    if (out_ref_slot_ >= 0) {  // a batch step: output pointers from the table (stream_batch)
+        q.out_idx_ref = reinterpret_cast<unsigned* const*>(tab_ + kBatchMax + out_ref_slot_);
+        q.out_dist_ref = reinterpret_cast<float* const*>(tab_ + 2 * kBatchMax + out_ref_slot_);
+    }
     q.fallback_list = fallback_;
     q.counters = counters_;
     for (int a = 0; a < 3; ++a) q.tile[a] = ap_.tile[a];
@@ -330,6 +334,10 @@ kn_status Engine::tree_query_async() {
     q.n_queries = n_;
     q.out_idx = out_idx_;
     q.out_dist = out_dist_;
+    if (out_ref_slot_ >= 0) {
+        q.out_idx_ref = reinterpret_cast<unsigned* const*>(tab_ + kBatchMax + out_ref_slot_);
+        q.out_dist_ref = reinterpret_cast<float* const*>(tab_ + 2 * kBatchMax + out_ref_slot_);
+    }
     q.counters = counters_;
     return check(launch_tree_query(t, q, stream_), "tree query");
 }
@@ -578,6 +586,7 @@ void Engine::view_set(int s) {
 }
 
 void Engine::drop_pipeline(bool keep_grid) {
+    drop_batch();   // batch graphs are captured against both sets
     pipe_.reset();  // waits for both streams, destroys the stage graphs
     if (bstream_) {
         StreamSet ss;
@@ -814,6 +823,139 @@ kn_status Engine::stream_step(const float* d_pts, const float* d_next) {
     view_set(pipe_.last_set());
     other_stale_ = true;
     solved_ = true;
+    stored_valid_ = points3_valid_ = false;
+    return KN_OK;
+}
+
+void Engine::drop_batch() {
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    if (bstream_) (void)hipStreamSynchronize(bstream_);
+    for (auto& kv : bgraphs_) (void)hipGraphExecDestroy(kv.second);
+    bgraphs_.clear();
+    for (auto e : bev_) (void)hipEventDestroy(e);
+    bev_.clear();
+    if (tab_) { dfree(tab_); tab_ = nullptr; }
+}
+
+// Steps 0..L-1 of a batch in one graph, sets alternating (step j: set j & 1). Build stream: copy-in
+// + build of step 0; then per step j: (epilogue of step j-1 after its query) and the copy-in +
+// build of step j+1 into the set step j-1 released. Main stream: query of step j after its build.
+kn_status Engine::batch_graph(int L, hipGraphExec_t* out) {
+    auto it = bgraphs_.find(L);
+    if (it != bgraphs_.end()) { *out = it->second; return KN_OK; }
+    while (bev_.size() < 2 * (size_t)L + 2) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(KN_ERR_DEVICE, "hipEventCreate");
+        bev_.push_back(e);
+    }
+    hipEvent_t fork = bev_[0], join = bev_[1];
+    hipEvent_t* eb = bev_.data() + 2;      // step j built
+    hipEvent_t* eq = bev_.data() + 2 + L;  // step j queried
+    const bool epi = !use_tree_ && exact_epilogue(cfg_.k);
+    const size_t nf = (size_t)n_ * 3;
+    hipError_t e = hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) return check(e, "batch capture");
+    kn_status st = KN_OK;
+    auto H = [&](hipError_t r) { if (st == KN_OK && r != hipSuccess) st = check(r, "batch capture"); };
+    auto S = [&](kn_status r) { if (st == KN_OK) st = r; };
+    auto build = [&](int j) {
+        const int s = j & 1;
+        H(launch_copy_from_ref(reinterpret_cast<const float* const*>(tab_ + j), set_[s].points, nf, bstream_));
+        if (st == KN_OK) S(stage_build(s, bstream_));
+        H(hipEventRecord(eb[j], bstream_));
+    };
+    auto exact = [&](int j) {
+        out_ref_slot_ = j;
+        S(stage_exact(j & 1, bstream_));
+        out_ref_slot_ = -1;
+    };
+    H(hipEventRecord(fork, stream_));
+    H(hipStreamWaitEvent(bstream_, fork, 0));
+    build(0);
+    for (int j = 0; j < L && st == KN_OK; ++j) {
+        H(hipStreamWaitEvent(stream_, eb[j], 0));
+        out_ref_slot_ = j;
+        if (st == KN_OK) S(stage_query(j & 1, stream_));
+        out_ref_slot_ = -1;
+        H(hipEventRecord(eq[j], stream_));
+        if (j >= 1) {
+            H(hipStreamWaitEvent(bstream_, eq[j - 1], 0));
+            if (epi && st == KN_OK) exact(j - 1);
+        }
+        if (j + 1 < L && st == KN_OK) build(j + 1);
+    }
+    if (epi && st == KN_OK) {
+        H(hipStreamWaitEvent(bstream_, eq[L - 1], 0));
+        exact(L - 1);
+    }
+    H(hipEventRecord(join, bstream_));
+    H(hipStreamWaitEvent(stream_, join, 0));
+    hipGraph_t g = nullptr;
+    const hipError_t ee = hipStreamEndCapture(stream_, &g);
+    if (st != KN_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return st;
+    }
+    if ((st = check(ee, "batch end capture")) != KN_OK) return st;
+    hipGraphExec_t x = nullptr;
+    e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if ((st = check(e, "batch graph instantiate")) != KN_OK) return st;
+    bgraphs_[L] = x;
+    *out = x;
+    return KN_OK;
+}
+
+kn_status Engine::stream_batch(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist) {
+    if (!built_) return fail(KN_ERR_STATE, "stream_batch() before prepare()");
+    if (m < 0 || (m > 0 && (!d_in || !d_idx))) return fail(KN_ERR_INVALID_ARGUMENT, "stream_batch: null tables");
+    for (int j = 0; j < m; ++j)
+        if ((n_ > 0 && !d_in[j]) || !d_idx[j] || (d_dist && !d_dist[j]))
+            return fail(KN_ERR_INVALID_ARGUMENT, "stream_batch: null pointer in a table");
+    if (m == 0) return KN_OK;
+    kn_status st;
+    if ((st = ensure_pipeline()) != KN_OK) return st;
+    if (!tab_ && (st = check(dmalloc(reinterpret_cast<void**>(&tab_), 3 * kBatchMax * sizeof(void*)), "hipMalloc(batch table)")) != KN_OK)
+        return st;
+    // everything the pipeline enqueued (a primed build, an epilogue) is done before the batch
+    // graphs reuse both sets: the side stream's tail joins the main stream
+    if ((st = check(pipe_.unprime(), "pipeline")) != KN_OK) return st;
+    // chunks of power-of-two lengths (largest first, <= kBatchMax): six graphs serve any m, all
+    // captured at the first call, so a later (timed) call never captures. Each chunk starts with
+    // its first build not overlapped by a query (the chunk's graph follows the previous one).
+    if (bgraphs_.empty()) {
+        for (int L = 1; L <= kBatchMax; L *= 2) {
+            hipGraphExec_t g = nullptr;
+            if ((st = batch_graph(L, &g)) != KN_OK) return st;
+        }
+    }
+    int last_L = 1;
+    for (int c0 = 0; c0 < m;) {
+        int L = kBatchMax;
+        while (L > m - c0) L >>= 1;
+        hipGraphExec_t g = nullptr;
+        if ((st = batch_graph(L, &g)) != KN_OK) return st;
+        void* tab[3 * kBatchMax];
+        for (int j = 0; j < 3 * kBatchMax; ++j) tab[j] = nullptr;
+        for (int j = 0; j < L; ++j) {
+            tab[j] = const_cast<float*>(d_in[c0 + j]);
+            tab[kBatchMax + j] = d_idx[c0 + j];
+            tab[2 * kBatchMax + j] = d_dist ? d_dist[c0 + j] : nullptr;
+        }
+        if ((st = check(launch_set_ptr_table(tab, 3 * kBatchMax, tab_, stream_), "batch table")) != KN_OK) return st;
+        if ((st = check(hipGraphLaunch(g, stream_), "batch graph launch")) != KN_OK) return st;
+        c0 += L;
+        last_L = L;
+    }
+    // the last step's grid is the engine's grid (stats, stored-space views); its rows went to the
+    // caller, so the engine's own results are stale
+    view_set((last_L - 1) & 1);
+    // later pipeline work on the build stream (resident or stream steps) waits for the batch
+    if ((st = check(hipEventRecord(bev_[0], stream_), "batch event")) != KN_OK) return st;
+    if ((st = check(hipStreamWaitEvent(bstream_, bev_[0], 0), "batch event")) != KN_OK) return st;
+    other_stale_ = true;
+    stream_mode_ = true;
+    solved_ = false;
     stored_valid_ = points3_valid_ = false;
     return KN_OK;
 }

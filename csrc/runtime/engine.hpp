@@ -73,6 +73,17 @@ public:
     // (may be null) is the next step's cloud, binned now, while this step queries. The results
     // (original space) and the grid are this step's until the next call; sync() waits.
     kn_status stream_step(const float* d_pts, const float* d_next);
+    // A batch of m distinct clouds of n points each (device pointers; the reference's repeated
+    // kn_prepare + kn_solve on new points, knearests.cu:235-392): step j bins d_in[j] and writes its
+    // original-space rows to d_idx[j] (n x K) and d_dist[j] (n x K, may be null). Steps run through
+    // graphs of up to kBatchMax steps, captured once per batch length: each replays its steps'
+    // copy-in + build on the build stream and queries on the main stream, step j+1's build under
+    // step j's queries (as the resident unrolled pipeline); the steps' pointers come from a device
+    // table written by a one-block kernel before each launch. Asynchronous (sync() waits). The
+    // engine's own result buffers are not written (results() after a batch is an error); the
+    // grid of the last step stays (stats, stored-space views of the last cloud).
+    static constexpr int kBatchMax = kPtrTableMax / 3;
+    kn_status stream_batch(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist);
     kn_status sync();  // both streams
     // Device-to-device copy of the original-space results into caller buffers.
     kn_status copy_results(unsigned* d_idx, float* d_dist);
@@ -154,6 +165,15 @@ private:
     hipStream_t bstream_ = nullptr;
     hipEvent_t pev_[4] = {nullptr, nullptr, nullptr, nullptr};  // the side stream's pooled events
     Pipeline pipe_;
+    // batched streams (stream_batch): device pointer table {in, idx, dist} x kBatchMax, graphs by
+    // batch length, capture events; out_ref_slot_ >= 0 while a batch step is captured (its
+    // query / exact / tree launches read their output pointers from the table slot)
+    void** tab_ = nullptr;
+    std::unordered_map<int, hipGraphExec_t> bgraphs_;
+    std::vector<hipEvent_t> bev_;
+    int out_ref_slot_ = -1;
+    kn_status batch_graph(int L, hipGraphExec_t* out);
+    void drop_batch();
     size_t arena_used_ = 0;  // bytes of arena_ carved by allocate() (arena2_ has the same carve)
 
     EngineConfig cfg_;

@@ -1150,6 +1150,36 @@ public:
         KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
         TORCH_CHECK(e_->stream_step(points.data_ptr<float>(), np) == KN_OK, e_->error());
     }
+    // a batch of distinct clouds (kn::Engine::stream_batch): points[j] (N, 3) float32 GPU ->
+    // idx[j] (N, K) int32 and d2[j] (N, K) float32 (optional) in original space. Asynchronous on
+    // the engine's streams: call sync() before reading the outputs.
+    void stream_batch(std::vector<torch::Tensor> points, std::vector<torch::Tensor> idx,
+                      c10::optional<std::vector<torch::Tensor>> d2) {
+        const size_t m = points.size();
+        TORCH_CHECK(idx.size() == m && (!d2.has_value() || d2->size() == m), "one output per cloud");
+        std::vector<const float*> in(m);
+        std::vector<unsigned*> oi(m);
+        std::vector<float*> od(m);
+        for (size_t j = 0; j < m; ++j) {
+            check_points(points[j], true);
+            TORCH_CHECK(points[j].size(0) == e_->n(), "stream_batch: every cloud must have the prepared N points");
+            TORCH_CHECK(idx[j].is_cuda() && idx[j].scalar_type() == torch::kInt32 && idx[j].is_contiguous() &&
+                            idx[j].numel() == (int64_t)e_->n() * e_->k(), "idx[j]: contiguous (N, K) int32 GPU");
+            in[j] = points[j].data_ptr<float>();
+            oi[j] = reinterpret_cast<unsigned*>(idx[j].data_ptr<int>());
+            if (d2.has_value()) {
+                const auto& t = (*d2)[j];
+                TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous() &&
+                                t.numel() == (int64_t)e_->n() * e_->k(), "d2[j]: contiguous (N, K) float32 GPU");
+                od[j] = t.data_ptr<float>();
+            }
+        }
+        if (m == 0) return;
+        const c10::DeviceGuard guard(points[0].device());
+        KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
+        TORCH_CHECK(e_->stream_batch((int)m, in.data(), oi.data(), d2.has_value() ? od.data() : nullptr) == KN_OK,
+                    e_->error());
+    }
     // stored -> original permutation of the engine's current grid (host int32)
     torch::Tensor permutation() {
         unsigned* p = e_->get_permutation();
@@ -1703,6 +1733,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
         .def("launch_pipelined", &PyEngine::launch_pipelined, py::arg("iters") = 1, py::arg("unroll") = -1)
         .def("stream_step", &PyEngine::stream_step, py::arg("points"), py::arg("next") = py::none())
+        .def("stream_batch", &PyEngine::stream_batch, py::arg("points"), py::arg("idx"), py::arg("d2") = py::none())
         .def("get_permutation", &PyEngine::permutation)
         .def("sync", &PyEngine::sync)
         .def("results", &PyEngine::results)

@@ -16,8 +16,9 @@ plan = ops.Plan.auto(n, k)
 s, cs, perm, geom = A.build(pts, plan.dims, True, None)
 inf = float("inf")
 args = lambda: (s, cs, geom, plan.dims, k, n, None, [-inf, -inf, -inf, inf, inf, inf], plan.tile, plan.halo, plan.lds_capacity, True, True, 0)
-ref = A.query(*args())
-out = B.query(*args())
+kw = {"xsub": plan.xsub}  # the plan's x sub-cells (dims[0] and tile[0] count sub-cells)
+ref = A.query(*args(), **kw)
+out = B.query(*args(), **kw)
 torch.cuda.synchronize()
 print("identical:", torch.equal(ref[0], out[0]) and torch.equal(ref[1], out[1]), flush=True)
 if "chk" in var:
@@ -25,9 +26,11 @@ if "chk" in var:
 ta, tb = [], []
 ev = lambda: torch.cuda.Event(enable_timing=True)
 for r in range(rounds):
-    for mod, acc in ((A, ta), (B, tb)):
+    # alternate which variant runs first in a round (no position bias)
+    order = ((A, ta), (B, tb)) if r % 2 == 0 else ((B, tb), (A, ta))
+    for mod, acc in order:
         e0, e1 = ev(), ev()
-        e0.record(); mod.query(*args()); e1.record(); e1.synchronize()
+        e0.record(); mod.query(*args(), **kw); e1.record(); e1.synchronize()
         acc.append(e0.elapsed_time(e1))
 ta.sort(); tb.sort()
 print(f"baseline median {ta[len(ta)//2]:.4f} min {ta[0]:.4f} | {var} median {tb[len(tb)//2]:.4f} min {tb[0]:.4f} ms", flush=True)

@@ -221,23 +221,64 @@ def test_engine_stream_of_clouds(cuda, unroll):
     _check(clouds[-1], idx, d2, k)
 
 
+@pytest.mark.parametrize("k,gen", [(16, "uniform"), (50, "uniform"), (16, "clustered")])
+def test_engine_stream_batch(cuda, k, gen):
+    """kn::Engine::stream_batch: a batch of DISTINCT clouds through one graph per power-of-two
+    chunk (copy-in + build on the build stream, queries on the main stream, pointer table
+    written per launch); every step's rows, written straight into the caller's buffers, equal
+    the kd-tree oracle's on its own cloud. K=50 runs the exact finish as the side-stream epilogue,
+    clustered clouds the tree path. 11 steps = chunks of 8, 2 and 1; a resident pipelined launch
+    and a stream step afterwards still solve their clouds."""
+    from cuda_knearests_amd._ext import load
+    from cuda_knearests_amd.utils import clustered_cloud
+
+    C = load()
+    n = 30000
+    mk = uniform_cloud if gen == "uniform" else clustered_cloud
+    clouds = [mk(n, seed=700 + j).to(cuda) for j in range(11)]
+    clouds[4] = (clouds[4] * 0.25 + 300.0).contiguous()  # another domain: the bbox is per build
+    e = C.Engine(k)
+    e.prepare(clouds[0])
+    e.launch_pipelined(4, 2)  # a primed resident pipeline first
+    idx = [torch.empty(n, k, dtype=torch.int32, device=cuda) for _ in clouds]
+    d2 = [torch.empty(n, k, dtype=torch.float32, device=cuda) for _ in clouds]
+    e.stream_batch(clouds, idx, d2)
+    e.sync()
+    for j, c in enumerate(clouds):
+        _check(c, idx[j], d2[j], k)
+    # a second batch reuses the captured graphs (and the same output buffers)
+    e.stream_batch(clouds[::-1][:3], idx[:3], d2[:3])
+    e.sync()
+    for j, c in enumerate(clouds[::-1][:3]):
+        _check(c, idx[j], d2[j], k)
+    e.launch_pipelined(2, 0)  # the resident cloud after a batch: the last batch cloud
+    e.sync()
+    i2, e2 = e.results(cuda)
+    _check(clouds[::-1][2], i2, e2, k)
+    e.stream_step(clouds[5], None)
+    e.sync()
+    i3, e3 = e.results(cuda)
+    _check(clouds[5], i3, e3, k)
+
+
 def test_tree_long_axis(cuda):
     """Tree path on a grid with more than 1,024 cells along one axis (the cells'
-    Morton codes overflowed 32 bits past 128 bricks): a uniform 1000 x 8 x 8 slab, forced onto the
-    tree, equals the oracle."""
+    Morton codes were u32 and overflowed past 128 bricks per axis). Multi-GPU ranks build such
+    grids from their box extents (slab-shaped shares); here a uniform 1000 x 8 x 8 slab is binned
+    into a 2048 x 8 x 8 grid and queried through the tree: rows equal the oracle's."""
     from cuda_knearests_amd._ext import load
 
     C = load()
     k = 16
-    n = 400000
+    n = 120000
     g = torch.Generator().manual_seed(17)
     p = (torch.rand(n, 3, generator=g) * torch.tensor([1000.0, 8.0, 8.0])).contiguous()
-    e = C.Engine(k, algo=2)
-    e.prepare(p.to(cuda))
-    e.solve()
-    info = e.info()
-    assert info["algo"] == "tree" and max(info["dims"]) > 1024, info
-    idx, d2 = e.results(cuda)
+    dims = [2048, 8, 8]
+    s, cs, perm, geom = C.build(p.to(cuda), dims, True, None)
+    ws, nodes, leaves = C.tree_build(s, cs, geom, dims, True)
+    assert leaves > 0
+    idx, d2, counters = C.tree_query(ws, nodes, dims, n, k, n)
+    torch.cuda.synchronize()
     _check(p, idx, d2, k)
 
 
