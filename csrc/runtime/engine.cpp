@@ -745,7 +745,16 @@ kn_status Engine::ensure_pipeline() {
         Pipeline::Stage x;
         if (!use_tree_ && exact_epilogue(cfg_.k))  // the tree query finishes its own exact-path queries
             x = [this](int s, hipStream_t st2) { return stage_exact(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
-        if ((st = check(pipe_.init(stream_, bstream_, b, q, x), "pipeline init")) != KN_OK) return st;
+        // Two query streams (default; KN_PIPE_QSTREAMS=1: one): odd sets' queries on a second
+        // stream, so step i+1's queries start as soon as its build is done instead of after step
+        // i's last workgroup and the kernel boundary (~15 us per step inside a 10-step graph,
+        // profiles/r4_pipe_unroll.txt). 900K K=16, interleaved processes on one box: 200 steps
+        // 0.2894 -> 0.2756 ms, the driver's 20 / 5 0.3080 -> 0.3048 (profiles/r5_qstreams.txt)
+        static const int qstreams = [] {
+            const char* v = std::getenv("KN_PIPE_QSTREAMS");
+            return v ? std::atoi(v) : 2;
+        }();
+        if ((st = check(pipe_.init(stream_, bstream_, b, q, x, false, qstreams), "pipeline init")) != KN_OK) return st;
     }
     return KN_OK;
 }

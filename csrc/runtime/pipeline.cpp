@@ -22,7 +22,8 @@ void destroy(hipEvent_t& e) {
 }
 }  // namespace
 
-hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r, bool capture_from_side) {
+hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r, bool capture_from_side,
+                          int query_streams) {
     reset();
     main_ = main;
     side_ = side;
@@ -39,11 +40,7 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
     }
     KN_TRY(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming));
     KN_TRY(hipEventRecord(last_done_, main_));
-    static const int qstreams = [] {
-        const char* v = std::getenv("KN_PIPE_QSTREAMS");
-        return v ? std::atoi(v) : 1;
-    }();
-    if (qstreams >= 2) {
+    if (query_streams >= 2) {
         int lo = 0, hi = 0;
         KN_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
         (void)hi;
@@ -172,9 +169,10 @@ hipError_t Pipeline::enqueue_build(int s) {
 }
 
 hipError_t Pipeline::enqueue_query(int s) {
-    KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
-    KN_TRY(eager_ ? q_(s, main_) : hipGraphLaunch(gQ_[s], main_));
-    return hipEventRecord(evQ_[s], main_);
+    hipStream_t qs = qstream(s);
+    KN_TRY(hipStreamWaitEvent(qs, evB_[s], 0));
+    KN_TRY(eager_ ? q_(s, qs) : hipGraphLaunch(gQ_[s], qs));
+    return hipEventRecord(evQ_[s], qs);
 }
 
 hipError_t Pipeline::enqueue_epilogue(int s) {
@@ -198,6 +196,7 @@ void Pipeline::set_eager(bool eager) {
     if (eager == eager_) return;
     if (main_) (void)hipStreamSynchronize(main_);
     if (side_) (void)hipStreamSynchronize(side_);
+    if (aux_) (void)hipStreamSynchronize(aux_);
     // a failed capture may have left a stream in capture mode: end it (the graph is dropped)
     for (hipStream_t st : {main_, side_}) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -224,7 +223,14 @@ hipError_t Pipeline::flush() {
         KN_TRY(enqueue_epilogue(last_set_));
         return hipEventRecord(last_done_, side_);
     }
-    if (!r_ && last_set_ >= 0) return hipEventRecord(last_done_, main_);
+    if (!r_ && last_set_ >= 0) {
+        if (aux_) {
+            // both query streams' last queries (they do not depend on each other) before last_done
+            KN_TRY(hipEventRecord(evQ_[last_set_ ^ 1], qstream(last_set_ ^ 1)));
+            KN_TRY(hipStreamWaitEvent(qstream(last_set_), evQ_[last_set_ ^ 1], 0));
+        }
+        return hipEventRecord(last_done_, qstream(last_set_));
+    }
     return hipSuccess;
 }
 
@@ -240,6 +246,12 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
     if (!main_) return hipErrorNotInitialized;
     KN_TRY(fallback_if(graphs()));
     if (unroll < 2 || (unroll & 1) || eager_) unroll = 0;
+    // Two query streams run per-step graphs: a graph whose queries alternate between two streams
+    // crashes the HIP runtime from 4 unrolled steps on (ROCm 7.0: unbounded recursion in
+    // libamdhip64 while capturing, profiles/r5_qstreams.txt), and 2-step graphs measured slower
+    // than per-step launches (900K K=16, 200 steps: 0.2828 vs 0.2756 ms; one query stream with
+    // 10-step graphs 0.2894)
+    if (aux_) unroll = 0;
     if (unroll) {
         // both start parities up front (also by a call of fewer steps, e.g. a warm-up): a capture
         // never lands inside a later (timed) call
@@ -263,6 +275,12 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
             // writes set s^1, released by the last query (main, stream order) and R (side)
             KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
             if (r_) KN_TRY(hipStreamWaitEvent(main_, evF_[s ^ 1], 0));
+            if (aux_) {
+                // a per-step query of set s^1 may still run on the second query stream: the graph's
+                // first build writes that set
+                KN_TRY(hipEventRecord(evQ_[s ^ 1], qstream(s ^ 1)));
+                KN_TRY(hipStreamWaitEvent(main_, evQ_[s ^ 1], 0));
+            }
             KN_TRY(hipGraphLaunch(gU_[s], main_));
             // U is even: the last query used set s^1, the primed build (B(next)) wrote set s.
             // Every per-set event is re-recorded after the graph: its queries read both sets and
@@ -329,6 +347,7 @@ hipError_t Pipeline::step_with(const Stage& pre, const Stage* next_pre) {
 
 hipError_t Pipeline::sync() {
     if (!main_) return hipSuccess;
+    if (aux_) KN_TRY(hipStreamSynchronize(aux_));
     KN_TRY(hipStreamSynchronize(side_));
     return hipStreamSynchronize(main_);
 }

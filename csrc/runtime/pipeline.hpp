@@ -39,8 +39,11 @@ public:
     // capture_from_side: unrolled captures start on the side stream (the main stream joins it):
     // RCCL point-to-point calls in the build stage crash when captured on a JOINED stream
     // (measured on MI355X, RCCL 2.26.6), so the stages with collectives must be on the origin.
+    // query_streams = 2: the queries of odd sets go to a second (pipeline-owned) stream, so a
+    // step's queries need not wait for the previous step's last workgroups: each depends only on
+    // its own build (sets, counters and outputs are per set)
     hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage(),
-                    bool capture_from_side = false);
+                    bool capture_from_side = false, int query_streams = 1);
     bool ready() const { return main_ != nullptr; }
     // Enqueue `iters` resident-mode steps; unroll >= 2 (even): whole groups of `unroll` steps go
     // through one unrolled graph, the rest through per-step graphs. keep_primed = false: the call
@@ -83,7 +86,8 @@ private:
     hipError_t unrolled(int start_set, int U);
     hipError_t capture(const Stage& st, int set, hipGraphExec_t* out);
     hipError_t enqueue_build(int set);   // side: wait set free, B(set), record evB
-    hipError_t enqueue_query(int set);   // main: wait evB, Q(set), record evQ
+    hipError_t enqueue_query(int set);   // query stream of the set: wait evB, Q(set), record evQ
+    hipStream_t qstream(int set) const { return (aux_ && (set & 1)) ? aux_ : main_; }
     hipError_t enqueue_epilogue(int set);
 
     hipStream_t main_ = nullptr, side_ = nullptr;
