@@ -297,7 +297,14 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     // KN_DIST_CAPTURE_JOINED=1 (diagnostics): start unrolled captures on the main stream, so the
     // RCCL calls of the build stage are captured on a JOINED stream (the round-4 segfault)
     const char* joined = std::getenv("KN_DIST_CAPTURE_JOINED");
-    if (pipe_.init(main_, side_, b, q, r, !(joined && joined[0] == '1')) != hipSuccess) { fail("pipeline init"); return; }
+    // KN_DIST_QSTREAMS: query streams of the rank pipeline (pipeline.hpp; 2 = odd sets' queries on
+    // a second stream, per-step launches)
+    const char* qsv = std::getenv("KN_DIST_QSTREAMS");
+    const int qstreams = qsv ? std::atoi(qsv) : 1;
+    if (pipe_.init(main_, side_, b, q, r, !(joined && joined[0] == '1'), qstreams) != hipSuccess) {
+        fail("pipeline init");
+        return;
+    }
     // RCCL stages run eagerly until prepare_graphs() captured them (set_eager(false) below)
     pipe_.set_eager(true);
     ok_ = true;
