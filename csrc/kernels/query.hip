@@ -80,6 +80,7 @@ struct TileArgs {
     int cap;        // LDS point capacity (multiple of 64)
     int slot_bits;  // log2(cap)
     int ntx, nty, ntz;
+    int tblock;     // tile blocking of the workgroup order (tile_coords; KN_TILE_BLOCK)
     int cb_stride;  // max staged cells per row + 1
     int max_rows;
     int flags;      // kQueryForceRescan: every query takes the exact re-scan (tests)
@@ -238,6 +239,36 @@ __device__ unsigned long long g_phase[kPhN];
 #define KN_PH_FLUSH() ((void)0)
 #endif
 
+// Tile of a workgroup. xcd_remap gives each XCD a contiguous run of tile numbers; with B > 1 the
+// numbers run through B x B x B blocks of tiles (x-fastest blocks, x-fastest inside a block; edge
+// blocks are partial), so the ~128 workgroups an XCD holds at once form compact 3-D groups whose
+// halos overlap in that XCD's L2 -- x-fastest order makes them a 1-2 tile-row slab, whose z halos
+// are fetched again by the next slab (10M K=32: FETCH_SIZE 1.43x the sorted array, SQ_WAIT_ANY
+// 59 % of wave cycles vs 34 % at 900K; profiles/pmc_r5_10m_k32.txt). A bijection of [0, ntiles).
+__device__ __forceinline__ void tile_coords(int lin, int ntx, int nty, int ntz, int B, int& tx, int& ty, int& tz) {
+    if (B <= 1) {
+        tx = lin % ntx;
+        ty = (lin / ntx) % nty;
+        tz = lin / (ntx * nty);
+        return;
+    }
+    const int slab = B * nty * ntx;             // tiles of a full z-slab of blocks
+    const int bz = min(lin / slab, (ntz - 1) / B);
+    int r = lin - bz * slab;
+    const int hz = min(B, ntz - bz * B);        // this slab's height
+    const int row = B * ntx * hz;               // tiles of a full y-row of blocks in the slab
+    const int by = min(r / row, (nty - 1) / B);
+    r -= by * row;
+    const int hy = min(B, nty - by * B);
+    const int blk = B * hy * hz;                // tiles of a full block in the row
+    const int bx = min(r / blk, (ntx - 1) / B);
+    r -= bx * blk;
+    const int hx = min(B, ntx - bx * B);
+    tx = bx * B + r % hx;
+    ty = by * B + (r / hx) % hy;
+    tz = bz * B + r / (hx * hy);
+}
+
 // LANE = false: wave-uniform candidate stream over the union of the chunk's needs (LDS
 // broadcast reads). LANE = true ("lane walk"): each lane walks ITS OWN rows of the staged
 // block -- centre-out over the (2H+1)^2 row offsets around its cell, x-range cut by its own
@@ -276,8 +307,8 @@ __global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
 
     const GridGeom g = *a.geom;
     const int ntiles = a.ntx * a.nty * a.ntz;
-    const int tile = xcd_remap(blockIdx.x, ntiles);
-    const int tx = tile % a.ntx, ty = (tile / a.ntx) % a.nty, tz = tile / (a.ntx * a.nty);
+    int tx, ty, tz;
+    tile_coords(xcd_remap(blockIdx.x, ntiles), a.ntx, a.nty, a.ntz, a.tblock, tx, ty, tz);
     const int tx0 = tx * a.TX, ty0 = ty * a.TY, tz0 = tz * a.TZ;
     const int tx1 = min(a.X, tx0 + a.TX), ty1 = min(a.Y, ty0 + a.TY), tz1 = min(a.Z, tz0 + a.TZ);
     // Staged block: the tile + H rings, clipped to the grid. With the whole-block lane walk
@@ -1781,6 +1812,15 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         while ((1 << sb) < q.lds_capacity) ++sb;
         a.slot_bits = sb;
         a.ntx = (X + a.TX - 1) / a.TX; a.nty = (Y + a.TY - 1) / a.TY; a.ntz = (Z + a.TZ - 1) / a.TZ;
+        // workgroup order in blocks of tiles (tile_coords): 900K / 10M uniform, 200 / 30 / 100 steps,
+        // two interleaved passes (profiles/ab_r5_tile_block.txt): 10M K=32 6.56 -> 6.37 ms (B 2 or
+        // 4), K=50 0.777 -> 0.759 (B 4), K=16 within +-0.5 % for B 2 (+1 % for B 4).
+        // KN_TILE_BLOCK=B overrides (1 = plain x-fastest order)
+        static const int tblock_env = [] {
+            const char* v = std::getenv("KN_TILE_BLOCK");
+            return v ? std::max(1, std::atoi(v)) : 0;
+        }();
+        a.tblock = tblock_env ? tblock_env : (KT > 16 ? 4 : 2);
         a.cb_stride = std::min(X, a.TX + 2 * a.Hx) + 1;
         a.max_rows = std::min(Y, a.TY + 2 * a.H) * std::min(Z, a.TZ + 2 * a.H);
         const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
