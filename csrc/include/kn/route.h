@@ -189,6 +189,8 @@ hipError_t launch_steady_flag_local(const float* pts, int n, unsigned* words, co
 // Sticky step flag (pipelined distributed steps, after the flag's all-reduce): sticky =
 // max(sticky, flag), also stored to host_flag (device pointer to pinned host memory).
 hipError_t launch_flag_sink(const int* flag, int* sticky, int* host_flag, hipStream_t s);
+// *pending = max(*pending, *flag), atomically (steps on different streams accumulate into one word)
+hipError_t launch_flag_accum(const int* flag, int* pending, hipStream_t s);
 hipError_t launch_steady_flag(const double* local, const double* planned_meta, const int* totals,
                               const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                               hipStream_t s);

@@ -866,6 +866,14 @@ hipError_t launch_flag_sink(const int* flag, int* sticky, int* host_flag, hipStr
     return hipGetLastError();
 }
 
+__global__ void flag_accum_kernel(const int* __restrict__ flag, int* __restrict__ pending) {
+    if (threadIdx.x == 0) atomicMax(pending, flag[0]);
+}
+hipError_t launch_flag_accum(const int* flag, int* pending, hipStream_t s) {
+    flag_accum_kernel<<<1, 64, 0, s>>>(flag, pending);
+    return hipGetLastError();
+}
+
 hipError_t launch_global_w(float4* sorted, const unsigned* perm, const int* gids, int n, int n_owned, hipStream_t s) {
     if (n > 0) global_w_kernel<<<cdiv(n, kRT), kRT, 0, s>>>(sorted, perm, gids, n, n_owned);
     return hipGetLastError();

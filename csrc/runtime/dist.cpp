@@ -119,6 +119,7 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     }
     if (own + halo >= (1ll << 31) - 1) { fail("too many local rows"); return; }
     n_owned_ = (int)own;
+    n_route_ = n_flag_ = p_.n;
     rows_ = (int)(own + halo);
     // send / receive layouts (route_scatter self-last: the other destinations in rank order, then
     // the rank's own segment; the receive buffer holds the other sources in rank order)
@@ -239,7 +240,19 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     };
     Set probe{};
     const size_t bytes = layout(nullptr, probe);
-    for (int s = 0; s < 2; ++s) {
+    // KN_DIST_QSTREAMS: query streams of the rank pipeline (pipeline.hpp). Two query streams run
+    // three grid sets (the next step's route + exchange + build then waits for the query two steps
+    // back, not the previous one still in flight)
+    const char* qsv = std::getenv("KN_DIST_QSTREAMS");
+    const int qstreams = comm_ ? (qsv ? std::atoi(qsv) : 1) : 1;
+    nsets_ = qstreams >= 2 ? 3 : 2;
+    // With two query streams the step's flag is reduced once per launch() (KN_DIST_DEFER=0: per step):
+    // a per-step epilogue on the build stream (flag + all-reduce) would wait for each query and hold
+    // the next build behind it, and an all-reduce on a third stream could reorder RCCL calls of one
+    // communicator across ranks
+    const char* dfv = std::getenv("KN_DIST_DEFER");
+    deferred_ = comm_ && qstreams >= 2 && !(dfv && dfv[0] == '0');
+    for (int s = 0; s < nsets_; ++s) {
         Set& S = set_[s];
         void* b = nullptr;
         if (device_malloc(&b, bytes) != hipSuccess) { fail("hipMalloc(distributed set)"); return; }
@@ -264,6 +277,10 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     tot_dev_ = static_cast<int*>(v);
     if (device_malloc(&v, sizeof(int)) != hipSuccess) { fail("hipMalloc(sticky)"); return; }
     sticky_ = static_cast<int*>(v);
+    if (device_malloc(&v, 2 * sizeof(int)) != hipSuccess) { fail("hipMalloc(pending)"); return; }
+    pending_ = static_cast<int*>(v);
+    reduced_ = pending_ + 1;
+    if (hipMemset(pending_, 0, 2 * sizeof(int)) != hipSuccess) { fail("hipMemset"); return; }
     if (hipHostMalloc(&v, sizeof(int), hipHostMallocDefault) != hipSuccess) { fail("hipHostMalloc(flag)"); return; }
     host_flag_ = static_cast<int*>(v);
     *host_flag_ = 0;
@@ -297,11 +314,8 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     // KN_DIST_CAPTURE_JOINED=1 (diagnostics): start unrolled captures on the main stream, so the
     // RCCL calls of the build stage are captured on a JOINED stream (the round-4 segfault)
     const char* joined = std::getenv("KN_DIST_CAPTURE_JOINED");
-    // KN_DIST_QSTREAMS: query streams of the rank pipeline (pipeline.hpp; 2 = odd sets' queries on
-    // a second stream, per-step launches)
-    const char* qsv = std::getenv("KN_DIST_QSTREAMS");
-    const int qstreams = qsv ? std::atoi(qsv) : 1;
-    if (pipe_.init(main_, side_, b, q, r, !(joined && joined[0] == '1'), qstreams) != hipSuccess) {
+    if (pipe_.init(main_, side_, b, q, deferred_ ? Pipeline::Stage() : Pipeline::Stage(r), !(joined && joined[0] == '1'),
+                   qstreams, nsets_) != hipSuccess) {
         fail("pipeline init");
         return;
     }
@@ -368,18 +382,23 @@ kn_status DistPipeline::prepare_graphs(int unroll) {
 
 void DistPipeline::set_eager(bool eager) { pipe_.set_eager(eager); }
 
-kn_status DistPipeline::rebind(const float* points, const int* ids) {
+kn_status DistPipeline::rebind(const float* points, const int* ids, int n) {
     if (!ok_) return KN_ERR_STATE;
-    if ((p_.ids == nullptr) != (ids == nullptr) || (p_.n > 0 && !points)) {
-        err_ = "rebind: input layout differs from the plan";
+    if (n < 0 || (n > 0 && !points)) {
+        err_ = "rebind: bad input";
         return KN_ERR_INVALID_ARGUMENT;
     }
-    if (points == p_.points && ids == p_.ids) return KN_OK;
+    if (points == p_.points && ids == p_.ids && n == n_flag_) return KN_OK;
     if (!pipe_.eager()) pipe_.set_eager(true);
     // a primed build read the old input: the next launch rebuilds from the new one
     if (pipe_.unprime() != hipSuccess) { err_ = "rebind: sync"; return KN_ERR_DEVICE; }
     p_.points = points;
     p_.ids = ids;
+    // A share of another size cannot be the validated plan's: route at most the planned number of
+    // points (the buffers' size) and let the step's flag see the true count, so the step is
+    // invalid on every rank (MAX all-reduce) while every rank issues the same collectives
+    n_route_ = std::min(n, p_.n);
+    n_flag_ = n;
     return KN_OK;
 }
 
@@ -392,7 +411,7 @@ DistPipeline::~DistPipeline() {
         if (S.tree_ws) (void)hipFree(S.tree_ws);
         if (S.tree_nodes) (void)hipFree(S.tree_nodes);
     }
-    for (void* v : {route_dev_, (void*)metas_dev_, (void*)tot_dev_, (void*)sticky_})
+    for (void* v : {route_dev_, (void*)metas_dev_, (void*)tot_dev_, (void*)sticky_, (void*)pending_})
         if (v) (void)hipFree(v);
     if (host_flag_) (void)hipHostFree(host_flag_);
     for (auto e : ring_) (void)hipEventDestroy(e);
@@ -430,13 +449,13 @@ hipError_t DistPipeline::exchange(int s, hipStream_t st) {
 hipError_t DistPipeline::stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks) {
     Set& S = set_[s];
     const auto* rp = static_cast<const RouteParams*>(route_dev_);
-    if (p_.n > 0) {
-        KN_TRY(launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, st, S.partials));
+    if (n_route_ > 0) {
+        KN_TRY(launch_route_count(p_.points, n_route_, rp, p_.world, S.bc, S.totals, st, S.partials));
         if (p_.self_via_comm) {
-            KN_TRY(launch_route_scatter(p_.points, p_.ids, p_.n, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank, st));
+            KN_TRY(launch_route_scatter(p_.points, p_.ids, n_route_, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank, st));
         } else {
             SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
-            KN_TRY(launch_route_scatter(p_.points, p_.ids, p_.n, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank,
+            KN_TRY(launch_route_scatter(p_.points, p_.ids, n_route_, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank,
                                         st, &sp));
         }
     } else {
@@ -488,13 +507,24 @@ hipError_t DistPipeline::stage_query(int s, hipStream_t st) {
             // the complete-box certification the grid kernels do inline
             KN_TRY(launch_certify_rows(S.lpts, n_owned_, p_.k, S.d2, complete_, S.geom, S.counters, S.uncert, st));
         }
+        if (deferred_) KN_TRY(step_flag(s, st));
         return hipSuccess;
     }
     // the tile kernel and its exact finish (KN_PIPE_EXACT=1: the exact finish opens the epilogue
-    // on the side stream instead, engine.cpp exact_epilogue)
+    // on the side stream instead, engine.cpp exact_epilogue; deferred mode: always here)
     QueryBuffers q = query_proto(s);
-    q.exact_mode = exact_epilogue(p_.k) ? 1 : 0;
-    return launch_query(q, st);
+    q.exact_mode = (!deferred_ && exact_epilogue(p_.k)) ? 1 : 0;
+    KN_TRY(launch_query(q, st));
+    if (deferred_) KN_TRY(step_flag(s, st));
+    return hipSuccess;
+}
+
+// deferred mode: the step's local flag on its query stream, max-accumulated into pending_
+hipError_t DistPipeline::step_flag(int s, hipStream_t st) {
+    Set& S = set_[s];
+    KN_TRY(launch_steady_flag_partials(S.partials, n_flag_, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
+                                       S.counters, S.flag, st));
+    return launch_flag_accum(S.flag, pending_, st);
 }
 
 QueryBuffers DistPipeline::query_proto(int s) const {
@@ -522,7 +552,7 @@ hipError_t DistPipeline::stage_flag(int s, hipStream_t st) {
         q.exact_mode = 2;
         KN_TRY(launch_query(q, st));
     }
-    KN_TRY(launch_steady_flag_partials(S.partials, p_.n, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
+    KN_TRY(launch_steady_flag_partials(S.partials, n_flag_, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
                                        S.counters, S.flag, st));
     if (!comm_) return hipSuccess;  // loopback mode: the caller reduces the ranks' flags
     if (ncclAllReduce(S.flag, S.flag, 1, ncclInt32, ncclMax, as_comm(comm_), st) != ncclSuccess) return hipErrorUnknown;
@@ -536,11 +566,11 @@ kn_status DistPipeline::loopback_stage(int stage) {
         // the routing half of stage_build (exchange and local build follow in stage 1)
         Set& S = set_[0];
         const auto* rp = static_cast<const RouteParams*>(route_dev_);
-        if (p_.n > 0) {
-            e = launch_route_count(p_.points, p_.n, rp, p_.world, S.bc, S.totals, main_, S.partials);
+        if (n_route_ > 0) {
+            e = launch_route_count(p_.points, n_route_, rp, p_.world, S.bc, S.totals, main_, S.partials);
             SelfPlace sp{S.lpts, S.lgids, p_.place[0], p_.place[1], p_.place[2], p_.place[3], p_.place[4]};
             if (e == hipSuccess)
-                e = launch_route_scatter(p_.points, p_.ids, p_.n, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank,
+                e = launch_route_scatter(p_.points, p_.ids, n_route_, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank,
                                          main_, &sp);
         } else {
             e = hipMemsetAsync(S.totals, 0, (size_t)2 * p_.world * sizeof(int), main_);
@@ -593,10 +623,17 @@ kn_status DistPipeline::launch(int iters, int unroll, bool keep_primed, hipStrea
         if (e == hipSuccess) e = hipStreamWaitEvent(side_, in_ev_, 0);
     }
     if (e == hipSuccess) e = pipe_.launch(iters, unroll, keep_primed);
+    if (e == hipSuccess && deferred_) {
+        // one all-reduce for the call's steps: after both query streams' last steps (last_done),
+        // on the build stream, in the same place of every rank's RCCL call sequence
+        e = hipStreamWaitEvent(side_, pipe_.last_done(), 0);
+        if (e == hipSuccess && ncclAllReduce(pending_, reduced_, 1, ncclInt32, ncclMax, as_comm(comm_), side_) != ncclSuccess)
+            e = hipErrorUnknown;
+        if (e == hipSuccess) e = launch_flag_sink(reduced_, sticky_, host_flag_dev_, side_);
+    }
     if (e == hipSuccess && caller) {
         // later work on the caller's stream (e.g. refilling the points) waits for the builds
-        e = hipStreamWaitEvent(caller, pipe_.build_event(0), 0);
-        if (e == hipSuccess) e = hipStreamWaitEvent(caller, pipe_.build_event(1), 0);
+        for (int s = 0; s < nsets_ && e == hipSuccess; ++s) e = hipStreamWaitEvent(caller, pipe_.build_event(s), 0);
     }
     if (e != hipSuccess) {
         err_ = std::string("distributed pipelined launch: ") + hipGetErrorString(e);
@@ -639,7 +676,7 @@ kn_status DistPipeline::profile(float ms[5]) {
     for (auto& e : ev)
         if (hipEventCreate(&e) != hipSuccess) { err_ = "hipEventCreate"; return KN_ERR_DEVICE; }
     // the set the pipeline will build next is free (nothing primed): profile in it
-    const int s = (int)(pipe_.steps() & 1);
+    const int s = (int)(pipe_.steps() % nsets_);
     std::vector<hipEvent_t> marks = {ev[1], ev[2]};
     hipError_t e = hipEventRecord(ev[0], main_);
     if (e == hipSuccess) e = stage_build(s, main_, &marks);

@@ -100,12 +100,13 @@ public:
     kn_status prepare_graphs(int unroll);
     void set_eager(bool eager);
     bool eager() const { return pipe_.eager(); }
-    // Read the steps' input from other device buffers (same n; ids null <=> built without ids):
-    // a caller passing a fresh tensor every step keeps its pipeline. Eager stages read the new
-    // pointers at once; captured graphs hold the old ones, so a graph-mode pipeline switches to
-    // eager (one wait for both streams, once). The launch() caller-stream ordering still covers
-    // the old buffers' last reads.
-    kn_status rebind(const float* points, const int* ids);
+    // Read the steps' input from other device buffers (ids null: id offset + i): a caller passing a
+    // fresh tensor every step keeps its pipeline, without anything collective. Eager stages read
+    // the new pointers at once; captured graphs hold the old ones, so a graph-mode pipeline
+    // switches to eager (one wait for the streams, once). A share of another size n routes at most
+    // the planned rows and fails the step's flag on every rank. The launch() caller-stream
+    // ordering still covers the old buffers' last reads.
+    kn_status rebind(const float* points, const int* ids, int n);
     int capture_fallbacks() const { return pipe_.fallbacks(); }
     // Enqueue `iters` pipelined steps (unroll >= 2, even: steps per graph launch); *last_step = the
     // index of the last one. The steps read the caller's points in place: `caller` (may be null)
@@ -118,6 +119,7 @@ public:
     kn_status wait(long long step, double timeout_s, int* flag);
     kn_status sync();
     int last_set() const { return pipe_.last_set(); }
+    int sets() const { return nsets_; }
     // One serial step on the main stream with events between its phases (ms): route, exchange,
     // unpack + build, query (tile kernel / tree + certification), epilogue (exact finish, flag,
     // all-reduce). Unprimes the pipeline.
@@ -158,6 +160,7 @@ private:
     hipError_t stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks = nullptr);
     hipError_t stage_query(int s, hipStream_t st);
     hipError_t stage_flag(int s, hipStream_t st);  // epilogue: exact finish, flag, all-reduce
+    hipError_t step_flag(int s, hipStream_t st);   // deferred mode: local flag -> pending_
     QueryBuffers query_proto(int s) const;
     // wait for `ev`, polling RCCL's async error; past the deadline the communicator is aborted
     kn_status poll(hipEvent_t ev, double timeout_s, const char* what);
@@ -170,17 +173,24 @@ private:
     bool ok_ = false;
     bool warm_ = false;
     int rows_ = 0, n_owned_ = 0, C_ = 0;
+    int n_route_ = 0, n_flag_ = 0;  // rows routed per step / the share's true size (rebind)
     int rows_cross_ = 0, recv_rows_ = 0;
     std::vector<long long> soff_, roff_;  // send / recv row offsets per peer
     UnpackTable table_{};
     BuildBuffers bproto_{};
     QueryBuffers qproto_{};
     CompleteBox complete_{};
-    Set set_[2]{};
+    Set set_[Pipeline::kMaxSets]{};
+    int nsets_ = 2;
     void* route_dev_ = nullptr;
     double* metas_dev_ = nullptr;
     int* tot_dev_ = nullptr;
     int* sticky_ = nullptr;
+    // deferred flag reduction (two query streams): every step's flag is max-accumulated on the
+    // device (pending_, atomic), one all-reduce per launch() call into reduced_ then the sticky flag
+    bool deferred_ = false;
+    int* pending_ = nullptr;
+    int* reduced_ = nullptr;
     int* host_flag_ = nullptr;      // pinned
     int* host_flag_dev_ = nullptr;  // its device pointer
     hipStream_t main_ = nullptr, side_ = nullptr;

@@ -23,15 +23,17 @@ void destroy(hipEvent_t& e) {
 }  // namespace
 
 hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r, bool capture_from_side,
-                          int query_streams) {
+                          int query_streams, int sets) {
     reset();
+    if (sets < 2 || sets > kMaxSets) return hipErrorInvalidValue;
+    ns_ = sets;
     main_ = main;
     side_ = side;
     capture_from_side_ = capture_from_side;
     b_ = std::move(b);
     q_ = std::move(q);
     r_ = std::move(r);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < ns_; ++s) {
         for (hipEvent_t* e : {&evB_[s], &evQ_[s], &evF_[s]})
             KN_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
         // both sets start free
@@ -45,6 +47,10 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
         KN_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
         (void)hi;
         KN_TRY(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, lo));
+        for (auto& e : evQS_) {
+            KN_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            KN_TRY(hipEventRecord(e, main_));
+        }
     }
     return hipSuccess;
 }
@@ -52,15 +58,18 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
 void Pipeline::reset() {
     if (main_) (void)hipStreamSynchronize(main_);
     if (side_) (void)hipStreamSynchronize(side_);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kMaxSets; ++s) {
         destroy(gB_[s]);
         destroy(gQ_[s]);
         destroy(gR_[s]);
-        destroy(gU_[s]);
-        gU_len_[s] = 0;
         destroy(evB_[s]);
         destroy(evQ_[s]);
         destroy(evF_[s]);
+    }
+    for (int s = 0; s < 2; ++s) {
+        destroy(gU_[s]);
+        gU_len_[s] = 0;
+        destroy(evQS_[s]);
     }
     destroy(last_done_);
     if (aux_) {
@@ -93,7 +102,7 @@ hipError_t Pipeline::capture(const Stage& st, int set, hipGraphExec_t* out) {
 
 hipError_t Pipeline::graphs() {
     if (eager_) return hipSuccess;
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < ns_; ++s) {
         if (!gB_[s]) KN_TRY(capture(b_, s, &gB_[s]));
         if (!gQ_[s]) KN_TRY(capture(q_, s, &gQ_[s]));
         if (r_ && !gR_[s]) KN_TRY(capture(r_, s, &gR_[s]));
@@ -169,10 +178,14 @@ hipError_t Pipeline::enqueue_build(int s) {
 }
 
 hipError_t Pipeline::enqueue_query(int s) {
-    hipStream_t qs = qstream(s);
+    // with two query streams, consecutive STEPS alternate streams (whatever the number of sets)
+    const int qi = (aux_ && (next_ & 1)) ? 1 : 0;
+    hipStream_t qs = qi ? aux_ : main_;
     KN_TRY(hipStreamWaitEvent(qs, evB_[s], 0));
     KN_TRY(eager_ ? q_(s, qs) : hipGraphLaunch(gQ_[s], qs));
-    return hipEventRecord(evQ_[s], qs);
+    KN_TRY(hipEventRecord(evQ_[s], qs));
+    last_qs_ = qi;
+    return aux_ ? hipEventRecord(evQS_[qi], qs) : hipSuccess;
 }
 
 hipError_t Pipeline::enqueue_epilogue(int s) {
@@ -185,7 +198,7 @@ hipError_t Pipeline::prepare(int unroll) {
     if (!main_) return hipErrorNotInitialized;
     if (eager_) return hipSuccess;
     KN_TRY(graphs());
-    if (unroll >= 2 && !(unroll & 1)) {
+    if (unroll >= 2 && !(unroll & 1) && ns_ == 2 && !aux_) {  // (launch() runs unrolled graphs only then)
         KN_TRY(unrolled(0, unroll));
         KN_TRY(unrolled(1, unroll));
     }
@@ -207,10 +220,12 @@ void Pipeline::set_eager(bool eager) {
         }
     }
     (void)hipGetLastError();
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kMaxSets; ++s) {
         destroy(gB_[s]);
         destroy(gQ_[s]);
         destroy(gR_[s]);
+    }
+    for (int s = 0; s < 2; ++s) {
         destroy(gU_[s]);
         gU_len_[s] = 0;
     }
@@ -224,12 +239,10 @@ hipError_t Pipeline::flush() {
         return hipEventRecord(last_done_, side_);
     }
     if (!r_ && last_set_ >= 0) {
-        if (aux_) {
-            // both query streams' last queries (they do not depend on each other) before last_done
-            KN_TRY(hipEventRecord(evQ_[last_set_ ^ 1], qstream(last_set_ ^ 1)));
-            KN_TRY(hipStreamWaitEvent(qstream(last_set_), evQ_[last_set_ ^ 1], 0));
-        }
-        return hipEventRecord(last_done_, qstream(last_set_));
+        hipStream_t ql = last_qs_ ? aux_ : main_;
+        // both query streams' last queries (they do not depend on each other) before last_done
+        if (aux_) KN_TRY(hipStreamWaitEvent(ql, evQS_[last_qs_ ^ 1], 0));
+        return hipEventRecord(last_done_, ql);
     }
     return hipSuccess;
 }
@@ -251,7 +264,7 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
     // libamdhip64 while capturing, profiles/r5_qstreams.txt), and 2-step graphs measured slower
     // than per-step launches (900K K=16, 200 steps: 0.2828 vs 0.2756 ms; one query stream with
     // 10-step graphs 0.2894)
-    if (aux_) unroll = 0;
+    if (aux_ || ns_ != 2) unroll = 0;
     if (unroll) {
         // both start parities up front (also by a call of fewer steps, e.g. a warm-up): a capture
         // never lands inside a later (timed) call
@@ -262,7 +275,7 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
     }
     int done = 0;
     while (done < iters) {
-        const int s = (int)(next_ & 1);
+        const int s = (int)(next_ % ns_);
         // an unrolled graph ends with the next step's build: only when the call keeps it primed,
         // or more steps follow in this call
         if (unroll && iters - done >= unroll + (keep_primed ? 0 : 1)) {
@@ -275,12 +288,6 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
             // writes set s^1, released by the last query (main, stream order) and R (side)
             KN_TRY(hipStreamWaitEvent(main_, evB_[s], 0));
             if (r_) KN_TRY(hipStreamWaitEvent(main_, evF_[s ^ 1], 0));
-            if (aux_) {
-                // a per-step query of set s^1 may still run on the second query stream: the graph's
-                // first build writes that set
-                KN_TRY(hipEventRecord(evQ_[s ^ 1], qstream(s ^ 1)));
-                KN_TRY(hipStreamWaitEvent(main_, evQ_[s ^ 1], 0));
-            }
             KN_TRY(hipGraphLaunch(gU_[s], main_));
             // U is even: the last query used set s^1, the primed build (B(next)) wrote set s.
             // Every per-set event is re-recorded after the graph: its queries read both sets and
@@ -305,7 +312,7 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
         }
         last_set_ = s;
         if (keep_primed || done + 1 < iters) {
-            KN_TRY(enqueue_build(s ^ 1));  // B(i+1) overlaps Q(i)
+            KN_TRY(enqueue_build((s + 1) % ns_));  // B(i+1) overlaps Q(i)
             primed_ = true;
         } else {
             primed_ = false;
@@ -320,7 +327,8 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
 hipError_t Pipeline::step_with(const Stage& pre, const Stage* next_pre) {
     if (!main_) return hipErrorNotInitialized;
     KN_TRY(fallback_if(graphs()));
-    const int s = (int)(next_ & 1);
+    const int s = (int)(next_ % ns_);
+    const int sn = (s + 1) % ns_;
     if (!primed_) {
         // this step's input into set s, then its build
         KN_TRY(hipStreamWaitEvent(side_, r_ ? evF_[s] : evQ_[s], 0));
@@ -335,9 +343,9 @@ hipError_t Pipeline::step_with(const Stage& pre, const Stage* next_pre) {
     last_set_ = s;
     primed_ = false;
     if (next_pre) {
-        KN_TRY(hipStreamWaitEvent(side_, r_ ? evF_[s ^ 1] : evQ_[s ^ 1], 0));
-        KN_TRY((*next_pre)(s ^ 1, side_));
-        KN_TRY(enqueue_build(s ^ 1));
+        KN_TRY(hipStreamWaitEvent(side_, r_ ? evF_[sn] : evQ_[sn], 0));
+        KN_TRY((*next_pre)(sn, side_));
+        KN_TRY(enqueue_build(sn));
         primed_ = true;
     }
     r_pending_ = (bool)r_;

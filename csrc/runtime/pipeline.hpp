@@ -42,8 +42,13 @@ public:
     // query_streams = 2: the queries of odd sets go to a second (pipeline-owned) stream, so a
     // step's queries need not wait for the previous step's last workgroups: each depends only on
     // its own build (sets, counters and outputs are per set)
+    // sets = 3: step i uses set i % 3, so step i+1's build waits for step i-2's query instead of
+    // step i-1's (with two query streams two queries are in flight; the build of the next step
+    // then need not wait for the older of them). Unrolled graphs need 2 sets and one query stream.
+    static constexpr int kMaxSets = 3;
     hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage(),
-                    bool capture_from_side = false, int query_streams = 1);
+                    bool capture_from_side = false, int query_streams = 1, int sets = 2);
+    int sets() const { return ns_; }
     bool ready() const { return main_ != nullptr; }
     // Enqueue `iters` resident-mode steps; unroll >= 2 (even): whole groups of `unroll` steps go
     // through one unrolled graph, the rest through per-step graphs. keep_primed = false: the call
@@ -87,7 +92,7 @@ private:
     hipError_t capture(const Stage& st, int set, hipGraphExec_t* out);
     hipError_t enqueue_build(int set);   // side: wait set free, B(set), record evB
     hipError_t enqueue_query(int set);   // query stream of the set: wait evB, Q(set), record evQ
-    hipStream_t qstream(int set) const { return (aux_ && (set & 1)) ? aux_ : main_; }
+
     hipError_t enqueue_epilogue(int set);
 
     hipStream_t main_ = nullptr, side_ = nullptr;
@@ -96,12 +101,15 @@ private:
     bool eager_ = false;
     int fallbacks_ = 0;
     Stage b_, q_, r_;
-    hipGraphExec_t gB_[2] = {nullptr, nullptr}, gQ_[2] = {nullptr, nullptr}, gR_[2] = {nullptr, nullptr};
+    int ns_ = 2;  // grid sets
+    hipGraphExec_t gB_[kMaxSets] = {}, gQ_[kMaxSets] = {}, gR_[kMaxSets] = {};
     hipGraphExec_t gU_[2] = {nullptr, nullptr};
     int gU_len_[2] = {0, 0};
-    hipEvent_t evB_[2] = {nullptr, nullptr};  // set built
-    hipEvent_t evQ_[2] = {nullptr, nullptr};  // set queried
-    hipEvent_t evF_[2] = {nullptr, nullptr};  // set free (after Q and R)
+    hipEvent_t evB_[kMaxSets] = {};  // set built
+    hipEvent_t evQ_[kMaxSets] = {};  // set queried
+    hipEvent_t evF_[kMaxSets] = {};  // set free (after Q and R)
+    hipEvent_t evQS_[2] = {nullptr, nullptr};  // tail of each query stream (two query streams)
+    int last_qs_ = 0;                          // query stream of the last query
     hipEvent_t last_done_ = nullptr;
     std::vector<hipEvent_t> cap_ev_;  // fork / join events of the unrolled captures
     long long next_ = 0;       // index of the next step to query

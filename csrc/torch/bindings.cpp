@@ -1474,9 +1474,7 @@ public:
     // new input tensors for the following steps (same n, same ids presence); keeps them alive
     void rebind(torch::Tensor points, c10::optional<torch::Tensor> ids) {
         check_points(points, true);
-        TORCH_CHECK(points.size(0) == points_.size(0) && points.get_device() == points_.get_device(),
-                    "rebind: same number of points on the same device");
-        TORCH_CHECK(ids.has_value() == ids_.defined(), "rebind: ids given iff the pipeline was built with ids");
+        TORCH_CHECK(points.get_device() == points_.get_device(), "rebind: same device");
         const int* ip = nullptr;
         if (ids.has_value()) {
             TORCH_CHECK(ids->is_cuda() && ids->scalar_type() == torch::kInt32 && ids->numel() == points.size(0) &&
@@ -1484,9 +1482,9 @@ public:
             ip = ids->data_ptr<int>();
         }
         const c10::DeviceGuard guard(points.device());
-        TORCH_CHECK(d_->rebind(points.data_ptr<float>(), ip) == KN_OK, d_->error());
+        TORCH_CHECK(d_->rebind(points.data_ptr<float>(), ip, (int)points.size(0)) == KN_OK, d_->error());
         points_ = points;
-        if (ids.has_value()) ids_ = *ids;
+        ids_ = ids.has_value() ? *ids : torch::Tensor();
     }
     std::string mode() { return d_->eager() ? "eager" : "graph"; }
     int64_t capture_fallbacks() { return d_->capture_fallbacks(); }
@@ -1545,11 +1543,12 @@ public:
     }
     void sync() { TORCH_CHECK(d_->sync() == KN_OK, d_->error()); }
     int64_t last_set() { return d_->last_set(); }
+    int64_t sets() { return d_->sets(); }
     // (owned global ids, idx, d2) of grid set s: views of the pipeline's buffers, overwritten by
     // the step after next. Each view holds a reference to the pipeline (its deleter), so the
     // buffers outlive every tensor that views them, whatever the Python side drops
     std::vector<torch::Tensor> outputs(int64_t s) {
-        TORCH_CHECK(s == 0 || s == 1, "set is 0 or 1");
+        TORCH_CHECK(s >= 0 && s < d_->sets(), "set out of range");
         auto opt = torch::TensorOptions().device(points_.device());
         const int64_t no = d_->n_owned(), k = d_->k();
         std::shared_ptr<kn::DistPipeline> keep = d_;
@@ -1561,7 +1560,7 @@ public:
         return {g, i, d};
     }
     std::vector<int64_t> counters(int64_t s) {
-        TORCH_CHECK(s == 0 || s == 1, "set is 0 or 1");
+        TORCH_CHECK(s >= 0 && s < d_->sets(), "set out of range");
         TORCH_CHECK(d_->sync() == KN_OK, d_->error());
         unsigned c[kn::kNumCounters];
         KN_CHECK_HIP(hipMemcpy(c, d_->counters((int)s), sizeof(c), hipMemcpyDeviceToHost));
@@ -1714,6 +1713,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("wait", &PyDistPipe::wait, py::arg("step"), py::arg("timeout_s") = 300.0)
         .def("sync", &PyDistPipe::sync)
         .def("last_set", &PyDistPipe::last_set)
+        .def("sets", &PyDistPipe::sets)
         .def("outputs", &PyDistPipe::outputs)
         .def("counters", &PyDistPipe::counters)
         .def("profile", &PyDistPipe::profile)

@@ -811,11 +811,13 @@ class DistributedKNearests:
                 and (ids32 is None or p["ids"].data_ptr() == ids32.data_ptr()))
         if same:
             return p
-        if (p is not None and p["st"] is st and p["n"] == points.size(0) and (p["ids"] is None) == (ids32 is None)):
-            # other storage of the same shape (a caller passing a fresh tensor every step): the
-            # pipeline reads the new tensors from now on (local: no collective, no rebuild)
+        if p is not None and p["st"] is st:
+            # other input tensors under the same steady plan (a caller passing a fresh tensor every
+            # step, or a share whose size changed): the pipeline reads them from now on -- local,
+            # no rebuild, so no rank ever enters a collective its peers do not (a changed size
+            # fails the step's flag on every rank; the next step then takes the full path together)
             p["pipe"].rebind(points, ids32)
-            p["pts"], p["ids"] = points, ids32
+            p["pts"], p["ids"], p["n"] = points, ids32, points.size(0)
             self.pipe_mode = p["pipe"].mode()
             return p
         self._pipe = None  # release the old pipeline's buffers first
@@ -851,7 +853,7 @@ class DistributedKNearests:
                 pipe.set_eager(True)
         self.pipe_mode = mode
         p = self._pipe = {"pipe": pipe, "st": st, "pts": points, "ids": ids32, "n": points.size(0),
-                          "outs": [pipe.outputs(0), pipe.outputs(1)], "primed": False}
+                          "outs": [pipe.outputs(i) for i in range(pipe.sets())], "primed": False}
         return p
 
     def _solve_pipe(self, points: torch.Tensor, ids: Optional[torch.Tensor], iters: int = 1,
