@@ -245,7 +245,8 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     // back, not the previous one still in flight)
     const char* qsv = std::getenv("KN_DIST_QSTREAMS");
     const int qstreams = comm_ ? (qsv ? std::atoi(qsv) : 1) : 1;
-    nsets_ = qstreams >= 2 ? 3 : 2;
+    const char* nsv = std::getenv("KN_DIST_SETS");  // A/B override: 2 or 3 grid sets
+    nsets_ = nsv ? std::max(2, std::min(Pipeline::kMaxSets, std::atoi(nsv))) : (qstreams >= 2 ? 3 : 2);
     // With two query streams the step's flag is reduced once per launch() (KN_DIST_DEFER=0: per step):
     // a per-step epilogue on the build stream (flag + all-reduce) would wait for each query and hold
     // the next build behind it, and an all-reduce on a third stream could reorder RCCL calls of one

@@ -784,16 +784,15 @@ class DistributedKNearests:
 
     def _capture_mode(self) -> bool:
         """Graph capture of the native pipeline's stages (RCCL calls included): KN_DIST_CAPTURE=1
-        always, =0 never; default at world 1 only. At world > 1 the stages run eagerly on the two
-        streams (same order and overlap, one enqueue per kernel): captured multi-peer RCCL
-        point-to-point has never run on more than one rank here, and an eager RCCL step is the
-        library's ordinary use."""
+        captures, default eager at every world size: the stages are enqueued per step on the two
+        streams (same order and overlap, one enqueue per kernel). Eager measured FASTER than the
+        captured per-stage graphs at world 1 (900K K=16, 200 / 50, two passes: 0.3191 / 0.3210 vs
+        0.3280 / 0.3271 ms, profiles/r5_dist.txt), and at world > 1 an eager RCCL step is the
+        library's ordinary use (captured multi-peer point-to-point has never run on more than one
+        rank here), so every world size now times the same mode."""
         import os
 
-        env = os.environ.get("KN_DIST_CAPTURE")
-        if env in ("0", "1"):
-            return env == "1"
-        return self.world == 1
+        return os.environ.get("KN_DIST_CAPTURE") == "1"
 
     def _pipe_for(self, points: torch.Tensor, ids: Optional[torch.Tensor]):
         """The native pipeline of the current steady plan over these input tensors (read in

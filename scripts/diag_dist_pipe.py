@@ -5,7 +5,7 @@ resident priming), in-place refills of the input between calls (caller-stream or
 share (flag fails, the synchronous call recovers), per-phase profile. Rows are compared bit for
 bit with the torch-path reference (DistributedKNearests(native_pipeline=False)).
 Every combination runs in three pipeline modes: captured hipGraphs (KN_DIST_CAPTURE=1), eager
-stages (=0, the default at world > 1) and an injected capture failure (KN_DIST_CAPTURE_FAIL=1),
+stages (=0, the default) and an injected capture failure (KN_DIST_CAPTURE_FAIL=1),
 which must fall back to the eager mode and stay exact.
 usage: python scripts/diag_dist_pipe.py [steps] [n] [force modes, e.g. 0,1] [capture modes, e.g. 1,0,fail]"""
 import os

@@ -10,3 +10,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail $O/bench.err; exit 1; }
 cat $O/bench.json
+timeout -k 10 200 python bench.py --dist --steps 20 --warmup 5 > $O/bench_dist.json 2> $O/bench_dist.err || { echo DIST_BENCH_FAIL; tail $O/bench_dist.err; exit 1; }
+cat $O/bench_dist.json
