@@ -20,6 +20,18 @@ void destroy(hipEvent_t& e) {
     if (e) (void)hipEventDestroy(e);
     e = nullptr;
 }
+// Flags of the events that order the pipeline's streams on the device (never waited on by the
+// host). KN_EVENT_SCOPE (A/B): 0 default system-scope release, 1 device-scope release
+// (hipEventReleaseToDevice), 2 no system fence (hipEventDisableSystemFence).
+unsigned order_event_flags() {
+    static const unsigned f = [] {
+        const char* v = std::getenv("KN_EVENT_SCOPE");
+        const int m = v ? std::atoi(v) : 0;
+        return (unsigned)hipEventDisableTiming |
+               (m == 1 ? (unsigned)hipEventReleaseToDevice : m == 2 ? (unsigned)hipEventDisableSystemFence : 0u);
+    }();
+    return f;
+}
 }  // namespace
 
 hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r, bool capture_from_side,
@@ -35,7 +47,7 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
     r_ = std::move(r);
     for (int s = 0; s < ns_; ++s) {
         for (hipEvent_t* e : {&evB_[s], &evQ_[s], &evF_[s]})
-            KN_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            KN_TRY(hipEventCreateWithFlags(e, order_event_flags()));
         // both sets start free
         KN_TRY(hipEventRecord(evF_[s], main_));
         KN_TRY(hipEventRecord(evQ_[s], main_));
@@ -48,7 +60,7 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
         (void)hi;
         KN_TRY(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, lo));
         for (auto& e : evQS_) {
-            KN_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            KN_TRY(hipEventCreateWithFlags(&e, order_event_flags()));
             KN_TRY(hipEventRecord(e, main_));
         }
     }
@@ -120,7 +132,7 @@ hipError_t Pipeline::unrolled(int s0, int U) {
     const size_t need = 2 * (size_t)U + 3;
     while (cap_ev_.size() < need) {
         hipEvent_t e = nullptr;
-        KN_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        KN_TRY(hipEventCreateWithFlags(&e, order_event_flags()));
         cap_ev_.push_back(e);
     }
     hipEvent_t fork = cap_ev_[0], join = cap_ev_[1], join2 = cap_ev_[2];

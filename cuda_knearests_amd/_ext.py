@@ -24,6 +24,8 @@ def load():
     import torch  # noqa: F401  (libtorch / torch's HIP runtime must be loaded first)
 
     name = "cuda_knearests_amd._C_checked" if os.environ.get("KN_CHECKED") == "1" else "cuda_knearests_amd._C"
+    if os.environ.get("KN_C_VARIANT"):  # A/B of compile-time variants (_build.build_variant)
+        name = "cuda_knearests_amd._C_" + os.environ["KN_C_VARIANT"]
     try:
         _C = importlib.import_module(name)
     except ImportError as e:  # pragma: no cover - exercised only without a build
