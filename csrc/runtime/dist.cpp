@@ -294,8 +294,15 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
         fail("plan upload");
         return;
     }
+    // KN_DIST_SIDE_PRIO (A/B): 1 the build stream at the device's greatest priority, 2 at its least
+    const char* spv = std::getenv("KN_DIST_SIDE_PRIO");
+    const int sprio = spv ? std::atoi(spv) : 0;
+    int p_least = 0, p_greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&p_least, &p_greatest);
     if (hipStreamCreateWithFlags(&main_, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&side_, hipStreamNonBlocking) != hipSuccess) {
+        ((sprio == 1 || sprio == 2)
+             ? hipStreamCreateWithPriority(&side_, hipStreamNonBlocking, sprio == 2 ? p_least : p_greatest)
+             : hipStreamCreateWithFlags(&side_, hipStreamNonBlocking)) != hipSuccess) {
         fail("hipStreamCreate");
         return;
     }

@@ -565,9 +565,11 @@ kn_status Engine::run_graph(int iters, float* ms_per_iter) {
     return KN_OK;
 }
 
+// build stream priority of the pipeline: 0 default, 1 the device's greatest, 2 its least
 static int pipe_prio() {
     const char* v = std::getenv("KN_PIPE_PRIO");
-    return v && std::atoi(v) == 1 ? 1 : 0;
+    const int p = v ? std::atoi(v) : 0;
+    return (p == 1 || p == 2) ? p : 0;
 }
 
 Engine::GridSet Engine::members() const {

@@ -336,7 +336,9 @@ hipError_t streamset_acquire(int device, StreamSet* out, int priority) {
     if (priority) {
         int least = 0, greatest = 0;
         e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking, greatest);
+        // 1: the device's greatest priority, 2: its least (KN_PIPE_PRIO)
+        if (e == hipSuccess)
+            e = hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking, priority == 2 ? least : greatest);
     } else {
         e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     }

@@ -58,7 +58,13 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
         int lo = 0, hi = 0;
         KN_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
         (void)hi;
-        KN_TRY(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, lo));
+        // the second query stream at the default priority, like the first (the device's least
+        // priority, KN_PIPE_AUXPRIO=0, measured slower: 900K K=16 200 / 50 steps 0.276 -> 0.268
+        // ms, the driver's 20 / 5 0.304 -> 0.297, K=50 0.766 -> 0.747; three interleaved passes,
+        // profiles/ab_r5_stream_prio.txt)
+        const char* ap = std::getenv("KN_PIPE_AUXPRIO");
+        if (ap && std::atoi(ap) == 0) KN_TRY(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, lo));
+        else KN_TRY(hipStreamCreateWithFlags(&aux_, hipStreamNonBlocking));
         for (auto& e : evQS_) {
             KN_TRY(hipEventCreateWithFlags(&e, order_event_flags()));
             KN_TRY(hipEventRecord(e, main_));
