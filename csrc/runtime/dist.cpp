@@ -243,8 +243,11 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     // KN_DIST_QSTREAMS: query streams of the rank pipeline (pipeline.hpp). Two query streams run
     // three grid sets (the next step's route + exchange + build then waits for the query two steps
     // back, not the previous one still in flight)
+    // Default two (900K K=16 world 1, 200 / 50 steps, two passes: one stream 0.3145 / 0.3196 ms,
+    // two streams + three sets + per-launch flag 0.2838 / 0.2886; profiles/r5_dist.txt). They lost
+    // until the second query stream ran at the device's least priority no more (pipeline.cpp).
     const char* qsv = std::getenv("KN_DIST_QSTREAMS");
-    const int qstreams = comm_ ? (qsv ? std::atoi(qsv) : 1) : 1;
+    const int qstreams = comm_ ? (qsv ? std::atoi(qsv) : 2) : 1;
     const char* nsv = std::getenv("KN_DIST_SETS");  // A/B override: 2 or 3 grid sets
     nsets_ = nsv ? std::max(2, std::min(Pipeline::kMaxSets, std::atoi(nsv))) : (qstreams >= 2 ? 3 : 2);
     // With two query streams the step's flag is reduced once per launch() (KN_DIST_DEFER=0: per step):
