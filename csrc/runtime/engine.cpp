@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <cstring>
 #include <fstream>
 
@@ -254,6 +255,10 @@ QueryBuffers Engine::query_buffers() const {
         q.out_idx_ref = reinterpret_cast<unsigned* const*>(tab_ + kBatchMax + out_ref_slot_);
         q.out_dist_ref = reinterpret_cast<float* const*>(tab_ + 2 * kBatchMax + out_ref_slot_);
     }
+    if (out_ovr_set_ >= 0) {  // an eager batch step: the caller's buffers
+        q.out_idx = bout_idx_[out_ovr_set_];
+        q.out_dist = bout_dist_[out_ovr_set_];
+    }
     q.fallback_list = fallback_;
     q.counters = counters_;
     for (int a = 0; a < 3; ++a) q.tile[a] = ap_.tile[a];
@@ -337,6 +342,10 @@ kn_status Engine::tree_query_async() {
     if (out_ref_slot_ >= 0) {
         q.out_idx_ref = reinterpret_cast<unsigned* const*>(tab_ + kBatchMax + out_ref_slot_);
         q.out_dist_ref = reinterpret_cast<float* const*>(tab_ + 2 * kBatchMax + out_ref_slot_);
+    }
+    if (out_ovr_set_ >= 0) {
+        q.out_idx = bout_idx_[out_ovr_set_];
+        q.out_dist = bout_dist_[out_ovr_set_];
     }
     q.counters = counters_;
     return check(launch_tree_query(t, q, stream_), "tree query");
@@ -841,10 +850,16 @@ kn_status Engine::stream_step(const float* d_pts, const float* d_next) {
 void Engine::drop_batch() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (bstream_) (void)hipStreamSynchronize(bstream_);
+    bpipe_.reset();  // (shares pipe_'s second query stream: reset before pipe_)
     for (auto& kv : bgraphs_) (void)hipGraphExecDestroy(kv.second);
     bgraphs_.clear();
     for (auto e : bev_) (void)hipEventDestroy(e);
     bev_.clear();
+    if (qstream2_) {
+        (void)hipStreamSynchronize(qstream2_);
+        (void)hipStreamDestroy(qstream2_);
+        qstream2_ = nullptr;
+    }
     if (tab_) { dfree(tab_); tab_ = nullptr; }
 }
 
@@ -854,12 +869,24 @@ void Engine::drop_batch() {
 kn_status Engine::batch_graph(int L, hipGraphExec_t* out) {
     auto it = bgraphs_.find(L);
     if (it != bgraphs_.end()) { *out = it->second; return KN_OK; }
-    while (bev_.size() < 2 * (size_t)L + 2) {
+    // KN_BATCH_QSTREAMS=2 (diagnostics): consecutive steps' queries on two streams inside the
+    // graph. Crashes the HIP runtime during capture (segfault after the first graphs, as the
+    // resident pipeline's unrolled graphs with two query streams, profiles/r5_qstreams.txt): the
+    // eager batch pipeline (stream_batch_eager) overlaps consecutive clouds' queries instead
+    static const int bqs = [] {
+        const char* v = std::getenv("KN_BATCH_QSTREAMS");
+        return v ? std::atoi(v) : 1;
+    }();
+    if (bqs >= 2 && !qstream2_ &&
+        hipStreamCreateWithFlags(&qstream2_, hipStreamNonBlocking) != hipSuccess)
+        return fail(KN_ERR_DEVICE, "hipStreamCreate");
+    hipStream_t qst[2] = {stream_, bqs >= 2 ? qstream2_ : stream_};
+    while (bev_.size() < 2 * (size_t)L + 3) {
         hipEvent_t e = nullptr;
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(KN_ERR_DEVICE, "hipEventCreate");
         bev_.push_back(e);
     }
-    hipEvent_t fork = bev_[0], join = bev_[1];
+    hipEvent_t fork = bev_[0], join = bev_[1], join2 = bev_[2 + 2 * L];
     hipEvent_t* eb = bev_.data() + 2;      // step j built
     hipEvent_t* eq = bev_.data() + 2 + L;  // step j queried
     const bool epi = !use_tree_ && exact_epilogue(cfg_.k);
@@ -882,13 +909,15 @@ kn_status Engine::batch_graph(int L, hipGraphExec_t* out) {
     };
     H(hipEventRecord(fork, stream_));
     H(hipStreamWaitEvent(bstream_, fork, 0));
+    if (qst[1] != stream_) H(hipStreamWaitEvent(qst[1], fork, 0));
     build(0);
     for (int j = 0; j < L && st == KN_OK; ++j) {
-        H(hipStreamWaitEvent(stream_, eb[j], 0));
+        hipStream_t qs = qst[j & 1];
+        H(hipStreamWaitEvent(qs, eb[j], 0));
         out_ref_slot_ = j;
-        if (st == KN_OK) S(stage_query(j & 1, stream_));
+        if (st == KN_OK) S(stage_query(j & 1, qs));
         out_ref_slot_ = -1;
-        H(hipEventRecord(eq[j], stream_));
+        H(hipEventRecord(eq[j], qs));
         if (j >= 1) {
             H(hipStreamWaitEvent(bstream_, eq[j - 1], 0));
             if (epi && st == KN_OK) exact(j - 1);
@@ -901,6 +930,10 @@ kn_status Engine::batch_graph(int L, hipGraphExec_t* out) {
     }
     H(hipEventRecord(join, bstream_));
     H(hipStreamWaitEvent(stream_, join, 0));
+    if (qst[1] != stream_) {
+        H(hipEventRecord(join2, qst[1]));
+        H(hipStreamWaitEvent(stream_, join2, 0));
+    }
     hipGraph_t g = nullptr;
     const hipError_t ee = hipStreamEndCapture(stream_, &g);
     if (st != KN_OK) {
@@ -917,6 +950,81 @@ kn_status Engine::batch_graph(int L, hipGraphExec_t* out) {
     return KN_OK;
 }
 
+// Eager batch (default, KN_BATCH_MODE=graph: the captured batch graphs below): the clouds go
+// through a second Pipeline over the same grid sets and streams in eager mode, one step_with()
+// per cloud -- copy-in + build on the build stream, queries alternating between the two query
+// streams (consecutive clouds' queries overlap as in the resident pipeline; a captured graph whose
+// queries alternate between two streams crashes the HIP runtime), rows
+// straight into the caller's buffers (set s's stages read bout_*_[s] when they are enqueued).
+kn_status Engine::stream_batch_eager(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist) {
+    kn_status st;
+    if (!bpipe_.ready()) {
+        auto b = [this](int s, hipStream_t st2) { return stage_build(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
+        auto q = [this](int s, hipStream_t st2) {
+            out_ovr_set_ = s;
+            const kn_status r = stage_query(s, st2);
+            out_ovr_set_ = -1;
+            return r == KN_OK ? hipSuccess : hipErrorUnknown;
+        };
+        Pipeline::Stage x;
+        if (!use_tree_ && exact_epilogue(cfg_.k))
+            x = [this](int s, hipStream_t st2) {
+                out_ovr_set_ = s;
+                const kn_status r = stage_exact(s, st2);
+                out_ovr_set_ = -1;
+                return r == KN_OK ? hipSuccess : hipErrorUnknown;
+            };
+        hipStream_t aux = pipe_.aux_stream();
+        if ((st = check(bpipe_.init(stream_, bstream_, b, q, x, false, aux ? 2 : 1, 2, aux), "batch pipeline init")) != KN_OK)
+            return st;
+        bpipe_.set_eager(true);
+    }
+    // the resident pipeline's last queries (joined into stream_ by launch_pipelined / stream_step)
+    // read the sets this batch rebuilds: its builds wait for stream_'s tail
+    if ((st = check(pipe_.unprime(), "pipeline")) != KN_OK) return st;
+    if (bev_.empty()) {
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(KN_ERR_DEVICE, "hipEventCreate");
+        bev_.push_back(ev);
+    }
+    if ((st = check(hipEventRecord(bev_[0], stream_), "batch event")) != KN_OK) return st;
+    if ((st = check(hipStreamWaitEvent(bstream_, bev_[0], 0), "batch event")) != KN_OK) return st;
+    const size_t bytes = (size_t)n_ * 12;
+    auto pre = [this, bytes, d_in, d_idx, d_dist](int j) {
+        const float* src = d_in[j];
+        unsigned* oi = d_idx[j];
+        float* od = d_dist ? d_dist[j] : nullptr;
+        return Pipeline::Stage([this, bytes, src, oi, od](int s, hipStream_t sd) {
+            bout_idx_[s] = oi;
+            bout_dist_[s] = od;
+            return bytes ? hipMemcpyAsync(set_[s].points, src, bytes, hipMemcpyDeviceToDevice, sd) : hipSuccess;
+        });
+    };
+    hipError_t e = hipSuccess;
+    for (int j = 0; j < m && e == hipSuccess; ++j) {
+        const Pipeline::Stage p = pre(j);
+        if (j + 1 < m) {
+            const Pipeline::Stage nx = pre(j + 1);
+            e = bpipe_.step_with(p, &nx);
+        } else {
+            e = bpipe_.step_with(p, nullptr);
+        }
+    }
+    // later work on either stream (getters, resident or stream steps) follows the batch
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream_, bpipe_.last_done(), 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(bstream_, bpipe_.last_done(), 0);
+    if (e != hipSuccess) {
+        drop_pipeline();
+        return check(e == hipErrorUnknown ? hipErrorLaunchFailure : e, "batch step");
+    }
+    view_set(bpipe_.last_set());
+    other_stale_ = true;
+    stream_mode_ = true;
+    solved_ = false;
+    stored_valid_ = points3_valid_ = false;
+    return KN_OK;
+}
+
 kn_status Engine::stream_batch(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist) {
     if (!built_) return fail(KN_ERR_STATE, "stream_batch() before prepare()");
     if (m < 0 || (m > 0 && (!d_in || !d_idx))) return fail(KN_ERR_INVALID_ARGUMENT, "stream_batch: null tables");
@@ -926,6 +1034,11 @@ kn_status Engine::stream_batch(int m, const float* const* d_in, unsigned* const*
     if (m == 0) return KN_OK;
     kn_status st;
     if ((st = ensure_pipeline()) != KN_OK) return st;
+    static const bool graph_mode = [] {
+        const char* v = std::getenv("KN_BATCH_MODE");
+        return v && std::string(v) == "graph";
+    }();
+    if (!graph_mode) return stream_batch_eager(m, d_in, d_idx, d_dist);
     if (!tab_ && (st = check(dmalloc(reinterpret_cast<void**>(&tab_), 3 * kBatchMax * sizeof(void*)), "hipMalloc(batch table)")) != KN_OK)
         return st;
     // everything the pipeline enqueued (a primed build, an epilogue) is done before the batch

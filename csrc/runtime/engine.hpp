@@ -171,6 +171,14 @@ private:
     void** tab_ = nullptr;
     std::unordered_map<int, hipGraphExec_t> bgraphs_;
     std::vector<hipEvent_t> bev_;
+    hipStream_t qstream2_ = nullptr;  // batch graphs: odd steps' queries (KN_BATCH_QSTREAMS=2)
+    // eager batch pipeline (stream_batch default): the same stages over the same grid sets and
+    // streams as pipe_, enqueued per step; a step's outputs are the caller's buffers of set s
+    Pipeline bpipe_;
+    unsigned* bout_idx_[2] = {nullptr, nullptr};
+    float* bout_dist_[2] = {nullptr, nullptr};
+    int out_ovr_set_ = -1;  // >= 0 while a batch stage of that set is enqueued
+    kn_status stream_batch_eager(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist);
     int out_ref_slot_ = -1;
     kn_status batch_graph(int L, hipGraphExec_t* out);
     void drop_batch();

@@ -35,7 +35,7 @@ unsigned order_event_flags() {
 }  // namespace
 
 hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r, bool capture_from_side,
-                          int query_streams, int sets) {
+                          int query_streams, int sets, hipStream_t aux) {
     reset();
     if (sets < 2 || sets > kMaxSets) return hipErrorInvalidValue;
     ns_ = sets;
@@ -63,8 +63,10 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
         // ms, the driver's 20 / 5 0.304 -> 0.297, K=50 0.766 -> 0.747; three interleaved passes,
         // profiles/ab_r5_stream_prio.txt)
         const char* ap = std::getenv("KN_PIPE_AUXPRIO");
-        if (ap && std::atoi(ap) == 0) KN_TRY(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, lo));
+        if (aux) aux_ = aux;
+        else if (ap && std::atoi(ap) == 0) KN_TRY(hipStreamCreateWithPriority(&aux_, hipStreamNonBlocking, lo));
         else KN_TRY(hipStreamCreateWithFlags(&aux_, hipStreamNonBlocking));
+        aux_owned_ = !aux;
         for (auto& e : evQS_) {
             KN_TRY(hipEventCreateWithFlags(&e, order_event_flags()));
             KN_TRY(hipEventRecord(e, main_));
@@ -92,8 +94,9 @@ void Pipeline::reset() {
     destroy(last_done_);
     if (aux_) {
         (void)hipStreamSynchronize(aux_);
-        (void)hipStreamDestroy(aux_);
+        if (aux_owned_) (void)hipStreamDestroy(aux_);
         aux_ = nullptr;
+        aux_owned_ = false;
     }
     for (auto& e : cap_ev_) destroy(e);
     cap_ev_.clear();

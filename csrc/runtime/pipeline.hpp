@@ -46,8 +46,12 @@ public:
     // step i-1's (with two query streams two queries are in flight; the build of the next step
     // then need not wait for the older of them). Unrolled graphs need 2 sets and one query stream.
     static constexpr int kMaxSets = 3;
+    // aux (query_streams = 2): an existing stream for the odd steps' queries (not owned, e.g. a
+    // second pipeline over the same grid sets sharing the first one's), else one is created
     hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage(),
-                    bool capture_from_side = false, int query_streams = 1, int sets = 2);
+                    bool capture_from_side = false, int query_streams = 1, int sets = 2,
+                    hipStream_t aux = nullptr);
+    hipStream_t aux_stream() const { return aux_; }
     int sets() const { return ns_; }
     bool ready() const { return main_ != nullptr; }
     // Enqueue `iters` resident-mode steps; unroll >= 2 (even): whole groups of `unroll` steps go
@@ -97,6 +101,7 @@ private:
 
     hipStream_t main_ = nullptr, side_ = nullptr;
     hipStream_t aux_ = nullptr;  // second query stream of the unrolled graphs (KN_PIPE_QSTREAMS=2)
+    bool aux_owned_ = false;
     bool capture_from_side_ = false;
     bool eager_ = false;
     int fallbacks_ = 0;
