@@ -1755,16 +1755,19 @@ template <int KT>
 hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     // margin slots beyond K: a query is lost to the exact path only if the K-th and (K+M)-th
     // distances collide within one truncation ulp (~2^-(23-SB)); M=3 makes that ~1e-7/query.
-    // The lane-walk kernel (the default) takes M = 1 above K = 32: at K = 50 one slot less per
-    // candidate outweighs the 3x longer exact list (900K uniform: 0.967 -> 0.884 ms/step, 110 ->
-    // 360 exact queries; at K = 16 M = 1 loses, 0.294 -> 0.329; profiles/ab_r4_tiles_margin.txt).
-    // The union-stream and staging-free kernels keep M = 2 (the stream kernel's rows differ from
-    // the oracle with M = 1 at K = 50). KN_TOPK_MARGIN=m forces m for the lane walk.
+    // Round 4 gave the lane-walk kernel (the default) M = 1 above K = 32: at K = 50 one slot less
+    // per candidate outweighed the 3x longer exact list then (900K uniform: 0.967 -> 0.884
+    // ms/step, 110 -> 360 exact queries; profiles/ab_r4_tiles_margin.txt); at K = 16 M = 1 loses,
+    // 0.294 -> 0.329. The union-stream and staging-free kernels keep M = 2 (the stream kernel's
+    // rows differ from the oracle with M = 1 at K = 50). KN_TOPK_MARGIN=m forces m for the lane walk.
 #ifndef KN_TOPK_MARGIN
 #define KN_TOPK_MARGIN -1
 #endif
     constexpr int M = 2;
-    constexpr int ML = KN_TOPK_MARGIN >= 0 ? KN_TOPK_MARGIN : (KT > 32 ? 1 : 2);
+    // Round 5: with two query streams the longer exact list of M = 1 no longer pays for the slot
+    // it saves: M = 2 at K = 50 0.748 -> 0.736 ms (110 instead of 360 exact queries), K = 64
+    // 0.949 -> 0.917 (profiles/ab_r5_k50.txt)
+    constexpr int ML = KN_TOPK_MARGIN >= 0 ? KN_TOPK_MARGIN : 2;
     const int X = q.dims[0], Y = q.dims[1], Z = q.dims[2];
     hipError_t e = hipSuccess;
     if (q.exact_mode != 2 && !q.counters_zeroed &&

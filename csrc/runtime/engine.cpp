@@ -652,14 +652,17 @@ kn_status Engine::stage_build(int s, hipStream_t st) {
 // profiles/ab_r4_exact_k50.txt); K=32 0.518 -> 0.500 (profiles/ab_r4_m1_epilogue.txt). At K=16
 // and K=24 it loses (0.2946 -> 0.2976, 0.396 -> 0.403; r3: 0.2954 -> 0.3016,
 // profiles/r4_ab_exact.txt): the extra cross-stream dependency and the exact kernel's workgroups
-// competing with the next query cost more than the few us of exact work. KN_PIPE_EXACT=0 / 1
-// forces it off / on.
+// competing with the next query cost more than the few us of exact work. Round 5 (two query
+// streams, two margin slots at every K): above K = 40 the exact finish on the query stream
+// overlaps the next step's query on the other query stream and wins again (900K K=50 100 / 30
+// steps 0.7358 -> 0.7276 ms, K=64 equal; profiles/ab_r5_k50.txt), so the epilogue covers the
+// buckets 25..40. KN_PIPE_EXACT=0 / 1 forces it off / on.
 bool exact_epilogue(int k) {
     static const int mode = [] {
         const char* v = std::getenv("KN_PIPE_EXACT");
         return v ? std::atoi(v) : -1;
     }();
-    return mode == 1 || (mode < 0 && k > 24 && k <= 64);
+    return mode == 1 || (mode < 0 && k > 24 && k <= 40);
 }
 
 kn_status Engine::stage_query(int s, hipStream_t st) {
