@@ -20,7 +20,11 @@ namespace {
 
 constexpr unsigned SENT = 0xFFFFFFFFu;
 constexpr int kLeafBits = KN_TREE_LEAF_BITS;  // kTreeLeaf = 32 points per leaf (default)
-constexpr int kVisitBits = 13 - kLeafBits;    // key slot = visit index | point in leaf: 13 bits
+#ifndef KN_TREE_SLOT_BITS
+#define KN_TREE_SLOT_BITS 13
+#endif
+constexpr int kVisitBits = KN_TREE_SLOT_BITS - kLeafBits;  // key slot = visit index | point in leaf
+static_assert(kLeafBits <= 6, "a leaf is scanned by one wave (<= 64 points)");
 constexpr int kMaxVisit = 1 << kVisitBits;    // leaves a wave may visit before its queries go exact
 constexpr unsigned kMask = (1u << (kVisitBits + kLeafBits)) - 1u;
 static_assert((1 << kLeafBits) == kTreeLeaf, "leaf size");
@@ -740,9 +744,9 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
         };
         // A finite bound (listed queries: the (K+1)-th truncated key, rounded up) is already tight:
         // sweep the tree breadth-first, 64 nodes per step (one dependent global round per level
-        // instead of per node), collect the leaves within the bound, then scan them two per step
-        // (a half-wave per leaf). The kept set is order-independent (the bound only ever tightens to
-        // a K-th distance found, ties break by id), so rows equal the depth-first walk's. A
+        // instead of per node), collect the leaves within the bound, then scan them 64 / kTreeLeaf
+        // per step (one lane per point). The kept set is order-independent (the bound only ever
+        // tightens to a K-th distance found, ties break by id), so rows equal the depth-first walk's. A
         // frontier or leaf list past kFrontier falls back to that walk.
         bool dfs = !(thr < INFINITY);
         if (!dfs) {
@@ -787,15 +791,17 @@ __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
                 ncur = nn;
             }
             if (!dfs) {
-                const int half = lane >> 5, sub = lane & 31;
-                for (int j = 0; j < nleaf; j += 2) {
+                // 64 / kTreeLeaf leaves per step, one lane per point
+                constexpr int LPS = 64 / kTreeLeaf;
+                const int grp = lane / kTreeLeaf, sub = lane % kTreeLeaf;
+                for (int j = 0; j < nleaf; j += LPS) {
                     if (cnt + 64 > kTCap) compact();
                     bool pass = false;
                     unsigned long long key = 0;
-                    if (j + half < nleaf) {
-                        const int lf = lfl[j + half];
+                    if (j + grp < nleaf) {
+                        const int lf = lfl[j + grp];
                         const int p = (int)a.leaf_start[lf] + sub;
-                        if (sub < kTreeLeaf && p < (int)a.leaf_start[lf + 1] && (unsigned)p != qpos) {
+                        if (p < (int)a.leaf_start[lf + 1] && (unsigned)p != qpos) {
                             const float4 c = a.pts[KN_IDX(p, a.n, 416)];
                             const float dx = c.x - qx, dy = c.y - qy, dz = c.z - qz;
                             const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
