@@ -153,6 +153,9 @@ def run_native(args) -> dict:
     launch(args.warmup)
     e.sync()
     log("warmup done")
+    gap = float(os.environ.get("KN_BENCH_GAP_MS", "0"))  # diagnostics: idle gap before the timed steps
+    if gap > 0:
+        time.sleep(gap / 1e3)
     t0 = time.perf_counter()
     launch(args.steps)
     e.sync()

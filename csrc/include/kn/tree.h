@@ -37,8 +37,12 @@
 
 namespace kn {
 
+// Leaves of <= 64 points (round 5; 32 before): half the traversal rounds for the latency-bound
+// query waves, one 64-lane load per leaf visit. 900K, pipelined: clustered K=16 1.193 -> 1.096
+// ms, surfaces 0.751 -> 0.744, clustered K=50 4.30 -> 3.78 (more waves pass the 128-leaf visit
+// cap and finish in the exact kernel: 2,135 -> 8,145 queries); profiles/ab_r5_tree_leaf64.txt.
 #ifndef KN_TREE_LEAF_BITS
-#define KN_TREE_LEAF_BITS 5
+#define KN_TREE_LEAF_BITS 6
 #endif
 constexpr int kTreeLeaf = 1 << KN_TREE_LEAF_BITS;  // points per leaf (at most)
 

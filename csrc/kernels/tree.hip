@@ -19,7 +19,7 @@ namespace kn {
 namespace {
 
 constexpr unsigned SENT = 0xFFFFFFFFu;
-constexpr int kLeafBits = KN_TREE_LEAF_BITS;  // kTreeLeaf = 32 points per leaf (default)
+constexpr int kLeafBits = KN_TREE_LEAF_BITS;  // kTreeLeaf = 64 points per leaf (default)
 #ifndef KN_TREE_SLOT_BITS
 #define KN_TREE_SLOT_BITS 13
 #endif
