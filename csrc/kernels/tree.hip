@@ -433,11 +433,20 @@ __global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, 
 }
 
 // ---- query: one wave per 64 consecutive points of the Morton order (lanes = queries) -------------
-// (Round 4: asking the compiler for 6 / 8 waves per SIMD at K <= 16 (82 -> 80 / 64 VGPRs, 3 / 12
-// spilled) was mixed -- clustered 1.440 -> 1.422 / 1.404 ms, surfaces 0.825 -> 0.854 / 0.853;
-// profiles/ab_r4_tree_waves.txt -- and is not used.)
+// (Round 4, 32-point leaves: asking the compiler for 6 / 8 waves per SIMD at K <= 16 (82 -> 80 / 64
+// VGPRs, 3 / 12 spilled) was mixed -- clustered 1.440 -> 1.422 / 1.404 ms, surfaces 0.825 -> 0.854 /
+// 0.853; profiles/ab_r4_tree_waves.txt. Round 5, 64-point leaves: 8 waves wins, KN_TREE_WPE.)
+// Waves per SIMD requested for the K <= 16 buckets (a VGPR cap: K=16 82 -> 64 VGPRs, 12 spilled).
+// With 64-point leaves the latency-bound traversal gains from the occupancy: 900K, pipelined,
+// clustered K=16 1.098 -> 1.041 ms, surfaces 0.742 -> 0.717, K=8 unchanged (6 waves: +0..2 %;
+// profiles/ab_r5_tree_waves.txt; with 32-point leaves it was mixed, round 4). KN_TREE_WPE=1: no cap.
+#ifndef KN_TREE_WPE
+#define KN_TREE_WPE 8
+#endif
+template <int KT>
+constexpr int tree_wpe() { return KT <= 16 ? KN_TREE_WPE : 1; }
 template <int KT, int M>
-__global__ __launch_bounds__(256) void knn_tree_kernel(TArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(tree_wpe<KT>(), 8))) void knn_tree_kernel(TArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
     // stream of clouds); locals, so the kernel argument block stays read-only
     unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;

@@ -16,7 +16,7 @@ for v in base $VARS; do
   if [ $v = base ]; then unset KN_C_VARIANT; else export KN_C_VARIANT=$v; fi
   one "$v clustered k16" --gen clustered --n 900000 --k 16 --steps 60 --warmup 20
   one "$v surface k16" --gen surface --n 900000 --k 16 --steps 60 --warmup 20
-  one "$v clustered k50" --gen clustered --n 900000 --k 50 --steps 20 --warmup 10
+  one "$v clustered k8" --gen clustered --n 900000 --k 8 --steps 60 --warmup 20
 done
 done
 sort $O/ab.txt
