@@ -274,8 +274,16 @@ __device__ __forceinline__ void tile_coords(int lin, int ntx, int nty, int ntz, 
 // block -- centre-out over the (2H+1)^2 row offsets around its cell, x-range cut by its own
 // bound -- as a divergent loop with per-lane LDS gathers. ~90 candidates per query instead of
 // the ~535 the union stream feeds every lane, at the price of divergent trip counts.
+// Waves per SIMD requested for the K > 50 buckets (a VGPR cap: 145 -> 128 VGPRs, 13 spilled): the
+// LDS plan allows 4 workgroups per CU, the registers 3 without the cap. 900K K=64 0.909 -> 0.848
+// ms/step (profiles/ab_r5_tree_waves.txt). KN_TILE_WPE64=1: no cap.
+#ifndef KN_TILE_WPE64
+#define KN_TILE_WPE64 4
+#endif
+template <int KT>
+constexpr int tile_wpe() { return KT > 50 ? KN_TILE_WPE64 : 1; }
 template <int KT, int M, bool LANE, bool WIDE = false>
-__global__ __launch_bounds__(kWG) void knn_tile_kernel(TileArgs a) {
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT>(), 8))) void knn_tile_kernel(TileArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
     // stream of clouds); locals, so the kernel argument block stays read-only
     unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;

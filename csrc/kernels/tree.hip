@@ -443,8 +443,29 @@ __global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, 
 #ifndef KN_TREE_WPE
 #define KN_TREE_WPE 8
 #endif
+// K=24 / K=32 buckets: 5 / 4 waves (114 -> 96 VGPRs, 7 spilled; 146 -> 128, 5 spilled): clustered
+// K=24 1.368 -> 1.296 ms, K=32 1.893 -> 1.672, surfaces K=32 1.022 -> 0.995 (profiles/ab_r5_tree_waves.txt)
+#ifndef KN_TREE_WPE24
+#define KN_TREE_WPE24 5
+#endif
+#ifndef KN_TREE_WPE32
+#define KN_TREE_WPE32 4
+#endif
+// K=40 / K=50 buckets: 3 waves (178 / 222 -> 168 VGPRs, 3 / 25 spilled): clustered K=40 3.09 -> 2.38
+// ms, K=50 3.80 -> 2.82, surfaces K=50 1.96 -> 1.56 (profiles/ab_r5_tree_waves.txt)
+#ifndef KN_TREE_WPE50
+#define KN_TREE_WPE50 3
+#endif
+// K=64 bucket: 2 waves (259 -> 256 VGPRs, 3 spilled): clustered K=64 8.78 -> 5.02 ms, surfaces
+// 4.64 -> 2.65
+#ifndef KN_TREE_WPE64
+#define KN_TREE_WPE64 2
+#endif
 template <int KT>
-constexpr int tree_wpe() { return KT <= 16 ? KN_TREE_WPE : 1; }
+constexpr int tree_wpe() {
+    return KT <= 16 ? KN_TREE_WPE
+                    : KT <= 24 ? KN_TREE_WPE24 : KT <= 32 ? KN_TREE_WPE32 : KT <= 50 ? KN_TREE_WPE50 : KN_TREE_WPE64;
+}
 template <int KT, int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(tree_wpe<KT>(), 8))) void knn_tree_kernel(TArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
