@@ -1335,9 +1335,17 @@ void handler(int sig, siginfo_t* info, void*) {
     char buf[64];
     const int n = std::snprintf(buf, sizeof(buf), "signal %d, fault address %p\n", sig, info ? info->si_addr : nullptr);
     if (n > 0) (void)!write(2, buf, (size_t)n);
-    void* frames[64];
-    const int nf = backtrace(frames, 64);
-    backtrace_symbols_fd(frames, nf, 2);
+    // innermost frames and the outermost ones (a runaway recursion fills the middle)
+    static void* frames[1 << 16];
+    const int nf = backtrace(frames, 1 << 16);
+    if (nf <= 64) {
+        backtrace_symbols_fd(frames, nf, 2);
+    } else {
+        backtrace_symbols_fd(frames, 8, 2);
+        const int m = std::snprintf(buf, sizeof(buf), "... %d frames ...\n", nf - 48);
+        if (m > 0) (void)!write(2, buf, (size_t)m);
+        backtrace_symbols_fd(frames + nf - 40, 40, 2);
+    }
     sigaction(sig, &g_prev[sig], nullptr);
     raise(sig);
 }
@@ -1346,6 +1354,14 @@ bool install() {
     if (done) return true;
     void* warm[2];
     (void)backtrace(warm, 2);  // loads libgcc's unwinder now, not inside the handler
+    // an alternate signal stack for the calling (main) thread: a fault from unbounded recursion
+    // (the HIP / RCCL capture crashes of round 5) leaves no stack for the handler otherwise
+    static std::vector<char> alt(1 << 18);
+    stack_t ss;
+    std::memset(&ss, 0, sizeof(ss));
+    ss.ss_sp = alt.data();
+    ss.ss_size = alt.size();
+    (void)sigaltstack(&ss, nullptr);
     struct sigaction sa;
     std::memset(&sa, 0, sizeof(sa));
     sa.sa_sigaction = handler;
