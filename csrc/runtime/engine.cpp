@@ -1041,7 +1041,7 @@ kn_status Engine::stream_batch(int m, const float* const* d_in, unsigned* const*
         const char* v = std::getenv("KN_BATCH_MODE");
         return v && std::string(v) == "graph";
     }();
-    if (!graph_mode) return stream_batch_eager(m, d_in, d_idx, d_dist);
+    if (!(batch_mode_ >= 0 ? batch_mode_ == 1 : graph_mode)) return stream_batch_eager(m, d_in, d_idx, d_dist);
     if (!tab_ && (st = check(dmalloc(reinterpret_cast<void**>(&tab_), 3 * kBatchMax * sizeof(void*)), "hipMalloc(batch table)")) != KN_OK)
         return st;
     // everything the pipeline enqueued (a primed build, an epilogue) is done before the batch

@@ -84,6 +84,8 @@ public:
     // grid of the last step stays (stats, stored-space views of the last cloud).
     static constexpr int kBatchMax = kPtrTableMax / 3;
     kn_status stream_batch(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist);
+    // stream_batch mode: 0 eager batch pipeline, 1 captured batch graphs, -1 KN_BATCH_MODE (default eager)
+    void set_batch_mode(int mode) { batch_mode_ = mode; }
     kn_status sync();  // both streams
     // Device-to-device copy of the original-space results into caller buffers.
     kn_status copy_results(unsigned* d_idx, float* d_dist);
@@ -178,6 +180,7 @@ private:
     unsigned* bout_idx_[2] = {nullptr, nullptr};
     float* bout_dist_[2] = {nullptr, nullptr};
     int out_ovr_set_ = -1;  // >= 0 while a batch stage of that set is enqueued
+    int batch_mode_ = -1;
     kn_status stream_batch_eager(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist);
     int out_ref_slot_ = -1;
     kn_status batch_graph(int L, hipGraphExec_t* out);

@@ -1153,8 +1153,13 @@ public:
     // a batch of distinct clouds (kn::Engine::stream_batch): points[j] (N, 3) float32 GPU ->
     // idx[j] (N, K) int32 and d2[j] (N, K) float32 (optional) in original space. Asynchronous on
     // the engine's streams: call sync() before reading the outputs.
+    // mode: "eager" (default: the eager batch pipeline) or "graph" (captured batch graphs)
     void stream_batch(std::vector<torch::Tensor> points, std::vector<torch::Tensor> idx,
-                      c10::optional<std::vector<torch::Tensor>> d2) {
+                      c10::optional<std::vector<torch::Tensor>> d2, c10::optional<std::string> mode) {
+        if (mode.has_value()) {
+            TORCH_CHECK(*mode == "eager" || *mode == "graph", "stream_batch: mode is 'eager' or 'graph'");
+            e_->set_batch_mode(*mode == "graph" ? 1 : 0);
+        }
         const size_t m = points.size();
         TORCH_CHECK(idx.size() == m && (!d2.has_value() || d2->size() == m), "one output per cloud");
         std::vector<const float*> in(m);
@@ -1749,7 +1754,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("launch_graph", &PyEngine::launch_graph, py::arg("iters") = 1)
         .def("launch_pipelined", &PyEngine::launch_pipelined, py::arg("iters") = 1, py::arg("unroll") = -1)
         .def("stream_step", &PyEngine::stream_step, py::arg("points"), py::arg("next") = py::none())
-        .def("stream_batch", &PyEngine::stream_batch, py::arg("points"), py::arg("idx"), py::arg("d2") = py::none())
+        .def("stream_batch", &PyEngine::stream_batch, py::arg("points"), py::arg("idx"), py::arg("d2") = py::none(),
+             py::arg("mode") = py::none())
         .def("get_permutation", &PyEngine::permutation)
         .def("sync", &PyEngine::sync)
         .def("results", &PyEngine::results)

@@ -221,14 +221,16 @@ def test_engine_stream_of_clouds(cuda, unroll):
     _check(clouds[-1], idx, d2, k)
 
 
-@pytest.mark.parametrize("k,gen", [(16, "uniform"), (50, "uniform"), (16, "clustered")])
-def test_engine_stream_batch(cuda, k, gen):
-    """kn::Engine::stream_batch: a batch of DISTINCT clouds through one graph per power-of-two
-    chunk (copy-in + build on the build stream, queries on the main stream, pointer table
-    written per launch); every step's rows, written straight into the caller's buffers, equal
-    the kd-tree oracle's on its own cloud. K=50 runs the exact finish as the side-stream epilogue,
-    clustered clouds the tree path. 11 steps = chunks of 8, 2 and 1; a resident pipelined launch
-    and a stream step afterwards still solve their clouds."""
+@pytest.mark.parametrize("mode", ["eager", "graph"])
+@pytest.mark.parametrize("k,gen", [(16, "uniform"), (50, "uniform"), (32, "uniform"), (16, "clustered")])
+def test_engine_stream_batch(cuda, k, gen, mode):
+    """kn::Engine::stream_batch: a batch of DISTINCT clouds, every step's rows written straight
+    into the caller's buffers and equal to the kd-tree oracle's on its own cloud. mode "eager"
+    (default): a second pipeline over the same grid sets, one step_with() per cloud, queries
+    alternating between the two query streams; "graph": one captured graph per power-of-two chunk
+    (pointer table written per launch; 11 steps = chunks of 8, 2 and 1). K=32 runs the exact finish
+    as the build-stream epilogue, K=50 on the query stream, clustered clouds the tree path; a
+    resident pipelined launch and a stream step afterwards still solve their clouds."""
     from cuda_knearests_amd._ext import load
     from cuda_knearests_amd.utils import clustered_cloud
 
@@ -242,12 +244,12 @@ def test_engine_stream_batch(cuda, k, gen):
     e.launch_pipelined(4, 2)  # a primed resident pipeline first
     idx = [torch.empty(n, k, dtype=torch.int32, device=cuda) for _ in clouds]
     d2 = [torch.empty(n, k, dtype=torch.float32, device=cuda) for _ in clouds]
-    e.stream_batch(clouds, idx, d2)
+    e.stream_batch(clouds, idx, d2, mode=mode)
     e.sync()
     for j, c in enumerate(clouds):
         _check(c, idx[j], d2[j], k)
-    # a second batch reuses the captured graphs (and the same output buffers)
-    e.stream_batch(clouds[::-1][:3], idx[:3], d2[:3])
+    # a second batch reuses the pipeline / captured graphs (and the same output buffers)
+    e.stream_batch(clouds[::-1][:3], idx[:3], d2[:3], mode=mode)
     e.sync()
     for j, c in enumerate(clouds[::-1][:3]):
         _check(c, idx[j], d2[j], k)
