@@ -607,26 +607,30 @@ void Engine::drop_pipeline(bool keep_grid) {
         bstream_ = nullptr;
         for (auto& e : pev_) e = nullptr;
     }
-    if (live_ == 1) {
-        // the live grid sits in arena2_, which is about to go back to the block cache: copy it (with
-        // its input points) to arena_ when it is still needed, view set 0 again and drop the graph
-        // captured against set 1
+    if (live_ != 0) {
+        // the live grid sits in arena2_ / arena3_, which is about to go back to the block cache:
+        // copy it (with its input points) to arena_ when it is still needed, view set 0 again and
+        // drop the graph captured against the live set
         if (graph_) { (void)hipGraphExecDestroy(graph_); graph_ = nullptr; }
-        if (keep_grid && arena2_ && arena_used_)
-            (void)hipMemcpyAsync(arena_, arena2_, arena_used_, hipMemcpyDeviceToDevice, stream_);
-        // the live tree and result buffers (same sizes in both sets) stay with the live view
-        std::swap(set_[0].tree_ws, set_[1].tree_ws);
-        std::swap(set_[0].tree_nodes, set_[1].tree_nodes);
-        std::swap(set_[0].out_idx, set_[1].out_idx);
-        std::swap(set_[0].out_dist, set_[1].out_dist);
+        char* src = live_ == 1 ? arena2_ : arena3_;
+        if (keep_grid && src && arena_used_)
+            (void)hipMemcpyAsync(arena_, src, arena_used_, hipMemcpyDeviceToDevice, stream_);
+        // the live tree and result buffers (same sizes in every set) stay with the live view
+        std::swap(set_[0].tree_ws, set_[live_].tree_ws);
+        std::swap(set_[0].tree_nodes, set_[live_].tree_nodes);
+        std::swap(set_[0].out_idx, set_[live_].out_idx);
+        std::swap(set_[0].out_dist, set_[live_].out_dist);
         view_set(0);
     }
     if (arena2_) { dfree(arena2_); arena2_ = nullptr; }  // dfree waits for stream_ (the copy)
-    if (set_[1].tree_ws) dfree(set_[1].tree_ws);
-    if (set_[1].tree_nodes) dfree(set_[1].tree_nodes);
-    if (set_[1].out_idx) dfree(set_[1].out_idx);
-    if (set_[1].out_dist) dfree(set_[1].out_dist);
-    set_[1] = GridSet{};
+    if (arena3_) { dfree(arena3_); arena3_ = nullptr; }
+    for (int s = 1; s < 3; ++s) {
+        if (set_[s].tree_ws) dfree(set_[s].tree_ws);
+        if (set_[s].tree_nodes) dfree(set_[s].tree_nodes);
+        if (set_[s].out_idx) dfree(set_[s].out_idx);
+        if (set_[s].out_dist) dfree(set_[s].out_dist);
+        set_[s] = GridSet{};
+    }
     set_[0] = members();
     other_stale_ = true;
 }
@@ -699,46 +703,87 @@ kn_status Engine::stage_exact(int s, hipStream_t st) {
     return r;
 }
 
-// The second grid set (same carve as allocate(), its own input points) + the build stream +
-// the pipeline's stage graphs.
+// Grid set s carved from base (the carve of allocate(), its own input points).
+kn_status Engine::carve_set(int s, char* base) {
+    const int C = C_, n = n_;
+    const size_t nb = scan_block_count(C) + 1;
+    char* p = base;
+    GridSet& g = set_[s];
+    g.points = carve<float>(p, (size_t)n * 3);
+    g.bbox = carve<unsigned>(p, kBBoxWords);
+    g.geom = carve<GridGeom>(p, 1);
+    g.cell_count = carve<int>(p, C + 1);
+    g.cell_scan = carve<int>(p, C + 1);
+    g.cell_start = carve<int>(p, C + 1);
+    g.block_sums = carve<int>(p, nb);
+    g.bin_tmp = carve<float4>(p, n);
+    g.cell_rank = reinterpret_cast<int2*>(g.bin_tmp);
+    g.sorted = carve<float4>(p, n);
+    g.perm = carve<unsigned>(p, n);
+    g.fallback = carve<unsigned>(p, n);
+    g.counters = carve<unsigned>(p, kNumCounters);
+    g.occ = carve<unsigned long long>(p, 1);
+    g.tree_ws = g.tree_nodes = nullptr;
+    g.out_idx = nullptr;
+    g.out_dist = nullptr;
+    if (use_tree_) {
+        kn_status st;
+        if ((st = check(dmalloc(&g.tree_ws, tree_workspace_bytes(n_, ap_.dims)), "hipMalloc(tree 2)")) != KN_OK ||
+            (st = check(dmalloc(&g.tree_nodes, tree_node_bytes(n_)), "hipMalloc(tree nodes 2)")) != KN_OK)
+            return st;
+    }
+    return KN_OK;
+}
+
+// The other grid sets + the build stream + the pipeline's stage graphs.
 kn_status Engine::ensure_pipeline() {
     kn_status st;
     if ((st = ensure_outputs()) != KN_OK) return st;
     set_[live_] = members();  // tree buffers allocated since the last carve
-    if (!arena2_) {
-        if ((st = check(dmalloc(&arena2_, arena_bytes_), "hipMalloc(grid set 2)")) != KN_OK) return st;
-        const int C = C_, n = n_;
-        const size_t nb = scan_block_count(C) + 1;
-        char* p = arena2_;
-        GridSet& g = set_[live_ ^ 1];
-        g.points = carve<float>(p, (size_t)n * 3);
-        g.bbox = carve<unsigned>(p, kBBoxWords);
-        g.geom = carve<GridGeom>(p, 1);
-        g.cell_count = carve<int>(p, C + 1);
-        g.cell_scan = carve<int>(p, C + 1);
-        g.cell_start = carve<int>(p, C + 1);
-        g.block_sums = carve<int>(p, nb);
-        g.bin_tmp = carve<float4>(p, n);
-        g.cell_rank = reinterpret_cast<int2*>(g.bin_tmp);
-        g.sorted = carve<float4>(p, n);
-        g.perm = carve<unsigned>(p, n);
-        g.fallback = carve<unsigned>(p, n);
-        g.counters = carve<unsigned>(p, kNumCounters);
-        g.occ = carve<unsigned long long>(p, 1);
-        g.tree_ws = g.tree_nodes = nullptr;
-        if (use_tree_) {
-            if ((st = check(dmalloc(&g.tree_ws, tree_workspace_bytes(n_, ap_.dims)), "hipMalloc(tree 2)")) != KN_OK ||
-                (st = check(dmalloc(&g.tree_nodes, tree_node_bytes(n_)), "hipMalloc(tree nodes 2)")) != KN_OK) {
-                drop_pipeline();
-                return st;
-            }
+    // Two query streams (default; KN_PIPE_QSTREAMS=1: one): odd steps' queries on a second
+    // stream, so step i+1's queries start as soon as its build is done instead of after step
+    // i's last workgroup and the kernel boundary (~15 us per step inside a 10-step graph,
+    // profiles/r4_pipe_unroll.txt). 900K K=16, interleaved processes on one box: 200 steps
+    // 0.2894 -> 0.2756 ms, the driver's 20 / 5 0.3080 -> 0.3048 (profiles/r5_qstreams.txt)
+    static const int qstreams = [] {
+        const char* v = std::getenv("KN_PIPE_QSTREAMS");
+        return v ? std::atoi(v) : 2;
+    }();
+    if (!pipe_.ready()) {
+        // Three grid sets with two query streams (KN_PIPE_SETS=2: two): step i+1's build then
+        // waits for step i-2's query instead of step i-1's, which still runs beside step i's; with
+        // two sets the build (~170 us beside a query) ran only after step i-1's query ended and
+        // step i+1's query started after step i's, leaving the GPU without any query kernel 10 %
+        // of the time (rocprof, gpurun_out/r5engprof2). Needs one more set in memory: only when it
+        // fits comfortably.
+        static const int sets_env = [] {
+            const char* v = std::getenv("KN_PIPE_SETS");
+            return v ? std::atoi(v) : 3;
+        }();
+        nsets_ = 2;
+        if (qstreams >= 2 && sets_env >= 3) {
+            size_t fr = 0, tot = 0;
+            const size_t need = arena_bytes_ + 2 * std::max<size_t>(1, (size_t)n_ * cfg_.k) * sizeof(float) +
+                                (use_tree_ ? tree_workspace_bytes(n_, ap_.dims) + tree_node_bytes(n_) : 0);
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && need < fr / 4) nsets_ = 3;
+        }
+    }
+    for (int s = 1; s < nsets_; ++s) {
+        char*& ar = s == 1 ? arena2_ : arena3_;
+        if (ar) continue;
+        if ((st = check(dmalloc(&ar, arena_bytes_), s == 1 ? "hipMalloc(grid set 2)" : "hipMalloc(grid set 3)")) != KN_OK)
+            return st;
+        if ((st = carve_set(s, ar)) != KN_OK) {
+            drop_pipeline();
+            return st;
         }
         other_stale_ = true;
     }
-    {
-        // the other set's results (per-set outputs: the exact finish of step i runs while step
+    for (int s = 0; s < nsets_; ++s) {
+        // the other sets' results (per-set outputs: the exact finish of step i runs while step
         // i+1 queries)
-        GridSet& g = set_[live_ ^ 1];
+        if (s == live_) continue;
+        GridSet& g = set_[s];
         const size_t nk = std::max<size_t>(1, (size_t)n_ * cfg_.k);
         if (!g.out_idx && (st = check(dmalloc(&g.out_idx, nk * sizeof(unsigned)), "hipMalloc(knn 2)")) != KN_OK) return st;
         if (cfg_.with_distances && !g.out_dist &&
@@ -759,16 +804,8 @@ kn_status Engine::ensure_pipeline() {
         Pipeline::Stage x;
         if (!use_tree_ && exact_epilogue(cfg_.k))  // the tree query finishes its own exact-path queries
             x = [this](int s, hipStream_t st2) { return stage_exact(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
-        // Two query streams (default; KN_PIPE_QSTREAMS=1: one): odd sets' queries on a second
-        // stream, so step i+1's queries start as soon as its build is done instead of after step
-        // i's last workgroup and the kernel boundary (~15 us per step inside a 10-step graph,
-        // profiles/r4_pipe_unroll.txt). 900K K=16, interleaved processes on one box: 200 steps
-        // 0.2894 -> 0.2756 ms, the driver's 20 / 5 0.3080 -> 0.3048 (profiles/r5_qstreams.txt)
-        static const int qstreams = [] {
-            const char* v = std::getenv("KN_PIPE_QSTREAMS");
-            return v ? std::atoi(v) : 2;
-        }();
-        if ((st = check(pipe_.init(stream_, bstream_, b, q, x, false, qstreams), "pipeline init")) != KN_OK) return st;
+        if ((st = check(pipe_.init(stream_, bstream_, b, q, x, false, qstreams, nsets_), "pipeline init")) != KN_OK)
+            return st;
     }
     return KN_OK;
 }
@@ -793,9 +830,11 @@ kn_status Engine::launch_pipelined(int iters, int unroll) {
         // the other set's input takes the live cloud (resident mode: both sets bin it); the
         // primed build of a previous stream read other points
         if ((st = check(pipe_.unprime(), "pipeline")) != KN_OK) return st;
-        if (n_ > 0 && (st = check(hipMemcpyAsync(set_[live_ ^ 1].points, points_, (size_t)n_ * 12,
-                                                 hipMemcpyDeviceToDevice, stream_), "D2D points")) != KN_OK)
-            return st;
+        for (int s = 0; s < nsets_; ++s)
+            if (s != live_ && n_ > 0 &&
+                (st = check(hipMemcpyAsync(set_[s].points, points_, (size_t)n_ * 12, hipMemcpyDeviceToDevice, stream_),
+                            "D2D points")) != KN_OK)
+                return st;
         if ((st = check(hipStreamSynchronize(stream_), "sync")) != KN_OK) return st;
         other_stale_ = false;
     }

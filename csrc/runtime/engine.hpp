@@ -138,9 +138,10 @@ private:
     QueryBuffers query_buffers() const;
     BuildBuffers build_buffers() const;
     void release();
-    // pipelined steps (pipeline.hpp): two grid sets, set 0 carved from arena_, set 1 from arena2_
-    // (same carve, input points included); the members above always view the LIVE set (the one
-    // the last step queried), so getters, stats and serial steps see the last step's grid
+    // pipelined steps (pipeline.hpp): two or three grid sets, set 0 carved from arena_, set 1 from
+    // arena2_, set 2 from arena3_ (same carve, input points included); the members above always
+    // view the LIVE set (the one the last step queried), so getters, stats and serial steps see the
+    // last step's grid
     struct GridSet {
         float* points; unsigned* bbox; GridGeom* geom; int* cell_count; int* cell_scan; int* block_sums;
         int* cell_start; int2* cell_rank; float4* bin_tmp; float4* sorted; unsigned* perm; unsigned* fallback;
@@ -158,12 +159,15 @@ private:
     kn_status stage_exact(int s, hipStream_t st);  // the fallback list's exact finish (epilogue)
     // keep_grid: the live grid (maybe in arena2_) must survive into arena_ (set_k keeps solving it)
     void drop_pipeline(bool keep_grid = false);
-    GridSet set_[2]{};
+    GridSet set_[3]{};
+    int nsets_ = 2;            // grid sets of the resident pipeline (3 with two query streams)
+    kn_status carve_set(int s, char* base);
     int live_ = 0;             // set the members view
     int graph_set_ = -1;       // set graph_ was captured against
-    bool other_stale_ = true;  // set live_^1's input differs from the live input
+    bool other_stale_ = true;  // another set's input differs from the live input
     bool stream_mode_ = false; // the last pipelined steps were stream_step()s (distinct clouds)
     char* arena2_ = nullptr;
+    char* arena3_ = nullptr;
     hipStream_t bstream_ = nullptr;
     hipEvent_t pev_[4] = {nullptr, nullptr, nullptr, nullptr};  // the side stream's pooled events
     Pipeline pipe_;
