@@ -772,13 +772,20 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         const size_t T = (size_t)bp.nbuckets * bp.nblocks;
         // global ids fused into the sort unless the in-cell order pass follows (it orders by w)
         const bool fuse_gid = b.gids && !b.deterministic;
-        // streaming blocks of 1024 threads: ~220 blocks at 900K points is one block per CU, so
-        // the LDS-atomic loops need 16 waves per CU to hide their latency (KN_BIN_THREADS A/B)
-        static const int bin_threads = [] {
+        // Streaming blocks of 256 threads up to 4M points, 1024 above (KN_BIN_THREADS overrides).
+        // Serially 1024 is faster (~220 blocks at 900K points is one block per CU, and the
+        // LDS-atomic loops need 16 waves per CU: 900K build 0.050 vs 0.054 ms), but the pipelined
+        // build runs beside one or two query kernels, where a 1024-thread block must find 16 free
+        // wave slots on one CU and waits: 900K K=16 200 / 50 steps 0.2669 -> 0.2541 ms, the
+        // driver's 20 / 5 0.296 -> 0.287, K=32 0.474 -> 0.410, clustered 1.044 -> 0.952, surfaces
+        // 0.712 -> 0.652, world-1 distributed 0.286 -> 0.274; 10M K=32 +1.5 % (kept at 1024
+        // there). Two interleaved passes, profiles/ab_r5_bin_threads.txt
+        static const int bin_env = [] {
             const char* v = std::getenv("KN_BIN_THREADS");
-            const int t = v ? std::atoi(v) : 1024;
-            return (t == 256 || t == 512 || t == 1024) ? t : 1024;
+            const int t = v ? std::atoi(v) : 0;
+            return (t == 256 || t == 512 || t == 1024) ? t : 0;
         }();
+        const int bin_threads = bin_env ? bin_env : (n <= (4 << 20) ? 256 : 1024);
         bucket_count_kernel<<<bp.nblocks, bin_threads, bp.nbuckets * sizeof(int), s>>>(
             b.points, n, src, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count, b.zero_words,
             b.n_zero_words);

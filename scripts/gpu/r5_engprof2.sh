@@ -2,7 +2,7 @@
 # engine pipeline timeline (two query streams at equal priority), 900K K=16, 80 / 10
 set -o pipefail
 export PYTHONPATH=$PWD TMPDIR=/tmp
-O=gpurun_out/r5engprof2
+O=gpurun_out/${OUT:-r5engprof2}
 mkdir -p $O
 (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/$O/t -o run -- python3 $GRAFT_REPO_ROOT/bench.py --no-check --steps 80 --warmup 10 > $GRAFT_REPO_ROOT/$O/t.log 2>&1) || { echo PROF_FAIL; tail $O/t.log; exit 1; }
 python - $O/t/run_results.db <<'PY'
