@@ -142,6 +142,8 @@ struct BuildBuffers {
     // local index. Fused into the bucket sort (non-deterministic bucketed build), else one extra pass.
     const int* gids;
     int n_owned;
+    // points per bucketed-binning block (0: automatic, build.hip bin_plan)
+    int bin_items;
 };
 
 size_t scan_block_count(int num_cells);
@@ -156,7 +158,7 @@ struct BinPlan {
     int nblocks;   // streaming blocks
     int per_block; // points per streaming block (multiple of 256)
 };
-bool bin_plan(int n, int num_cells, BinPlan* out);
+bool bin_plan(int n, int num_cells, BinPlan* out, int items = 0);
 hipError_t launch_build(const BuildBuffers& b, hipStream_t stream);
 
 // Batched streams of clouds (Engine::stream_batch): write `count` (<= kPtrTableMax) pointers into

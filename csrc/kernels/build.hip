@@ -708,14 +708,26 @@ hipError_t launch_cell_sort(const int* cell_start, const GridGeom* geom, int n, 
     return hipGetLastError();
 }
 
-bool bin_plan(int n, int num_cells, BinPlan* out) {
+bool bin_plan(int n, int num_cells, BinPlan* out, int items_req) {
     if (n <= 0 || num_cells <= 0) return false;
-    // points per streaming block (KN_BIN_ITEMS, A/B): fewer -> more blocks, more bucket columns
-    static const int items = [] {
+    // Points per streaming block (KN_BIN_ITEMS overrides): ~64 blocks up to 4M points (the power
+    // of two nearest n / 64, within 4096..16384), 4096 above. Beside the running query kernels a
+    // few large 256-thread blocks finish sooner than many small ones: 900K K=16 20 / 5 steps 0.282
+    // -> 0.273 ms, 200 / 50 0.244 -> 0.241 (three sets), world-1 distributed 0.270 -> 0.262; 300K
+    // and pts20K want 4096 (16384: +9 % / +31 %); 10M equal (profiles/ab_r5_bin_items.txt)
+    static const int items_env = [] {
         const char* v = std::getenv("KN_BIN_ITEMS");
-        const int t = v ? std::atoi(v) : 4096;
-        return (t >= 512 && t <= 65536) ? t : 4096;
+        const int t = v ? std::atoi(v) : 0;
+        return (t >= 512 && t <= 65536) ? t : 0;
     }();
+    int items = items_env ? items_env : items_req;
+    if (!items) {
+        items = 4096;
+        if (n <= (4 << 20)) {
+            const double l = std::log2(std::max(1.0, (double)n / 64.0));
+            items = 1 << std::max(12, std::min(14, (int)std::lround(l)));
+        }
+    }
     const int nblocks = std::max(1, std::min((int)cdiv((size_t)n, (size_t)items), 1024));
     const int per_block = (int)(cdiv(cdiv((size_t)n, nblocks), 256) * 256);
     for (int shift = 8; shift <= 14; ++shift) {
@@ -759,7 +771,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
             b.zero_words ? b.n_zero_words : 0);
         return hipGetLastError();
     }
-    if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp)) {
+    if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp, b.bin_items)) {
         // geometry folded into bucket_count; scan top level folded into its consumers
         GeomSrc src{};
         src.use_box = b.use_box;

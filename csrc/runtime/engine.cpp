@@ -1017,7 +1017,9 @@ kn_status Engine::stream_batch_eager(int m, const float* const* d_in, unsigned* 
                 return r == KN_OK ? hipSuccess : hipErrorUnknown;
             };
         hipStream_t aux = pipe_.aux_stream();
-        if ((st = check(bpipe_.init(stream_, bstream_, b, q, x, false, aux ? 2 : 1, 2, aux), "batch pipeline init")) != KN_OK)
+        // as many grid sets as the resident pipeline (three with two query streams)
+        if ((st = check(bpipe_.init(stream_, bstream_, b, q, x, false, aux ? 2 : 1, nsets_, aux), "batch pipeline init")) !=
+            KN_OK)
             return st;
         bpipe_.set_eager(true);
     }

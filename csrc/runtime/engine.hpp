@@ -181,8 +181,8 @@ private:
     // eager batch pipeline (stream_batch default): the same stages over the same grid sets and
     // streams as pipe_, enqueued per step; a step's outputs are the caller's buffers of set s
     Pipeline bpipe_;
-    unsigned* bout_idx_[2] = {nullptr, nullptr};
-    float* bout_dist_[2] = {nullptr, nullptr};
+    unsigned* bout_idx_[3] = {nullptr, nullptr, nullptr};
+    float* bout_dist_[3] = {nullptr, nullptr, nullptr};
     int out_ovr_set_ = -1;  // >= 0 while a batch stage of that set is enqueued
     int batch_mode_ = -1;
     kn_status stream_batch_eager(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist);
