@@ -720,9 +720,11 @@ bool bin_plan(int n, int num_cells, BinPlan* out, int items_req) {
         const int t = v ? std::atoi(v) : 0;
         return (t >= 512 && t <= 65536) ? t : 0;
     }();
+    // (above 4M points, 1024-thread blocks of 16384 points: 12.5M K=16 distributed share 4.616
+    // -> 4.554 ms, 10M K=32 equal; profiles/ab_r5_bin_items.txt)
     int items = items_env ? items_env : items_req;
     if (!items) {
-        items = 4096;
+        items = 16384;
         if (n <= (4 << 20)) {
             const double l = std::log2(std::max(1.0, (double)n / 64.0));
             items = 1 << std::max(12, std::min(14, (int)std::lround(l)));
