@@ -544,7 +544,8 @@ __global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsign
                                             const int* __restrict__ ptotals, int nt,
                                             const unsigned* __restrict__ counters, int* __restrict__ flag,
                                             int* __restrict__ sticky, int* __restrict__ host_flag) {
-    // block-wide reduction of the nb x 6 partials (1024 threads: one pass at ~900K points)
+    // block-wide reduction of the nb x 6 partials (launched with 256 threads: a 1024-thread block
+    // beside the running query kernels waits for 16 free wave slots on one CU)
     __shared__ unsigned red[6][16];
     __shared__ unsigned words_s[6];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -846,7 +847,7 @@ hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const do
                                        const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
                                        hipStream_t s) {
     const int nb = route_block_count(n);
-    steady_flag_partials_kernel<<<1, 1024, 0, s>>>(partials, nb, nb, n, planned_meta, totals, planned_totals, n_totals,
+    steady_flag_partials_kernel<<<1, 256, 0, s>>>(partials, nb, nb, n, planned_meta, totals, planned_totals, n_totals,
                                                  counters, flag, nullptr, nullptr);
     return hipGetLastError();
 }
@@ -856,7 +857,7 @@ hipError_t launch_steady_flag_local(const float* pts, int n, unsigned* words, co
     if ((sticky == nullptr) != (host_flag == nullptr)) return hipErrorInvalidValue;
     hipError_t e;
     if ((e = launch_bbox_partials(pts, n, words, s)) != hipSuccess) return e;
-    steady_flag_partials_kernel<<<1, 1024, 0, s>>>(words, n > 0 ? bbox_block_count(n) : 0, kBBoxBlocks, n,
+    steady_flag_partials_kernel<<<1, 256, 0, s>>>(words, n > 0 ? bbox_block_count(n) : 0, kBBoxBlocks, n,
                                                  planned_meta, nullptr, nullptr, 0, counters, flag, sticky, host_flag);
     return hipGetLastError();
 }

@@ -255,13 +255,16 @@ __global__ __launch_bounds__(256) void tscan_sums_kernel(const unsigned* __restr
     __syncthreads();
     if (threadIdx.x == 0) sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
-__global__ __launch_bounds__(1024) void tscan_top_kernel(unsigned* __restrict__ sums, int nb) {
-    __shared__ unsigned wsum[16];
+// (256 threads: a 1024-thread block beside the running query kernels waits for 16 free wave slots
+// on one CU)
+constexpr int kTScanTop = 256;
+__global__ __launch_bounds__(kTScanTop) void tscan_top_kernel(unsigned* __restrict__ sums, int nb) {
+    __shared__ unsigned wsum[kTScanTop / 64];
     __shared__ unsigned carry_s;
     if (threadIdx.x == 0) carry_s = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int base = 0; base < nb; base += 1024) {
+    for (int base = 0; base < nb; base += kTScanTop) {
         const int i = base + threadIdx.x;
         const unsigned v = (i < nb) ? sums[i] : 0u;
         const unsigned incl = (unsigned)wave_inclusive_scan_add((int)v);
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(1024) void tscan_top_kernel(unsigned* __restrict__ 
         const unsigned carry = carry_s;
         if (i < nb) sums[i] = carry + woff + incl - v;
         __syncthreads();
-        if (threadIdx.x == 1023) carry_s = carry + woff + incl;
+        if (threadIdx.x == kTScanTop - 1) carry_s = carry + woff + incl;
         __syncthreads();
     }
 }
@@ -303,7 +306,7 @@ hipError_t tscan(const unsigned* in, int n, unsigned* out, unsigned* sums, bool 
     if (n <= 0) return hipSuccess;
     const unsigned nb = cdiv_((size_t)n, kTScanItems);
     tscan_sums_kernel<<<nb, 256, 0, s>>>(in, n, sums);
-    tscan_top_kernel<<<1, 1024, 0, s>>>(sums, (int)nb);
+    tscan_top_kernel<<<1, kTScanTop, 0, s>>>(sums, (int)nb);
     tscan_apply_kernel<<<nb, 256, 0, s>>>(in, n, sums, out, inclusive ? 1 : 0);
     return hipGetLastError();
 }

@@ -266,8 +266,10 @@ QueryBuffers Engine::query_buffers() const {
     q.xsub = ap_.xsub;
     q.lds_capacity = ap_.lds_capacity;
     q.use_tiles = cfg_.use_tiles;
-    // fallback grid from the last observed fallback count: 256 workgroups when it was short
-    q.exact_grid = last_fallback_ < 4096u ? 256 : 0;
+    // fallback grid from the last observed fallback count: 32 workgroups when it was (nearly)
+    // empty -- a launch beside the running queries whose workgroups all find nothing to do --,
+    // 256 when it was short, the default (KN_EXACT_GRID) otherwise
+    q.exact_grid = last_fallback_ < 128u ? 32 : last_fallback_ < 4096u ? 256 : 0;
     // many cooperative re-rank finishes last time (exactly equal distances): the wide window
     if ((unsigned long long)last_coop_ * 64 > (unsigned long long)n_) q.flags |= kQueryFlagWide;
     return q;
