@@ -13,7 +13,10 @@
 namespace kn {
 
 constexpr int kRouteMaxWorld = 64;
-constexpr int kRouteItems = 1024;  // points per routing block
+#ifndef KN_ROUTE_ITEMS
+#define KN_ROUTE_ITEMS 1024
+#endif
+constexpr int kRouteItems = KN_ROUTE_ITEMS;  // points per routing block
 
 struct RouteParams {
     float lo[3];    // global domain lower corner
