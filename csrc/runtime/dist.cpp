@@ -260,6 +260,10 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     // communicator across ranks
     const char* dfv = std::getenv("KN_DIST_DEFER");
     deferred_ = comm_ && qstreams >= 2 && !(dfv && dfv[0] == '0');
+    // KN_DIST_TAIL=1: tail mode (measured neutral at world 1: 200 / 50 0.2661 vs 0.2657 ms, 20 / 5
+    // -1.5 %, K=50 equal; profiles/r5_dist.txt), off by default
+    const char* tlv = std::getenv("KN_DIST_TAIL");
+    tail_ = deferred_ && (tlv && tlv[0] == '1');
     for (int s = 0; s < nsets_; ++s) {
         Set& S = set_[s];
         void* b = nullptr;
@@ -322,6 +326,7 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     auto b = [this](int s, hipStream_t st) { return stage_build(s, st); };
     auto q = [this](int s, hipStream_t st) { return stage_query(s, st); };
     auto r = [this](int s, hipStream_t st) { return stage_flag(s, st); };
+    auto t = [this](int s, hipStream_t st) { return stage_tail(s, st); };
     if (!comm_) {  // loopback mode: eager stages driven by the caller
         ok_ = true;
         return;
@@ -329,8 +334,8 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     // KN_DIST_CAPTURE_JOINED=1 (diagnostics): start unrolled captures on the main stream, so the
     // RCCL calls of the build stage are captured on a JOINED stream (the round-4 segfault)
     const char* joined = std::getenv("KN_DIST_CAPTURE_JOINED");
-    if (pipe_.init(main_, side_, b, q, deferred_ ? Pipeline::Stage() : Pipeline::Stage(r), !(joined && joined[0] == '1'),
-                   qstreams, nsets_) != hipSuccess) {
+    const Pipeline::Stage rs = !deferred_ ? Pipeline::Stage(r) : tail_ ? Pipeline::Stage(t) : Pipeline::Stage();
+    if (pipe_.init(main_, side_, b, q, rs, !(joined && joined[0] == '1'), qstreams, nsets_, nullptr, tail_) != hipSuccess) {
         fail("pipeline init");
         return;
     }
@@ -522,16 +527,27 @@ hipError_t DistPipeline::stage_query(int s, hipStream_t st) {
             // the complete-box certification the grid kernels do inline
             KN_TRY(launch_certify_rows(S.lpts, n_owned_, p_.k, S.d2, complete_, S.geom, S.counters, S.uncert, st));
         }
-        if (deferred_) KN_TRY(step_flag(s, st));
+        if (deferred_ && !tail_) KN_TRY(step_flag(s, st));
         return hipSuccess;
     }
     // the tile kernel and its exact finish (KN_PIPE_EXACT=1: the exact finish opens the epilogue
     // on the side stream instead, engine.cpp exact_epilogue; deferred mode: always here)
     QueryBuffers q = query_proto(s);
-    q.exact_mode = (!deferred_ && exact_epilogue(p_.k)) ? 1 : 0;
+    q.exact_mode = tail_ ? 1 : (!deferred_ && exact_epilogue(p_.k)) ? 1 : 0;
     KN_TRY(launch_query(q, st));
-    if (deferred_) KN_TRY(step_flag(s, st));
+    if (deferred_ && !tail_) KN_TRY(step_flag(s, st));
     return hipSuccess;
+}
+
+// Tail mode: the fallback list's exact finish and the step's local flag, on the pipeline's tail
+// stream after the step's tile kernel (pipeline.hpp tail_stream).
+hipError_t DistPipeline::stage_tail(int s, hipStream_t st) {
+    if (!p_.use_tree) {
+        QueryBuffers q = query_proto(s);
+        q.exact_mode = 2;
+        KN_TRY(launch_query(q, st));
+    }
+    return step_flag(s, st);
 }
 
 // deferred mode: the step's local flag on its query stream, max-accumulated into pending_
@@ -562,7 +578,7 @@ QueryBuffers DistPipeline::query_proto(int s) const {
 // as planned, no uncertified row), its MAX all-reduce and the sticky host flag.
 hipError_t DistPipeline::stage_flag(int s, hipStream_t st) {
     Set& S = set_[s];
-    if (!p_.use_tree && exact_epilogue(p_.k)) {
+    if (!p_.use_tree && (exact_epilogue(p_.k) || tail_)) {  // (tail mode: the query left the list)
         QueryBuffers q = query_proto(s);
         q.exact_mode = 2;
         KN_TRY(launch_query(q, st));

@@ -159,6 +159,7 @@ private:
     };
     hipError_t stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks = nullptr);
     hipError_t stage_query(int s, hipStream_t st);
+    hipError_t stage_tail(int s, hipStream_t st);  // tail mode: the exact finish + the step's flag
     hipError_t stage_flag(int s, hipStream_t st);  // epilogue: exact finish, flag, all-reduce
     hipError_t step_flag(int s, hipStream_t st);   // deferred mode: local flag -> pending_
     QueryBuffers query_proto(int s) const;
@@ -189,6 +190,9 @@ private:
     // deferred flag reduction (two query streams): every step's flag is max-accumulated on the
     // device (pending_, atomic), one all-reduce per launch() call into reduced_ then the sticky flag
     bool deferred_ = false;
+    // deferred mode, KN_DIST_TAIL=1 (opt-in): the exact finish and the step's flag run as the
+    // pipeline's epilogue on a stream of their own, so a query stream's next tile follows its tile
+    bool tail_ = false;
     int* pending_ = nullptr;
     int* reduced_ = nullptr;
     int* host_flag_ = nullptr;      // pinned

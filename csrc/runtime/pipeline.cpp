@@ -35,7 +35,7 @@ unsigned order_event_flags() {
 }  // namespace
 
 hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r, bool capture_from_side,
-                          int query_streams, int sets, hipStream_t aux) {
+                          int query_streams, int sets, hipStream_t aux, bool tail_stream) {
     reset();
     if (sets < 2 || sets > kMaxSets) return hipErrorInvalidValue;
     ns_ = sets;
@@ -54,6 +54,7 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
     }
     KN_TRY(hipEventCreateWithFlags(&last_done_, hipEventDisableTiming));
     KN_TRY(hipEventRecord(last_done_, main_));
+    if (tail_stream && r_) KN_TRY(hipStreamCreateWithFlags(&tail_, hipStreamNonBlocking));
     if (query_streams >= 2) {
         int lo = 0, hi = 0;
         KN_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -78,6 +79,11 @@ hipError_t Pipeline::init(hipStream_t main, hipStream_t side, Stage b, Stage q, 
 void Pipeline::reset() {
     if (main_) (void)hipStreamSynchronize(main_);
     if (side_) (void)hipStreamSynchronize(side_);
+    if (tail_) {
+        (void)hipStreamSynchronize(tail_);
+        (void)hipStreamDestroy(tail_);
+        tail_ = nullptr;
+    }
     for (int s = 0; s < kMaxSets; ++s) {
         destroy(gB_[s]);
         destroy(gQ_[s]);
@@ -210,9 +216,10 @@ hipError_t Pipeline::enqueue_query(int s) {
 }
 
 hipError_t Pipeline::enqueue_epilogue(int s) {
-    KN_TRY(hipStreamWaitEvent(side_, evQ_[s], 0));
-    KN_TRY(eager_ ? r_(s, side_) : hipGraphLaunch(gR_[s], side_));
-    return hipEventRecord(evF_[s], side_);
+    hipStream_t rs = rstream();
+    KN_TRY(hipStreamWaitEvent(rs, evQ_[s], 0));
+    KN_TRY(eager_ ? r_(s, rs) : hipGraphLaunch(gR_[s], rs));
+    return hipEventRecord(evF_[s], rs);
 }
 
 hipError_t Pipeline::prepare(int unroll) {
@@ -231,6 +238,7 @@ void Pipeline::set_eager(bool eager) {
     if (main_) (void)hipStreamSynchronize(main_);
     if (side_) (void)hipStreamSynchronize(side_);
     if (aux_) (void)hipStreamSynchronize(aux_);
+    if (tail_) (void)hipStreamSynchronize(tail_);
     // a failed capture may have left a stream in capture mode: end it (the graph is dropped)
     for (hipStream_t st : {main_, side_}) {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -257,7 +265,7 @@ hipError_t Pipeline::flush() {
     if (r_pending_) {
         r_pending_ = false;
         KN_TRY(enqueue_epilogue(last_set_));
-        return hipEventRecord(last_done_, side_);
+        return hipEventRecord(last_done_, rstream());
     }
     if (!r_ && last_set_ >= 0) {
         hipStream_t ql = last_qs_ ? aux_ : main_;
@@ -377,6 +385,7 @@ hipError_t Pipeline::step_with(const Stage& pre, const Stage* next_pre) {
 hipError_t Pipeline::sync() {
     if (!main_) return hipSuccess;
     if (aux_) KN_TRY(hipStreamSynchronize(aux_));
+    if (tail_) KN_TRY(hipStreamSynchronize(tail_));
     KN_TRY(hipStreamSynchronize(side_));
     return hipStreamSynchronize(main_);
 }
@@ -384,6 +393,7 @@ hipError_t Pipeline::sync() {
 hipError_t Pipeline::unprime() {
     if (!main_) return hipSuccess;
     KN_TRY(hipStreamSynchronize(side_));
+    if (tail_) KN_TRY(hipStreamSynchronize(tail_));
     primed_ = false;
     return hipSuccess;
 }

@@ -48,9 +48,11 @@ public:
     static constexpr int kMaxSets = 3;
     // aux (query_streams = 2): an existing stream for the odd steps' queries (not owned, e.g. a
     // second pipeline over the same grid sets sharing the first one's), else one is created
+    // tail_stream: the epilogue R runs on a pipeline-owned stream of its own instead of the side
+    // stream (it then delays neither the next build nor the next query on its query stream)
     hipError_t init(hipStream_t main, hipStream_t side, Stage b, Stage q, Stage r = Stage(),
                     bool capture_from_side = false, int query_streams = 1, int sets = 2,
-                    hipStream_t aux = nullptr);
+                    hipStream_t aux = nullptr, bool tail_stream = false);
     hipStream_t aux_stream() const { return aux_; }
     int sets() const { return ns_; }
     bool ready() const { return main_ != nullptr; }
@@ -102,6 +104,8 @@ private:
     hipStream_t main_ = nullptr, side_ = nullptr;
     hipStream_t aux_ = nullptr;  // second query stream of the unrolled graphs (KN_PIPE_QSTREAMS=2)
     bool aux_owned_ = false;
+    hipStream_t tail_ = nullptr;  // epilogue stream (init tail_stream), else R runs on side_
+    hipStream_t rstream() const { return tail_ ? tail_ : side_; }
     bool capture_from_side_ = false;
     bool eager_ = false;
     int fallbacks_ = 0;
