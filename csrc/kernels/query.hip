@@ -1831,7 +1831,10 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             const char* v = std::getenv("KN_TILE_BLOCK");
             return v ? std::max(1, std::atoi(v)) : 0;
         }();
-        a.tblock = tblock_env ? tblock_env : (KT > 16 ? 4 : 2);
+        // round 5 (two query streams, three sets, 16K-point binning blocks): the K=32 bucket up to
+        // 4M points runs fastest in plain order (900K: 0.451 -> 0.408 ms, two passes; K=24 / 50 /
+        // 64, 300K and 10M keep their blocks; profiles/ab_r5_tile_block.txt)
+        a.tblock = tblock_env ? tblock_env : (KT == 32 && q.n <= (4 << 20)) ? 1 : (KT > 16 ? 4 : 2);
         a.cb_stride = std::min(X, a.TX + 2 * a.Hx) + 1;
         a.max_rows = std::min(Y, a.TY + 2 * a.H) * std::min(Z, a.TZ + 2 * a.H);
         const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
