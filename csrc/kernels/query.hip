@@ -1834,7 +1834,14 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         // round 5 (two query streams, three sets, 16K-point binning blocks): the K=32 bucket up to
         // 4M points runs fastest in plain order (900K: 0.451 -> 0.408 ms, two passes; K=24 / 50 /
         // 64, 300K and 10M keep their blocks; profiles/ab_r5_tile_block.txt)
-        a.tblock = tblock_env ? tblock_env : (KT == 32 && q.n <= (4 << 20)) ? 1 : (KT > 16 ? 4 : 2);
+        // K <= 16 by cloud size (gpurun_out/r5tb4, two passes, B 1 / 2 / 4): 300K 0.136 / 0.134 /
+        // 0.130 ms, 2M 0.594 / 0.575 / 0.565, 4M 1.35 / 1.30 / 1.22; 600K-900K plain order by 0-1 %
+        // (900K 200 / 50 0.238 / 0.239 / 0.240)
+        const bool mid = q.n >= (512 << 10) && q.n <= (1536 << 10);
+        a.tblock = tblock_env ? tblock_env
+                 : KT == 32 ? (q.n <= (4 << 20) ? 1 : 4)
+                 : KT > 16  ? 4
+                 : mid ? 1 : 4;
         a.cb_stride = std::min(X, a.TX + 2 * a.Hx) + 1;
         a.max_rows = std::min(Y, a.TY + 2 * a.H) * std::min(Z, a.TZ + 2 * a.H);
         const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
