@@ -1831,17 +1831,15 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
             const char* v = std::getenv("KN_TILE_BLOCK");
             return v ? std::max(1, std::atoi(v)) : 0;
         }();
-        // round 5 (two query streams, three sets, 16K-point binning blocks): the K=32 bucket up to
-        // 4M points runs fastest in plain order (900K: 0.451 -> 0.408 ms, two passes; K=24 / 50 /
-        // 64, 300K and 10M keep their blocks; profiles/ab_r5_tile_block.txt)
-        // K <= 16 by cloud size (gpurun_out/r5tb4, two passes, B 1 / 2 / 4): 300K 0.136 / 0.134 /
-        // 0.130 ms, 2M 0.594 / 0.575 / 0.565, 4M 1.35 / 1.30 / 1.22; 600K-900K plain order by 0-1 %
-        // (900K 200 / 50 0.238 / 0.239 / 0.240)
+        // round 5 (two query streams, three sets, 16K-point binning blocks): the K=32 bucket at 900K
+        // runs fastest in plain order (0.451 -> 0.408 ms, two passes; K=24 / 50 / 64 and 10M keep
+        // their blocks; profiles/ab_r5_tile_block.txt)
+        // K <= 16 and K=32 by cloud size (gpurun_out/r5tb4, r5tb6, two passes, B 1 / 2 / 4): K=16
+        // 300K 0.136 / 0.134 / 0.130 ms, 2M 0.594 / 0.575 / 0.565, 4M 1.35 / 1.30 / 1.22, 600K-900K
+        // plain order by 0-1 % (900K 200 / 50 0.238 / 0.239 / 0.240); K=32 300K 0.246 / 0.264 /
+        // 0.216, 4M 2.50 / 2.37 / 2.35; K=8 300K 0.096 / 0.094 / 0.087
         const bool mid = q.n >= (512 << 10) && q.n <= (1536 << 10);
-        a.tblock = tblock_env ? tblock_env
-                 : KT == 32 ? (q.n <= (4 << 20) ? 1 : 4)
-                 : KT > 16  ? 4
-                 : mid ? 1 : 4;
+        a.tblock = tblock_env ? tblock_env : ((KT <= 16 || KT == 32) && mid) ? 1 : 4;
         a.cb_stride = std::min(X, a.TX + 2 * a.Hx) + 1;
         a.max_rows = std::min(Y, a.TY + 2 * a.H) * std::min(Z, a.TZ + 2 * a.H);
         const unsigned nt = (unsigned)(a.ntx * a.nty * a.ntz);
