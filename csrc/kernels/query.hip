@@ -2084,12 +2084,15 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
     // Small clouds: fewer 4^3 tiles than CUs leave most of the chip idle; 2^3 tiles give 8x the
     // workgroups (20K points, K=8: 0.049 -> 0.046 ms; at 300K 4^3 stays faster, 0.185 vs 0.197
     // for 4x4x2; profiles/sweep_r1_small.txt)
-    // KN_HALF_TILE_MAX=T (diagnostic, default off): 4x2x4 tiles below T 4^3 tiles. Round 5
+    // KN_HALF_TILE_MAX=T: 4x2x4 tiles below T 4^3 tiles (0 = never). Round 5
     // (bench.py, two passes, profiles/sweep_r5_tiles.txt): 200K 0.098 -> 0.093 ms, 300K 0.130 ->
     // 0.108, but 350K 0.101 -> 0.122 and 450K 0.126 -> 0.154. The per-query cost of the 4^3 plan
     // depends on the density after whole-tile rounding: 300K / 400K (3.5-3.6 points per cell)
     // 0.43 / 0.39 ns per query, 350K / 450K (3.2) 0.29 / 0.28; a power-of-two LDS capacity (11-bit
     // slot field) at 300K / 400K was neutral, so the cause is open.
+    // Candidate default: T = 1,500 (~1.4 rounds of 1,024 workgroup slots): 200K (1,000 tiles) and
+    // 300K (1,331) win, 350K / 400K (1,728) and 450K (2,197) lose or tie; not yet measured at
+    // 100K-320K with bench.py (scripts/gpu/r5_half3.sh), so off by default.
     static const double half_max = [] {
         const char* v = std::getenv("KN_HALF_TILE_MAX");
         return v ? std::atof(v) : 0.0;
@@ -2098,8 +2101,8 @@ AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_h
     if (!(tile_hint && (tile_hint[0] > 0 || tile_hint[1] > 0 || tile_hint[2] > 0))) {
         if (tiles4 < 256.0)
             for (int a = 0; a < 3; ++a) p.tile[a] = 2;
-        else if (tiles4 < half_max)
-            p.tile[1] = 2;
+        else if (std::lround(x[0] / 4) * std::lround(x[1] / 4) * std::lround(x[2] / 4) < half_max)
+            p.tile[1] = 2;  // (whole 4^3 tiles after rounding: 300K 11^3, 350K 12^3)
     }
     // Whole tiles: a partial edge tile costs a full halo staging for a fraction of the queries
     // (66 cells = 16.5 tiles of 4 -> 17 % of the tiles partial), so axes of >= 4 tiles are
