@@ -455,6 +455,35 @@ def emit(line: dict) -> None:
     out.flush()
 
 
+def supervised(args, world: int) -> int:
+    """This process (a torchrun worker, or the plain 1-GPU run) never touches the GPU: the timed job
+    runs in a child, and a failed attempt on ANY rank (crash, CollectiveError, deadline, no JSON
+    line) is re-run by fresh children on the next, more conservative path
+    (cuda_knearests_amd/utils/supervise.py). N GPUs: the native RCCL pipeline, then the torch steady
+    path (KN_DIST_PIPE=0), then validated synchronous steps. 1 GPU: pipelined, then serial steps.
+    KN_BENCH_SUPERVISE=0 runs the job in this process instead."""
+    from cuda_knearests_amd.utils.supervise import Attempt, annotate, make_store, supervise
+
+    rank = int(os.environ.get("RANK", "0"))
+    t1 = float(os.environ.get("KN_BENCH_ATTEMPT_S", "420"))
+    if world > 1 or args.dist:
+        attempts = [Attempt("native_pipeline", {}, [], t1),
+                    Attempt("torch_steady", {"KN_DIST_PIPE": "0"}, [], 300.0),
+                    Attempt("torch_sync_steps", {"KN_DIST_PIPE": "0"}, ["--sync-steps"], 300.0)]
+    else:
+        attempts = [Attempt("pipelined" if args.pipeline else "serial", {}, [], t1),
+                    Attempt("serial", {}, ["--no-pipeline"], 300.0)]
+    store = make_store(rank, world)
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    ok, outs = supervise(cmd, attempts, rank, world, store)
+    if ok < 0:
+        log("every attempt failed")
+        return 1
+    if rank == 0:
+        emit(annotate(outs[ok].line, attempts, ok, outs))
+    return 0
+
+
 def main() -> int:
     global _JSON_OUT
     sys.stdout.flush()
@@ -515,6 +544,10 @@ def main() -> int:
     ap.add_argument("--sync-steps", action="store_true",
                     help="N GPUs: validate every step before the next (no asynchronous steady-state steps)")
     args = ap.parse_args()
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if (os.environ.get("KN_BENCH_CHILD") != "1" and os.environ.get("KN_BENCH_SUPERVISE", "1") != "0"
+            and not args.cpu_oracle and not args.loopback and not (args.gpus > 1 and world_env == 1)):
+        return supervised(args, world_env)
     if not args.cpu_oracle:
         # a native backtrace if anything in the native stack (HIP runtime, RCCL) faults
         from cuda_knearests_amd._ext import load as _load_ext
@@ -524,7 +557,6 @@ def main() -> int:
         import faulthandler
 
         faulthandler.dump_traceback_later(float(os.environ["KN_BENCH_WATCHDOG"]), exit=True)
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world_env == 1:
         # convenience: relaunch under torch.distributed.run (before any GPU init)
         import subprocess

@@ -181,9 +181,11 @@ hipError_t launch_local_meta(const float* pts, int n, unsigned* words, double* o
 // send counts differ from the planned ones) + (any uncertified query). No host involvement.
 // Steady step check with the share's bbox taken from route_count's partials (route_block_count(n)
 // blocks x 6 words, [a * nb + block]) instead of a local_meta pass.
-hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const double* planned_meta, const int* totals,
-                                       const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
-                                       hipStream_t stream);
+// n_routed: rows route_count ran over (the partials' block count and stride); n: the share's true
+// size (the meta comparison). n_routed <= n.
+hipError_t launch_steady_flag_partials(const unsigned* partials, int n_routed, int n, const double* planned_meta,
+                                       const int* totals, const int* planned_totals, int n_totals,
+                                       const unsigned* counters, int* flag, hipStream_t stream);
 // World-1 steady step check (no routing pass): one bbox pass over the share + the same flag
 // kernel. sticky / host_flag (both or neither): also max-accumulate the flag into the device word
 // `sticky` and store it to `host_flag`, a device-visible pointer to pinned host memory.

@@ -77,8 +77,24 @@ size_t tree_workspace_bytes(int n, const int dims[3]);
 // The Morton brick codes hold 10 bits of brick coordinate per axis (8 cells a brick): grids of at
 // most 8,192 cells per axis. Larger grids stay on the grid path (callers check this).
 constexpr int kTreeMaxAxisCells = 8192;
+// The brick counts live in a cube of pow2(max bricks per axis)^3 slots (Morton order over the
+// longest axis), so an elongated grid (8192 x 8 x 8 cells: 1024^3 slots, 4 GB) would cost far more
+// than its cells. Bound the padded space itself: 2^24 slots (64 MB, e.g. 2048 x 8 x 8 or 2048^3
+// cells); larger spaces stay on the grid path.
+constexpr size_t kTreeMaxBrickSlots = (size_t)1 << 24;
+inline size_t tree_brick_slots(const int dims[3]) {
+    int m = 1;  // bricks along the longest axis
+    for (int a = 0; a < 3; ++a) {
+        const int b = (dims[a] + 7) / 8;
+        if (b > m) m = b;
+    }
+    size_t side = 1;
+    while ((int)side < m) side <<= 1;
+    return side * side * side;
+}
 inline bool tree_supports(const int dims[3]) {
-    return dims[0] <= kTreeMaxAxisCells && dims[1] <= kTreeMaxAxisCells && dims[2] <= kTreeMaxAxisCells;
+    return dims[0] <= kTreeMaxAxisCells && dims[1] <= kTreeMaxAxisCells && dims[2] <= kTreeMaxAxisCells &&
+           tree_brick_slots(dims) <= kTreeMaxBrickSlots;
 }
 TreeView tree_view(void* ws, int n, const int dims[3]);
 // Phase 1 (stream-ordered, no host sync): the grid's sorted points in the Morton order of their

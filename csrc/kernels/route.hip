@@ -843,10 +843,13 @@ hipError_t launch_steady_flag(const double* local, const double* planned_meta, c
     return hipGetLastError();
 }
 
-hipError_t launch_steady_flag_partials(const unsigned* partials, int n, const double* planned_meta, const int* totals,
-                                       const int* planned_totals, int n_totals, const unsigned* counters, int* flag,
-                                       hipStream_t s) {
-    const int nb = route_block_count(n);
+hipError_t launch_steady_flag_partials(const unsigned* partials, int n_routed, int n, const double* planned_meta,
+                                       const int* totals, const int* planned_totals, int n_totals,
+                                       const unsigned* counters, int* flag, hipStream_t s) {
+    // the partials' layout is route_count's over the ROUTED rows (block count and stride); n is the
+    // share's true size, compared with the planned meta (a grown share routes only the planned rows)
+    if (n_routed < 0 || n_routed > n) return hipErrorInvalidValue;
+    const int nb = n_routed > 0 ? route_block_count(n_routed) : 0;
     steady_flag_partials_kernel<<<1, 256, 0, s>>>(partials, nb, nb, n, planned_meta, totals, planned_totals, n_totals,
                                                  counters, flag, nullptr, nullptr);
     return hipGetLastError();

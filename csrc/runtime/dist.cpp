@@ -553,7 +553,7 @@ hipError_t DistPipeline::stage_tail(int s, hipStream_t st) {
 // deferred mode: the step's local flag on its query stream, max-accumulated into pending_
 hipError_t DistPipeline::step_flag(int s, hipStream_t st) {
     Set& S = set_[s];
-    KN_TRY(launch_steady_flag_partials(S.partials, n_flag_, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
+    KN_TRY(launch_steady_flag_partials(S.partials, n_route_, n_flag_, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
                                        S.counters, S.flag, st));
     return launch_flag_accum(S.flag, pending_, st);
 }
@@ -583,7 +583,7 @@ hipError_t DistPipeline::stage_flag(int s, hipStream_t st) {
         q.exact_mode = 2;
         KN_TRY(launch_query(q, st));
     }
-    KN_TRY(launch_steady_flag_partials(S.partials, n_flag_, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
+    KN_TRY(launch_steady_flag_partials(S.partials, n_route_, n_flag_, metas_dev_ + 8 * p_.rank, S.totals, tot_dev_, 2 * p_.world,
                                        S.counters, S.flag, st));
     if (!comm_) return hipSuccess;  // loopback mode: the caller reduces the ranks' flags
     if (ncclAllReduce(S.flag, S.flag, 1, ncclInt32, ncclMax, as_comm(comm_), st) != ncclSuccess) return hipErrorUnknown;
@@ -690,9 +690,28 @@ kn_status DistPipeline::wait(long long step, double timeout_s, int* flag) {
         ev = ring_[done_.front().second];  // older than the ring: its flag is final (sticky)
     }
     const kn_status st = poll(ev, timeout_s, "distributed step");
-    if (st != KN_OK) return st;
+    if (st != KN_OK) {
+        err_ = "step " + std::to_string(step) + ", " + pending_stage(step) + ": " + err_;
+        return st;
+    }
     if (flag) *flag = *reinterpret_cast<volatile int*>(host_flag_);
     return KN_OK;
+}
+
+std::string DistPipeline::pending_stage(long long step) const {
+    const int s = (int)(step % nsets_);
+    const hipEvent_t eb = pipe_.build_event(s), eq = pipe_.query_event(s);
+    if (eb && hipEventQuery(eb) == hipErrorNotReady) {
+        // the build stage holds the grouped send / recv: name the peers it exchanges rows with
+        std::string peers;
+        for (int d = 0; d < p_.world; ++d)
+            if (d != p_.rank && (p_.cross_send[d] > 0 || p_.cross_recv[d] > 0))
+                peers += (peers.empty() ? "" : ",") + std::to_string(d) + "(send " + std::to_string(p_.cross_send[d]) +
+                         " recv " + std::to_string(p_.cross_recv[d]) + ")";
+        return "stage route+exchange+build pending, peers [" + peers + "]";
+    }
+    if (eq && hipEventQuery(eq) == hipErrorNotReady) return "stage query pending";
+    return "stage flag all-reduce pending (all " + std::to_string(p_.world) + " ranks)";
 }
 
 kn_status DistPipeline::sync() {

@@ -165,6 +165,9 @@ private:
     QueryBuffers query_proto(int s) const;
     // wait for `ev`, polling RCCL's async error; past the deadline the communicator is aborted
     kn_status poll(hipEvent_t ev, double timeout_s, const char* what);
+    // which stage of step `step` is still pending (route + exchange + build with its peers /
+    // query / flag all-reduce): prefixed to wait()'s error, so a CollectiveError names it
+    std::string pending_stage(long long step) const;
     hipError_t exchange(int s, hipStream_t st);
     bool fail(const std::string& m) { err_ = m; ok_ = false; return false; }
 

@@ -73,6 +73,8 @@ public:
     int fallbacks() const { return fallbacks_; }
     // Event recorded after the most recent build of set s (its input has been read).
     hipEvent_t build_event(int s) const { return evB_[s]; }
+    // Event recorded after the most recent query of set s (diagnostics: which stage is pending)
+    hipEvent_t query_event(int s) const { return evQ_[s]; }
     // One step whose input is provided by `pre` (run on the side stream before B, e.g. a copy of
     // the step's cloud into set s's input buffer); `next_pre` != null: also the next step's input
     // is known, so its build is enqueued now (overlapping this step's queries). Unprimes the

@@ -234,6 +234,7 @@ std::tuple<torch::Tensor, torch::Tensor, int64_t> tree_build_impl(torch::Tensor 
     const c10::DeviceGuard guard(sorted.device());
     const int n = (int)sorted.size(0);
     const int d[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
+    TORCH_CHECK(kn::tree_supports(d), "tree path: grid too elongated / too large (padded brick space > 2^24 slots)");
     auto u8 = sorted.options().dtype(torch::kUInt8);
     auto ws = torch::empty({(int64_t)kn::tree_workspace_bytes(n, d)}, u8);
     auto nodes = torch::empty({(int64_t)kn::tree_node_bytes(n)}, u8);
@@ -1041,7 +1042,7 @@ torch::Tensor steady_flag_partials(torch::Tensor partials, int64_t n, torch::Ten
     const c10::DeviceGuard guard(partials.device());
     auto flag = torch::empty({1}, counters.options());
     const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
-    KN_CHECK_HIP(kn::launch_steady_flag_partials(reinterpret_cast<const unsigned*>(partials.data_ptr<int>()), (int)n,
+    KN_CHECK_HIP(kn::launch_steady_flag_partials(reinterpret_cast<const unsigned*>(partials.data_ptr<int>()), (int)n, (int)n,
                                                  metas.data_ptr<double>() + 8 * rank, totals.data_ptr<int>(),
                                                  planned_totals.data_ptr<int>(), (int)totals.numel(),
                                                  reinterpret_cast<const unsigned*>(counters.data_ptr<int>()),
@@ -1512,14 +1513,21 @@ public:
     std::string error() { return d_->error(); }
     // loopback mode: one synchronous stage (0 route, 1 unpack + build + query + local flag)
     void loopback_stage(int64_t stage) { TORCH_CHECK(d_->loopback_stage((int)stage) == KN_OK, d_->error()); }
-    // views (float32, (rows, 4)) of set 0's send rows for destination d / receive rows from source s
+    // views (float32, (rows, 4)) of set 0's send rows for destination d / receive rows from source s.
+    // Like outputs(), each view's deleter holds the pipeline, so the buffers outlive the views
     torch::Tensor send_view(int64_t d, int64_t rows) {
-        auto opt = torch::TensorOptions().device(points_.device()).dtype(torch::kFloat32);
-        return torch::from_blob(reinterpret_cast<float*>(d_->send_rows(0) + d_->send_offset((int)d)), {rows, 4}, opt);
+        TORCH_CHECK(d >= 0 && d < comm_world_ && rows >= 0, "send_view: destination out of range");
+        return owned_view(d_->send_rows(0) + d_->send_offset((int)d), rows);
     }
     torch::Tensor recv_view(int64_t src, int64_t rows) {
+        TORCH_CHECK(src >= 0 && src < comm_world_ && rows >= 0, "recv_view: source out of range");
+        return owned_view(d_->recv_rows(0) + d_->recv_offset((int)src), rows);
+    }
+    torch::Tensor owned_view(float4* base, int64_t rows) {
         auto opt = torch::TensorOptions().device(points_.device()).dtype(torch::kFloat32);
-        return torch::from_blob(reinterpret_cast<float*>(d_->recv_rows(0) + d_->recv_offset((int)src)), {rows, 4}, opt);
+        std::shared_ptr<kn::DistPipeline> keep = d_;
+        std::shared_ptr<PyRankComm> keepc = comm_;
+        return torch::from_blob(reinterpret_cast<float*>(base), {rows, 4}, [keep, keepc](void*) {}, opt);
     }
     int64_t flag_local() { return d_->flag_local(0); }
     // diagnostics (loopback mode): set 0's query counters and routed column totals
@@ -1630,6 +1638,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "LDS bytes per workgroup of the tile query kernel for a plan", py::arg("tile"), py::arg("halo"),
         py::arg("cap"), py::arg("xsub") = 1);
     m.def("to_stored_space", &to_stored_space, "original-space result -> reference stored-space view");
+    m.def(
+        "tree_supports",
+        [](std::vector<int64_t> dims) {
+            TORCH_CHECK(dims.size() == 3, "dims = [X, Y, Z]");
+            const int d[3] = {(int)dims[0], (int)dims[1], (int)dims[2]};
+            return py::make_tuple(kn::tree_supports(d), (int64_t)kn::tree_brick_slots(d));
+        },
+        "whether the tree path takes a grid of these dims: (supported, padded brick slots)", py::arg("dims"));
     m.def("tree_build", &tree_build,
           "Morton-leaf tree over a grid's sorted points, stream-ordered: (workspace, nodes, leaves or -1)",
           py::arg("sorted"), py::arg("cell_start"), py::arg("geom"), py::arg("dims"), py::arg("count_leaves") = false);

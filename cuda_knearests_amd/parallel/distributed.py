@@ -907,6 +907,7 @@ class DistributedKNearests:
         points = points.contiguous().float()
         if iters <= 0:
             raise ValueError("iters must be positive")
+        self._maybe_inject_failure()
         res = None
         left = iters
         while left > 0:
@@ -919,6 +920,21 @@ class DistributedKNearests:
             res = self.solve(points, ids, async_=True)
             left -= 1
         return res
+
+    def _maybe_inject_failure(self) -> None:
+        """Test hook (bench supervisor, tests/test_gpu_distributed.py): KN_DIST_INJECT_FAIL=r makes
+        rank r raise in its first run_steps() call -- the pipelined launch of the bench's timed path
+        -- while the native pipeline is enabled (KN_DIST_PIPE != 0), so a fallback attempt with
+        KN_DIST_PIPE=0 runs clean. Its peers are then blocked in the step's collectives, as after a
+        real failure."""
+        import os
+
+        inj = os.environ.get("KN_DIST_INJECT_FAIL", "")
+        if (inj.strip() and int(inj) == self.rank and os.environ.get("KN_DIST_PIPE", "1") != "0"
+                and not getattr(self, "_injected", False)):
+            self._injected = True
+            raise CollectiveError(f"rank {self.rank}: injected failure (KN_DIST_INJECT_FAIL) at its first pipelined "
+                                  "launch (stage: launch)")
 
     def profile_step(self, points: torch.Tensor, ids: Optional[torch.Tensor] = None) -> dict:
         """Per-phase device times (ms) of one serial steady step of the native pipeline

@@ -217,3 +217,18 @@ def test_bench_prints_one_json_line():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["unit"] == "queries/s" and d["value"] > 0
+
+
+def test_tree_supports_bounds_padded_brick_space():
+    """the tree path's brick counts live in a pow2(max bricks per axis)^3 cube, so an
+    elongated grid must not be admitted by its per-axis cell count alone (8192 x 8 x 8 would need
+    1024^3 slots, 4 GB per grid set). Admitted: up to 2^24 slots (2048 x 8 x 8 -- the GPU long-axis
+    test -- and isotropic 2048^3); refused past it (the engine keeps such grids on the grid path)."""
+    from cuda_knearests_amd._ext import load
+
+    C = load()
+    assert C.tree_supports([2048, 8, 8]) == (True, 256 ** 3)
+    assert C.tree_supports([2048, 2048, 2048])[0]
+    assert C.tree_supports([2049, 8, 8]) == (False, 512 ** 3)
+    assert C.tree_supports([8192, 8, 8]) == (False, 1024 ** 3)
+    assert C.tree_supports([64, 64, 64]) == (True, 8 ** 3)

@@ -664,3 +664,38 @@ def test_halo_field(cuda, world, gen):
         assert halo1 < halo0, (halo1, halo0)
     else:
         assert halo1 >= halo0, (halo1, halo0)
+
+
+@pytest.mark.parametrize("inject", [None, "1"])
+def test_bench_two_ranks_supervised_fallback(cuda, inject):
+    """the N-GPU bench must not lose its number. `bench.py --gpus 2` on this one
+    GPU (KN_SAME_DEVICE=1, gloo process group). With KN_DIST_INJECT_FAIL=1 rank 1 raises in its first
+    pipelined launch: the supervisors kill the first attempt's children on BOTH ranks (rank 0's is
+    blocked in a collective) and the fallback attempt (KN_DIST_PIPE=0) prints the one JSON line,
+    naming its path and the failure, with 0 bad rows on every rank."""
+    import json
+    import subprocess
+    import sys
+
+    from cuda_knearests_amd.utils import REPO
+    from cuda_knearests_amd.utils.supervise import free_port
+
+    env = dict(os.environ, KN_SAME_DEVICE="1", KN_DIST_BACKEND="gloo", MASTER_PORT=str(free_port()))
+    env.pop("KN_DIST_INJECT_FAIL", None)
+    if inject:
+        env["KN_DIST_INJECT_FAIL"] = inject
+    r = subprocess.run([sys.executable, str(REPO / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+                        "--points", "60000"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["check"]["bad_rows_all_ranks"] == 0
+    if inject:
+        assert d["dist_path"] == "torch_steady"
+        fa = d["failed_attempts"][0]
+        assert fa["path"] == "native_pipeline" and fa["failed_rank"] == 1 and fa["rc"] != 0
+        assert any("injected failure" in s for s in fa["stderr_tail"]), fa
+    else:
+        assert d["dist_path"] == "native_pipeline" and d["first_attempt_rc"] == 0
