@@ -144,6 +144,10 @@ struct BuildBuffers {
     int n_owned;
     // points per bucketed-binning block (0: automatic, build.hip bin_plan)
     int bin_items;
+    // launch context of the build (build.hip launch_build): 0 = pipelined (beside running query
+    // kernels: 256-thread streaming blocks of ~16K points up to 4M points), 1 = serial (alone on the
+    // device: 1024-thread blocks of 4096 points, one block per CU at 900K)
+    int serial;
 };
 
 size_t scan_block_count(int num_cells);

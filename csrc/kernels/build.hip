@@ -773,7 +773,13 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
             b.zero_words ? b.n_zero_words : 0);
         return hipGetLastError();
     }
-    if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp, b.bin_items)) {
+    // Serial builds (nothing else on the device: kn_prepare, the serial graph step) use 1024-thread
+    // blocks of 4096 points up to 4M points: ~220 blocks at 900K, one per CU, 16 waves each to hide
+    // the LDS-atomic latency (900K build 0.050 ms vs 0.054 with 256-thread blocks and 0.083 with the
+    // pipelined ~16K-point blocks; profiles/ab_r5_bin_threads.txt, BENCH_r04/r05 ms_build)
+    const bool serial_small = b.serial && n <= (4 << 20);
+    const int items_req = b.bin_items ? b.bin_items : (serial_small ? 4096 : 0);
+    if (b.bin_tmp && !force_atomic && bin_plan(n, C, &bp, items_req)) {
         // geometry folded into bucket_count; scan top level folded into its consumers
         GeomSrc src{};
         src.use_box = b.use_box;
@@ -799,7 +805,7 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
             const int t = v ? std::atoi(v) : 0;
             return (t == 256 || t == 512 || t == 1024) ? t : 0;
         }();
-        const int bin_threads = bin_env ? bin_env : (n <= (4 << 20) ? 256 : 1024);
+        const int bin_threads = bin_env ? bin_env : (n <= (4 << 20) && !b.serial ? 256 : 1024);
         bucket_count_kernel<<<bp.nblocks, bin_threads, bp.nbuckets * sizeof(int), s>>>(
             b.points, n, src, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count, b.zero_words,
             b.n_zero_words);

@@ -277,8 +277,9 @@ QueryBuffers Engine::query_buffers() const {
 
 // fused_step: build + grid query in one stream-ordered step (the captured graph): the build's
 // first binning kernel zeroes the query counters, so the step has no memset node
-kn_status Engine::build_async(bool fused_step) {
+kn_status Engine::build_async(bool fused_step, bool serial) {
     BuildBuffers b = build_buffers();
+    b.serial = serial ? 1 : 0;
     if (fused_step && !use_tree_) {
         b.zero_words = counters_;
         b.n_zero_words = kNumCounters;
@@ -392,6 +393,7 @@ kn_status Engine::prepare_from(const float* src, int n, hipMemcpyKind kind) {
         points3_valid_ = false;
         // adaptive: probe grids are binned without the in-cell order (see launch_cell_sort)
         BuildBuffers b = build_buffers();
+        b.serial = 1;
         if (cfg_.adaptive) b.deterministic = 0;
         if ((st = check(launch_build(b, stream_), "build")) != KN_OK) return st;
         (void)hipEventRecord(ev_[1], stream_);
@@ -644,7 +646,7 @@ kn_status Engine::stage_build(int s, hipStream_t st) {
     hipStream_t ks = stream_;
     view_set(s);
     stream_ = st;
-    kn_status r = build_async(true);
+    kn_status r = build_async(true, /*serial=*/false);  // beside the running queries
     if (r == KN_OK && use_tree_) r = tree_build_async();
     stream_ = ks;
     view_set(keep);

@@ -128,7 +128,8 @@ private:
     kn_status prepare_from(const float* src, int n, hipMemcpyKind kind);
     kn_status occupancy(double* w);
     kn_status ensure_outputs();
-    kn_status build_async(bool fused_step = false);
+    // serial: alone on the device (BuildBuffers::serial); the pipeline stages pass false
+    kn_status build_async(bool fused_step = false, bool serial = true);
     kn_status query_async(bool fused_step = false);
     // Morton-leaf tree over the built grid's points + its query (stream-ordered, capturable)
     kn_status tree_query();

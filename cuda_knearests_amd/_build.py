@@ -31,6 +31,7 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 KERNELS = ["kernels/build.hip", "kernels/query.hip", "kernels/route.hip", "kernels/tree.hip"]
 HOST = ["host/host.cpp"]
 RUNTIME = ["runtime/engine.cpp", "runtime/api.cpp", "runtime/hostio.cpp", "runtime/pipeline.cpp", "runtime/dist.cpp"]
+HIP_TOOLS = ["tools/cu_mask_probe.hip", "tools/repro_capture.hip"]
 MULTI = "runtime/multi.cpp"  # C-API multi-GPU runtime: libknearests.so only (links RCCL)
 RCCL_OK = os.path.exists(os.path.join(ROCM, "include", "rccl", "rccl.h"))
 
@@ -121,8 +122,11 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
             ("multi", MULTI)
         futs[ex.submit(_compile, "tools/knn_cli.cpp", HOSTFLAGS, "tool", force)] = ("tool", "cli")
         futs[ex.submit(_compile, "tools/knn_unit.cpp", HOSTFLAGS, "tool", force)] = ("tool", "unit")
+        # standalone HIP diagnostics (no library): CU-mask -> XCD / CU probe, the capture reproducer
+        for t in HIP_TOOLS:
+            futs[ex.submit(_compile, t, HIPFLAGS, "hiptool", force)] = ("hiptool", t)
         objs: dict[str, list[Path]] = {"kern": [], "kernchk": [], "host": [], "rt": [], "torch": [],
-                                       "torchchk": [], "tool": [], "multi": []}
+                                       "torchchk": [], "tool": [], "multi": [], "hiptool": []}
         tools: dict[str, Path] = {}
         for f in cf.as_completed(futs):
             kind, name = futs[f]
@@ -154,6 +158,10 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> dict:
         _run([HIPCC, "-o", str(exe), str(o), str(lib), f"-Wl,-rpath,{libdir}", f"-Wl,-rpath,$ORIGIN/../cuda_knearests_amd/lib"]
              + hiplink)
         exes[name] = exe
+    for o in objs["hiptool"]:
+        exe = bindir / o.stem.replace("hiptool_tools_", "").replace(".hip", "")
+        _run([HIPCC, "-o", str(exe), str(o)] + hiplink)
+        exes[exe.name] = exe
     res = {"ext": cext, "ext_checked": cchk, "lib": lib, **{f"bin_{k}": v for k, v in exes.items()}}
     if verbose:
         for k, v in res.items():
