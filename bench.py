@@ -545,7 +545,10 @@ def main() -> int:
                     help="N GPUs: validate every step before the next (no asynchronous steady-state steps)")
     args = ap.parse_args()
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if (os.environ.get("KN_BENCH_CHILD") != "1" and os.environ.get("KN_BENCH_SUPERVISE", "1") != "0"
+    # Under a profiler (rocprofv3 preloads its tool library, which initialises the GPU in THIS
+    # process) a supervised child would be forked from a GPU-initialised process: run in-process
+    profiled = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", "")
+    if (os.environ.get("KN_BENCH_CHILD") != "1" and os.environ.get("KN_BENCH_SUPERVISE", "1") != "0" and not profiled
             and not args.cpu_oracle and not args.loopback and not (args.gpus > 1 and world_env == 1)):
         return supervised(args, world_env)
     if not args.cpu_oracle:

@@ -158,8 +158,17 @@ constexpr bool outer_pack_k() {
 #ifndef KN_WIN
 #define KN_WIN 1
 #endif
+// Unrolled re-rank walk for the K buckets with KM <= 24 (key shifts and window rotations become
+// register renames). Round 5 measured it at +-1 %; with the pairwise compare below it wins:
+// in-process A/B, 900K uniform, identical rows (profiles/ab_r6_rerank.txt): K=16 query 0.2878 ->
+// 0.2804 ms, K=8 0.2013 -> 0.1966; K=32 (KM = 35, rolled either way) unchanged.
 #ifndef KN_RERANK_UNROLL
-#define KN_RERANK_UNROLL 0
+#define KN_RERANK_UNROLL 1
+#endif
+// kWin = 1: compare each adjacent pair of kept keys once (see window_pass): 900K K=16 query
+// 0.2914 -> 0.2880 ms, K=32 0.5273 -> 0.5209, K=8 0.2026 -> 0.1992 (profiles/ab_r6_rerank.txt)
+#ifndef KN_RERANK_PAIR
+#define KN_RERANK_PAIR 1
 #endif
 constexpr int kWin = KN_WIN;  // exact re-rank window: same-bucket neighbours within +-kWin
 // Second, wider window for the lanes whose bucket runs overflow +-kWin but fit +-kWin2 (point
@@ -475,16 +484,22 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
           if constexpr (LANE) {
             const int side = 2 * a.H + 1;
             // LDS slot range [s0, s1) of cells [x0, x1] of staged row (y, z); empty if x0 > x1
-            auto lane_span = [&](int y, int z, int x0, int x1) {
+            // (row index r and r * cbs given: the row-synchronous inner loop derives both from the
+            // lane's own row plus a uniform offset, without a per-row integer multiply)
+            auto lane_span_r = [&](int r, int rcb, int x0, int x1) {
                 int2 sp = make_int2(0, 0);
                 if (x0 <= x1) {
-                    const int r = y + nys * z;
                     const int rb = rowbase[r];
-                    sp.x = rb + (int)cbr[r * cbs + x0];
-                    sp.y = KN_IDX(rb + (int)cbr[r * cbs + x1 + 1], S + 1, 212);
+                    sp.x = rb + (int)cbr[rcb + x0];
+                    sp.y = KN_IDX(rb + (int)cbr[rcb + x1 + 1], S + 1, 212);
                 }
                 return sp;
             };
+            auto lane_span = [&](int y, int z, int x0, int x1) {
+                const int r = y + nys * z;
+                return lane_span_r(r, r * cbs, x0, x1);
+            };
+            const int qr0 = cy + nys * cz, qr0cb = qr0 * cbs;  // the lane's own row
             auto body = [&](int2 sp) { body2(sp.x, sp.y); };
             if constexpr (kRowOrder) {
             const int nent = side * side;
@@ -525,13 +540,15 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
             const bool pack = outer_pack_k<KT>() && a.n_outer > 0;
             const int sidein = pack ? 3 : side;  // rows visited row-synchronously
             for (int tz_ = 0; tz_ < sidein; ++tz_) {
-                const int z = cz + ((tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1));
+                const int oz = (tz_ & 1) ? ((tz_ + 1) >> 1) : -(tz_ >> 1);
+                const int z = cz + oz;
                 const float dzb = slab_dist(g, 2, qz, sz0 + z, sz0 + z);
                 const float dz2 = dzb * dzb;
                 const bool zin = live && z >= hz0 && z <= hz1;
                 if (!__builtin_amdgcn_ballot_w64(zin && dz2 <= lane_tau())) continue;
                 for (int ty_ = 0; ty_ < sidein; ++ty_) {
-                    const int y = cy + ((ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1));
+                    const int oy = (ty_ & 1) ? ((ty_ + 1) >> 1) : -(ty_ >> 1);
+                    const int y = cy + oy;
                     const float dyb = slab_dist(g, 1, qy, sy0 + y, sy0 + y);
                     const float dyz2 = fmaf(dyb, dyb, dz2);
                     const float tau = lane_tau();
@@ -546,7 +563,8 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                         }
                     }
                     if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
-                    body(lane_span(y, z, lx0, lx1));
+                    const int ro = oy + nys * oz;  // uniform
+                    body(lane_span_r(qr0 + ro, qr0cb + ro * cbs, lx0, lx1));
                 }
             }
             if (outer_pack_k<KT>() && pack) {
@@ -880,10 +898,24 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
 #pragma unroll
             for (int t = 0; t < NW; ++t) ld((t >= W && t - W < KM) ? keys[t - W] : SENT, t);
             int base = 0;
+            // W = 1 (KN_RERANK_PAIR): each adjacent pair is compared ONCE. c = "entry j+1 precedes
+            // entry j in exact (d2, id) order and shares its truncation bucket"; entry j's position
+            // is base - c(j-1, j) + c(j, j+1), the first term carried from the previous entry. (The
+            // general form compares j with both neighbours, i.e. every pair twice. The validity
+            // test of the earlier entry can be dropped: a SENT key never shares a finite key's
+            // bucket, and an invalid entry's own position is never used.)
+            int c_prev = 0;
             auto entry = [&](int j) __attribute__((always_inline)) {
                 (void)j;
                 const bool vj = wk[W] != SENT;
                 int pos = base;
+                if constexpr (W == 1 && KN_RERANK_PAIR) {
+                    const int same = (int)(wk[2] != SENT) & (int)(((wk[2] ^ wk[1]) & HIMASK) == 0u);
+                    const int lt = (int)(wd[2] < wd[1]) | ((int)(wd[2] == wd[1]) & (int)(wi[2] < wi[1]));
+                    const int c_next = same & lt;
+                    pos += c_next - c_prev;
+                    c_prev = c_next;
+                } else {
 #pragma unroll
                 for (int t = 0; t < NW; ++t) {
                     if (t == W) continue;
@@ -893,6 +925,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     const unsigned ia = t > W ? wi[t] : wi[W], ib = t > W ? wi[W] : wi[t];
                     const int lt = (int)(da < db) | ((int)(da == db) & (int)(ia < ib));
                     pos += (t > W ? 1 : -1) * (same & lt);
+                }
                 }
                 if (vj && act && pos < k) {
                     const size_t o = KN_IDX(row + pos, (size_t)a.n_queries * k, 209);

@@ -749,10 +749,11 @@ kn_status Engine::ensure_pipeline() {
     // i's last workgroup and the kernel boundary (~15 us per step inside a 10-step graph,
     // profiles/r4_pipe_unroll.txt). 900K K=16, interleaved processes on one box: 200 steps
     // 0.2894 -> 0.2756 ms, the driver's 20 / 5 0.3080 -> 0.3048 (profiles/r5_qstreams.txt)
-    static const int qstreams = [] {
+    static const int qstreams_env = [] {
         const char* v = std::getenv("KN_PIPE_QSTREAMS");
         return v ? std::atoi(v) : 2;
     }();
+    const int qstreams = qstreams_cfg_ > 0 ? qstreams_cfg_ : qstreams_env;
     if (!pipe_.ready()) {
         // Three grid sets with two query streams (KN_PIPE_SETS=2: two): step i+1's build then
         // waits for step i-2's query instead of step i-1's, which still runs beside step i's; with
@@ -760,10 +761,11 @@ kn_status Engine::ensure_pipeline() {
         // step i+1's query started after step i's, leaving the GPU without any query kernel 10 %
         // of the time (rocprof, gpurun_out/r5engprof2). Needs one more set in memory: only when it
         // fits comfortably.
-        static const int sets_env = [] {
+        static const int sets_env0 = [] {
             const char* v = std::getenv("KN_PIPE_SETS");
             return v ? std::atoi(v) : 3;
         }();
+        const int sets_env = sets_cfg_ > 0 ? sets_cfg_ : sets_env0;
         nsets_ = 2;
         if (qstreams >= 2 && sets_env >= 3) {
             size_t fr = 0, tot = 0;
@@ -811,6 +813,17 @@ kn_status Engine::ensure_pipeline() {
         if ((st = check(pipe_.init(stream_, bstream_, b, q, x, false, qstreams, nsets_), "pipeline init")) != KN_OK)
             return st;
     }
+    return KN_OK;
+}
+
+kn_status Engine::set_pipeline_shape(int query_streams, int sets) {
+    if (query_streams != -1 && query_streams != 1 && query_streams != 2)
+        return fail(KN_ERR_INVALID_ARGUMENT, "set_pipeline_shape: query streams must be 1, 2 or -1");
+    if (sets != -1 && sets != 2 && sets != 3) return fail(KN_ERR_INVALID_ARGUMENT, "set_pipeline_shape: sets must be 2, 3 or -1");
+    if (query_streams == qstreams_cfg_ && sets == sets_cfg_) return KN_OK;
+    qstreams_cfg_ = query_streams;
+    sets_cfg_ = sets;
+    if (pipe_.ready()) drop_pipeline(/*keep_grid=*/true);  // rebuilt with the new shape on next use
     return KN_OK;
 }
 

@@ -86,6 +86,11 @@ public:
     kn_status stream_batch(int m, const float* const* d_in, unsigned* const* d_idx, float* const* d_dist);
     // stream_batch mode: 0 eager batch pipeline, 1 captured batch graphs, -1 KN_BATCH_MODE (default eager)
     void set_batch_mode(int mode) { batch_mode_ = mode; }
+    // Shape of the resident / batch pipeline for THIS engine (-1: the process-wide KN_PIPE_QSTREAMS /
+    // KN_PIPE_SETS defaults, read once): query streams 1 or 2, grid sets 2 or 3. A change drops a
+    // pipeline already built (its graphs and extra grid sets); tests use it to cover the unrolled
+    // one-query-stream path in-process.
+    kn_status set_pipeline_shape(int query_streams, int sets);
     kn_status sync();  // both streams
     // Device-to-device copy of the original-space results into caller buffers.
     kn_status copy_results(unsigned* d_idx, float* d_dist);
@@ -160,6 +165,7 @@ private:
     kn_status stage_exact(int s, hipStream_t st);  // the fallback list's exact finish (epilogue)
     // keep_grid: the live grid (maybe in arena2_) must survive into arena_ (set_k keeps solving it)
     void drop_pipeline(bool keep_grid = false);
+    int qstreams_cfg_ = -1, sets_cfg_ = -1;  // set_pipeline_shape (-1: environment defaults)
     GridSet set_[3]{};
     int nsets_ = 2;            // grid sets of the resident pipeline (3 with two query streams)
     kn_status carve_set(int s, char* base);

@@ -1,6 +1,7 @@
 // pipeline.cpp -- see pipeline.hpp.
 #include "pipeline.hpp"
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace kn {
@@ -161,6 +162,12 @@ hipError_t Pipeline::unrolled(int s0, int U) {
     // own builds, so step j+1's workgroups fill the CUs that step j's tail leaves idle instead of
     // waiting for its last workgroup and the kernel boundary
     hipStream_t qst[2] = {main_, aux_ ? aux_ : main_};
+    // KN_PIPE_TRACE=1 (diagnostics): stderr marks around the capture's phases
+    static const bool trace = [] {
+        const char* v = std::getenv("KN_PIPE_TRACE");
+        return v && v[0] == '1';
+    }();
+    if (trace) std::fprintf(stderr, "[pipeline] unrolled(%d, U=%d): begin capture (aux %d)\n", s0, U, aux_ ? 1 : 0);
     KN_TRY(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
     hipError_t e = hipEventRecord(fork, origin);
     if (e == hipSuccess) e = hipStreamWaitEvent(other, fork, 0);
@@ -182,13 +189,16 @@ hipError_t Pipeline::unrolled(int s0, int U) {
     if (e == hipSuccess) e = hipStreamWaitEvent(origin, join, 0);
     if (e == hipSuccess && aux_) e = hipEventRecord(join2, aux_);
     if (e == hipSuccess && aux_) e = hipStreamWaitEvent(origin, join2, 0);
+    if (trace) std::fprintf(stderr, "[pipeline] unrolled(%d): stages enqueued (%s), end capture\n", s0, hipGetErrorString(e));
     const hipError_t ee = hipStreamEndCapture(origin, &g);
+    if (trace) std::fprintf(stderr, "[pipeline] unrolled(%d): captured (%s), instantiate\n", s0, hipGetErrorString(ee));
     if (e != hipSuccess) {
         if (g) (void)hipGraphDestroy(g);
         return e;
     }
     KN_TRY(ee);
     e = hipGraphInstantiate(&gU_[s0], g, nullptr, nullptr, 0);
+    if (trace) std::fprintf(stderr, "[pipeline] unrolled(%d): instantiated (%s)\n", s0, hipGetErrorString(e));
     (void)hipGraphDestroy(g);
     if (e == hipSuccess) gU_len_[s0] = U;
     return e;
@@ -293,7 +303,13 @@ hipError_t Pipeline::launch(int iters, int unroll, bool keep_primed) {
     // libamdhip64 while capturing, profiles/r5_qstreams.txt), and 2-step graphs measured slower
     // than per-step launches (900K K=16, 200 steps: 0.2828 vs 0.2756 ms; one query stream with
     // 10-step graphs 0.2894)
-    if (aux_ || ns_ != 2) unroll = 0;
+    // (KN_PIPE_UNROLL_QS2=1, diagnostics: capture the unrolled graphs with both query streams anyway;
+    // tools/repro_capture.hip is the standalone reproducer, profiles/r6_capture_repro.txt)
+    static const bool force_qs2 = [] {
+        const char* v = std::getenv("KN_PIPE_UNROLL_QS2");
+        return v && v[0] == '1';
+    }();
+    if ((aux_ && !force_qs2) || ns_ != 2) unroll = 0;
     if (unroll) {
         // both start parities up front (also by a call of fewer steps, e.g. a warm-up): a capture
         // never lands inside a later (timed) call

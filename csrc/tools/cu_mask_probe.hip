@@ -4,8 +4,8 @@
 //
 // For every mask bit i < multiProcessorCount: a stream whose mask holds only bit i runs 64
 // one-wave workgroups; each records HW_REG_XCC_ID and HW_REG_HW_ID (vector stores). Prints one
-// line per bit: "bit xcc hw_id(hex) distinct" (distinct: how many different (xcc, hw cu) the
-// workgroups saw; 1 = the mask pinned them to one CU).
+// line per bit: its first workgroup's XCC / SE / SH / CU, and how many distinct (xcc, se, sh, cu)
+// and XCCs its 64 workgroups saw (1 = the mask pinned them to one CU).
 //   hipcc --offload-arch=gfx950 -O2 csrc/tools/cu_mask_probe.hip -o bin/cu_mask_probe
 #include <hip/hip_runtime.h>
 
@@ -42,7 +42,7 @@ int main() {
     unsigned* d = nullptr;
     CK(hipMalloc(&d, 2 * kBlocks * sizeof(unsigned)));
     std::vector<unsigned> h(2 * kBlocks);
-    std::printf("# %s, %d CUs; bit xcc hw_id distinct\n", prop.gcnArchName, ncu);
+    std::printf("# %s, %d CUs\n", prop.gcnArchName, ncu);
     for (int bit = 0; bit < ncu; ++bit) {
         std::vector<uint32_t> mask(words, 0u);
         mask[bit / 32] = 1u << (bit % 32);
@@ -54,9 +54,16 @@ int main() {
         CK(hipMemcpyAsync(h.data(), d, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
         CK(hipStreamDestroy(s));
+        // HW_ID: [11:8] cu_id, [12] sh_id, [14:13] se_id (tg / vm / queue ids above vary per launch)
         std::set<std::pair<unsigned, unsigned>> seen;
-        for (int b = 0; b < kBlocks; ++b) seen.insert({h[2 * b], (h[2 * b + 1] >> 8) & 0xffffu});
-        std::printf("%d %u %08x %zu\n", bit, h[0], h[1], seen.size());
+        std::set<unsigned> xccs;
+        for (int b = 0; b < kBlocks; ++b) {
+            seen.insert({h[2 * b], (h[2 * b + 1] >> 8) & 0x7fu});
+            xccs.insert(h[2 * b]);
+        }
+        const unsigned w = (h[1] >> 8) & 0x7fu;
+        std::printf("%d xcc %u se %u sh %u cu %u distinct %zu xccs %zu\n", bit, h[0], (w >> 5) & 3u, (w >> 4) & 1u,
+                    w & 15u, seen.size(), xccs.size());
     }
     CK(hipFree(d));
     return 0;

@@ -6,7 +6,10 @@
 // with empty kernels for the stages: three streams (main = capture origin, side = builds, aux =
 // second query stream), U steps; step j: Q(j) on qst[j & 1] after B(j) (event eb[j-1]); then,
 // on the side stream, after Q(j-1) (event eq[j-1]) the optional epilogue R(j-1), and B(j+1).
-//   repro_capture [U=4] [aux=1] [epilogue=0] [build_kernels=5] [query_kernels=2] [from_side=0]
+//   repro_capture [U=4] [aux=1] [epilogue=0] [build_kernels=5] [query_kernels=2] [from_side=0] [captures=2] [pre=1]
+// captures = 2: both start parities are captured with the SAME events, one after the other, as
+// Pipeline::launch does (unrolled(0), unrolled(1)). Run it against torch's bundled HIP runtime
+// (LD_LIBRARY_PATH=<torch>/lib) to match the extension's process: the round-5 crash was there.
 // Prints "captured ... launched ... ok" or dies (a host crash inside the runtime is a segfault:
 // exit status 139).
 #include <hip/hip_runtime.h>
@@ -35,8 +38,15 @@ int main(int argc, char** argv) {
     const int nb = argc > 4 ? std::atoi(argv[4]) : 5;
     const int nq = argc > 5 ? std::atoi(argv[5]) : 2;
     const bool from_side = argc > 6 ? std::atoi(argv[6]) != 0 : false;
-    std::printf("U=%d aux=%d epilogue=%d build_kernels=%d query_kernels=%d capture_from_side=%d\n", U, use_aux,
-                use_r, nb, nq, from_side);
+    const int ncap = argc > 7 ? std::atoi(argv[7]) : 2;
+    // pre = 1: first capture every stage alone on the main stream, per set (Pipeline::graphs()),
+    // as launch() does before the unrolled captures
+    const bool pre = argc > 8 ? std::atoi(argv[8]) != 0 : true;
+    int rtv = 0, drv = 0;
+    CK(hipRuntimeGetVersion(&rtv));
+    CK(hipDriverGetVersion(&drv));
+    std::printf("HIP runtime %d driver %d; U=%d aux=%d epilogue=%d build_kernels=%d query_kernels=%d "
+                "capture_from_side=%d captures=%d pre=%d\n", rtv, drv, U, use_aux, use_r, nb, nq, from_side, ncap, pre);
     std::fflush(stdout);
     int* d = nullptr;
     CK(hipMalloc(&d, 64 * sizeof(int)));
@@ -55,6 +65,22 @@ int main(int argc, char** argv) {
     hipEvent_t* eb = ev.data() + 3 + U;
     hipStream_t origin = from_side ? side_s : main_s, other = from_side ? main_s : side_s;
     hipStream_t qst[2] = {main_s, aux_s ? aux_s : main_s};
+    std::vector<hipGraphExec_t> execs;
+    if (pre) {
+        for (int set = 0; set < 2; ++set)
+            for (int kind = 0; kind < (use_r ? 3 : 2); ++kind) {
+                hipGraph_t g = nullptr;
+                CK(hipStreamBeginCapture(main_s, hipStreamCaptureModeThreadLocal));
+                CK(stage(kind == 0 ? nb : kind == 1 ? nq : 1, 10 + kind, main_s));
+                CK(hipStreamEndCapture(main_s, &g));
+                hipGraphExec_t gx = nullptr;
+                CK(hipGraphInstantiate(&gx, g, nullptr, nullptr, 0));
+                CK(hipGraphDestroy(g));
+                execs.push_back(gx);
+            }
+        std::printf("per-stage graphs: %zu\n", execs.size());
+    }
+    for (int c = 0; c < ncap; ++c) {
     hipGraph_t g = nullptr;
     CK(hipStreamBeginCapture(origin, hipStreamCaptureModeThreadLocal));
     CK(hipEventRecord(fork, origin));
@@ -81,17 +107,20 @@ int main(int argc, char** argv) {
     CK(hipStreamEndCapture(origin, &g));
     size_t nodes = 0;
     CK(hipGraphGetNodes(g, nullptr, &nodes));
-    std::printf("captured: %zu nodes\n", nodes);
+    std::printf("capture %d: %zu nodes\n", c, nodes);
     std::fflush(stdout);
     hipGraphExec_t gx = nullptr;
     CK(hipGraphInstantiate(&gx, g, nullptr, nullptr, 0));
-    std::printf("instantiated\n");
+    CK(hipGraphDestroy(g));
+    std::printf("instantiated %d\n", c);
     std::fflush(stdout);
-    for (int i = 0; i < 3; ++i) CK(hipGraphLaunch(gx, main_s));
+    execs.push_back(gx);
+    }
+    for (int i = 0; i < 3; ++i)
+        for (auto gx : execs) CK(hipGraphLaunch(gx, main_s));
     CK(hipStreamSynchronize(main_s));
     std::printf("launched 3x: ok\n");
-    CK(hipGraphExecDestroy(gx));
-    CK(hipGraphDestroy(g));
+    for (auto gx : execs) CK(hipGraphExecDestroy(gx));
     for (auto e : ev) CK(hipEventDestroy(e));
     CK(hipFree(d));
     return 0;

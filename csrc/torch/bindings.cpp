@@ -1185,6 +1185,18 @@ public:
         KN_CHECK_HIP(hipStreamSynchronize(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream()));
         TORCH_CHECK(e_->stream_batch((int)m, in.data(), oi.data(), d2.has_value() ? od.data() : nullptr) == KN_OK,
                     e_->error());
+        // the batch still reads / writes these tensors on the engine's private streams: hold them
+        // until sync() (a caller dropping one early must not let the caching allocator
+        // hand its memory to other work while the batch runs)
+        for (size_t j = 0; j < m; ++j) {
+            held_.push_back(points[j]);
+            held_.push_back(idx[j]);
+            if (d2.has_value()) held_.push_back((*d2)[j]);
+        }
+    }
+    // per-engine pipeline shape (query streams 1 / 2, grid sets 2 / 3; -1: KN_PIPE_* defaults)
+    void set_pipeline_shape(int64_t query_streams, int64_t sets) {
+        TORCH_CHECK(e_->set_pipeline_shape((int)query_streams, (int)sets) == KN_OK, e_->error());
     }
     // stored -> original permutation of the engine's current grid (host int32)
     torch::Tensor permutation() {
@@ -1195,7 +1207,10 @@ public:
         free(p);
         return t;
     }
-    void sync() { TORCH_CHECK(e_->sync() == KN_OK, e_->error()); }
+    void sync() {
+        TORCH_CHECK(e_->sync() == KN_OK, e_->error());
+        held_.clear();  // every batch enqueued so far has finished with its tensors
+    }
     std::vector<torch::Tensor> results(torch::Device dev) {
         const int64_t n = e_->n(), k = e_->k();
         auto opt = torch::TensorOptions().device(dev);
@@ -1236,6 +1251,7 @@ public:
 
 private:
     std::unique_ptr<kn::Engine> e_;
+    std::vector<torch::Tensor> held_;  // stream_batch inputs / outputs in flight (released by sync())
 };
 
 // -DKN_PHASES=1 builds: knn_tile_kernel wave cycles per phase (kn/kernels.h); empty otherwise
@@ -1772,6 +1788,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         .def("stream_step", &PyEngine::stream_step, py::arg("points"), py::arg("next") = py::none())
         .def("stream_batch", &PyEngine::stream_batch, py::arg("points"), py::arg("idx"), py::arg("d2") = py::none(),
              py::arg("mode") = py::none())
+        .def("set_pipeline_shape", &PyEngine::set_pipeline_shape, py::arg("query_streams") = -1, py::arg("sets") = -1)
         .def("get_permutation", &PyEngine::permutation)
         .def("sync", &PyEngine::sync)
         .def("results", &PyEngine::results)

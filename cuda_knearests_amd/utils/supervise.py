@@ -50,6 +50,7 @@ class Outcome:
     stderr_tail: list
     first_failure: Optional[dict] = None   # {"rank", "rc", "stderr_tail"} of the rank that failed first
     rcs: Optional[list] = None             # every rank's exit code (rank 0 only; None: unknown)
+    failures: Optional[list] = None        # every failing rank's {"rank", "rc", "stderr_tail"} (rank 0)
 
 
 def free_port(host: str = "127.0.0.1") -> int:
@@ -213,10 +214,14 @@ def supervise(cmd: list, attempts: list, rank: int = 0, world: int = 1, store=No
         failed = False
 
         def report_failure(rc_desc):
-            # fail before done, so done == world implies fail is final; the first failing rank
-            # leaves its exit code and last stderr lines for rank 0's JSON line
+            # every failing rank leaves its exit code and last stderr lines for rank 0's JSON line
+            # (written BEFORE fail is raised, so a rank that sees fail > 0 and passes the exit barrier
+            # finds them); fail before done, so done == world implies fail is final. The first to
+            # fail is not always the cause: a peer blocked in a collective may die first
+            rec = {"rank": rank, "rc": rc_desc, "stderr_tail": list(child.err)[-12:]}
+            co.set(f"a{i}/failrec/{rank}", json.dumps(rec))
             if co.add(f"a{i}/fail", 1) == 1:
-                co.set(f"a{i}/first", json.dumps({"rank": rank, "rc": rc_desc, "stderr_tail": list(child.err)[-12:]}))
+                co.set(f"a{i}/first", json.dumps(rec))
 
         while True:
             rc = child.poll()
@@ -256,6 +261,8 @@ def supervise(cmd: list, attempts: list, rank: int = 0, world: int = 1, store=No
         if rank == 0:
             rcs = [co.get(f"a{i}/rc/{r}") for r in range(world)]
             out.rcs = [int(v) if v is not None else None for v in rcs]
+            recs = [co.get(f"a{i}/failrec/{r}") for r in range(world)]
+            out.failures = [json.loads(v) for v in recs if v]
     co.leave("end")
     return -1, outcomes
 
@@ -271,7 +278,10 @@ def annotate(line: dict, attempts: list, ok_index: int, outcomes: list) -> dict:
         line["failed_attempts"] = []
         for j in range(ok_index):
             f = outcomes[j].first_failure or {}
+            fails = outcomes[j].failures or ([f] if f else [])
             line["failed_attempts"].append({
                 "path": attempts[j].name, "failed_rank": f.get("rank"), "rc": f.get("rc", outcomes[j].rc),
-                "rank_rcs": outcomes[j].rcs, "stderr_tail": f.get("stderr_tail", outcomes[j].stderr_tail[-12:])})
+                "rank_rcs": outcomes[j].rcs, "stderr_tail": f.get("stderr_tail", outcomes[j].stderr_tail[-12:]),
+                "failed_ranks": [{"rank": x.get("rank"), "rc": x.get("rc"), "stderr_tail": x.get("stderr_tail", [])[-6:]}
+                                 for x in fails]})
     return line

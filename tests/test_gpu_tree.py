@@ -284,13 +284,16 @@ def test_tree_long_axis(cuda):
     _check(p, idx, d2, k)
 
 
+@pytest.mark.parametrize("qstreams", [1, 2])
 @pytest.mark.parametrize("k", [16, 50])
-def test_engine_stream_after_unrolled(cuda, k):
+def test_engine_stream_after_unrolled(cuda, k, qstreams):
     """A stream step issued right after an UNROLLED resident launch, with no sync in between
     (the unrolled graph's last queries and its primed build use both grid sets, so the
     stream step's copy into a set must wait for the whole graph, not for a pre-graph event).
     K=16 has no epilogue (nothing on the side stream follows the graph), K=50 has one. Every
-    stream step's rows equal the oracle's on its own cloud."""
+    stream step's rows equal the oracle's on its own cloud. One query stream and two sets
+    (set_pipeline_shape) is the shape that really runs unrolled graphs; with the default
+    two query streams the same calls run per-step graphs."""
     from cuda_knearests_amd._ext import load
 
     C = load()
@@ -299,6 +302,8 @@ def test_engine_stream_after_unrolled(cuda, k):
     base = uniform_cloud(n, seed=41).to(cuda)
     clouds = [uniform_cloud(n, seed=950 + j).to(cuda) for j in range(3)]
     e = C.Engine(k)
+    if qstreams == 1:
+        e.set_pipeline_shape(1, 2)
     e.prepare(base)
     for rep in range(2):
         e.launch_pipelined(2 * unroll, unroll)  # unrolled graphs, primed at the end
@@ -312,16 +317,20 @@ def test_engine_stream_after_unrolled(cuda, k):
         e.prepare(base)
 
 
+@pytest.mark.parametrize("qstreams", [1, 2])
 @pytest.mark.parametrize("unroll", [2, 4, 8])
-def test_engine_unrolled_pipeline(cuda, unroll):
+def test_engine_unrolled_pipeline(cuda, unroll, qstreams):
     """Unrolled pipelined graphs (U steps per graph launch, pipeline.hpp) give the serial step's
     rows bit for bit, for step counts that are not multiples of U, and mix with per-step launches
-    and serial graph replays."""
+    and serial graph replays. qstreams 1 (two sets) runs the unrolled graphs themselves; 2 the
+    default per-step graphs of two query streams."""
     from cuda_knearests_amd._ext import load
 
     C = load()
     p = uniform_cloud(60000, seed=57).to(cuda)
     e = C.Engine(16)
+    if qstreams == 1:
+        e.set_pipeline_shape(1, 2)
     e.prepare(p)
     e.solve()
     idx, d2 = e.results(cuda)

@@ -98,6 +98,7 @@ def test_world2_parents_agree(case):
     assert line["dist_path"] == "torch" and line["tag"] == "b"
     fa = line["failed_attempts"][0]
     assert fa["failed_rank"] == (1 if case == "peer_fails_rank0_hangs" else 0) and fa["rc"] == 3
+    assert [x["rank"] for x in fa["failed_ranks"]] == [fa["failed_rank"]]
     assert line["first_attempt_rc"] == 3 and len(fa["rank_rcs"]) == 2
     assert any("CollectiveError" in s for s in fa["stderr_tail"])
 

@@ -15,7 +15,9 @@ shift || true
 stamp=$(date +%Y%m%d_%H%M%S)
 O=$R/gpurun_out/profile/${mode}_$stamp
 mkdir -p "$O"
-export PYTHONPATH=$R TMPDIR=/tmp
+# KN_BENCH_SUPERVISE=0: bench.py runs its job in-process (no child forked from a process the
+# profiler's preload has already attached to the GPU)
+export PYTHONPATH=$R TMPDIR=/tmp KN_BENCH_SUPERVISE=0
 cd /tmp
 case $mode in
   kstats|timeline)
