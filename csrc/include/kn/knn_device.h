@@ -158,8 +158,20 @@ __device__ __forceinline__ unsigned cand_key_v(const float4& p, float qx, float 
 // (scripts/sim_wave_order.py machinery, /tmp replays recorded in DESIGN.md): med3 slots per wave
 // K=16 -8 % (half) / -6 % (quarters), K=50 -13 % / -17 %. 0 = one network, 1 = halves,
 // 2 = quarters.
+//
+// Gated tiers (KN_TOPK_TIERS = T > 1, round 6): the SAME network, run top-down in T slices, each
+// lower slice behind its own uniform ballot. new[j] only reads old[j-1], old[j] and the key, so
+// slices [LO, HI) computed from the top keep every read an old value; and for a lane whose key is
+// >= old[LO-1], every slot below LO is unchanged by its own formula, so a slice that no lane of
+// the wave reaches is skipped exactly. Unlike the split networks above there is ONE copy of every
+// med3 (no duplicated upper part): per candidate step a slice costs one compare + branch, and saves
+// its med3s whenever no inserting lane's key falls into it (late in a walk most insertions land in
+// the upper ranks of a full list).
 #ifndef KN_TOPK_SPLIT
 #define KN_TOPK_SPLIT 0
+#endif
+#ifndef KN_TOPK_TIERS
+#define KN_TOPK_TIERS 1
 #endif
 template <int KM, int LO>
 __device__ __forceinline__ void topk_net(unsigned (&keys)[KM], unsigned key) {
@@ -168,10 +180,30 @@ __device__ __forceinline__ void topk_net(unsigned (&keys)[KM], unsigned key) {
     if constexpr (LO == 0) keys[0] = min(keys[0], key);
     else keys[LO] = med3_u32(keys[LO - 1], key, keys[LO]);
 }
-template <int KM, int SPLIT = KN_TOPK_SPLIT>
+// slots [LO, HI) of the network (top-down); LO = 0 takes the plain min at slot 0
+template <int KM, int LO, int HI>
+__device__ __forceinline__ void topk_slice(unsigned (&keys)[KM], unsigned key) {
+#pragma unroll
+    for (int j = HI - 1; j >= LO; --j) keys[j] = j == 0 ? min(keys[0], key) : med3_u32(keys[j - 1], key, keys[j]);
+}
+// tier t of T covers slots [lo(t), lo(t - 1)) from the top: t = 0 is the top slice
+template <int KM, int T, int t>
+__device__ __forceinline__ void topk_tiers(unsigned (&keys)[KM], unsigned key) {
+    constexpr int HI = t == 0 ? KM : (KM * (T - t)) / T;
+    constexpr int LO = (KM * (T - t - 1)) / T;
+    topk_slice<KM, LO, HI>(keys, key);
+    if constexpr (t + 1 < T && LO > 0) {
+        // the next slice changes only lanes whose key is below old[LO - 1] (still old: the slices
+        // above never write below LO)
+        if (__builtin_amdgcn_ballot_w64(key < keys[LO - 1])) topk_tiers<KM, T, t + 1>(keys, key);
+    }
+}
+template <int KM, int SPLIT = KN_TOPK_SPLIT, int TIERS = KN_TOPK_TIERS>
 __device__ __forceinline__ unsigned topk_push(unsigned (&keys)[KM], unsigned key) {
     if (__builtin_amdgcn_ballot_w64(key < keys[KM - 1])) {
-        if constexpr (SPLIT == 0 || KM < 8) {
+        if constexpr (TIERS > 1 && KM >= 2 * TIERS) {
+            topk_tiers<KM, TIERS, 0>(keys, key);
+        } else if constexpr (SPLIT == 0 || KM < 8) {
             topk_net<KM, 0>(keys, key);
         } else if constexpr (SPLIT == 1) {
             constexpr int H = KM / 2;

@@ -291,6 +291,16 @@ __device__ __forceinline__ void tile_coords(int lin, int ntx, int nty, int ntz, 
 #endif
 template <int KT>
 constexpr int tile_wpe() { return KT > 50 ? KN_TILE_WPE64 : 1; }
+// Gated-tier top-K networks (kn/knn_device.h topk_tiers) per K bucket: in-process A/B at 900K
+// uniform, identical rows (profiles/ab_r6_tiers.txt): K=50 bucket 3 tiers 0.904 -> 0.877 ms
+// (2 tiers -1.6 %), K=64 bucket 4 tiers 1.009 -> 0.912 (3 tiers -8 %); at K <= 32 every tier count
+// lost (K=16 +0.2 / +2 / +6.5 %, K=32 +2.4 ... +12 %, K=8 +1.6 ... +5 %): their lists are short and
+// a slice's compare + branch costs more than the med3s it skips. KN_TILE_TIERS=T forces T.
+#ifndef KN_TILE_TIERS
+#define KN_TILE_TIERS 0
+#endif
+template <int KT>
+constexpr int tile_tiers() { return KN_TILE_TIERS > 0 ? KN_TILE_TIERS : KT > 50 ? 4 : KT > 40 ? 3 : 1; }
 template <int KT, int M, bool LANE, bool WIDE = false>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT>(), 8))) void knn_tile_kernel(TileArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
@@ -778,12 +788,12 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                         for (int u = 0; u < kUnroll; ++u) kk[u] = cand_key_v(p[u], qx, qy, qz, HIMASK, s + u);
 #pragma unroll
                         for (int u = 0; u < kUnroll; ++u) {
-                            const unsigned i0 = topk_push<KM>(keys, kk[u]);
+                            const unsigned i0 = topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, kk[u]);
                             if constexpr (kStats) st_ins += i0;
                         }
                     }
                     for (; s < s1; ++s) {
-                        const unsigned i0 = topk_push<KM>(keys, cand_key_v(pts[s], qx, qy, qz, HIMASK, s));
+                        const unsigned i0 = topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, cand_key_v(pts[s], qx, qy, qz, HIMASK, s));
                         if constexpr (kStats) st_ins += i0;
                     }
                     return;
@@ -803,10 +813,10 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                         const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, sb + 2, qslot);
                         const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, sb + 3, qslot);
                         asm volatile("" ::"v"(k0), "v"(k1), "v"(k2), "v"(k3));
-                        const unsigned i0 = topk_push<KM>(keys, k0);
-                        const unsigned i1 = topk_push<KM>(keys, k1);
-                        const unsigned i2 = topk_push<KM>(keys, k2);
-                        const unsigned i3 = topk_push<KM>(keys, k3);
+                        const unsigned i0 = topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k0);
+                        const unsigned i1 = topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k1);
+                        const unsigned i2 = topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k2);
+                        const unsigned i3 = topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k3);
                         if constexpr (kStats) st_ins += i0 + i1 + i2 + i3;
                     };
                     while (true) {
@@ -821,7 +831,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     }
                 }
                 for (; s < s1; ++s) {
-                    const unsigned i0 = topk_push<KM>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
+                    const unsigned i0 = topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, cand_key(pts[s], qx, qy, qz, HIMASK, s, qslot));
                     if constexpr (kStats) st_ins += i0;
                 }
                 }
@@ -1314,12 +1324,12 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
                     const unsigned k2 = cand_key(p2, qx, qy, qz, HIMASK, (int)pp + 2, 0);
                     const unsigned k3 = cand_key(p3, qx, qy, qz, HIMASK, (int)pp + 3, 0);
                     asm volatile("" ::"v"(k0), "v"(k1), "v"(k2), "v"(k3));
-                    topk_push<KM>(keys, k0);
-                    topk_push<KM>(keys, k1);
-                    topk_push<KM>(keys, k2);
-                    topk_push<KM>(keys, k3);
+                    topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k0);
+                    topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k1);
+                    topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k2);
+                    topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, k3);
                 }
-                for (; i < i1; ++i, ++pp) topk_push<KM>(keys, cand_key(ring[i], qx, qy, qz, HIMASK, (int)pp, 0));
+                for (; i < i1; ++i, ++pp) topk_push<KM, KN_TOPK_SPLIT, tile_tiers<KT>()>(keys, cand_key(ring[i], qx, qy, qz, HIMASK, (int)pp, 0));
             }
             pos += (unsigned)(s1 - s0);
         }
