@@ -465,14 +465,17 @@ def supervised(args, world: int) -> int:
     from cuda_knearests_amd.utils.supervise import Attempt, annotate, make_store, supervise
 
     rank = int(os.environ.get("RANK", "0"))
-    t1 = float(os.environ.get("KN_BENCH_ATTEMPT_S", "420"))
+    # per-attempt limits: a normal 8-GPU run takes ~1-2 min (RCCL init, the validating step, 25
+    # steps, the spot check); a hung attempt must leave time for the fallbacks
+    t1 = float(os.environ.get("KN_BENCH_ATTEMPT_S", "300"))
+    t2 = float(os.environ.get("KN_BENCH_FALLBACK_S", "240"))
     if world > 1 or args.dist:
         attempts = [Attempt("native_pipeline", {}, [], t1),
-                    Attempt("torch_steady", {"KN_DIST_PIPE": "0"}, [], 300.0),
-                    Attempt("torch_sync_steps", {"KN_DIST_PIPE": "0"}, ["--sync-steps"], 300.0)]
+                    Attempt("torch_steady", {"KN_DIST_PIPE": "0"}, [], t2),
+                    Attempt("torch_sync_steps", {"KN_DIST_PIPE": "0"}, ["--sync-steps"], t2)]
     else:
         attempts = [Attempt("pipelined" if args.pipeline else "serial", {}, [], t1),
-                    Attempt("serial", {}, ["--no-pipeline"], 300.0)]
+                    Attempt("serial", {}, ["--no-pipeline"], t2)]
     store = make_store(rank, world)
     cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     ok, outs = supervise(cmd, attempts, rank, world, store)

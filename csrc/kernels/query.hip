@@ -184,6 +184,18 @@ template <int V>
 struct IntC {
     static constexpr int value = V;
 };
+// f(IntC<I>{}) ... f(IntC<N - 1>{}): a compile-time unrolled loop whose body sees a constant index
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F& f) {
+    if constexpr (I < N) {
+        f(IntC<I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+// entries per shift of the rolled re-rank walk (KM > 24; see window_pass)
+#ifndef KN_RERANK_GROUP
+#define KN_RERANK_GROUP 4
+#endif
 // Round-3 A/Bs of the lane walk that LOST against this kernel (900K uniform, interleaved in
 // process, identical rows; profiles/ab_r3_lane_variants.jsonl, profiles/ab_r3_collect.jsonl):
 //  * collect-then-select (d2-only scan + per-lane LDS queue of candidate slots, bulk med3
@@ -915,8 +927,9 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
             // test of the earlier entry can be dropped: a SENT key never shares a finite key's
             // bucket, and an invalid entry's own position is never used.)
             int c_prev = 0;
-            auto entry = [&](int j) __attribute__((always_inline)) {
-                (void)j;
+            // entry(u): the next kept key; u = its compile-time offset since the last shift of keys[]
+            auto entry = [&](auto uc) __attribute__((always_inline)) {
+                constexpr int u = decltype(uc)::value;
                 const bool vj = wk[W] != SENT;
                 int pos = base;
                 if constexpr (W == 1 && KN_RERANK_PAIR) {
@@ -946,20 +959,24 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                 base += vj ? 1 : 0;
 #pragma unroll
                 for (int t = 0; t + 1 < NW; ++t) { wk[t] = wk[t + 1]; wd[t] = wd[t + 1]; wi[t] = wi[t + 1]; }
-                // entry j + W + 1 sits at keys[W + 1] after j + 1 shifts
-                ld(KM > W + 1 ? keys[W + 1 < KM ? W + 1 : KM - 1] : SENT, NW - 1);
-#pragma unroll
-                for (int t = 0; t + 1 < KM; ++t) keys[t] = keys[t + 1];
-                keys[KM - 1] = SENT;
+                // entry j + W + 1 sits at keys[W + 1 + u] (keys[] shifted j - u times so far)
+                constexpr int nx = W + 1 + u;
+                ld(nx < KM ? keys[nx < KM ? nx : KM - 1] : SENT, NW - 1);
             };
-            // KN_RERANK_UNROLL: the K buckets with KM <= 24 unroll the walk, so the key shifts and
-            // window rotations become register renames instead of ~KM + 3 * NW moves per entry
+            // KN_RERANK_UNROLL: the K buckets with KM <= 24 unroll the whole walk (no key shifts:
+            // register renames). Larger lists run a rolled loop over groups of KN_RERANK_GROUP
+            // entries, shifting keys[] once per group (KM - G moves per G entries instead of per
+            // entry; the < G padding entries past the end see SENT keys and write nothing).
             if constexpr (KN_RERANK_UNROLL && KM <= 24) {
-#pragma unroll
-                for (int j = 0; j < KM; ++j) entry(j);
+                static_for<0, KM>(entry);
             } else {
+                constexpr int G = KN_RERANK_GROUP;
 #pragma unroll 1
-                for (int j = 0; j < KM; ++j) entry(j);
+                for (int jj = 0; jj < KM; jj += G) {
+                    static_for<0, G>(entry);
+#pragma unroll
+                    for (int t = 0; t < KM; ++t) keys[t] = t + G < KM ? keys[t + G < KM ? t + G : KM - 1] : SENT;
+                }
             }
             nfound = base;
         };

@@ -464,6 +464,16 @@ __global__ __launch_bounds__(64) void node_box_kernel(float4* __restrict__ nlo, 
 #ifndef KN_TREE_WPE64
 #define KN_TREE_WPE64 2
 #endif
+// Gated-tier top-K networks in the tree query (kn/knn_device.h topk_tiers): KN_TREE_TIERS = T > 0
+// forces T, -1 = the tile kernel's rule (3 tiers for the K=50 bucket, 4 for K=64), 0 (default)
+// one network
+#ifndef KN_TREE_TIERS
+#define KN_TREE_TIERS 0
+#endif
+template <int KT>
+constexpr int tree_tiers() {
+    return KN_TREE_TIERS > 0 ? KN_TREE_TIERS : KN_TREE_TIERS < 0 ? (KT > 50 ? 4 : KT > 40 ? 3 : 1) : 1;
+}
 template <int KT>
 constexpr int tree_wpe() {
     return KT <= 16 ? KN_TREE_WPE
@@ -512,7 +522,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(tree_wpe<KT
 #pragma unroll 4
         for (int j = 0; j < cnt; ++j) {
             const float4 c = buf[j];
-            nnet += topk_push(keys, cand_key(c, qx, qy, qz, ~kMask, sb + j, 0));
+            nnet += topk_push<KM, KN_TOPK_SPLIT, tree_tiers<KT>()>(keys, cand_key(c, qx, qy, qz, ~kMask, sb + j, 0));
         }
         ++nv;
         __builtin_amdgcn_wave_barrier();

@@ -1,6 +1,8 @@
 """In-process interleaved A/B of tree-path kernel variants on the native engine (900K clustered /
-surface, K=16): configs = extension suffixes built by cuda_knearests_amd._build.build_variant.
-Rows must equal the baseline's. usage: python scripts/ab_tree.py suffix[,suffix...] [rounds] [steps]"""
+surface, K=16; AB_K=k for another K): configs = extension suffixes built by
+cuda_knearests_amd._build.build_variant. Rows must equal the baseline's.
+usage: python scripts/ab_tree.py suffix[,suffix...] [rounds] [steps]"""
+import os
 import importlib
 import sys
 import time
@@ -18,7 +20,7 @@ for gen, fn in (("clustered", clustered_cloud), ("surface", surface_cloud)):
     engines, ref = [], None
     for suf in sufs:
         C = importlib.import_module("cuda_knearests_amd._C" + suf)
-        e = C.Engine(16)
+        e = C.Engine(int(os.environ.get("AB_K", "16")))
         e.prepare(pts)
         e.solve()
         i, d = e.results(dev)
