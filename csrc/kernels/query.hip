@@ -165,6 +165,18 @@ constexpr bool outer_pack_k() {
 #ifndef KN_RERANK_UNROLL
 #define KN_RERANK_UNROLL 1
 #endif
+// Staging of the tile + halo rows (knn_tile_kernel steps 1 and 3): 1 = per-row (cell bounds by
+// half-wave rows without integer division; points by one direct global -> LDS load per 64 points of
+// a row), 0 = round 5 (boundaries with a division per entry, points with a binary search each)
+#ifndef KN_STAGE_ROWS
+#define KN_STAGE_ROWS 1
+#endif
+#if defined(KN_CHECKED) && KN_CHECKED
+constexpr bool kChecked = true;
+#else
+constexpr bool kChecked = false;
+#endif
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // kWin = 1: compare each adjacent pair of kept keys once (see window_pass): 900K K=16 query
 // 0.2914 -> 0.2880 ms, K=32 0.5273 -> 0.5209, K=8 0.2026 -> 0.1992 (profiles/ab_r6_rerank.txt)
 #ifndef KN_RERANK_PAIR
@@ -375,6 +387,28 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
 
     // ---- 1. cell boundaries of every staged row ----------------------------------------
     auto row_cell = [&](int r) { return ((sz0 + r / nys) * a.Y + sy0 + r % nys) * a.X + sx0; };
+    if constexpr (KN_STAGE_ROWS) {
+        // one row per half-wave (cbs <= 32) or per wave: no integer division per boundary, the row's
+        // first boundary broadcast from its first lane instead of loaded again by every lane
+        const int seg = cbs <= 32 ? 32 : 64;
+        const int rpw = 64 / seg;  // rows per wave iteration
+        const int sl = lane & (seg - 1), sbase = lane & ~(seg - 1);
+        for (int r0 = wid * rpw; r0 < nrows; r0 += kWaves * rpw) {
+            const int r = r0 + (lane >> (seg == 32 ? 5 : 6));
+            const int c0 = r < nrows ? row_cell(r) : 0;
+            int v0 = 0;
+            for (int i0 = 0; i0 < cbs; i0 += seg) {
+                const int i = i0 + sl;
+                const int v = (r < nrows && i < cbs) ? a.cell_start[KN_IDX(c0 + i, a.X * a.Y * a.Z + 1, 201)] : 0;
+                if (i0 == 0) v0 = __shfl(v, sbase, 64);  // the row's first boundary (uniform loop)
+                if (r < nrows && i < cbs) {
+                    cbr[r * cbs + i] = (unsigned short)(v - v0);
+                    if (i == 0) rowst[r] = v;
+                    if (i == nxs) rowend[r] = v;
+                }
+            }
+        }
+    } else {
     for (int t = threadIdx.x; t < nrows * cbs; t += kWG) {
         const int r = t / cbs, i = t - r * cbs;
         const int c0 = row_cell(r);
@@ -383,6 +417,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
         cbr[r * cbs + i] = (unsigned short)(v - v0);
         if (i == 0) rowst[r] = v;
         if (i == nxs) rowend[r] = v;
+    }
     }
     __syncthreads();
     // ---- 2. row prefix (LDS offsets) and tile-row query prefix (wave 0) ----------------
@@ -433,11 +468,35 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
         if (threadIdx.x == 0) atomicAdd(a.counters + 2, 1u);
         return;
     }
-    // ---- 3. stage the points (16-B coalesced loads, row found by binary search) --------
+    // ---- 3. stage the points ------------------------------------------------------------
+    if constexpr (KN_STAGE_ROWS && !kChecked) {
+        // one row per wave iteration: its points are one contiguous run of the sorted array and
+        // land in one contiguous LDS range, so a wave copies 64 of them with ONE direct
+        // global -> LDS load (global_load_lds_dwordx4: per-lane source, LDS base in M0 + lane * 16;
+        // lanes past the row end are masked off). No per-point binary search, no VGPR round trip.
+        // The barrier below waits for the loads (vmcnt) before any wave reads the points.
+        for (int r = wid; r < nrows; r += kWaves) {
+            const int st = __builtin_amdgcn_readfirstlane(rowst[r]);
+            const int len = __builtin_amdgcn_readfirstlane(rowend[r]) - st;
+            const int dst = __builtin_amdgcn_readfirstlane(rowbase[r]);
+            for (int c = 0; c < len; c += 64) {
+                if (c + lane < len)
+                    __builtin_amdgcn_global_load_lds(a.sorted + st + c + lane, (lds_ptr_t)(pts + dst + c), 16, 0, 0);
+            }
+        }
+    } else if constexpr (KN_STAGE_ROWS) {
+        // checked builds: the same per-row copy through registers, every index bounds-checked
+        for (int r = wid; r < nrows; r += kWaves) {
+            const int st = rowst[r], len = rowend[r] - st, dst = rowbase[r];
+            for (int c = lane; c < len; c += 64) pts[KN_IDX(dst + c, a.cap, 203)] = a.sorted[KN_IDX(st + c, a.n, 202)];
+        }
+    } else {
+    // (round 5: 16-B coalesced loads, each point's row found by binary search over rowbase)
     for (int s = threadIdx.x; s < S; s += kWG) {
         int lo = 0, hi = nrows - 1;
         while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (rowbase[mid] <= s) lo = mid; else hi = mid - 1; }
         pts[KN_IDX(s, a.cap, 203)] = a.sorted[KN_IDX(rowst[lo] + (s - rowbase[lo]), a.n, 202)];
+    }
     }
     __syncthreads();
     (void)misc;

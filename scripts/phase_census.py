@@ -26,14 +26,14 @@ for k in ks:
     args = (s, cs, geom, plan.dims, k, n, None, [-inf, -inf, -inf, inf, inf, inf], plan.tile, plan.halo,
             plan.lds_capacity, True, True, 0)
     for _ in range(3):
-        B.query(*args)
+        B.query(*args, xsub=plan.xsub)
     torch.cuda.synchronize()
     B.debug_phase_cycles(True)
     reps = 10
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for _ in range(reps):
-        B.query(*args)
+        B.query(*args, xsub=plan.xsub)
     ev1.record()
     ev1.synchronize()
     v = B.debug_phase_cycles(True)
