@@ -48,6 +48,24 @@ __device__ __forceinline__ float complete_margin3(const CompleteBox& cb, float x
     return m;
 }
 
+// Output pointers in the global address space. The kernels pick their output pointers at run time
+// (the launch's, or a device slot's for batched graphs), which leaves them generic to the compiler:
+// it then emits FLAT stores, which count on the LDS counter as well, so every later LDS wait (the
+// re-rank's point reads) also waits for the stores in flight. A global pointer gives global_store.
+// KN_GLOBAL_OUT=0: the generic pointers (round 5).
+#ifndef KN_GLOBAL_OUT
+#define KN_GLOBAL_OUT 1
+#endif
+#if KN_GLOBAL_OUT
+typedef __attribute__((address_space(1))) unsigned out_u32_t;
+typedef __attribute__((address_space(1))) float out_f32_t;
+#else
+typedef unsigned out_u32_t;
+typedef float out_f32_t;
+#endif
+__device__ __forceinline__ out_u32_t* out_ptr(unsigned* p) { return (out_u32_t*)p; }
+__device__ __forceinline__ out_f32_t* out_ptr(float* p) { return (out_f32_t*)p; }
+
 __device__ __forceinline__ bool pair_less(float da, unsigned ia, float db, unsigned ib) {
     return da < db || (da == db && ia < ib);
 }

@@ -329,8 +329,8 @@ template <int KT, int M, bool LANE, bool WIDE = false>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT>(), 8))) void knn_tile_kernel(TileArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
     // stream of clouds); locals, so the kernel argument block stays read-only
-    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
-    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
+    out_u32_t* const o_idx = out_ptr(a.out_idx_ref ? *a.out_idx_ref : a.out_idx);
+    out_f32_t* const o_dist = out_ptr(a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist);
     // K + M margin slots + 1: the query itself is not filtered in the hot loop (that cost 3
     // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
     constexpr int KM = KT + M + 1;
@@ -1227,8 +1227,8 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(KN_STREAM_W
     TileArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
     // stream of clouds); locals, so the kernel argument block stays read-only
-    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
-    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
+    out_u32_t* const o_idx = out_ptr(a.out_idx_ref ? *a.out_idx_ref : a.out_idx);
+    out_f32_t* const o_dist = out_ptr(a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist);
     constexpr int KM = KT + M + 1;
     constexpr unsigned MASK = (1u << kStreamSlotBits) - 1u;
     constexpr unsigned HIMASK = ~MASK;
@@ -1603,8 +1603,8 @@ constexpr int kXCap = 256;
 __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
     // stream of clouds); locals, so the kernel argument block stays read-only
-    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
-    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
+    out_u32_t* const o_idx = out_ptr(a.out_idx_ref ? *a.out_idx_ref : a.out_idx);
+    out_f32_t* const o_dist = out_ptr(a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist);
     __shared__ unsigned long long s_buf[4][kXCap];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     unsigned long long* buf = s_buf[wid];

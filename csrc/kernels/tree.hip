@@ -483,8 +483,8 @@ template <int KT, int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(tree_wpe<KT>(), 8))) void knn_tree_kernel(TArgs a) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
     // stream of clouds); locals, so the kernel argument block stays read-only
-    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
-    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
+    out_u32_t* const o_idx = out_ptr(a.out_idx_ref ? *a.out_idx_ref : a.out_idx);
+    out_f32_t* const o_dist = out_ptr(a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist);
     constexpr int KM = KT + M + 1;  // + 1: the query itself enters its own list at d2 = 0
     __shared__ float4 s_pts[4][kTreeLeaf];
     __shared__ int s_visit[4][kMaxVisit];  // first point of each visited leaf
@@ -742,8 +742,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(tree_wpe<KT
 __global__ __launch_bounds__(256) void knn_tree_exact_kernel(TArgs a, int all) {
     // output pointers: the launch's, or read from device slots (graph replays of a batched
     // stream of clouds); locals, so the kernel argument block stays read-only
-    unsigned* const o_idx = a.out_idx_ref ? *a.out_idx_ref : a.out_idx;
-    float* const o_dist = a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist;
+    out_u32_t* const o_idx = out_ptr(a.out_idx_ref ? *a.out_idx_ref : a.out_idx);
+    out_f32_t* const o_dist = out_ptr(a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist);
     __shared__ unsigned long long s_buf[4][kTCap];
     __shared__ int s_stack[4][kStack];
     __shared__ float s_sbd[4][kStack];  // box distance of each stacked node (computed by its parent)
