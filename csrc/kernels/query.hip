@@ -177,6 +177,11 @@ constexpr bool kChecked = true;
 constexpr bool kChecked = false;
 #endif
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+// Checked builds, diagnostics: counters [4] / [5] count the lane walk's wave-uniform row
+// iterations and lockstep candidate steps (0: per-lane rows / candidates summed over live lanes)
+#ifndef KN_WALK_STATS
+#define KN_WALK_STATS 0
+#endif
 // kWin = 1: compare each adjacent pair of kept keys once (see window_pass): 900K K=16 query
 // 0.2914 -> 0.2880 ms, K=32 0.5273 -> 0.5209, K=8 0.2026 -> 0.1992 (profiles/ab_r6_rerank.txt)
 #ifndef KN_RERANK_PAIR
@@ -846,7 +851,15 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     // (vs 2: K=8 -3.8 %, 16 -1.5 %, 24 -3.6 %, 32 -1 to -3 %, 40 -3.1 %), 1 for
                     // the K=50 bucket (-2.4 %), 2 for K=64 (1 and 3 lose or tie)
                     constexpr int kUnroll = KT <= 40 ? 3 : (KT <= 50 ? 1 : KN_LANE_UNROLL);
-                    if constexpr (kStats) {
+                    if constexpr (kStats && KN_WALK_STATS) {
+                        // wave-uniform: row iterations and lockstep candidate steps (the unrolled
+                        // loop runs to the longest span, then the remainder loop)
+                        const unsigned L = (unsigned)max(0, s1 - s0);
+                        const unsigned steps = (unsigned)kUnroll * wave_max_u32(L / (unsigned)kUnroll) +
+                                               wave_max_u32(L % (unsigned)kUnroll);
+                        st_rows += steps > 0u ? 1u : 0u;
+                        st_cand += steps;
+                    } else if constexpr (kStats) {
                         st_rows += (s1 > s0) ? 1u : 0u;
                         st_cand += (unsigned)max(0, s1 - s0);
                     }
@@ -907,7 +920,14 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                 }
                 }
             });
-        if (kStats && LANE) {  // lane walk: per-lane rows / candidates, summed over live lanes
+        if (kStats && LANE && KN_WALK_STATS) {  // wave-uniform row iterations / steps / networks
+            if (lane == 0) {
+                atomicAdd(a.counters + 4, st_rows);
+                atomicAdd(a.counters + 5, st_cand);
+                atomicAdd(a.counters + 6, st_ins);
+                atomicAdd(a.counters + 7, 1u);
+            }
+        } else if (kStats && LANE) {  // lane walk: per-lane rows / candidates, summed over live lanes
             if (live && in_range) {
                 atomicAdd(a.counters + 4, st_rows);
                 atomicAdd(a.counters + 5, st_cand);

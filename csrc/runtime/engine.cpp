@@ -812,6 +812,13 @@ kn_status Engine::ensure_pipeline() {
             x = [this](int s, hipStream_t st2) { return stage_exact(s, st2) == KN_OK ? hipSuccess : hipErrorUnknown; };
         if ((st = check(pipe_.init(stream_, bstream_, b, q, x, false, qstreams, nsets_), "pipeline init")) != KN_OK)
             return st;
+        // KN_PIPE_EAGER=1 (diagnostics): the resident pipeline's stages enqueued per step instead of
+        // replayed from their graphs (the 20-step cold start, profiles/r6_coldstart.txt)
+        static const bool eager_env = [] {
+            const char* v = std::getenv("KN_PIPE_EAGER");
+            return v && v[0] == '1';
+        }();
+        if (eager_env) pipe_.set_eager(true);
     }
     return KN_OK;
 }

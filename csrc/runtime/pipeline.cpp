@@ -125,6 +125,13 @@ hipError_t Pipeline::capture(const Stage& st, int set, hipGraphExec_t* out) {
     KN_TRY(e2);
     const hipError_t e3 = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
+    // KN_PIPE_GRAPH_UPLOAD=1 (diagnostics): upload the executable graph to the device now instead
+    // of at its first launches (the 20-step cold start, profiles/r6_coldstart.txt)
+    static const bool upload = [] {
+        const char* v = std::getenv("KN_PIPE_GRAPH_UPLOAD");
+        return v && v[0] == '1';
+    }();
+    if (e3 == hipSuccess && upload) KN_TRY(hipGraphUpload(*out, main_));
     return e3;
 }
 
