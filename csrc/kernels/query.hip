@@ -177,6 +177,13 @@ constexpr bool kChecked = true;
 constexpr bool kChecked = false;
 #endif
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+// Lane walk: 1 = the query itself in its own top-K list (default), 0 = its own row scanned as two
+// spans around it, no self slot (see knn_tile_kernel's KM). Measured: no gain -- the extra span
+// pass costs what the med3 slot and the re-rank entry save (900K, in-process A/B, identical rows:
+// K=16 0.2762 vs 0.2784 ms, K=50 0.845 vs 0.848, K=64 0.885 vs 0.888; profiles/ab_r6_self_slot.txt)
+#ifndef KN_SELF_SLOT
+#define KN_SELF_SLOT 1
+#endif
 // Checked builds, diagnostics: counters [4] / [5] count the lane walk's wave-uniform row
 // iterations and lockstep candidate steps (0: per-lane rows / candidates summed over live lanes)
 #ifndef KN_WALK_STATS
@@ -336,9 +343,12 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
     // stream of clouds); locals, so the kernel argument block stays read-only
     out_u32_t* const o_idx = out_ptr(a.out_idx_ref ? *a.out_idx_ref : a.out_idx);
     out_f32_t* const o_dist = out_ptr(a.out_idx_ref ? (a.out_dist_ref ? *a.out_dist_ref : nullptr) : a.out_dist);
-    // K + M margin slots + 1: the query itself is not filtered in the hot loop (that cost 3
-    // VALU per candidate); it enters its own list at d2 = 0 and is dropped at the re-rank.
-    constexpr int KM = KT + M + 1;
+    // K + M margin slots (+ 1 for the query itself on the union stream, where it enters its own
+    // list at d2 = 0 and is dropped at the re-rank). The lane walk scans the query's own row as two
+    // spans around the query's slot instead (KN_SELF_SLOT=0), so its list has no self slot: one
+    // med3 less per network and one re-rank entry less, for one extra span per walk.
+    constexpr bool kSelfSlot = !LANE || KN_SELF_SLOT;
+    constexpr int KM = KT + M + (kSelfSlot ? 1 : 0);
     constexpr bool kFull = LANE && (KN_LANE_FULL == 2 || (KN_LANE_FULL == 1 && KT > 40));
     // (KN_OUTER_PACK=3: the whole-block walk packs its outer rows instead of the sorted table)
     constexpr bool kRowOrder = LANE && (KN_ROW_ORDER == 1 || (KN_ROW_ORDER == 2 && kFull && !outer_pack_k<KT>()));
@@ -586,7 +596,21 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                 return lane_span_r(r, r * cbs, x0, x1);
             };
             const int qr0 = cy + nys * cz, qr0cb = qr0 * cbs;  // the lane's own row
-            auto body = [&](int2 sp) { body2(sp.x, sp.y); };
+            // own (uniform): the query's own row (offset (0, 0)). Without a self slot it is scanned as
+            // the two spans around the query's own slot (either may be empty), through the SAME call
+            // site in a uniform loop of two passes: a second inlined copy of the scan loop raised the
+            // register allocation of the large-K buckets (K=50 119 -> 177 VGPRs, K=64 spills)
+            auto body = [&](int2 sp, bool own = false) {
+                int e = sp.y;
+                if (!kSelfSlot && own) e = min(sp.y, qslot);
+                const int passes = (!kSelfSlot && own) ? 2 : 1;
+#pragma unroll 1
+                for (int pass = 0; pass < passes; ++pass) {
+                    body2(sp.x, e);
+                    sp.x = max(sp.x, qslot + 1);
+                    e = sp.y;
+                }
+            };
             if constexpr (kRowOrder) {
             const int nent = side * side;
             // mirror the table so that offset +1 is the near neighbour row of the query's cell
@@ -620,7 +644,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     }
                 }
                 if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
-                body(lane_span(y, z, lx0, lx1));
+                body(lane_span(y, z, lx0, lx1), oy == 0 && oz == 0);
             }
             } else {
             const bool pack = outer_pack_k<KT>() && a.n_outer > 0;
@@ -650,7 +674,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     }
                     if (!__builtin_amdgcn_ballot_w64(lx0 <= lx1)) continue;
                     const int ro = oy + nys * oz;  // uniform
-                    body(lane_span_r(qr0 + ro, qr0cb + ro * cbs, lx0, lx1));
+                    body(lane_span_r(qr0 + ro, qr0cb + ro * cbs, lx0, lx1), ro == 0);
                 }
             }
             if (outer_pack_k<KT>() && pack) {
@@ -957,7 +981,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
         // runs later on the same stream. Runs longer than kWin + 1 (lattices, heavy
         // duplication) take the wave-cooperative sort below.
         const unsigned qs = (unsigned)qslot;
-        auto kvalid = [&](unsigned key) { return key != SENT && (key & MASK) != qs; };
+        auto kvalid = [&](unsigned key) { return key != SENT && (!kSelfSlot || (key & MASK) != qs); };
         const bool force = (a.flags & kQueryForceRescan) != 0;
         bool ovf = force;
         // wider-window overflow (== ovf when the second window is off)
