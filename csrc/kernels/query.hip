@@ -184,6 +184,20 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #ifndef KN_SELF_SLOT
 #define KN_SELF_SLOT 1
 #endif
+// x halo of the tile path in x sub-cells (xsub > 1): 0 = halo * xsub (whole cells, the y / z halo
+// width), T > 0 = min(T, halo * xsub). The lane walk's own box is the query's sub-cell +- this many
+// sub-cells in x, and certification measures against that box, so a narrower x halo stays exact.
+// Measured with its own plan (scripts/ab_plan.py, profiles/ab_r6_xhalo.txt): T = 3 (1.5 cells)
+// shrinks the K <= 16 plan to 32.5 KB (5 workgroups per CU) but sends 72 / 27 queries of 900K /
+// 300K to the exact path at K=16: 900K K=16 0.280 -> 0.306 ms, 300K 0.145 -> 0.177; only K=8 and 3M
+// gain (-1 %, -5..-7 %). Off.
+#ifndef KN_XHALO_SUB
+#define KN_XHALO_SUB 0
+#endif
+inline int x_halo(int halo, int xsub) {
+    const int full = halo * std::max(1, xsub);
+    return (KN_XHALO_SUB > 0 && xsub > 1) ? std::min(KN_XHALO_SUB, full) : full;
+}
 // Checked builds, diagnostics: counters [4] / [5] count the lane walk's wave-uniform row
 // iterations and lockstep candidate steps (0: per-lane rows / candidates summed over live lanes)
 #ifndef KN_WALK_STATS
@@ -1957,7 +1971,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
         a.out_idx_ref = q.out_idx_ref; a.out_dist_ref = q.out_dist_ref;
         a.fallback_list = q.fallback_list; a.counters = q.counters;
         a.TX = q.tile[0]; a.TY = q.tile[1]; a.TZ = q.tile[2]; a.H = q.halo;
-        a.Hx = q.halo * std::max(1, q.xsub);
+        a.Hx = x_halo(q.halo, q.xsub);
         a.cap = q.lds_capacity;
         a.flags = q.flags;
         {
@@ -2063,7 +2077,7 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
 
 size_t query_lds_bytes(const int tile[3], int halo, int lds_capacity, int xsub) {
     const int rows = (tile[1] + 2 * halo) * (tile[2] + 2 * halo);
-    const int cbs = tile[0] + 2 * halo * std::max(1, xsub) + 1;
+    const int cbs = tile[0] + 2 * x_halo(halo, xsub) + 1;
     size_t b = (size_t)lds_capacity * 16;
     b += ((size_t)rows * cbs * 2 + 3) & ~(size_t)3;  // u16 row-relative cell boundaries
     b += (size_t)(rows + 1) * 4;                      // rowbase
@@ -2225,8 +2239,8 @@ int default_xsub(int k) {
 }
 
 double staged_points(const AutoParams& p, double ppc_cell) {
-    const int xs = std::max(1, p.xsub);
-    return (double)(p.tile[0] + 2 * p.halo * xs) * (p.tile[1] + 2 * p.halo) * (p.tile[2] + 2 * p.halo) * ppc_cell;
+    return (double)(p.tile[0] + 2 * x_halo(p.halo, p.xsub)) * (p.tile[1] + 2 * p.halo) * (p.tile[2] + 2 * p.halo) *
+           ppc_cell;
 }
 
 AutoParams auto_params(int n, int k, float ppc, const int* tile_hint, int halo_hint,
