@@ -93,6 +93,11 @@ struct TileArgs {
 };
 constexpr int kRowOrderMax = 128;
 
+// gathers in flight per lane in the K=50 bucket's walk (1 measured best in round 2; re-checked with
+// the gated-tier networks of round 6, profiles/ab_r6_k50.txt)
+#ifndef KN_LANE_UNROLL50
+#define KN_LANE_UNROLL50 1
+#endif
 #ifndef KN_LANE_UNROLL
 #define KN_LANE_UNROLL 2
 #endif
@@ -888,7 +893,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     // interleaved A/Bs at 900K (profiles/ab_r2_lane_unroll.txt): 3 for K <= 40
                     // (vs 2: K=8 -3.8 %, 16 -1.5 %, 24 -3.6 %, 32 -1 to -3 %, 40 -3.1 %), 1 for
                     // the K=50 bucket (-2.4 %), 2 for K=64 (1 and 3 lose or tie)
-                    constexpr int kUnroll = KT <= 40 ? 3 : (KT <= 50 ? 1 : KN_LANE_UNROLL);
+                    constexpr int kUnroll = KT <= 40 ? 3 : (KT <= 50 ? KN_LANE_UNROLL50 : KN_LANE_UNROLL);
                     if constexpr (kStats && KN_WALK_STATS) {
                         // wave-uniform: row iterations and lockstep candidate steps (the unrolled
                         // loop runs to the longest span, then the remainder loop)
