@@ -93,10 +93,11 @@ struct TileArgs {
 };
 constexpr int kRowOrderMax = 128;
 
-// gathers in flight per lane in the K=50 bucket's walk (1 measured best in round 2; re-checked with
-// the gated-tier networks of round 6, profiles/ab_r6_k50.txt)
+// gathers in flight per lane in the K=50 bucket's walk: 1 measured best in round 2; with the round-6
+// gated-tier networks and grouped re-rank, 2 (together with KN_RERANK_GROUP=8): K=50 query 0.854 ->
+// 0.810 ms, pipelined 100 / 30 0.559 -> 0.546, 20 / 5 0.626 -> 0.612 (profiles/ab_r6_k50.txt)
 #ifndef KN_LANE_UNROLL50
-#define KN_LANE_UNROLL50 1
+#define KN_LANE_UNROLL50 2
 #endif
 #ifndef KN_LANE_UNROLL
 #define KN_LANE_UNROLL 2
@@ -235,9 +236,11 @@ __device__ __forceinline__ void static_for(F& f) {
         static_for<I + 1, N>(f);
     }
 }
-// entries per shift of the rolled re-rank walk (KM > 24; see window_pass)
+// entries per shift of the rolled re-rank walk (KM > 24; see window_pass): 4 against 1 measured
+// K=50 -2 %, K=64 -3.6 % (profiles/ab_r6_rerank_group.txt); 8 a further -1 % at K=50, equal at K=32
+// and K=64 (profiles/ab_r6_k50.txt)
 #ifndef KN_RERANK_GROUP
-#define KN_RERANK_GROUP 4
+#define KN_RERANK_GROUP 8
 #endif
 // Round-3 A/Bs of the lane walk that LOST against this kernel (900K uniform, interleaved in
 // process, identical rows; profiles/ab_r3_lane_variants.jsonl, profiles/ab_r3_collect.jsonl):
