@@ -96,6 +96,10 @@ constexpr int kRowOrderMax = 128;
 // gathers in flight per lane in the K=50 bucket's walk: 1 measured best in round 2; with the round-6
 // gated-tier networks and grouped re-rank, 2 (together with KN_RERANK_GROUP=8): K=50 query 0.854 ->
 // 0.810 ms, pipelined 100 / 30 0.559 -> 0.546, 20 / 5 0.626 -> 0.612 (profiles/ab_r6_k50.txt)
+// ... and in the K <= 40 buckets (3 since round 2, profiles/ab_r2_lane_unroll.txt)
+#ifndef KN_LANE_UNROLL40
+#define KN_LANE_UNROLL40 3
+#endif
 #ifndef KN_LANE_UNROLL50
 #define KN_LANE_UNROLL50 2
 #endif
@@ -896,7 +900,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     // interleaved A/Bs at 900K (profiles/ab_r2_lane_unroll.txt): 3 for K <= 40
                     // (vs 2: K=8 -3.8 %, 16 -1.5 %, 24 -3.6 %, 32 -1 to -3 %, 40 -3.1 %), 1 for
                     // the K=50 bucket (-2.4 %), 2 for K=64 (1 and 3 lose or tie)
-                    constexpr int kUnroll = KT <= 40 ? 3 : (KT <= 50 ? KN_LANE_UNROLL50 : KN_LANE_UNROLL);
+                    constexpr int kUnroll = KT <= 40 ? KN_LANE_UNROLL40 : (KT <= 50 ? KN_LANE_UNROLL50 : KN_LANE_UNROLL);
                     if constexpr (kStats && KN_WALK_STATS) {
                         // wave-uniform: row iterations and lockstep candidate steps (the unrolled
                         // loop runs to the longest span, then the remainder loop)
