@@ -92,7 +92,9 @@ int bbox_block_count(int n);
 // partials[a * kBBoxBlocks + b]: a < 3: max of ~ord(min_a), a >= 3: max of ord(max_a) over
 // block b's points (ord = order-preserving float -> uint). Blocks past bbox_block_count(n)
 // are not written.
-hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hipStream_t s);
+// zero_ints / n_zero: ints block 0 zeroes on the way (the bucketed build's bucket totals)
+hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hipStream_t s, int* zero_ints = nullptr,
+                                int n_zero = 0);
 
 // Query counters (device, zeroed by every launch_query):
 //  [0] queries sent to the exact kernel   [1] uncertified (multi-GPU: K-th leaves complete box)

@@ -53,7 +53,10 @@ __device__ __forceinline__ float unord_float(unsigned u) {
 // per iteration (x0 y0 z0 x1 | y1 z1 x2 y2 | z2 x3 y3 z3); needs a 16-B aligned base.
 template <bool VEC>
 __global__ __launch_bounds__(KN_BBOX_THREADS) void bbox_partials_kernel(const float* __restrict__ pts, int n,
-                                                            unsigned* __restrict__ partials) {
+                                                            unsigned* __restrict__ partials,
+                                                            int* __restrict__ zero_ints, int n_zero) {
+    if (blockIdx.x == 0)
+        for (int j = threadIdx.x; j < n_zero; j += blockDim.x) zero_ints[j] = 0;
     float mn[3] = {INFINITY, INFINITY, INFINITY};
     float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
     auto acc = [&](int a, float v) { mn[a] = fminf(mn[a], v); mx[a] = fmaxf(mx[a], v); };
@@ -343,13 +346,15 @@ int bbox_block_count(int n) {
                                 kBBoxBlocks));
 }
 
-hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hipStream_t s) {
+hipError_t launch_bbox_partials(const float* pts, int n, unsigned* partials, hipStream_t s, int* zero_ints,
+                                int n_zero) {
     if (n <= 0) return hipSuccess;
     const int grid = bbox_block_count(n);
+    if (!zero_ints) n_zero = 0;
     if ((reinterpret_cast<uintptr_t>(pts) & 15u) == 0)
-        bbox_partials_kernel<true><<<grid, KN_BBOX_THREADS, 0, s>>>(pts, n, partials);
+        bbox_partials_kernel<true><<<grid, KN_BBOX_THREADS, 0, s>>>(pts, n, partials, zero_ints, n_zero);
     else
-        bbox_partials_kernel<false><<<grid, KN_BBOX_THREADS, 0, s>>>(pts, n, partials);
+        bbox_partials_kernel<false><<<grid, KN_BBOX_THREADS, 0, s>>>(pts, n, partials, zero_ints, n_zero);
     return hipGetLastError();
 }
 
@@ -380,15 +385,56 @@ __device__ __forceinline__ void load_pts4(const float* __restrict__ pts, int i, 
     }
 }
 
-// A1: per-(bucket, block) counts with LDS atomics, table column = bucket (bucket-major, so the
-// exclusive scan of the table gives every block its write offset inside every bucket).
+// Bucket offsets without a table scan (KN_BIN_ATOMIC, default): every streaming block claims its
+// sub-range of every bucket with ONE device-scope atomicAdd on the bucket's total (the returned old
+// total is the block's offset inside the bucket, in arrival order); the scatter blocks scan the
+// <= 4096 bucket totals themselves, so the build has no scan kernel between count and scatter.
+// The totals are zeroed by the bbox kernel (or a memset with a fixed box) earlier in the same
+// build. Bucket segments hold their blocks' points in arrival order; the bucket sort places them
+// with LDS atomics anyway (the in-cell order is only fixed by the deterministic cell sort).
+// KN_BIN_ATOMIC=0: the bucket-major table + scan_blocks_kernel of rounds 2-5.
+// KN_BIN_PREFETCH: points per thread the count / scatter blocks load before their set-up
+// (geometry, bucket offsets), so the load latency overlaps it.
+#ifndef KN_BIN_ATOMIC
+#define KN_BIN_ATOMIC 1
+#endif
+#ifndef KN_BIN_PREFETCH
+#define KN_BIN_PREFETCH 4
+#endif
+
+template <int R>
+struct PrefetchPts {
+    float p[R > 0 ? R : 1][3];
+    __device__ __forceinline__ void load(const float* __restrict__ pts, int i0, int i1) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t j = 3 * (size_t)min(i0 + (int)threadIdx.x + r * (int)blockDim.x, i1 - 1);
+            p[r][0] = pts[j]; p[r][1] = pts[j + 1]; p[r][2] = pts[j + 2];
+        }
+    }
+    // first index the plain loop continues at
+    __device__ __forceinline__ static int rest(int i0) { return i0 + (int)threadIdx.x + R * (int)blockDim.x; }
+    __device__ __forceinline__ static bool valid(int i0, int i1, int r) {
+        return i0 + (int)threadIdx.x + r * (int)blockDim.x < i1;
+    }
+};
+
+// A1: per-(bucket, block) counts with LDS atomics. KN_BIN_ATOMIC: block-major offsets
+// table[block][bucket] from the totals' atomics; else the bucket-major count table (its exclusive
+// scan gives every block its write offset inside every bucket).
 __global__ __launch_bounds__(1024) void bucket_count_kernel(const float* __restrict__ pts, int n, GeomSrc src,
                                                            GridGeom* __restrict__ gout, int shift,
                                                            int nbuckets, int nblocks, int per_block,
-                                                           int* __restrict__ table, unsigned* __restrict__ zero_words,
-                                                           int n_zero_words) {
+                                                           int* __restrict__ table, int* __restrict__ totals,
+                                                           unsigned* __restrict__ zero_words, int n_zero_words) {
     extern __shared__ int hist[];
     __shared__ GridGeom gs;
+    const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
+#if !KN_BUILD_BATCH
+    constexpr int R = KN_BIN_PREFETCH;
+    PrefetchPts<R> pf;
+    pf.load(pts, i0, i1);
+#endif
     // the step's query counters, zeroed here instead of by a separate memset node
     if (blockIdx.x == 0 && (int)threadIdx.x < n_zero_words) zero_words[threadIdx.x] = 0u;
     for (int j = threadIdx.x; j < nbuckets; j += blockDim.x) hist[j] = 0;
@@ -403,7 +449,6 @@ __global__ __launch_bounds__(1024) void bucket_count_kernel(const float* __restr
     }
     __syncthreads();
     const GridGeom g = gs;
-    const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
 #if KN_BUILD_BATCH
     const bool vec = (reinterpret_cast<uintptr_t>(pts) & 15u) == 0;
     for (int i = i0 + 4 * threadIdx.x; i < i1; i += 4 * blockDim.x) {
@@ -414,23 +459,80 @@ __global__ __launch_bounds__(1024) void bucket_count_kernel(const float* __restr
             if (i + u < i1) atomicAdd(&hist[cell_of(g, q.p[u]) >> shift], 1);
     }
 #else
-    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (pf.valid(i0, i1, r)) atomicAdd(&hist[cell_of(g, pf.p[r]) >> shift], 1);
+    for (int i = pf.rest(i0); i < i1; i += blockDim.x) {
         const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
         atomicAdd(&hist[cell_of(g, p) >> shift], 1);
     }
 #endif
     __syncthreads();
+#if KN_BIN_ATOMIC
+    int* row = table + (size_t)blockIdx.x * nbuckets;
+    for (int j = threadIdx.x; j < nbuckets; j += blockDim.x) {
+        const int h = hist[j];
+        row[j] = h ? atomicAdd(&totals[j], h) : 0;
+    }
+#else
+    (void)totals;
     for (int j = threadIdx.x; j < nbuckets; j += blockDim.x) table[(size_t)j * nblocks + blockIdx.x] = hist[j];
+#endif
 }
 
-// A3: every point to its bucket's segment of bin_tmp as {x, y, z, bits(original index)}
+// A3: every point to its bucket's segment of bin_tmp as {x, y, z, bits(original index)}.
+// KN_BIN_ATOMIC: the block scans the bucket totals (-> bucket starts; block 0 publishes them in
+// bstart[0..nbuckets], bstart[nbuckets] = n, for the bucket sort) and adds its own offsets.
 __global__ __launch_bounds__(1024) void bucket_scatter_kernel(const float* __restrict__ pts, int n,
                                                              const GridGeom* __restrict__ gp, int shift,
                                                              int nbuckets, int nblocks, int per_block,
                                                              const int* __restrict__ tscan,
                                                              const int* __restrict__ tsums, int nbt,
+                                                             const int* __restrict__ totals,
+                                                             int* __restrict__ bstart,
                                                              float4* __restrict__ tmp) {
     extern __shared__ int cur[];
+    const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
+#if !KN_BUILD_BATCH
+    constexpr int R = KN_BIN_PREFETCH;
+    PrefetchPts<R> pf;
+    pf.load(pts, i0, i1);
+#endif
+#if KN_BIN_ATOMIC
+    (void)tscan; (void)tsums; (void)nbt; (void)nblocks;
+    {
+        // thread t owns buckets [t * per, t * per + per), per <= 16 (nbuckets <= 4096, >= 256 threads)
+        __shared__ int wsum[16];
+        const int per = (nbuckets + (int)blockDim.x - 1) / (int)blockDim.x;
+        const int j0 = threadIdx.x * per;
+        const int* mine = tscan + (size_t)blockIdx.x * nbuckets;  // this block's offsets (count kernel)
+        int tv[16], ov[16];
+        int s = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const bool v = q < per && j0 + q < nbuckets;
+            tv[q] = v ? totals[j0 + q] : 0;
+            ov[q] = v ? mine[j0 + q] : 0;
+            s += tv[q];
+        }
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        const int incl = wave_inclusive_scan_add(s);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        int run = incl - s;
+        for (int w = 0; w < wid; ++w) run += wsum[w];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            if (q < per && j0 + q < nbuckets) {
+                cur[j0 + q] = run + ov[q];
+                if (blockIdx.x == 0) bstart[j0 + q] = run;
+                run += tv[q];
+            }
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) bstart[nbuckets] = n;
+    }
+#else
+    (void)totals; (void)bstart;
     __shared__ int pre[1024];  // exclusive prefix of the scan blocks' totals (nbt <= 1024)
     if (threadIdx.x < 64) {
         const int per = (nbt + 63) >> 6, j0 = threadIdx.x * per;
@@ -445,9 +547,9 @@ __global__ __launch_bounds__(1024) void bucket_scatter_kernel(const float* __res
         const size_t t = (size_t)j * nblocks + blockIdx.x;
         cur[j] = tscan[t] + pre[t / kScanItems];
     }
+#endif
     __syncthreads();
     const GridGeom g = *gp;
-    const int i0 = blockIdx.x * per_block, i1 = min(n, i0 + per_block);
 #if KN_BUILD_BATCH
     const bool vec = (reinterpret_cast<uintptr_t>(pts) & 15u) == 0;
     for (int i = i0 + 4 * threadIdx.x; i < i1; i += 4 * blockDim.x) {
@@ -464,7 +566,16 @@ __global__ __launch_bounds__(1024) void bucket_scatter_kernel(const float* __res
                     make_float4(q.p[u][0], q.p[u][1], q.p[u][2], __uint_as_float((unsigned)(i + u)));
     }
 #else
-    for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    int pos[R > 0 ? R : 1];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        pos[r] = pf.valid(i0, i1, r) ? atomicAdd(&cur[cell_of(g, pf.p[r]) >> shift], 1) : -1;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (pos[r] >= 0)
+            tmp[KN_IDX(pos[r], n, 104)] = make_float4(pf.p[r][0], pf.p[r][1], pf.p[r][2],
+                                                      __uint_as_float((unsigned)(i0 + (int)threadIdx.x + r * (int)blockDim.x)));
+    for (int i = pf.rest(i0); i < i1; i += blockDim.x) {
         const float p[3] = {pts[3 * (size_t)i], pts[3 * (size_t)i + 1], pts[3 * (size_t)i + 2]};
         const int pos = atomicAdd(&cur[cell_of(g, p) >> shift], 1);
         tmp[KN_IDX(pos, n, 104)] = make_float4(p[0], p[1], p[2], __uint_as_float((unsigned)i));
@@ -478,7 +589,8 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
                                                           const GridGeom* __restrict__ gp, int shift,
                                                           int nbuckets, int nblocks,
                                                           const int* __restrict__ tscan,
-                                                          const int* __restrict__ tsums, int num_cells,
+                                                          const int* __restrict__ tsums,
+                                                          const int* __restrict__ bstart, int num_cells,
                                                           int* __restrict__ cell_start,
                                                           float4* __restrict__ sorted,
                                                           unsigned* __restrict__ perm,
@@ -490,6 +602,14 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
     const int cells = 1 << shift;
     const int c0 = b << shift;
     for (int j = threadIdx.x; j < cells; j += 256) cur[j] = 0;
+#if KN_BIN_ATOMIC
+    (void)tscan; (void)tsums;
+    if (threadIdx.x == 0) {  // bucket segment [bs, be): the starts the scatter's block 0 published
+        seg[0] = bstart[b];
+        seg[1] = bstart[b + 1];
+    }
+#else
+    (void)bstart;
     if (threadIdx.x < 64) {  // bucket segment [bs, be): scanned table + prefix of raw block totals
         const size_t t0 = (size_t)b * nblocks, t1 = (size_t)(b + 1) * nblocks;
         const int i0 = (int)(t0 / kScanItems);
@@ -507,6 +627,7 @@ __global__ __launch_bounds__(256) void bucket_sort_kernel(const float4* __restri
             seg[1] = (b + 1 < nbuckets) ? tscan[t1] + s1 : n;
         }
     }
+#endif
     __syncthreads();
     const int bs = seg[0], be = seg[1];
     const GridGeom g = *gp;
@@ -736,6 +857,7 @@ bool bin_plan(int n, int num_cells, BinPlan* out, int items_req) {
         const long long nbuckets = ((long long)num_cells + (1ll << shift) - 1) >> shift;
         if (nbuckets > 4096) continue;
         if (nbuckets * nblocks > (long long)num_cells + 1) continue;
+        if (2 * nbuckets + 2 > (long long)num_cells + 1) continue;  // bucket totals + starts (KN_BIN_ATOMIC)
         *out = BinPlan{shift, (int)nbuckets, (int)cdiv((size_t)n, per_block), per_block};
         return true;
     }
@@ -784,10 +906,17 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         GeomSrc src{};
         src.use_box = b.use_box;
         for (int a = 0; a < 3; ++a) { src.lo[a] = b.box_lo[a]; src.hi[a] = b.box_hi[a]; src.dims[a] = b.dims[a]; }
+        // KN_BIN_ATOMIC: bucket totals + published bucket starts in the (otherwise unused)
+        // cell_scan buffer (bin_plan keeps 2 nbuckets + 2 <= C + 1), zeroed before the count
+        int* totals = b.cell_scan;
+        int* bstart = b.cell_scan + bp.nbuckets + 1;
+        const int n_tot = KN_BIN_ATOMIC ? bp.nbuckets : 0;
         if (!b.use_box) {
-            if ((e = launch_bbox_partials(b.points, n, b.bbox_words, s)) != hipSuccess) return e;
+            if ((e = launch_bbox_partials(b.points, n, b.bbox_words, s, totals, n_tot)) != hipSuccess) return e;
             src.partials = b.bbox_words;
             src.nbb = bbox_block_count(n);
+        } else if (n_tot && (e = hipMemsetAsync(totals, 0, (size_t)n_tot * sizeof(int), s)) != hipSuccess) {
+            return e;
         }
         const size_t T = (size_t)bp.nbuckets * bp.nblocks;
         // global ids fused into the sort unless the in-cell order pass follows (it orders by w)
@@ -807,16 +936,17 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
         }();
         const int bin_threads = bin_env ? bin_env : (n <= (4 << 20) && !b.serial ? 256 : 1024);
         bucket_count_kernel<<<bp.nblocks, bin_threads, bp.nbuckets * sizeof(int), s>>>(
-            b.points, n, src, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count, b.zero_words,
-            b.n_zero_words);
+            b.points, n, src, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_count, totals,
+            b.zero_words, b.n_zero_words);
         const unsigned nbt = (unsigned)scan_block_count((int)T);
-        scan_blocks_kernel<<<nbt, 256, 0, s>>>(b.cell_count, (int)T, b.cell_scan, b.block_sums);
+        if (!KN_BIN_ATOMIC) scan_blocks_kernel<<<nbt, 256, 0, s>>>(b.cell_count, (int)T, b.cell_scan, b.block_sums);
+        const int* tscan = KN_BIN_ATOMIC ? b.cell_count : b.cell_scan;
         bucket_scatter_kernel<<<bp.nblocks, bin_threads, bp.nbuckets * sizeof(int), s>>>(
-            b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, b.cell_scan, b.block_sums,
-            (int)nbt, b.bin_tmp);
+            b.points, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, bp.per_block, tscan, b.block_sums,
+            (int)nbt, totals, bstart, b.bin_tmp);
         bucket_sort_kernel<<<bp.nbuckets, 256, (1u << bp.shift) * sizeof(int), s>>>(
-            b.bin_tmp, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, b.cell_scan, b.block_sums, C, b.cell_start,
-            b.sorted, b.perm, fuse_gid ? b.gids : nullptr, b.n_owned);
+            b.bin_tmp, n, b.geom, bp.shift, bp.nbuckets, bp.nblocks, b.cell_scan, b.block_sums, bstart, C,
+            b.cell_start, b.sorted, b.perm, fuse_gid ? b.gids : nullptr, b.n_owned);
         if (b.deterministic && (e = launch_cell_sort(b.cell_start, b.geom, n, b.sorted, b.perm, b.bin_tmp, s)) != hipSuccess)
             return e;
         if (b.gids && !fuse_gid) return launch_global_w(b.sorted, b.perm, b.gids, n, b.n_owned, s);
