@@ -180,6 +180,22 @@ hipError_t launch_copy_from_ref(const float* const* src_ref, float* dst, size_t 
 hipError_t launch_cell_sort(const int* cell_start, const GridGeom* geom, int n, float4* sorted, unsigned* perm,
                             float4* tmp, hipStream_t stream);
 
+// A distributed step's steady-state check run by the last workgroup of the exact finish kernel
+// (deferred mode, DistPipeline::stage_query): the arguments of steady_flag_partials_kernel
+// (route.hip, kn/step_flag.h) plus the max-accumulator and the kernel's workgroup ticket (zeroed
+// at allocation; the last workgroup resets it).
+struct StepFlagJob {
+    const unsigned* partials;  // route_count's bbox partials: 6 x stride words
+    int nb, stride, n;         // partial blocks, their stride, the share's true size
+    const double* planned;     // planned {lo, hi, n} meta (8 doubles)
+    const int* totals;         // this step's send counts ...
+    const int* ptotals;        // ... and the planned ones
+    int nt;
+    int* flag;                 // the set's flag word
+    int* pending;              // atomicMax accumulator of the launch's steps
+    unsigned* ticket;          // workgroup ticket (self-resetting)
+};
+
 struct QueryBuffers {
     const float4* sorted;
     const int* cell_start;
@@ -219,6 +235,9 @@ struct QueryBuffers {
     // 2: the exact finish only (after a mode-1 launch on the same counters / list: pipelined
     // steps run it on the build stream, off the query stream's critical path)
     int exact_mode;
+    // optional (exact modes 0 and 2): DEVICE pointer to the step check the exact kernel's last
+    // workgroup runs
+    const StepFlagJob* step_flag = nullptr;
 };
 
 hipError_t launch_query(const QueryBuffers& q, hipStream_t stream);

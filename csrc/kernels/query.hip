@@ -44,6 +44,7 @@
 
 #include "kn/kernels.h"
 #include "kn/knn_device.h"
+#include "kn/step_flag.h"
 #include "kn/wave.h"
 
 namespace kn {
@@ -1651,6 +1652,11 @@ struct ExactArgs {
     // ext[2t] = {x, y, z, bits(gid)} and ext[2t + 1].x its origin's K-th squared distance (an
     // upper bound: seeds the threshold); gid 0xFFFFFFFF = empty slot, skipped
     int ext_stride;
+    // deferred distributed steps: the step check run by the last workgroup (kn/step_flag.h); a
+    // DEVICE pointer (the job's fields as kernel arguments pushed the kernel past its SGPR budget
+    // into scratch)
+    const StepFlagJob* fjp = nullptr;
+    int has_fj = 0;
 };
 
 // ---- wave-per-query exact kernel: threshold compaction + wave bitonic sort (any K <= 128) ----
@@ -1847,6 +1853,35 @@ __global__ __launch_bounds__(256) void knn_exact_coop_kernel(ExactArgs a) {
             if (o_dist) o_dist[o] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
         }
         __builtin_amdgcn_wave_barrier();
+    }
+    if (a.has_fj) {
+        const StepFlagJob& fj = *a.fjp;
+        // last workgroup (device-scope ticket; every workgroup reaches this point: the query loop
+        // has no early exit): the step check once every query of the step, tile and exact, has
+        // counted its uncertified rows; then the ticket is reset for the next launch. Replaces two
+        // one-block kernels on the query stream (flag partials + accumulate) that each waited for a
+        // free CU slot beside the other query stream's tile kernel.
+        // No release / acquire fences (on gfx950 an agent-scope fence writes back the L2, per
+        // workgroup): the only value read across workgroups is counters[1], and every workgroup's
+        // increments of it are RETURNING device-scope atomics, complete (vmcnt) before the barrier
+        // that precedes its ticket; the last workgroup reads it with another atomic on the same
+        // address (RMWs of one address are performed in one coherence order). The partials and
+        // totals come from earlier kernels (stream order).
+        __shared__ int last_s;
+        __builtin_amdgcn_s_waitcnt(0);  // every wave's counter atomics returned (vmcnt = 0) ...
+        __syncthreads();                // ... before workgroup thread 0 takes the ticket
+        if (threadIdx.x == 0) last_s = atomicAdd(fj.ticket, 1u) == gridDim.x - 1 ? 1 : 0;
+        __syncthreads();
+        if (last_s) {
+            const unsigned unc = atomicAdd(a.counters + 1, 0u);
+            const int f = step_flag_eval(fj.partials, fj.nb, fj.stride, fj.n, fj.planned, fj.totals,
+                                         fj.ptotals, fj.nt, unc);
+            if (threadIdx.x == 0) {
+                fj.flag[0] = f;
+                atomicMax(fj.pending, f);
+                __hip_atomic_store(fj.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 }
 
@@ -2078,6 +2113,10 @@ hipError_t launch_k(const QueryBuffers& q, hipStream_t s) {
     b.uncert_list = q.uncert_list;
     b.ext = nullptr;
     b.n_ext = 0;
+    if (q.step_flag) {
+        b.fjp = q.step_flag;
+        b.has_fj = 1;
+    }
     // one wave per query (threshold compaction, any K): 1024 waves for the fallback list
     const unsigned grid = tiles ? (unsigned)(q.exact_grid > 0 ? q.exact_grid : KN_EXACT_GRID)
                                 : std::max(1u, std::min(cdiv(q.n, 4), 16384u));

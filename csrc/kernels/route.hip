@@ -20,6 +20,7 @@
 #include <cmath>
 
 #include "kn/route.h"
+#include "kn/step_flag.h"
 #include "kn/wave.h"
 
 namespace kn {
@@ -545,45 +546,9 @@ __global__ __launch_bounds__(1024) void steady_flag_partials_kernel(const unsign
                                             const unsigned* __restrict__ counters, int* __restrict__ flag,
                                             int* __restrict__ sticky, int* __restrict__ host_flag) {
     // block-wide reduction of the nb x 6 partials (launched with 256 threads: a 1024-thread block
-    // beside the running query kernels waits for 16 free wave slots on one CU)
-    __shared__ unsigned red[6][16];
-    __shared__ unsigned words_s[6];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int nbr = n > 0 ? nb : 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        unsigned v = 0u;
-        for (int b = threadIdx.x; b < nbr; b += blockDim.x) v = max(v, partials[(size_t)a * stride + b]);
-        v = wave_max_u32(v);
-        if (lane == 0) red[a][wid] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < 6) {
-        unsigned v = 0u;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) v = max(v, red[threadIdx.x][w]);
-        words_s[threadIdx.x] = v;
-    }
-    __syncthreads();
-    if (wid != 0) return;
-    unsigned words[6];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) words[a] = words_s[a];
-    bool diff = false;
-    if (lane < 8) {
-        unsigned wt = words[0];
-#pragma unroll
-        for (int a = 1; a < 6; ++a) wt = (lane == a) ? words[a] : wt;
-        double v;
-        if (lane < 3) v = n > 0 ? (double)meta_unord(~wt) : (double)INFINITY;
-        else if (lane < 6) v = n > 0 ? (double)meta_unord(wt) : -(double)INFINITY;
-        else if (lane == 6) v = (double)n;
-        else v = 0.0;
-        diff = v != planned[lane];  // a NaN never matches
-    }
-    for (int i = lane; i < nt; i += 64) diff |= totals[i] != ptotals[i];
-    const bool any = __builtin_amdgcn_ballot_w64(diff) != 0ull;
-    if (lane == 0) {
-        int f = (any ? 1 : 0) + (counters[1] != 0u ? 1 : 0);
+    // beside the running query kernels waits for 16 free wave slots on one CU); kn/step_flag.h
+    int f = step_flag_eval(partials, nb, stride, n, planned, totals, ptotals, nt, counters[1]);
+    if (threadIdx.x == 0) {
         if (sticky) {
             f = max(f, sticky[0]);
             sticky[0] = f;

@@ -240,6 +240,7 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
         S.idx = carve<int>(q, (size_t)n_owned_ * K);
         S.d2 = carve<float>(q, (size_t)n_owned_ * K);
         S.flag = carve<int>(q, 1);
+        S.ticket = carve<unsigned>(q, 1);
         return (size_t)(q - base);
     };
     Set probe{};
@@ -264,13 +265,19 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     // -1.5 %, K=50 equal; profiles/r5_dist.txt), off by default
     const char* tlv = std::getenv("KN_DIST_TAIL");
     tail_ = deferred_ && (tlv && tlv[0] == '1');
+    // KN_DIST_FUSED_FLAG=0: the step check as its own two kernels on the query stream (rounds 5-6)
+    const char* ffv = std::getenv("KN_DIST_FUSED_FLAG");
+    fused_flag_ = deferred_ && !tail_ && !(ffv && ffv[0] == '0');
     for (int s = 0; s < nsets_; ++s) {
         Set& S = set_[s];
         void* b = nullptr;
         if (device_malloc(&b, bytes) != hipSuccess) { fail("hipMalloc(distributed set)"); return; }
         S.block = static_cast<char*>(b);
         layout(S.block, S);
-        if (hipMemset(S.flag, 0, sizeof(int)) != hipSuccess) { fail("hipMemset"); return; }
+        if (hipMemset(S.flag, 0, sizeof(int)) != hipSuccess || hipMemset(S.ticket, 0, sizeof(unsigned)) != hipSuccess) {
+            fail("hipMemset");
+            return;
+        }
         S.tree_ws = S.tree_nodes = nullptr;
         if (p_.use_tree) {
             if (device_malloc(&S.tree_ws, std::max<size_t>(1, tree_workspace_bytes(rows_, p_.dims))) != hipSuccess ||
@@ -298,6 +305,9 @@ DistPipeline::DistPipeline(const DistPlan& p, RankComm* comm) : p_(p), comm_(com
     *host_flag_ = 0;
     if (hipHostGetDevicePointer(&v, host_flag_, 0) != hipSuccess) { fail("hipHostGetDevicePointer"); return; }
     host_flag_dev_ = static_cast<int*>(v);
+    if (device_malloc(&v, (size_t)Pipeline::kMaxSets * sizeof(StepFlagJob)) != hipSuccess) { fail("hipMalloc(jobs)"); return; }
+    jobs_dev_ = static_cast<StepFlagJob*>(v);
+    if (upload_jobs() != hipSuccess) { fail("step check upload"); return; }
     if (hipMemcpy(route_dev_, p_.route, sizeof(RouteParams), hipMemcpyDeviceToDevice) != hipSuccess ||
         hipMemcpy(metas_dev_, p_.metas, (size_t)W * 8 * sizeof(double), hipMemcpyDeviceToDevice) != hipSuccess ||
         hipMemcpy(tot_dev_, p_.tot.data(), (size_t)2 * W * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
@@ -419,7 +429,15 @@ kn_status DistPipeline::rebind(const float* points, const int* ids, int n) {
     // invalid on every rank (MAX all-reduce) while every rank issues the same collectives
     n_route_ = std::min(n, p_.n);
     n_flag_ = n;
+    if (upload_jobs() != hipSuccess) { err_ = "rebind: step check upload"; return KN_ERR_DEVICE; }
     return KN_OK;
+}
+
+// the sets' step checks (step_flag_job) in device memory, for the exact kernel (fused flag)
+hipError_t DistPipeline::upload_jobs() {
+    StepFlagJob h[Pipeline::kMaxSets]{};
+    for (int s = 0; s < nsets_; ++s) h[s] = step_flag_job(s);
+    return hipMemcpy(jobs_dev_, h, sizeof(h), hipMemcpyHostToDevice);
 }
 
 DistPipeline::~DistPipeline() {
@@ -431,7 +449,7 @@ DistPipeline::~DistPipeline() {
         if (S.tree_ws) (void)hipFree(S.tree_ws);
         if (S.tree_nodes) (void)hipFree(S.tree_nodes);
     }
-    for (void* v : {route_dev_, (void*)metas_dev_, (void*)tot_dev_, (void*)sticky_, (void*)pending_})
+    for (void* v : {route_dev_, (void*)metas_dev_, (void*)tot_dev_, (void*)sticky_, (void*)pending_, (void*)jobs_dev_})
         if (v) (void)hipFree(v);
     if (host_flag_) (void)hipHostFree(host_flag_);
     for (auto e : ring_) (void)hipEventDestroy(e);
@@ -534,6 +552,11 @@ hipError_t DistPipeline::stage_query(int s, hipStream_t st) {
     // on the side stream instead, engine.cpp exact_epilogue; deferred mode: always here)
     QueryBuffers q = query_proto(s);
     q.exact_mode = tail_ ? 1 : (!deferred_ && exact_epilogue(p_.k)) ? 1 : 0;
+    if (fused_flag_ && n_route_ <= n_flag_) {
+        // the same check as step_flag(), in the exact finish kernel's last workgroup
+        q.step_flag = jobs_dev_ + s;
+        return launch_query(q, st);
+    }
     KN_TRY(launch_query(q, st));
     if (deferred_ && !tail_) KN_TRY(step_flag(s, st));
     return hipSuccess;
@@ -548,6 +571,22 @@ hipError_t DistPipeline::stage_tail(int s, hipStream_t st) {
         KN_TRY(launch_query(q, st));
     }
     return step_flag(s, st);
+}
+
+StepFlagJob DistPipeline::step_flag_job(int s) const {
+    const Set& S = set_[s];
+    StepFlagJob j{};
+    j.partials = S.partials;
+    j.nb = j.stride = n_route_ > 0 ? route_block_count(n_route_) : 0;  // launch_steady_flag_partials' layout
+    j.n = n_flag_;
+    j.planned = metas_dev_ + 8 * p_.rank;
+    j.totals = S.totals;
+    j.ptotals = tot_dev_;
+    j.nt = 2 * p_.world;
+    j.flag = S.flag;
+    j.pending = pending_;
+    j.ticket = S.ticket;
+    return j;
 }
 
 // deferred mode: the step's local flag on its query stream, max-accumulated into pending_

@@ -154,7 +154,7 @@ private:
         unsigned* bbox; GridGeom* geom; int* cell_count; int* cell_scan; int* block_sums; int* cell_start;
         float4* bin_tmp; float4* sorted; unsigned* perm;
         unsigned* fallback; unsigned* counters; unsigned* uncert;
-        int* idx; float* d2; int* flag;
+        int* idx; float* d2; int* flag; unsigned* ticket;
         void* tree_ws; void* tree_nodes;
     };
     hipError_t stage_build(int s, hipStream_t st, const std::vector<hipEvent_t>* marks = nullptr);
@@ -162,6 +162,7 @@ private:
     hipError_t stage_tail(int s, hipStream_t st);  // tail mode: the exact finish + the step's flag
     hipError_t stage_flag(int s, hipStream_t st);  // epilogue: exact finish, flag, all-reduce
     hipError_t step_flag(int s, hipStream_t st);   // deferred mode: local flag -> pending_
+    StepFlagJob step_flag_job(int s) const;        // step_flag's arguments (fused into the exact kernel)
     QueryBuffers query_proto(int s) const;
     // wait for `ev`, polling RCCL's async error; past the deadline the communicator is aborted
     kn_status poll(hipEvent_t ev, double timeout_s, const char* what);
@@ -196,6 +197,11 @@ private:
     // deferred mode, KN_DIST_TAIL=1 (opt-in): the exact finish and the step's flag run as the
     // pipeline's epilogue on a stream of their own, so a query stream's next tile follows its tile
     bool tail_ = false;
+    // deferred grid steps (KN_DIST_FUSED_FLAG, default on): the step's check runs in the exact
+    // finish kernel's last workgroup (QueryBuffers::step_flag) instead of two kernels after it
+    bool fused_flag_ = false;
+    StepFlagJob* jobs_dev_ = nullptr;  // per set, device copies of step_flag_job (upload_jobs)
+    hipError_t upload_jobs();
     int* pending_ = nullptr;
     int* reduced_ = nullptr;
     int* host_flag_ = nullptr;      // pinned
