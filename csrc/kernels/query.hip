@@ -244,6 +244,36 @@ __device__ __forceinline__ void static_for(F& f) {
 // entries per shift of the rolled re-rank walk (KM > 24; see window_pass): 4 against 1 measured
 // K=50 -2 %, K=64 -3.6 % (profiles/ab_r6_rerank_group.txt); 8 a further -1 % at K=50, equal at K=32
 // and K=64 (profiles/ab_r6_k50.txt)
+// Re-rank row stores (KN_VEC_OUT, window pass): positions per global store -- 4 where the K
+// bucket is a multiple of 4, 2 for K=50 (200-byte rows: 8-byte aligned); 0 = per-entry stores
+#ifndef KN_VEC_OUT
+#define KN_VEC_OUT 1
+#endif
+template <int KT>
+constexpr int out_vec_width() {
+    return !KN_VEC_OUT ? 1 : (KT % 4 == 0 ? 4 : KT % 2 == 0 ? 2 : 1);
+}
+typedef unsigned kn_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned kn_u32x4 __attribute__((ext_vector_type(4)));
+typedef float kn_f32x2 __attribute__((ext_vector_type(2)));
+typedef float kn_f32x4 __attribute__((ext_vector_type(4)));
+template <int V>
+__device__ __forceinline__ void store_vec(out_u32_t* p, const unsigned (&v)[V]) {
+    if constexpr (V == 4) *(__attribute__((address_space(1))) kn_u32x4*)p = kn_u32x4{v[0], v[1], v[2], v[3]};
+    else if constexpr (V == 2) *(__attribute__((address_space(1))) kn_u32x2*)p = kn_u32x2{v[0], v[1]};
+    else *p = v[0];
+}
+template <int V>
+__device__ __forceinline__ void store_vec(out_f32_t* p, const float (&v)[V]) {
+    if constexpr (V == 4) *(__attribute__((address_space(1))) kn_f32x4*)p = kn_f32x4{v[0], v[1], v[2], v[3]};
+    else if constexpr (V == 2) *(__attribute__((address_space(1))) kn_f32x2*)p = kn_f32x2{v[0], v[1]};
+    else *p = v[0];
+}
+// KN_DIAG_SKIP_OUT=1 (diagnostics only, wrong results): the re-rank writes no rows -- the cost
+// of the scattered per-entry output stores
+#ifndef KN_DIAG_SKIP_OUT
+#define KN_DIAG_SKIP_OUT 0
+#endif
 #ifndef KN_RERANK_GROUP
 #define KN_RERANK_GROUP 8
 #endif
@@ -1009,6 +1039,20 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
         // duplication) take the wave-cooperative sort below.
         const unsigned qs = (unsigned)qslot;
         auto kvalid = [&](unsigned key) { return key != SENT && (!kSelfSlot || (key & MASK) != qs); };
+        // precision reference taken before the window pass consumes the keys (and before the
+        // self key is dropped below)
+        const unsigned last = keys[KM - 1];
+        if constexpr (kSelfSlot && KN_VEC_OUT) {
+            // drop the query's own key (d2 = 0: nearly always keys[0]) so the valid keys form a
+            // prefix and entry j lands at position j (+-1): the in-order row stores of the window
+            // pass rely on it. One compare and select per key; the self mask is a scalar OR.
+            bool seen = false;
+#pragma unroll
+            for (int t = 0; t < KM; ++t) {
+                seen = seen | ((keys[t] != SENT) & ((keys[t] & MASK) == qs));
+                keys[t] = seen ? (t + 1 < KM ? keys[t + 1 < KM ? t + 1 : KM - 1] : SENT) : keys[t];
+            }
+        }
         const bool force = (a.flags & kQueryForceRescan) != 0;
         bool ovf = force;
         // wider-window overflow (== ovf when the second window is off)
@@ -1027,8 +1071,6 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
         const unsigned orow = act ? w_row(a, qorig, qsidx) : 0u;
         const size_t row = (size_t)orow * (size_t)k;
         float dK2 = INFINITY;
-        // precision reference taken before the window pass consumes the keys
-        const unsigned last = keys[KM - 1];
         auto window_pass = [&](auto wc) {
             constexpr int W = decltype(wc)::value;
             // Rolled loop over the kept keys with constant register indices only: the key array
@@ -1057,6 +1099,22 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
             // test of the earlier entry can be dropped: a SENT key never shares a finite key's
             // bucket, and an invalid entry's own position is never used.)
             int c_prev = 0;
+            // KN_VEC_OUT (window W = 1): with disjoint swaps, POSITION j's final entry is known at
+            // step j -- entry j-1 if it swapped forward (c_prev), entry j+1 if j swaps with it
+            // (c_next), else entry j -- so the row is written in order, V positions per global
+            // store instead of one scattered 4-byte store per entry and array (those stores were
+            // 8 % of the K=16 kernel and 23 % at K=50: profiles/ab_r6_vec_out.txt). Positions past
+            // the valid prefix get don't-care values: such a row has nfound < k, fails
+            // certification and is rewritten by the exact path. Needs k % V == 0 and V-aligned
+            // output pointers (checked here, uniform), else the per-entry stores below.
+            constexpr int V = out_vec_width<KT>();
+            constexpr bool kVec = W == 1 && KN_RERANK_PAIR && V > 1;
+            const bool vec = kVec && (k % V) == 0 &&
+                             ((reinterpret_cast<uintptr_t>(o_idx) | reinterpret_cast<uintptr_t>(o_dist)) &
+                              (uintptr_t)(4 * V - 1)) == 0;
+            unsigned ob_i[V];
+            float ob_d[V];
+            int jb = 0;  // absolute index of the entry at u = 0 (the rolled loop's group base)
             // entry(u): the next kept key; u = its compile-time offset since the last shift of keys[]
             auto entry = [&](auto uc) __attribute__((always_inline)) {
                 constexpr int u = decltype(uc)::value;
@@ -1067,6 +1125,21 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     const int lt = (int)(wd[2] < wd[1]) | ((int)(wd[2] == wd[1]) & (int)(wi[2] < wi[1]));
                     const int c_next = same & lt;
                     pos += c_next - c_prev;
+                    if constexpr (kVec) {
+                        if (vec) {
+                            constexpr int sl = u % V;
+                            ob_d[sl] = c_prev ? wd[0] : (c_next ? wd[2] : wd[1]);
+                            ob_i[sl] = out_id(a, c_prev ? wi[0] : (c_next ? wi[2] : wi[1]));
+                            if constexpr (sl == V - 1) {
+                                const int j0 = jb + u - (V - 1);
+                                if (act && j0 < k && !KN_DIAG_SKIP_OUT) {
+                                    const size_t o = KN_IDX(row + (size_t)j0 + (V - 1), (size_t)a.n_queries * k, 210) - (V - 1);
+                                    store_vec<V>(o_idx + o, ob_i);
+                                    if (o_dist) store_vec<V>(o_dist + o, ob_d);
+                                }
+                            }
+                        }
+                    }
                     c_prev = c_next;
                 } else {
 #pragma unroll
@@ -1080,7 +1153,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                     pos += (t > W ? 1 : -1) * (same & lt);
                 }
                 }
-                if (vj && act && pos < k) {
+                if (!vec && vj && act && pos < k && !KN_DIAG_SKIP_OUT) {
                     const size_t o = KN_IDX(row + pos, (size_t)a.n_queries * k, 209);
                     o_idx[o] = out_id(a, wi[W]);
                     if (o_dist) o_dist[o] = wd[W];
@@ -1103,6 +1176,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                 constexpr int G = KN_RERANK_GROUP;
 #pragma unroll 1
                 for (int jj = 0; jj < KM; jj += G) {
+                    jb = jj;
                     static_for<0, G>(entry);
 #pragma unroll
                     for (int t = 0; t < KM; ++t) keys[t] = t + G < KM ? keys[t + G < KM ? t + G : KM - 1] : SENT;
