@@ -66,6 +66,32 @@ typedef float out_f32_t;
 __device__ __forceinline__ out_u32_t* out_ptr(unsigned* p) { return (out_u32_t*)p; }
 __device__ __forceinline__ out_f32_t* out_ptr(float* p) { return (out_f32_t*)p; }
 
+// Row stores of the query kernels (KN_VEC_OUT: query.hip re-rank window pass, tree.hip leaf
+// search): positions per global store -- 4 where the K
+// bucket is a multiple of 4, 2 for K=50 (200-byte rows: 8-byte aligned); 0 = per-entry stores
+#ifndef KN_VEC_OUT
+#define KN_VEC_OUT 1
+#endif
+template <int KT>
+constexpr int out_vec_width() {
+    return !KN_VEC_OUT ? 1 : (KT % 4 == 0 ? 4 : KT % 2 == 0 ? 2 : 1);
+}
+typedef unsigned kn_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned kn_u32x4 __attribute__((ext_vector_type(4)));
+typedef float kn_f32x2 __attribute__((ext_vector_type(2)));
+typedef float kn_f32x4 __attribute__((ext_vector_type(4)));
+template <int V>
+__device__ __forceinline__ void store_vec(out_u32_t* p, const unsigned (&v)[V]) {
+    if constexpr (V == 4) *(__attribute__((address_space(1))) kn_u32x4*)p = kn_u32x4{v[0], v[1], v[2], v[3]};
+    else if constexpr (V == 2) *(__attribute__((address_space(1))) kn_u32x2*)p = kn_u32x2{v[0], v[1]};
+    else *p = v[0];
+}
+template <int V>
+__device__ __forceinline__ void store_vec(out_f32_t* p, const float (&v)[V]) {
+    if constexpr (V == 4) *(__attribute__((address_space(1))) kn_f32x4*)p = kn_f32x4{v[0], v[1], v[2], v[3]};
+    else if constexpr (V == 2) *(__attribute__((address_space(1))) kn_f32x2*)p = kn_f32x2{v[0], v[1]};
+    else *p = v[0];
+}
 __device__ __forceinline__ bool pair_less(float da, unsigned ia, float db, unsigned ib) {
     return da < db || (da == db && ia < ib);
 }

@@ -244,31 +244,6 @@ __device__ __forceinline__ void static_for(F& f) {
 // entries per shift of the rolled re-rank walk (KM > 24; see window_pass): 4 against 1 measured
 // K=50 -2 %, K=64 -3.6 % (profiles/ab_r6_rerank_group.txt); 8 a further -1 % at K=50, equal at K=32
 // and K=64 (profiles/ab_r6_k50.txt)
-// Re-rank row stores (KN_VEC_OUT, window pass): positions per global store -- 4 where the K
-// bucket is a multiple of 4, 2 for K=50 (200-byte rows: 8-byte aligned); 0 = per-entry stores
-#ifndef KN_VEC_OUT
-#define KN_VEC_OUT 1
-#endif
-template <int KT>
-constexpr int out_vec_width() {
-    return !KN_VEC_OUT ? 1 : (KT % 4 == 0 ? 4 : KT % 2 == 0 ? 2 : 1);
-}
-typedef unsigned kn_u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned kn_u32x4 __attribute__((ext_vector_type(4)));
-typedef float kn_f32x2 __attribute__((ext_vector_type(2)));
-typedef float kn_f32x4 __attribute__((ext_vector_type(4)));
-template <int V>
-__device__ __forceinline__ void store_vec(out_u32_t* p, const unsigned (&v)[V]) {
-    if constexpr (V == 4) *(__attribute__((address_space(1))) kn_u32x4*)p = kn_u32x4{v[0], v[1], v[2], v[3]};
-    else if constexpr (V == 2) *(__attribute__((address_space(1))) kn_u32x2*)p = kn_u32x2{v[0], v[1]};
-    else *p = v[0];
-}
-template <int V>
-__device__ __forceinline__ void store_vec(out_f32_t* p, const float (&v)[V]) {
-    if constexpr (V == 4) *(__attribute__((address_space(1))) kn_f32x4*)p = kn_f32x4{v[0], v[1], v[2], v[3]};
-    else if constexpr (V == 2) *(__attribute__((address_space(1))) kn_f32x2*)p = kn_f32x2{v[0], v[1]};
-    else *p = v[0];
-}
 // KN_DIAG_SKIP_OUT=1 (diagnostics only, wrong results): the re-rank writes no rows -- the cost
 // of the scattered per-entry output stores
 #ifndef KN_DIAG_SKIP_OUT

@@ -720,7 +720,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(tree_wpe<KT
         const unsigned nets = (unsigned)__builtin_amdgcn_readfirstlane((int)nnet);
         if (lane == 0) atomicAdd(a.counters + 6, nets);
     }
-    if (live && cert) {
+    // KN_VEC_OUT (kn/knn_device.h): V positions of the row per global store when k % V == 0 and the
+    // output pointers are V-aligned, instead of one scattered 4-byte store per entry and array
+    constexpr int V = out_vec_width<KT>();
+    const bool vec = V > 1 && (k % V) == 0 &&
+                     ((reinterpret_cast<uintptr_t>(o_idx) | reinterpret_cast<uintptr_t>(o_dist)) &
+                      (uintptr_t)(4 * V - 1)) == 0;
+    if (live && cert && vec) {
+        const unsigned row = w_row(a, qw, a.row_of ? a.src[KN_IDX(qpos, (unsigned)a.n, 419)] : qpos);
+#pragma unroll
+        for (int j0 = 0; j0 < KT; j0 += V) {
+            if (j0 < k) {
+                const size_t o = KN_IDX((size_t)row * (size_t)k + j0 + (V - 1), (size_t)a.n_queries * k, 407) - (V - 1);
+                unsigned vi[V];
+                float vd[V];
+#pragma unroll
+                for (int u = 0; u < V; ++u) {
+                    const unsigned long long v = has_self ? e[j0 + u + 1] : e[j0 + u];
+                    const bool empty = v == ~0ull;
+                    vi[u] = empty ? SENT : out_id(a, (unsigned)v);
+                    vd[u] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
+                }
+                store_vec<V>(o_idx + o, vi);
+                if (o_dist) store_vec<V>(o_dist + o, vd);
+            }
+        }
+    } else if (live && cert) {
         const unsigned row = w_row(a, qw, a.row_of ? a.src[KN_IDX(qpos, (unsigned)a.n, 419)] : qpos);
 #pragma unroll
         for (int j = 0; j < KT; ++j) {
