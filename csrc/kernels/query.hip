@@ -1104,7 +1104,9 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                         if (vec) {
                             constexpr int sl = u % V;
                             ob_d[sl] = c_prev ? wd[0] : (c_next ? wd[2] : wd[1]);
-                            ob_i[sl] = out_id(a, c_prev ? wi[0] : (c_next ? wi[2] : wi[1]));
+                            // (an invalid entry's id is SENT: never through out_id's id_map gather)
+                            const unsigned oid = c_prev ? wi[0] : (c_next ? wi[2] : wi[1]);
+                            ob_i[sl] = oid == SENT ? SENT : out_id(a, oid);
                             if constexpr (sl == V - 1) {
                                 const int j0 = jb + u - (V - 1);
                                 if (act && j0 < k && !KN_DIAG_SKIP_OUT) {
