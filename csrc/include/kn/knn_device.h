@@ -72,9 +72,26 @@ __device__ __forceinline__ out_f32_t* out_ptr(float* p) { return (out_f32_t*)p; 
 #ifndef KN_VEC_OUT
 #define KN_VEC_OUT 1
 #endif
+#ifndef KN_VEC_TAIL
+#define KN_VEC_TAIL 0
+#endif
 template <int KT>
 constexpr int out_vec_width() {
-    return !KN_VEC_OUT ? 1 : (KT % 4 == 0 ? 4 : KT % 2 == 0 ? 2 : 1);
+    return !KN_VEC_OUT ? 1 : (KT % 4 == 0 || (KN_VEC_TAIL && KT % 4 == 2) ? 4 : KT % 2 == 0 ? 2 : 1);
+}
+// KN_VEC_TAIL: a k with k % 4 == 2 (K=50, or k=6 in the K=8 bucket) is also stored 4 positions
+// at a time -- its rows are only 8-byte aligned (dword alignment is what the 16-byte global
+// stores need) -- plus one 2-position store for the row's last two. 0 (default): the K=50 bucket
+// stores 2 positions at a time, and other buckets' k % 4 == 2 queries one entry per store.
+// Measured: K=50 query 0.664 -> 0.729 ms with the tail, 100 / 30 steps 0.536 -> 0.600 (the
+// 16-byte stores at 8-byte aligned rows split); tree surfaces -1 % (profiles/ab_r6_vec_tail.txt).
+// run-time check of a query's k against the store width V (and the 2-position tail)
+template <int V>
+__device__ __forceinline__ bool out_vec_ok(int k, const void* p0, const void* p1) {
+    const bool kk = V == 4 ? ((k & 3) == 0 || (KN_VEC_TAIL && (k & 3) == 2)) : (k % V) == 0;
+    // row starts: k * 4 bytes apart; with the tail they are 8-byte aligned only
+    const uintptr_t amask = V == 4 && (k & 3) != 0 ? 7u : (uintptr_t)(4 * V - 1);
+    return V > 1 && kk && ((reinterpret_cast<uintptr_t>(p0) | reinterpret_cast<uintptr_t>(p1)) & amask) == 0;
 }
 typedef unsigned kn_u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned kn_u32x4 __attribute__((ext_vector_type(4)));

@@ -1084,9 +1084,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
             // output pointers (checked here, uniform), else the per-entry stores below.
             constexpr int V = out_vec_width<KT>();
             constexpr bool kVec = W == 1 && KN_RERANK_PAIR && V > 1;
-            const bool vec = kVec && (k % V) == 0 &&
-                             ((reinterpret_cast<uintptr_t>(o_idx) | reinterpret_cast<uintptr_t>(o_dist)) &
-                              (uintptr_t)(4 * V - 1)) == 0;
+            const bool vec = kVec && out_vec_ok<V>(k, (const void*)o_idx, (const void*)o_dist);
             unsigned ob_i[V];
             float ob_d[V];
             int jb = 0;  // absolute index of the entry at u = 0 (the rolled loop's group base)
@@ -1109,10 +1107,20 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(tile_wpe<KT
                             ob_i[sl] = oid == SENT ? SENT : out_id(a, oid);
                             if constexpr (sl == V - 1) {
                                 const int j0 = jb + u - (V - 1);
-                                if (act && j0 < k && !KN_DIAG_SKIP_OUT) {
+                                if (act && j0 + (V - 1) < k && !KN_DIAG_SKIP_OUT) {
                                     const size_t o = KN_IDX(row + (size_t)j0 + (V - 1), (size_t)a.n_queries * k, 210) - (V - 1);
                                     store_vec<V>(o_idx + o, ob_i);
                                     if (o_dist) store_vec<V>(o_dist + o, ob_d);
+                                }
+                            }
+                            if constexpr (V == 4 && KN_VEC_TAIL && sl == 1) {
+                                // the row's last two positions (k % 4 == 2)
+                                if (act && jb + u == k - 1 && !KN_DIAG_SKIP_OUT) {
+                                    const size_t o = KN_IDX(row + (size_t)k - 1, (size_t)a.n_queries * k, 211) - 1;
+                                    const unsigned ti[2] = {ob_i[0], ob_i[1]};
+                                    const float td[2] = {ob_d[0], ob_d[1]};
+                                    store_vec<2>(o_idx + o, ti);
+                                    if (o_dist) store_vec<2>(o_dist + o, td);
                                 }
                             }
                         }

@@ -723,26 +723,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(tree_wpe<KT
     // KN_VEC_OUT (kn/knn_device.h): V positions of the row per global store when k % V == 0 and the
     // output pointers are V-aligned, instead of one scattered 4-byte store per entry and array
     constexpr int V = out_vec_width<KT>();
-    const bool vec = V > 1 && (k % V) == 0 &&
-                     ((reinterpret_cast<uintptr_t>(o_idx) | reinterpret_cast<uintptr_t>(o_dist)) &
-                      (uintptr_t)(4 * V - 1)) == 0;
+    const bool vec = out_vec_ok<V>(k, (const void*)o_idx, (const void*)o_dist);
     if (live && cert && vec) {
         const unsigned row = w_row(a, qw, a.row_of ? a.src[KN_IDX(qpos, (unsigned)a.n, 419)] : qpos);
 #pragma unroll
         for (int j0 = 0; j0 < KT; j0 += V) {
-            if (j0 < k) {
-                const size_t o = KN_IDX((size_t)row * (size_t)k + j0 + (V - 1), (size_t)a.n_queries * k, 407) - (V - 1);
+            // a whole group, or (K % 4 == 2) the row's last two positions
+            const bool whole = j0 + (V - 1) < k;
+            if (whole || (V == 4 && KN_VEC_TAIL && j0 + 1 == k - 1)) {
                 unsigned vi[V];
                 float vd[V];
 #pragma unroll
                 for (int u = 0; u < V; ++u) {
-                    const unsigned long long v = has_self ? e[j0 + u + 1] : e[j0 + u];
+                    const int j = j0 + u < KT ? j0 + u : KT - 1;
+                    const unsigned long long v = has_self ? e[j + 1] : e[j];
                     const bool empty = v == ~0ull;
                     vi[u] = empty ? SENT : out_id(a, (unsigned)v);
                     vd[u] = empty ? INFINITY : __uint_as_float((unsigned)(v >> 32));
                 }
-                store_vec<V>(o_idx + o, vi);
-                if (o_dist) store_vec<V>(o_dist + o, vd);
+                if (whole) {
+                    const size_t o = KN_IDX((size_t)row * (size_t)k + j0 + (V - 1), (size_t)a.n_queries * k, 407) - (V - 1);
+                    store_vec<V>(o_idx + o, vi);
+                    if (o_dist) store_vec<V>(o_dist + o, vd);
+                } else {
+                    const size_t o = KN_IDX((size_t)row * (size_t)k + j0 + 1, (size_t)a.n_queries * k, 408) - 1;
+                    const unsigned ti[2] = {vi[0], vi[1]};
+                    const float td[2] = {vd[0], vd[1]};
+                    store_vec<2>(o_idx + o, ti);
+                    if (o_dist) store_vec<2>(o_dist + o, td);
+                }
             }
         }
     } else if (live && cert) {

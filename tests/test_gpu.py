@@ -42,6 +42,19 @@ def test_uniform_tile_vs_oracle(cuda, k):
     _assert_matches_oracle(p, idx, d2, k)
 
 
+@pytest.mark.parametrize("k", [6, 10, 12, 14, 30, 42, 45, 46, 48])
+@pytest.mark.parametrize("gen", ["uniform", "clustered"])
+def test_row_store_widths_vs_oracle(cuda, k, gen):
+    # the re-rank and tree kernels write rows 4 positions per store when k % 4 == 0, 4 plus a
+    # 2-position tail when k % 4 == 2 (8-byte aligned rows), else one entry per store
+    # (kn/knn_device.h KN_VEC_OUT / KN_VEC_TAIL): every width, inside K buckets, on the grid
+    # (uniform) and tree (clustered) paths
+    mk = uniform_cloud if gen == "uniform" else clustered_cloud
+    p = mk(30000, seed=300 + k, device=cuda)
+    idx, d2 = kn.knn(p, k)
+    _assert_matches_oracle(p, idx, d2, k)
+
+
 @pytest.mark.parametrize("k", [1, 16, 50])
 def test_forced_exact_rescan(cuda, k):
     # the wave-cooperative exact re-rank normally runs only for window overflows (long runs of
