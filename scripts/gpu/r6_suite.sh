@@ -16,3 +16,5 @@ for l in open("gpurun_out/r6suite/bench_suite.jsonl"):
     d = json.loads(l)
     print(f"{d['suite_label'][:60]:60s} {d['ms_per_step']:8.4f} ms  {d['value']:.3e} q/s  build {d.get('ms_build')} solve {d.get('ms_solve')} chk {d.get('check',{}).get('bad_rows', d.get('check',{}).get('bad_rows_all_ranks'))}")
 PY
+timeout -k 10 300 python scripts/diag_checked.py > $O/checked.log 2>&1 || { echo CHECKED_FAIL; tail -20 $O/checked.log; exit 1; }
+tail -3 $O/checked.log
