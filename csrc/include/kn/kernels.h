@@ -150,7 +150,12 @@ struct BuildBuffers {
     // kernels: 256-thread streaming blocks of ~16K points up to 4M points), 1 = serial (alone on the
     // device: 1024-thread blocks of 4096 points, one block per CU at 900K)
     int serial;
+    // 1: a kernel earlier on the stream zeroed cell_scan[0, bin_totals_words(C)) (the bucketed
+    // build's totals; DistPipeline's route_count): no memset node with a fixed box
+    int totals_zeroed = 0;
 };
+// ints of cell_scan that hold the bucketed build's bucket totals at most (nbuckets <= 4096, <= C + 1)
+inline int bin_totals_words(int num_cells) { return num_cells + 1 < 4096 ? num_cells + 1 : 4096; }
 
 size_t scan_block_count(int num_cells);
 

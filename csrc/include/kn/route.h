@@ -121,9 +121,11 @@ int route_block_count(int n);
 // meta -> plan -> count chain is enqueued without a host round trip. `world` = p->world.
 // block_counts: 2*world*route_block_count(n) ints (column-major, scanned in place);
 // totals: 2*world ints = (owned, halo) rows per destination.
+// zero_ints / n_zero (optional): ints block 0 zeroes on the way (the following build's bucket
+// totals, BuildBuffers::totals_zeroed)
 hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int world, int* block_counts,
                               int* totals, hipStream_t s,
-                              unsigned* partials = nullptr);
+                              unsigned* partials = nullptr, int* zero_ints = nullptr, int n_zero = 0);
 // ids == nullptr: global id = p->id_offset + local index.
 // self_last < 0: segments in destination order 0..world-1. self_last = rank: the other
 // destinations in order, then the rank's own segment at the end (kept out of the collective).

@@ -915,7 +915,8 @@ hipError_t launch_build(const BuildBuffers& b, hipStream_t s) {
             if ((e = launch_bbox_partials(b.points, n, b.bbox_words, s, totals, n_tot)) != hipSuccess) return e;
             src.partials = b.bbox_words;
             src.nbb = bbox_block_count(n);
-        } else if (n_tot && (e = hipMemsetAsync(totals, 0, (size_t)n_tot * sizeof(int), s)) != hipSuccess) {
+        } else if (n_tot && !b.totals_zeroed &&
+                   (e = hipMemsetAsync(totals, 0, (size_t)n_tot * sizeof(int), s)) != hipSuccess) {
             return e;
         }
         const size_t T = (size_t)bp.nbuckets * bp.nblocks;

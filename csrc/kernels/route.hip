@@ -96,8 +96,11 @@ __device__ __forceinline__ float meta_unord(unsigned u) {
 __global__ __launch_bounds__(kRT) void route_count_kernel(const float* __restrict__ pts, int n,
                                                           const RouteParams* __restrict__ pp,
                                                           int* __restrict__ block_counts, int nb,
-                                                          unsigned* __restrict__ partials) {
+                                                          unsigned* __restrict__ partials,
+                                                          int* __restrict__ zero_ints, int n_zero) {
     const RouteParams& p = *pp;
+    if (blockIdx.x == 0)
+        for (int j = threadIdx.x; j < n_zero; j += blockDim.x) zero_ints[j] = 0;
     __shared__ int cnt[2 * kRouteMaxWorld];
     __shared__ unsigned red[6][kRT / 64];
     const int cols = 2 * p.world;
@@ -725,10 +728,11 @@ int split_hist_blocks(int n) { return std::max(1, std::min((int)cdiv((size_t)n, 
 int route_block_count(int n) { return std::max(1, (int)cdiv((size_t)std::max(n, 0), kRouteItems)); }
 
 hipError_t launch_route_count(const float* pts, int n, const RouteParams* p, int world, int* block_counts,
-                              int* totals, hipStream_t s, unsigned* partials) {
+                              int* totals, hipStream_t s, unsigned* partials, int* zero_ints, int n_zero) {
     if (world < 1 || world > kRouteMaxWorld) return hipErrorInvalidValue;
     const int nb = route_block_count(n);
-    route_count_kernel<<<nb, kRT, 0, s>>>(pts, n, p, block_counts, nb, partials);
+    if (!zero_ints) n_zero = 0;
+    route_count_kernel<<<nb, kRT, 0, s>>>(pts, n, p, block_counts, nb, partials, zero_ints, n_zero);
     route_scan_kernel<<<2 * world, kRT, 0, s>>>(block_counts, nb, totals);
     return hipGetLastError();
 }

@@ -488,7 +488,9 @@ hipError_t DistPipeline::stage_build(int s, hipStream_t st, const std::vector<hi
     Set& S = set_[s];
     const auto* rp = static_cast<const RouteParams*>(route_dev_);
     if (n_route_ > 0) {
-        KN_TRY(launch_route_count(p_.points, n_route_, rp, p_.world, S.bc, S.totals, st, S.partials));
+        // block 0 also zeroes the build's bucket totals (no memset node before the build)
+        KN_TRY(launch_route_count(p_.points, n_route_, rp, p_.world, S.bc, S.totals, st, S.partials, S.cell_scan,
+                                  bin_totals_words(C_)));
         if (p_.self_via_comm) {
             KN_TRY(launch_route_scatter(p_.points, p_.ids, n_route_, rp, p_.world, S.bc, S.totals, S.send, p_.cap, p_.rank, st));
         } else {
@@ -518,6 +520,7 @@ hipError_t DistPipeline::stage_build(int s, hipStream_t st, const std::vector<hi
     b.perm = S.perm;
     b.gids = S.lgids;
     b.zero_words = S.counters;
+    b.totals_zeroed = n_route_ > 0 ? 1 : 0;
     KN_TRY(launch_build(b, st));
     if (p_.use_tree && rows_ > 0) {
         TreeView t = tree_view(S.tree_ws, rows_, p_.dims);
